@@ -1,0 +1,307 @@
+// TORCH_LIBRARY registration of the symmetry_amd CDNA4 kernels.
+//
+// Every op is out-parameter style (the caller pre-allocates), allocates
+// nothing, and launches on torch's current HIP stream, so the model runner can
+// capture a whole decode step into a hipGraph.  All shape / dtype / layout
+// preconditions the kernels and their grids assume are checked here, on the
+// host, before any launch.
+//
+// Note on names: ROCm builds of PyTorch report HIP tensors with the device
+// type spelled "cuda" (c10::DeviceType::CUDA); that is torch's enum, not a
+// compatibility layer in this code.
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include "launchers.h"
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream(const Tensor& t) { return c10::hip::getCurrentHIPStream(t.get_device()).stream(); }
+
+void check_gpu(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.device().type() == c10::DeviceType::CUDA, name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void check_dtype(const Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+}
+
+template <typename T>
+T* ptr(const Tensor& t) {
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+
+// bf16 [T][N] or fp32 slabs [S][T][N] (or fp32 [T][N] == one slab).
+LinOut linout(const Tensor& t, int64_t T, int64_t N, const char* name) {
+  check_gpu(t, name);
+  LinOut L{};
+  L.ptr = t.data_ptr();
+  if (t.scalar_type() == at::kBFloat16) {
+    TORCH_CHECK(t.dim() == 2 && t.size(0) == T && t.size(1) == N, name, ": expected bf16 [", T, ",", N, "], got ",
+                t.sizes());
+    L.is_f32 = 0;
+    L.nsplit = 1;
+    L.split_stride = 0;
+  } else {
+    check_dtype(t, at::kFloat, name);
+    if (t.dim() == 2) {
+      TORCH_CHECK(t.size(0) == T && t.size(1) == N, name, ": expected [", T, ",", N, "], got ", t.sizes());
+      L.nsplit = 1;
+    } else {
+      TORCH_CHECK(t.dim() == 3 && t.size(1) == T && t.size(2) == N, name, ": expected [S,", T, ",", N, "], got ",
+                  t.sizes());
+      L.nsplit = (int)t.size(0);
+    }
+    L.is_f32 = 1;
+    L.split_stride = T * N;
+  }
+  return L;
+}
+
+int64_t rows_of(const Tensor& t) { return t.dim() == 3 ? t.size(1) : t.size(0); }
+int64_t cols_of(const Tensor& t) { return t.size(t.dim() - 1); }
+
+// ----------------------------------------------------------------------------------------------
+void rms_norm(const Tensor& x, const Tensor& w, double eps, Tensor& out) {
+  const int64_t T = rows_of(x), d = cols_of(x);
+  check_gpu(w, "w");
+  check_gpu(out, "out");
+  check_dtype(w, at::kBFloat16, "w");
+  check_dtype(out, at::kBFloat16, "out");
+  TORCH_CHECK(d % 8 == 0 && d <= 16384, "rms_norm: d must be a multiple of 8 and <= 16384");
+  TORCH_CHECK(w.numel() == d && out.numel() == T * d, "rms_norm: shape mismatch");
+  const at::OptionalDeviceGuard g(x.device());
+  launch_rms_norm(linout(x, T, d, "x"), ptr<bf16>(w), ptr<bf16>(out), (int)T, (int)d, (float)eps, cur_stream(x));
+}
+
+void add_rms_norm(const Tensor& delta, Tensor& residual, const Tensor& w, double eps, Tensor& out) {
+  check_gpu(residual, "residual");
+  check_dtype(residual, at::kFloat, "residual");
+  TORCH_CHECK(residual.dim() == 2, "residual must be [T, d]");
+  const int64_t T = residual.size(0), d = residual.size(1);
+  check_gpu(w, "w");
+  check_gpu(out, "out");
+  check_dtype(w, at::kBFloat16, "w");
+  check_dtype(out, at::kBFloat16, "out");
+  TORCH_CHECK(d % 8 == 0 && d <= 16384, "add_rms_norm: d must be a multiple of 8 and <= 16384");
+  TORCH_CHECK(w.numel() == d && out.numel() == T * d, "add_rms_norm: shape mismatch");
+  const at::OptionalDeviceGuard g(residual.device());
+  launch_add_rms_norm(linout(delta, T, d, "delta"), ptr<float>(residual), ptr<bf16>(w), ptr<bf16>(out), (int)T,
+                      (int)d, (float)eps, cur_stream(residual));
+}
+
+void embed_rms_norm(const Tensor& ids, const Tensor& table, Tensor& residual, const Tensor& w, double eps,
+                    Tensor& out) {
+  check_gpu(ids, "ids");
+  check_gpu(table, "table");
+  check_gpu(residual, "residual");
+  check_dtype(ids, at::kInt, "ids");
+  check_dtype(table, at::kBFloat16, "table");
+  check_dtype(residual, at::kFloat, "residual");
+  check_dtype(out, at::kBFloat16, "out");
+  const int64_t T = ids.numel(), d = table.size(1);
+  TORCH_CHECK(residual.numel() == T * d && out.numel() == T * d && w.numel() == d, "embed_rms_norm: shape mismatch");
+  TORCH_CHECK(d % 8 == 0 && d <= 16384, "embed_rms_norm: bad d");
+  const at::OptionalDeviceGuard g(ids.device());
+  launch_embed_rms_norm(ptr<int>(ids), ptr<bf16>(table), ptr<float>(residual), ptr<bf16>(w), ptr<bf16>(out), (int)T,
+                        (int)d, (float)eps, cur_stream(ids));
+}
+
+void rope_cache(const Tensor& qkv, const Tensor& positions, const Tensor& slots, const Tensor& cos_sin,
+                Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t Hq, int64_t Hkv) {
+  check_gpu(positions, "positions");
+  check_gpu(slots, "slots");
+  check_gpu(cos_sin, "cos_sin");
+  check_gpu(q_out, "q_out");
+  check_gpu(k_cache, "k_cache");
+  check_gpu(v_cache, "v_cache");
+  check_dtype(positions, at::kInt, "positions");
+  check_dtype(slots, at::kInt, "slots");
+  check_dtype(cos_sin, at::kFloat, "cos_sin");
+  check_dtype(q_out, at::kBFloat16, "q_out");
+  check_dtype(k_cache, at::kBFloat16, "k_cache");
+  check_dtype(v_cache, at::kBFloat16, "v_cache");
+  const int64_t T = positions.numel();
+  TORCH_CHECK(k_cache.dim() == 4, "k_cache must be [NB, Hkv, BS, D]");
+  const int64_t BS = k_cache.size(2), D = k_cache.size(3);
+  TORCH_CHECK(k_cache.size(1) == Hkv, "k_cache head count mismatch");
+  TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(0) == k_cache.size(0) && v_cache.size(1) == Hkv &&
+                  v_cache.size(2) == D && v_cache.size(3) == BS,
+              "v_cache must be [NB, Hkv, D, BS]");
+  TORCH_CHECK(D % 16 == 0, "head dim must be a multiple of 16");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D, "cos_sin must be [max_pos, D]");
+  TORCH_CHECK(slots.numel() == T, "slots must have T entries");
+  TORCH_CHECK(q_out.numel() == T * Hq * D, "q_out shape mismatch");
+  const at::OptionalDeviceGuard g(positions.device());
+  launch_rope_cache(linout(qkv, T, (Hq + 2 * Hkv) * D, "qkv"), ptr<int>(positions), ptr<int>(slots),
+                    ptr<float>(cos_sin), ptr<bf16>(q_out), ptr<bf16>(k_cache), ptr<bf16>(v_cache), (int)T, (int)Hq,
+                    (int)Hkv, (int)D, (int)BS, cur_stream(positions));
+}
+
+void check_cache(const Tensor& k_cache, const Tensor& v_cache) {
+  check_gpu(k_cache, "k_cache");
+  check_gpu(v_cache, "v_cache");
+  check_dtype(k_cache, at::kBFloat16, "k_cache");
+  check_dtype(v_cache, at::kBFloat16, "v_cache");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(3) == 128, "attention kernels require head_dim == 128");
+  TORCH_CHECK(k_cache.size(2) % 32 == 0, "attention kernels require block_size % 32 == 0");
+  TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(2) == 128 && v_cache.size(3) == k_cache.size(2),
+              "v_cache must be [NB, Hkv, D, BS]");
+}
+
+void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
+                 const Tensor& ctx_lens, Tensor& out, Tensor& tmp_o, Tensor& tmp_ml, double scale) {
+  check_gpu(q, "q");
+  check_dtype(q, at::kBFloat16, "q");
+  check_cache(k_cache, v_cache);
+  check_gpu(block_tables, "block_tables");
+  check_gpu(ctx_lens, "ctx_lens");
+  check_dtype(block_tables, at::kInt, "block_tables");
+  check_dtype(ctx_lens, at::kInt, "ctx_lens");
+  check_gpu(out, "out");
+  check_dtype(out, at::kBFloat16, "out");
+  TORCH_CHECK(q.dim() == 3 && q.size(2) == 128, "q must be [num_seqs, Hq, 128]");
+  const int64_t S = q.size(0), Hq = q.size(1), Hkv = k_cache.size(1);
+  TORCH_CHECK(Hq % Hkv == 0 && Hq / Hkv <= 16, "GQA group must divide and be <= 16");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= S, "block_tables must be [>=num_seqs, max_blocks]");
+  TORCH_CHECK(ctx_lens.numel() >= S, "ctx_lens too short");
+  TORCH_CHECK(out.numel() == S * Hq * 128, "out shape mismatch");
+  check_gpu(tmp_o, "tmp_o");
+  check_gpu(tmp_ml, "tmp_ml");
+  TORCH_CHECK(tmp_o.dim() == 4 && tmp_o.size(0) >= S && tmp_o.size(1) == Hq && tmp_o.size(3) == 128,
+              "tmp_o must be [>=num_seqs, Hq, max_parts, 128]");
+  const int64_t max_parts = tmp_o.size(2);
+  TORCH_CHECK(tmp_ml.numel() >= S * Hq * max_parts * 2, "tmp_ml too small");
+  const int64_t BS = k_cache.size(2), max_blocks = block_tables.size(1);
+  TORCH_CHECK(max_parts * 256 >= max_blocks * BS, "tmp_o has too few partitions for the block table span");
+  const at::OptionalDeviceGuard g(q.device());
+  launch_attn_decode(ptr<bf16>(q), ptr<bf16>(k_cache), ptr<bf16>(v_cache), ptr<int>(block_tables), ptr<int>(ctx_lens),
+                     ptr<bf16>(out), ptr<float>(tmp_o), ptr<float>(tmp_ml), (int)S, (int)Hq, (int)Hkv, (int)BS,
+                     (int)max_blocks, (int)max_parts, (float)scale, cur_stream(q));
+}
+
+void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
+                  const Tensor& ctx_lens, const Tensor& cu_q, const Tensor& tiles, Tensor& out, double scale) {
+  check_gpu(q, "q");
+  check_dtype(q, at::kBFloat16, "q");
+  check_cache(k_cache, v_cache);
+  for (auto* t : {&block_tables, &ctx_lens, &cu_q, &tiles}) {
+    check_gpu(*t, "index tensor");
+    check_dtype(*t, at::kInt, "index tensor");
+  }
+  check_gpu(out, "out");
+  check_dtype(out, at::kBFloat16, "out");
+  TORCH_CHECK(q.dim() == 3 && q.size(2) == 128, "q must be [T, Hq, 128]");
+  const int64_t Hq = q.size(1), Hkv = k_cache.size(1);
+  TORCH_CHECK(Hq % Hkv == 0, "GQA group must divide");
+  TORCH_CHECK(tiles.dim() == 2 && tiles.size(1) == 2, "tiles must be [n, 2]");
+  TORCH_CHECK(out.numel() == q.numel(), "out shape mismatch");
+  TORCH_CHECK(cu_q.numel() == ctx_lens.numel() + 1, "cu_q must have num_seqs + 1 entries");
+  const at::OptionalDeviceGuard g(q.device());
+  launch_attn_prefill(ptr<bf16>(q), ptr<bf16>(k_cache), ptr<bf16>(v_cache), ptr<int>(block_tables),
+                      ptr<int>(ctx_lens), ptr<int>(cu_q), ptr<int>(tiles), (int)tiles.size(0), ptr<bf16>(out),
+                      (int)Hq, (int)Hkv, (int)k_cache.size(2), (int)block_tables.size(1), (float)scale, cur_stream(q));
+}
+
+void skinny_gemm(const Tensor& x, const Tensor& w, Tensor& y) {
+  check_gpu(x, "x");
+  check_gpu(w, "w");
+  check_gpu(y, "y");
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(w, at::kBFloat16, "w");
+  check_dtype(y, at::kFloat, "y");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 3, "skinny_gemm: x [M,K], w [N,K], y [S,M,N]");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0), S = y.size(0);
+  TORCH_CHECK(w.size(1) == K, "skinny_gemm: K mismatch");
+  TORCH_CHECK(M >= 1 && M <= 64, "skinny_gemm: M must be in [1, 64]");
+  TORCH_CHECK(N % 16 == 0, "skinny_gemm: N must be a multiple of 16");
+  TORCH_CHECK(S >= 1 && K % (S * 256) == 0, "skinny_gemm: K must be a multiple of 256 * nsplit");
+  TORCH_CHECK(y.size(1) == M && y.size(2) == N, "skinny_gemm: y shape mismatch");
+  const at::OptionalDeviceGuard g(x.device());
+  launch_skinny_gemm(ptr<bf16>(x), ptr<bf16>(w), ptr<float>(y), (int)M, (int)N, (int)K, (int)S, cur_stream(x));
+}
+
+void lm_head_sample(const Tensor& x, const Tensor& w, const Tensor& temps, const Tensor& seeds, const Tensor& step,
+                    Tensor& tile_keys, Tensor& out_keys, Tensor& out_ids, int64_t n_offset,
+                    const c10::optional<Tensor>& logits) {
+  check_gpu(x, "x");
+  check_gpu(w, "w");
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(w, at::kBFloat16, "w");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "lm_head_sample: K mismatch");
+  TORCH_CHECK(M >= 1 && M <= 64, "lm_head_sample: M must be in [1, 64]");
+  TORCH_CHECK(N % 16 == 0 && K % 256 == 0, "lm_head_sample: N % 16 and K % 256 required");
+  check_gpu(temps, "temps");
+  check_dtype(temps, at::kFloat, "temps");
+  check_gpu(seeds, "seeds");
+  check_dtype(seeds, at::kLong, "seeds");
+  check_gpu(step, "step");
+  check_dtype(step, at::kLong, "step");
+  TORCH_CHECK(temps.numel() >= M && seeds.numel() >= M && step.numel() >= 1, "lm_head_sample: sampling params");
+  check_gpu(tile_keys, "tile_keys");
+  check_dtype(tile_keys, at::kLong, "tile_keys");
+  TORCH_CHECK(tile_keys.numel() >= M * (N / 16), "tile_keys too small");
+  check_gpu(out_keys, "out_keys");
+  check_dtype(out_keys, at::kLong, "out_keys");
+  check_gpu(out_ids, "out_ids");
+  check_dtype(out_ids, at::kInt, "out_ids");
+  TORCH_CHECK(out_keys.numel() >= M && out_ids.numel() >= M, "outputs too small");
+  float* lp = nullptr;
+  if (logits.has_value()) {
+    check_gpu(*logits, "logits");
+    check_dtype(*logits, at::kFloat, "logits");
+    TORCH_CHECK(logits->numel() == M * N, "logits shape mismatch");
+    lp = ptr<float>(*logits);
+  }
+  const at::OptionalDeviceGuard g(x.device());
+  hipStream_t s = cur_stream(x);
+  auto* tk = reinterpret_cast<unsigned long long*>(tile_keys.data_ptr());
+  launch_skinny_gemm_argmax(ptr<bf16>(x), ptr<bf16>(w), lp, (int)M, (int)N, (int)K, ptr<float>(temps),
+                            reinterpret_cast<const unsigned long long*>(seeds.data_ptr()),
+                            reinterpret_cast<const long long*>(step.data_ptr()), tk, (int)n_offset, s);
+  launch_argmax_reduce(tk, (int)M, (int)(N / 16), reinterpret_cast<unsigned long long*>(out_keys.data_ptr()),
+                       ptr<int>(out_ids), s);
+}
+
+void swiglu(const Tensor& gu, Tensor& out) {
+  check_gpu(out, "out");
+  check_dtype(out, at::kBFloat16, "out");
+  TORCH_CHECK(out.dim() == 2, "out must be [T, F]");
+  const int64_t T = out.size(0), F = out.size(1);
+  TORCH_CHECK(F % 8 == 0, "swiglu: F must be a multiple of 8");
+  const at::OptionalDeviceGuard g(out.device());
+  launch_swiglu(linout(gu, T, 2 * F, "gu"), ptr<bf16>(out), (int)T, (int)F, cur_stream(out));
+}
+
+}  // namespace
+
+TORCH_LIBRARY(symmetry_amd, m) {
+  m.def("rms_norm(Tensor x, Tensor w, float eps, Tensor(a!) out) -> ()", &rms_norm);
+  m.def("add_rms_norm(Tensor delta, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out) -> ()", &add_rms_norm);
+  m.def("embed_rms_norm(Tensor ids, Tensor table, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out) -> ()",
+        &embed_rms_norm);
+  m.def(
+      "rope_cache(Tensor qkv, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(a!) q_out, Tensor(b!) k_cache, "
+      "Tensor(c!) v_cache, int Hq, int Hkv) -> ()",
+      &rope_cache);
+  m.def(
+      "attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, Tensor(a!) out, "
+      "Tensor(b!) tmp_o, Tensor(c!) tmp_ml, float scale) -> ()",
+      &attn_decode);
+  m.def(
+      "attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, Tensor cu_q, "
+      "Tensor tiles, Tensor(a!) out, float scale) -> ()",
+      &attn_prefill);
+  m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) y) -> ()", &skinny_gemm);
+  m.def(
+      "lm_head_sample(Tensor x, Tensor w, Tensor temps, Tensor seeds, Tensor step, Tensor(a!) tile_keys, "
+      "Tensor(b!) out_keys, Tensor(c!) out_ids, int n_offset, Tensor(d!)? logits) -> ()",
+      &lm_head_sample);
+  m.def("swiglu(Tensor gu, Tensor(a!) out) -> ()", &swiglu);
+}

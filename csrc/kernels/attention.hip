@@ -1,0 +1,313 @@
+// K4 / K5: paged attention on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16), D = 128.
+//
+// Cache layout (written by rope_cache.hip):
+//   k_cache [NB][Hkv][BS][D]   token-major
+//   v_cache [NB][Hkv][D][BS]   dim-major
+// Both kernels use the "swapped" products so that no operand needs an LDS
+// transpose and every operand fragment is a contiguous 16-byte load:
+//   S^T[tok][q] = K[tok][:] . Q[q][:]      A = K rows,   B = Q^T
+//   O^T[d][q]  += V^T[d][tok] . P^T[tok][q] A = V^T rows, B = P^T
+// The accumulator of S^T (lane: column q = lane&15, rows 4*(lane>>4)+r) is
+// turned into the P^T B-operand in registers: a 32-token group is computed as
+// two 16-token S^T tiles whose token lists interleave in 4s
+// (tile a holds tokens 8*(row>>2) + 4a + (row&3)), so lane group h owns tokens
+// 8h..8h+7 of the group = exactly the k-slice its B fragment needs.
+// The contraction over D uses a k permutation (lane group h covers dims
+// 32h..32h+31 across the 4 MFMAs), making each lane's K and Q reads 64
+// contiguous bytes.  Softmax is online (running max / sum per query column),
+// in base 2 with the 1/sqrt(D)*log2(e) scale folded into one multiply.
+//
+// Decode (K5): grid (seq, kv_head, partition); 4 waves x 64 tokens = 256
+// tokens per partition; the G = Hq/Hkv query heads of a kv head are the MFMA
+// columns (K/V are read once per kv head).  Multi-partition sequences write
+// fp32 partials reduced by attn_decode_reduce (split-KV, flash-decoding).
+// The grid is sized for the max context so the launch is hipGraph-capturable;
+// partitions past a sequence's context exit at once.
+//
+// Prefill (K4): grid (q tile, kv_head * G); each wave owns 16 query rows of
+// one head, causal + varlen + chunked prefill (queries are the LAST qlen
+// positions of a context of length ctx), reading K/V from the paged cache.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+constexpr int D = 128;
+constexpr int PART = 256;  // tokens per decode partition (4 waves x 64)
+
+SYM_DEV f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+SYM_DEV bf16x8 ld16(const bf16* p) {
+  Pack8 pk;
+  pk.u = *reinterpret_cast<const uint4*>(p);
+  return pk.v;
+}
+
+SYM_DEV bf16x8 zero8() {
+  Pack8 pk;
+  pk.u = make_uint4(0, 0, 0, 0);
+  return pk.v;
+}
+
+// One 32-token group: S^T for two 16-token tiles, online softmax update, P.V.
+// `valid(a, r)` tells whether token (8h + 4a + r) of the group is visible to this lane's query column.
+template <typename ValidFn>
+SYM_DEV void attend_group(const bf16* __restrict__ kb, const bf16* __restrict__ vb, int BS, const bf16x8 (&qf)[4],
+                          float scale_log2, ValidFn valid, f32x4 (&o)[8], float& m, float& lsum) {
+  const int lane = threadIdx.x & 63;
+  const int r16 = lane & 15, h = lane >> 4;
+  f32x4 s[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int trow = (r16 >> 2) * 8 + 4 * a + (r16 & 3);
+    const bf16* kr = kb + (long long)trow * D + 32 * h;
+    bf16x8 kf[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) kf[i] = ld16(kr + 8 * i);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc = mfma16(kf[i], qf[i], acc);
+    s[a] = acc;
+  }
+  bf16x8 vf[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) vf[dt] = ld16(vb + (long long)(16 * dt + r16) * BS + 8 * h);
+
+  float x[8];
+  float gmax = -INFINITY;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = valid(a, r) ? s[a][r] * scale_log2 : -INFINITY;
+      x[4 * a + r] = v;
+      gmax = fmaxf(gmax, v);
+    }
+  gmax = fmaxf(gmax, __shfl_xor(gmax, 16, 64));
+  gmax = fmaxf(gmax, __shfl_xor(gmax, 32, 64));
+  const float m_new = fmaxf(m, gmax);
+  // m_new == -inf only if this column saw no visible token yet (causal prefill rows); keep zeros.
+  const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m - m_new);
+  Pack8 pf;
+  float psum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float p = (m_new == -INFINITY) ? 0.f : exp2f(x[j] - m_new);
+    psum += p;
+    pf.h[j] = (bf16)p;
+  }
+  lsum = lsum * alpha + psum;
+  m = m_new;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    o[dt] *= alpha;
+    o[dt] = mfma16(vf[dt], pf.v, o[dt]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Decode
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_decode_kernel(
+    const bf16* __restrict__ q, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    const int* __restrict__ block_tables, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
+    float* __restrict__ tmp_o, float* __restrict__ tmp_ml, int Hq, int Hkv, int BS, int max_blocks, int max_parts,
+    float scale_log2) {
+  const int seq = blockIdx.x, kvh = blockIdx.y, part = blockIdx.z;
+  const int ctx = ctx_lens[seq];
+  if (part * PART >= ctx) return;
+  const int G = Hq / Hkv;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = lane & 15, h = lane >> 4;
+
+  bf16x8 qf[4];
+  if (c < G) {
+    const bf16* qp = q + ((long long)seq * Hq + kvh * G + c) * D + 32 * h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qf[i] = ld16(qp + 8 * i);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qf[i] = zero8();
+  }
+  f32x4 o[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;
+
+  const int* bt = block_tables + (long long)seq * max_blocks;
+  const int tok0 = part * PART + wid * 64;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int tbase = tok0 + 32 * g;
+    if (tbase >= ctx) break;
+    const long long blk = bt[tbase / BS];
+    const int boff = tbase % BS;
+    const bf16* kb = k_cache + ((blk * Hkv + kvh) * BS + boff) * D;
+    const bf16* vb = v_cache + (blk * Hkv + kvh) * (long long)D * BS + boff;
+    attend_group(kb, vb, BS, qf, scale_log2,
+                 [&](int a, int r) { return tbase + 8 * h + 4 * a + r < ctx; }, o, m, lsum);
+  }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+
+  __shared__ float sm_m[4][16], sm_l[4][16];
+  __shared__ float sm_o[4][16][D + 4];
+  if (h == 0) {
+    sm_m[wid][c] = m;
+    sm_l[wid][c] = lsum;
+  }
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sm_o[wid][c][16 * dt + 4 * h + r] = o[dt][r];
+  __syncthreads();
+
+  const int qq = threadIdx.x >> 4;        // 0..15 query column
+  const int d0 = (threadIdx.x & 15) * 8;  // 8 dims per thread
+  if (qq >= G) return;
+  float M = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) M = fmaxf(M, sm_m[w][qq]);
+  float L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const float mw = sm_m[w][qq];
+    const float f = (mw == -INFINITY) ? 0.f : exp2f(mw - M);
+    L += sm_l[w][qq] * f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += sm_o[w][qq][d0 + j] * f;
+  }
+  const int head = kvh * G + qq;
+  const int nparts = (ctx + PART - 1) / PART;
+  if (nparts == 1) {
+    const float inv = 1.f / L;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] *= inv;
+    store8(out + ((long long)seq * Hq + head) * D + d0, acc);
+  } else {
+    const long long pbase = ((long long)seq * Hq + head) * max_parts + part;
+    store8f(tmp_o + pbase * D + d0, acc);
+    if (d0 == 0) {
+      tmp_ml[pbase * 2] = M;
+      tmp_ml[pbase * 2 + 1] = L;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void attn_decode_reduce_kernel(const float* __restrict__ tmp_o,
+                                                              const float* __restrict__ tmp_ml,
+                                                              const int* __restrict__ ctx_lens, bf16* __restrict__ out,
+                                                              int Hq, int max_parts) {
+  const int seq = blockIdx.x, head = blockIdx.y;
+  const int ctx = ctx_lens[seq];
+  const int nparts = (ctx + PART - 1) / PART;
+  if (nparts <= 1) return;
+  const long long base = ((long long)seq * Hq + head) * max_parts;
+  float M = -INFINITY;
+  for (int p = 0; p < nparts; ++p) M = fmaxf(M, tmp_ml[(base + p) * 2]);
+  const int d = threadIdx.x * 2;
+  float L = 0.f, a0 = 0.f, a1 = 0.f;
+  for (int p = 0; p < nparts; ++p) {
+    const float f = exp2f(tmp_ml[(base + p) * 2] - M);
+    L += tmp_ml[(base + p) * 2 + 1] * f;
+    const float2 v = *reinterpret_cast<const float2*>(tmp_o + (base + p) * D + d);
+    a0 += v.x * f;
+    a1 += v.y * f;
+  }
+  const float inv = 1.f / L;
+  bf16* op = out + ((long long)seq * Hq + head) * D + d;
+  op[0] = (bf16)(a0 * inv);
+  op[1] = (bf16)(a1 * inv);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Prefill (varlen, causal, paged, chunked)
+// ---------------------------------------------------------------------------------------------
+// tiles[i] = {seq, first query row within the seq's new tokens}; a tile is 64 query rows
+// (4 waves x 16 rows) of one query head.
+__global__ __launch_bounds__(256) void attn_prefill_kernel(
+    const bf16* __restrict__ q, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    const int* __restrict__ block_tables, const int* __restrict__ ctx_lens, const int* __restrict__ cu_q,
+    const int* __restrict__ tiles, bf16* __restrict__ out, int Hq, int Hkv, int BS, int max_blocks,
+    float scale_log2) {
+  const int tile = blockIdx.x, head = blockIdx.y;
+  const int seq = tiles[2 * tile], qrow0 = tiles[2 * tile + 1];
+  const int G = Hq / Hkv, kvh = head / G;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = lane & 15, h = lane >> 4;
+  const int qstart = cu_q[seq], qlen = cu_q[seq + 1] - qstart;
+  const int ctx = ctx_lens[seq];
+  const int pos0 = ctx - qlen;  // absolute position of query row 0
+  const int row0 = qrow0 + 16 * wid;
+  if (row0 >= qlen) return;
+  const int myrow = row0 + c;
+  const bool row_ok = myrow < qlen;
+  const int mypos = pos0 + myrow;
+
+  bf16x8 qf[4];
+  if (row_ok) {
+    const bf16* qp = q + ((long long)(qstart + myrow) * Hq + head) * D + 32 * h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qf[i] = ld16(qp + 8 * i);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qf[i] = zero8();
+  }
+  f32x4 o[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;
+  const int* bt = block_tables + (long long)seq * max_blocks;
+  // last key any row of this wave may see
+  const int kend = min(ctx, pos0 + min(row0 + 16, qlen));
+  for (int tbase = 0; tbase < kend; tbase += 32) {
+    const long long blk = bt[tbase / BS];
+    const int boff = tbase % BS;
+    const bf16* kb = k_cache + ((blk * Hkv + kvh) * BS + boff) * D;
+    const bf16* vb = v_cache + (blk * Hkv + kvh) * (long long)D * BS + boff;
+    attend_group(kb, vb, BS, qf, scale_log2,
+                 [&](int a, int r) {
+                   const int t = tbase + 8 * h + 4 * a + r;
+                   return row_ok && t <= mypos && t < ctx;
+                 },
+                 o, m, lsum);
+  }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (!row_ok) return;
+  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+  bf16* op = out + ((long long)(qstart + myrow) * Hq + head) * D;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    bf16x4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[dt][r] * inv);
+    *reinterpret_cast<bf16x4*>(op + 16 * dt + 4 * h) = v;
+  }
+}
+
+}  // namespace
+
+void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,
+                        const int* ctx_lens, bf16* out, float* tmp_o, float* tmp_ml, int num_seqs, int Hq, int Hkv,
+                        int BS, int max_blocks, int max_parts, float scale, hipStream_t s) {
+  if (num_seqs == 0) return;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid(num_seqs, Hkv, max_parts);
+  attn_decode_kernel<<<grid, 256, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, Hq, Hkv,
+                                          BS, max_blocks, max_parts, scale_log2);
+  if (max_parts > 1) {
+    attn_decode_reduce_kernel<<<dim3(num_seqs, Hq), 64, 0, s>>>(tmp_o, tmp_ml, ctx_lens, out, Hq, max_parts);
+  }
+}
+
+void launch_attn_prefill(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,
+                         const int* ctx_lens, const int* cu_q, const int* tiles, int num_tiles, bf16* out, int Hq,
+                         int Hkv, int BS, int max_blocks, float scale, hipStream_t s) {
+  if (num_tiles == 0) return;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  attn_prefill_kernel<<<dim3(num_tiles, Hq), 256, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, cu_q, tiles,
+                                                          out, Hq, Hkv, BS, max_blocks, scale_log2);
+}

@@ -1,0 +1,98 @@
+// K1: RMSNorm with fused residual add / embedding gather / split-K reduce.
+//
+//   mode 0 (norm):      out = rmsnorm(x) * w                 x: LinOut (bf16 or fp32 slabs)
+//   mode 1 (add_norm):  residual += delta; out = rmsnorm(residual) * w
+//   mode 2 (embed_norm): residual = table[ids]; out = rmsnorm(residual) * w
+//
+// The residual stream is kept in fp32 ([T][d]) for accuracy; activations fed
+// to the projections are bf16.  One 256-thread workgroup per row, 16 B per
+// lane per access (8 bf16 / 2x4 fp32), the row held in registers between the
+// sum-of-squares and the scale pass, so each byte is read once (memory bound:
+// SURVEY.md §2.6 K1).  The split-K partial slabs of the skinny decode GEMM are
+// summed here, which removes the GEMM's own reduce launch.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+template <int NT, int MAXV, int MODE>
+__global__ __launch_bounds__(NT) void rms_norm_kernel(LinOut x, const int* __restrict__ ids,
+                                                      const bf16* __restrict__ table,
+                                                      float* __restrict__ residual,
+                                                      const bf16* __restrict__ w,
+                                                      bf16* __restrict__ out, int d, float eps) {
+  __shared__ float scratch[NT / 64];
+  const int row = blockIdx.x;
+  const int nvec = d >> 3;
+  const long long rbase = (long long)row * d;
+  float v[MAXV][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = threadIdx.x + k * NT;
+    if (vi < nvec) {
+      const long long off = rbase + vi * 8;
+      if constexpr (MODE == 0) {
+        linout_load8(x, off, v[k]);
+      } else if constexpr (MODE == 1) {
+        float r[8];
+        load8f(residual + off, r);
+        linout_load8(x, off, v[k]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[k][i] += r[i];
+        store8f(residual + off, v[k]);
+      } else {
+        const long long tok = ids[row];
+        load8(table + tok * d + vi * 8, v[k]);
+        store8f(residual + off, v[k]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += v[k][i] * v[k][i];
+    }
+  }
+  ss = block_sum<NT>(ss, scratch);
+  const float inv = rsqrtf(ss / (float)d + eps);
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = threadIdx.x + k * NT;
+    if (vi < nvec) {
+      float g[8];
+      load8(w + vi * 8, g);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] *= v[k][i] * inv;
+      store8(out + rbase + vi * 8, g);
+    }
+  }
+}
+
+template <int MODE>
+void launch_mode(LinOut x, const int* ids, const bf16* table, float* residual, const bf16* w, bf16* out,
+                 int T, int d, float eps, hipStream_t s) {
+  constexpr int NT = 256;
+  const int nvec = d / 8;
+  dim3 grid(T);
+  if (nvec <= NT * 2) {
+    rms_norm_kernel<NT, 2, MODE><<<grid, NT, 0, s>>>(x, ids, table, residual, w, out, d, eps);
+  } else if (nvec <= NT * 4) {
+    rms_norm_kernel<NT, 4, MODE><<<grid, NT, 0, s>>>(x, ids, table, residual, w, out, d, eps);
+  } else {
+    rms_norm_kernel<NT, 8, MODE><<<grid, NT, 0, s>>>(x, ids, table, residual, w, out, d, eps);
+  }
+}
+
+}  // namespace
+
+void launch_rms_norm(LinOut x, const bf16* w, bf16* out, int T, int d, float eps, hipStream_t s) {
+  launch_mode<0>(x, nullptr, nullptr, nullptr, w, out, T, d, eps, s);
+}
+
+void launch_add_rms_norm(LinOut delta, float* residual, const bf16* w, bf16* out, int T, int d, float eps,
+                         hipStream_t s) {
+  launch_mode<1>(delta, nullptr, nullptr, residual, w, out, T, d, eps, s);
+}
+
+void launch_embed_rms_norm(const int* ids, const bf16* table, float* residual, const bf16* w, bf16* out, int T,
+                           int d, float eps, hipStream_t s) {
+  LinOut none{nullptr, 0, 1, 0};
+  launch_mode<2>(none, ids, table, residual, w, out, T, d, eps, s);
+}

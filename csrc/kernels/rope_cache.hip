@@ -1,0 +1,82 @@
+// K2 + K3: rotary embedding on Q/K fused with the paged KV-cache write.
+//
+// Input is the QKV projection output (LinOut: bf16 [T][(Hq+2Hkv)*D] or fp32
+// split-K slabs), so the split-K reduce of the decode QKV GEMM happens here.
+// Outputs:
+//   q_out   bf16 [T][Hq][D]            rotated queries
+//   k_cache bf16 [NB][Hkv][BS][D]      token-major K blocks (rotated)
+//   v_cache bf16 [NB][Hkv][D][BS]      dim-major ("transposed") V blocks
+// The V layout makes the P.V MFMA B-operand (8 consecutive tokens of one
+// dim) a single 16-byte load in the attention kernels.
+// rotate_half (NeoX/Llama) convention; cos/sin come from a host-built fp32
+// table [max_pos][D] = [cos(0..D/2) | sin(0..D/2)] (no device trig).
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+__global__ __launch_bounds__(NT) void rope_cache_kernel(LinOut qkv, const int* __restrict__ positions,
+                                                        const int* __restrict__ slots,
+                                                        const float* __restrict__ cos_sin,
+                                                        bf16* __restrict__ q_out, bf16* __restrict__ k_cache,
+                                                        bf16* __restrict__ v_cache, int Hq, int Hkv, int D,
+                                                        int BS) {
+  const int t = blockIdx.x;
+  const int N = (Hq + 2 * Hkv) * D;
+  const long long row = (long long)t * N;
+  const int pos = positions[t];
+  const int slot = slots ? slots[t] : -1;
+  const int half = D / 2;
+  const int gpr = half / 8;  // 8-pair groups per head
+  const float* cs = cos_sin + (long long)pos * D;
+  const int rot_items = (Hq + Hkv) * gpr;
+  const int v_items = Hkv * (D / 8);
+  for (int it = threadIdx.x; it < rot_items + v_items; it += NT) {
+    if (it < rot_items) {
+      const int h = it / gpr;          // 0..Hq+Hkv-1 (q heads then k heads)
+      const int i0 = (it % gpr) * 8;   // pair index within the half
+      float x1[8], x2[8], c[8], s[8];
+      linout_load8(qkv, row + (long long)h * D + i0, x1);
+      linout_load8(qkv, row + (long long)h * D + half + i0, x2);
+      load8f(cs + i0, c);
+      load8f(cs + half + i0, s);
+      float o1[8], o2[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o1[j] = x1[j] * c[j] - x2[j] * s[j];
+        o2[j] = x2[j] * c[j] + x1[j] * s[j];
+      }
+      if (h < Hq) {
+        bf16* q = q_out + ((long long)t * Hq + h) * D;
+        store8(q + i0, o1);
+        store8(q + half + i0, o2);
+      } else if (slot >= 0) {
+        const int kh = h - Hq;
+        const long long blk = slot / BS, off = slot % BS;
+        bf16* k = k_cache + ((blk * Hkv + kh) * BS + off) * D;
+        store8(k + i0, o1);
+        store8(k + half + i0, o2);
+      }
+    } else if (slot >= 0) {
+      const int vi = it - rot_items;
+      const int kh = vi / (D / 8);
+      const int d0 = (vi % (D / 8)) * 8;
+      float x[8];
+      linout_load8(qkv, row + (long long)(Hq + Hkv + kh) * D + d0, x);
+      const long long blk = slot / BS, off = slot % BS;
+      bf16* v = v_cache + ((blk * Hkv + kh) * D + d0) * BS + off;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[(long long)j * BS] = (bf16)x[j];
+    }
+  }
+}
+
+}  // namespace
+
+void launch_rope_cache(LinOut qkv, const int* positions, const int* slots, const float* cos_sin, bf16* q_out,
+                       bf16* k_cache, bf16* v_cache, int T, int Hq, int Hkv, int D, int BS, hipStream_t s) {
+  if (T == 0) return;
+  rope_cache_kernel<<<T, NT, 0, s>>>(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D, BS);
+}

@@ -1,0 +1,194 @@
+"""Llama-3 / Mixtral decoder forward built on the symmetry_amd ops.
+
+One code path serves CPU (torch references, tests) and MI355X (HIP kernels).
+Per layer::
+
+    K1 add+RMSNorm -> QKV proj -> K2/K3 RoPE+paged-cache write -> K4/K5 attention
+    -> O proj -> [R1 all-reduce] -> K1 add+RMSNorm -> gate_up proj -> K7 SwiGLU
+    -> down proj -> [R1 all-reduce]            (Mixtral: K10-K12 MoE block, R3 all-to-all)
+
+Projections with <= 64 rows (every decode step, short prefills) run the
+skinny MFMA GEMM and hand fp32 split-K slabs straight to the next fused
+kernel; larger ones run the library GEMM (hipBLASLt through torch.matmul).
+The final norm + lm_head + sampling use the fused lm_head_sample kernel on the
+last row of each sequence only.  All intermediates live in a preallocated
+:class:`Workspace`, so the decode forward is hipGraph-capturable.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from .. import ops
+from ..ops import reference
+from .config import ModelConfig
+from .weights import ModelWeights
+
+SKINNY_MAX_M = 64
+SIGN64 = -(1 << 63)
+
+
+@dataclass
+class ForwardBatch:
+    """Device-side metadata of one engine step.
+
+    ``kind`` is ``"decode"`` (one new token per sequence, T == num_seqs) or
+    ``"prefill"`` (packed varlen prompts / prompt chunks).
+    """
+
+    kind: str
+    input_ids: torch.Tensor      # [T] int32
+    positions: torch.Tensor      # [T] int32
+    slot_mapping: torch.Tensor   # [T] int32 (-1: no cache write)
+    block_tables: torch.Tensor   # [num_seqs, max_blocks] int32
+    ctx_lens: torch.Tensor       # [num_seqs] int32 (context incl. this step's tokens)
+    temps: torch.Tensor          # [num_seqs] f32 (0 = greedy)
+    seeds: torch.Tensor          # [num_seqs] i64
+    step: torch.Tensor           # [1] i64 sampling step counter
+    num_seqs: int
+    # prefill only
+    cu_q: torch.Tensor | None = None        # [num_seqs + 1] int32
+    tiles: torch.Tensor | None = None       # [n_tiles, 2] int32
+    last_idx: torch.Tensor | None = None    # [num_seqs] int64 row of each sequence's last token
+    need_logits: bool = False
+
+    @property
+    def num_tokens(self) -> int:
+        return int(self.input_ids.numel())
+
+
+class KVCache:
+    """Paged KV cache: k [L, NB, Hkv, BS, D] (token-major), v [L, NB, Hkv, D, BS] (dim-major).
+
+    Zero-initialised: every cache byte is finite, so masked tail tokens of a
+    block contribute exactly 0 to P.V.
+    """
+
+    def __init__(self, num_layers: int, num_blocks: int, num_kv_heads: int, head_dim: int, block_size: int,
+                 device, dtype=torch.bfloat16):
+        self.num_layers, self.num_blocks, self.block_size = num_layers, num_blocks, block_size
+        self.k = torch.zeros(num_layers, num_blocks, num_kv_heads, block_size, head_dim, device=device, dtype=dtype)
+        self.v = torch.zeros(num_layers, num_blocks, num_kv_heads, head_dim, block_size, device=device, dtype=dtype)
+
+    def nbytes(self) -> int:
+        return 2 * self.k.numel() * self.k.element_size()
+
+
+@dataclass
+class Workspace:
+    buffers: dict = field(default_factory=dict)
+
+    def get(self, name: str, shape, dtype, device) -> torch.Tensor:
+        numel = math.prod(shape)
+        buf = self.buffers.get((name, dtype))
+        if buf is None or buf.numel() < numel:
+            buf = torch.empty(numel, dtype=dtype, device=device)
+            self.buffers[(name, dtype)] = buf
+        return buf[:numel].view(*shape)
+
+
+class TransformerLM:
+    def __init__(self, weights: ModelWeights, device, tp_comm=None, ep_comm=None, max_decode_ctx: int | None = None):
+        self.cfg: ModelConfig = weights.cfg
+        self.w = weights
+        self.device = torch.device(device)
+        self.tp = tp_comm
+        self.ep = ep_comm
+        self.tp_size = weights.shard.tp_size
+        self.tp_rank = weights.shard.tp_rank
+        cfg = self.cfg
+        self.hq = cfg.num_heads // self.tp_size
+        self.hkv = cfg.num_kv_heads // self.tp_size
+        self.D = cfg.head_dim
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.vocab_shard = cfg.vocab_size // self.tp_size
+        max_pos = min(cfg.max_position, max_decode_ctx or cfg.max_position)
+        self.cos_sin = reference.rope_table(max_pos, cfg.head_dim, cfg.rope_theta, cfg.rope_scaling,
+                                            device=self.device)
+        self.ws = Workspace()
+        self.moe = None
+        if cfg.is_moe:
+            from .moe import MoEBlock
+
+            self.moe = MoEBlock(self, ep_comm)
+
+    # ------------------------------------------------------------------------------------------
+    def _buf(self, name, shape, dtype):
+        return self.ws.get(name, shape, dtype, self.device)
+
+    def _linear(self, name: str, x: torch.Tensor, w: torch.Tensor, reduce: bool = False) -> torch.Tensor:
+        """x [T, K] bf16 -> LinOut: fp32 slabs [S, T, N] (skinny) or bf16 [T, N] (library GEMM)."""
+        T, K = x.shape
+        N = w.shape[0]
+        if T <= SKINNY_MAX_M:
+            S = ops.choose_splits(N, K)
+            y = self._buf(name + ".slab", (S, T, N), torch.float32)
+            ops.skinny_gemm(x, w, y)
+        else:
+            y = self._buf(name + ".bf16", (T, N), torch.bfloat16)
+            ops.linear(x, w, out=y)
+        if reduce and self.tp is not None and self.tp_size > 1:
+            self.tp.all_reduce(y)
+        return y
+
+    # ------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def forward(self, b: ForwardBatch, kv: KVCache) -> torch.Tensor:
+        """Run one step; returns sampled token ids [num_seqs] int32 (device)."""
+        cfg, w = self.cfg, self.w
+        T = b.num_tokens
+        d = cfg.hidden_size
+        eps = cfg.rms_eps
+        resid = self._buf("resid", (T, d), torch.float32)
+        x = self._buf("x", (T, d), torch.bfloat16)
+        q = self._buf("q", (T, self.hq, self.D), torch.bfloat16)
+        attn = self._buf("attn", (T, self.hq, self.D), torch.bfloat16)
+        ops.embed_rms_norm(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), eps, x)
+        for i in range(cfg.num_layers):
+            qkv = self._linear("qkv", x, w.layer(i, "wqkv"))
+            ops.rope_cache(qkv, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq, self.hkv)
+            if b.kind == "decode":
+                max_parts = (b.block_tables.shape[1] * kv.block_size + 255) // 256
+                tmp_o = self._buf("tmp_o", (b.num_seqs, self.hq, max_parts, self.D), torch.float32)
+                tmp_ml = self._buf("tmp_ml", (b.num_seqs, self.hq, max_parts, 2), torch.float32)
+                ops.attn_decode(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, attn, tmp_o, tmp_ml, self.scale)
+            else:
+                ops.attn_prefill(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, b.cu_q, b.tiles, attn, self.scale)
+            o = self._linear("o", attn.view(T, self.hq * self.D), w.layer(i, "wo"), reduce=True)
+            ops.add_rms_norm(o, resid, w.layer(i, "ln2"), eps, x)
+            if cfg.is_moe:
+                mlp = self.moe.forward(i, x)
+            else:
+                gu = self._linear("gu", x, w.layer(i, "w_gu"))
+                F = gu.shape[-1] // 2
+                act = self._buf("act", (T, F), torch.bfloat16)
+                ops.swiglu(gu, act)
+                mlp = self._linear("down", act, w.layer(i, "w_down"), reduce=True)
+            nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
+            ops.add_rms_norm(mlp, resid, nxt, eps, x)
+        return self.sample(b, x)
+
+    def sample(self, b: ForwardBatch, x: torch.Tensor) -> torch.Tensor:
+        """Fused lm_head + greedy/Gumbel sampling on each sequence's last row."""
+        n = b.num_seqs
+        xl = x if b.kind == "decode" else x.index_select(0, b.last_idx)
+        ids = self._buf("ids", (n,), torch.int32)
+        keys = self._buf("keys", (n,), torch.int64)
+        ntiles = self.vocab_shard // 16
+        logits = self._buf("logits", (n, self.vocab_shard), torch.float32) if b.need_logits else None
+        for m0 in range(0, n, SKINNY_MAX_M):
+            m1 = min(n, m0 + SKINNY_MAX_M)
+            tk = self._buf("tile_keys", ((m1 - m0) * ntiles,), torch.int64)
+            ops.lm_head_sample(xl[m0:m1].contiguous() if m0 or m1 < n else xl, self.w["lm_head"],
+                               b.temps[m0:m1], b.seeds[m0:m1], b.step, tk, keys[m0:m1], ids[m0:m1],
+                               self.tp_rank * self.vocab_shard, logits[m0:m1] if logits is not None else None)
+        if self.tp is not None and self.tp_size > 1:
+            # keys are u64 (order-preserving); flip the sign bit so signed MAX == unsigned max
+            keys.bitwise_xor_(SIGN64)
+            self.tp.all_reduce(keys, op="max")
+            keys.bitwise_xor_(SIGN64)
+            ids.copy_((0xFFFFFFFF - (keys & 0xFFFFFFFF)).to(torch.int32))
+        self.last_logits = logits
+        return ids

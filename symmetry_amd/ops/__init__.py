@@ -1,0 +1,115 @@
+"""Op layer: one Python entry point per kernel.
+
+Dispatch rule (no silent fallback): a GPU tensor always runs the CDNA4 HIP
+kernel from ``_C.so`` (``torch.ops.symmetry_amd.*``) and raises if the
+library is not built/loadable; a CPU tensor runs the fp32 torch reference
+(:mod:`symmetry_amd.ops.reference`).  All ops write into caller-provided
+outputs and allocate nothing on the GPU path, so the model runner can capture
+them in a hipGraph.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native, reference
+
+__all__ = [
+    "native_available",
+    "rms_norm",
+    "add_rms_norm",
+    "embed_rms_norm",
+    "rope_cache",
+    "attn_decode",
+    "attn_prefill",
+    "skinny_gemm",
+    "lm_head_sample",
+    "swiglu",
+    "linear",
+    "choose_splits",
+]
+
+
+def native_available() -> bool:
+    return _native.available()
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.device.type != "cpu"
+
+
+def rms_norm(x, w, eps, out):
+    if _gpu(out):
+        return _native.ops().rms_norm(x, w, float(eps), out)
+    return reference.rms_norm(x, w, eps, out)
+
+
+def add_rms_norm(delta, residual, w, eps, out):
+    if _gpu(residual):
+        return _native.ops().add_rms_norm(delta, residual, w, float(eps), out)
+    return reference.add_rms_norm(delta, residual, w, eps, out)
+
+
+def embed_rms_norm(ids, table, residual, w, eps, out):
+    if _gpu(residual):
+        return _native.ops().embed_rms_norm(ids, table, residual, w, float(eps), out)
+    return reference.embed_rms_norm(ids, table, residual, w, eps, out)
+
+
+def rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv):
+    if _gpu(q_out):
+        return _native.ops().rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, int(Hq), int(Hkv))
+    return reference.rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv)
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, scale):
+    if _gpu(q):
+        return _native.ops().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml,
+                                         float(scale))
+    return reference.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, scale)
+
+
+def attn_prefill(q, k_cache, v_cache, block_tables, ctx_lens, cu_q, tiles, out, scale):
+    if _gpu(q):
+        return _native.ops().attn_prefill(q, k_cache, v_cache, block_tables, ctx_lens, cu_q, tiles, out,
+                                          float(scale))
+    return reference.attn_prefill(q, k_cache, v_cache, block_tables, ctx_lens, cu_q, tiles, out, scale)
+
+
+def skinny_gemm(x, w, y):
+    if _gpu(x):
+        return _native.ops().skinny_gemm(x, w, y)
+    return reference.skinny_gemm(x, w, y)
+
+
+def lm_head_sample(x, w, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset=0, logits=None):
+    if _gpu(x):
+        return _native.ops().lm_head_sample(x, w, temps, seeds, step, tile_keys, out_keys, out_ids, int(n_offset),
+                                            logits)
+    return reference.lm_head_sample(x, w, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset, logits)
+
+
+def swiglu(gu, out):
+    if _gpu(out):
+        return _native.ops().swiglu(gu, out)
+    return reference.swiglu(gu, out)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Plain library GEMM ``x @ w.T`` (hipBLASLt via torch on the GPU) for prefill-sized M."""
+    return torch.matmul(x, w.t(), out=out)
+
+
+def choose_splits(N: int, K: int, target_wgs: int = 1024, min_k_per_wave: int = 128) -> int:
+    """k-split S of the skinny GEMM: the smallest divisor of K/256 giving >= target_wgs workgroups,
+    keeping each wave's k range >= min_k_per_wave (2 MFMA k-blocks)."""
+    tiles = max(1, N // 16)
+    if K % 256:
+        raise ValueError(f"skinny GEMM needs K % 256 == 0, got {K}")
+    best = 1
+    for s in range(1, K // 256 + 1):
+        if (K // 256) % s or (K // s) // 4 < min_k_per_wave:
+            continue
+        best = s
+        if tiles * s >= target_wgs:
+            break
+    return best

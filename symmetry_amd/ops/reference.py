@@ -1,0 +1,232 @@
+"""Plain-PyTorch fp32 reference implementations of every symmetry_amd kernel.
+
+They define the semantics the HIP kernels in ``csrc/kernels`` must match
+(tests compare the two) and are the execution path for CPU tensors (unit
+tests, the tiny CPU models).  Layout conventions are identical to the
+kernels':
+
+* ``LinOut``: a projection output is bf16 ``[T, N]`` or fp32 split-K slabs
+  ``[S, T, N]`` (summed by the consumer);
+* ``k_cache [NB, Hkv, BS, D]`` token-major, ``v_cache [NB, Hkv, D, BS]``
+  dim-major;
+* RoPE uses the rotate-half convention with a ``[max_pos, D]`` table
+  ``[cos | sin]``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+MASK32 = 0xFFFFFFFF
+
+
+def linout_sum(x: torch.Tensor) -> torch.Tensor:
+    """Collapse a LinOut to fp32 ``[T, N]``."""
+    if x.dtype == torch.float32 and x.dim() == 3:
+        return x.sum(0)
+    return x.float()
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor) -> None:
+    xf = linout_sum(x)
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    out.copy_(y.view_as(out).to(out.dtype))
+
+
+def add_rms_norm(delta, residual, w, eps, out) -> None:
+    residual.add_(linout_sum(delta).view_as(residual))
+    rms_norm(residual, w, eps, out)
+
+
+def embed_rms_norm(ids, table, residual, w, eps, out) -> None:
+    residual.copy_(table[ids.long()].float())
+    rms_norm(residual, w, eps, out)
+
+
+def rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq: int, Hkv: int) -> None:
+    T = positions.numel()
+    D = k_cache.shape[3]
+    BS = k_cache.shape[2]
+    x = linout_sum(qkv).view(T, Hq + 2 * Hkv, D)
+    cs = cos_sin[positions.long()]  # [T, D]
+    half = D // 2
+    cos, sin = cs[:, None, :half], cs[:, None, half:]
+    qk = x[:, : Hq + Hkv]
+    x1, x2 = qk[..., :half], qk[..., half:]
+    rot = torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1)
+    q_out.copy_(rot[:, :Hq].reshape(q_out.shape).to(q_out.dtype))
+    k = rot[:, Hq:].to(k_cache.dtype)
+    v = x[:, Hq + Hkv:].to(v_cache.dtype)
+    s = slots.long()
+    valid = s >= 0
+    if valid.any():
+        s, k, v = s[valid], k[valid], v[valid]
+        blk, off = s // BS, s % BS
+        k_cache[blk, :, off, :] = k
+        v_cache[blk, :, :, off] = v
+
+
+def _gather_kv(k_cache, v_cache, block_table, ctx: int):
+    """Contiguous K, V [ctx, Hkv, D] of one sequence (fp32)."""
+    BS = k_cache.shape[2]
+    nb = (ctx + BS - 1) // BS
+    blocks = block_table[:nb].long()
+    k = k_cache[blocks].permute(0, 2, 1, 3).reshape(nb * BS, k_cache.shape[1], -1)[:ctx]
+    v = v_cache[blocks].permute(0, 3, 1, 2).reshape(nb * BS, v_cache.shape[1], -1)[:ctx]
+    return k.float(), v.float()
+
+
+def _attend(q, k, v, scale, causal_offset=None):
+    """q [n, Hq, D], k/v [ctx, Hkv, D] -> [n, Hq, D] fp32 (GQA by repeat)."""
+    Hq, Hkv = q.shape[1], k.shape[1]
+    G = Hq // Hkv
+    k = k.repeat_interleave(G, dim=1)
+    v = v.repeat_interleave(G, dim=1)
+    s = torch.einsum("qhd,khd->hqk", q.float(), k) * scale
+    if causal_offset is not None:
+        n, ctx = q.shape[0], k.shape[0]
+        qpos = torch.arange(n, device=q.device)[:, None] + causal_offset
+        kpos = torch.arange(ctx, device=q.device)[None, :]
+        s = s.masked_fill(kpos > qpos, float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    return torch.einsum("hqk,khd->qhd", p, v)
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o=None, tmp_ml=None, scale=1.0) -> None:
+    S = q.shape[0]
+    res = torch.empty(q.shape, dtype=torch.float32, device=q.device)
+    for i in range(S):
+        ctx = int(ctx_lens[i])
+        k, v = _gather_kv(k_cache, v_cache, block_tables[i], ctx)
+        res[i] = _attend(q[i : i + 1], k, v, scale)[0]
+    out.copy_(res.view_as(out).to(out.dtype))
+
+
+def attn_prefill(q, k_cache, v_cache, block_tables, ctx_lens, cu_q, tiles, out, scale) -> None:
+    nseq = ctx_lens.numel()
+    res = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
+    for i in range(nseq):
+        a, b = int(cu_q[i]), int(cu_q[i + 1])
+        if b == a:
+            continue
+        ctx = int(ctx_lens[i])
+        k, v = _gather_kv(k_cache, v_cache, block_tables[i], ctx)
+        res[a:b] = _attend(q[a:b], k, v, scale, causal_offset=ctx - (b - a))
+    out.copy_(res.view_as(out).to(out.dtype))
+
+
+def skinny_gemm(x, w, y) -> None:
+    S = y.shape[0]
+    K = x.shape[1]
+    kc = K // S
+    for s in range(S):
+        y[s] = x[:, s * kc : (s + 1) * kc].float() @ w[:, s * kc : (s + 1) * kc].float().t()
+
+
+# ----- sampling: same counter-based RNG and packed keys as the kernel ----------------------------
+def _u32(x):
+    return x & MASK32
+
+
+def uniform01(seed: torch.Tensor, counter: torch.Tensor) -> torch.Tensor:
+    """Bit-exact torch port of ``uniform01`` in csrc/kernels/common.h (int64 tensors)."""
+    x0 = _u32(counter)
+    x1 = _u32(counter >> 32)
+    k0 = _u32(seed).expand_as(x0).clone()
+    k1 = _u32(seed >> 32).expand_as(x0).clone()
+    for _ in range(7):
+        p0h, p0l = _mulhilo(x0, 0xD2511F53)
+        p1h, p1l = _mulhilo(x1, 0xCD9E8D57)
+        n0 = p1h ^ k0 ^ p0l
+        n1 = p0h ^ k1 ^ p1l
+        x0, x1 = n0, n1
+        k0 = _u32(k0 + 0x9E3779B9)
+        k1 = _u32(k1 + 0xBB67AE85)
+    return ((x0 >> 8).double() + 0.5) * (1.0 / 16777216.0)
+
+
+def _mulhilo(a: torch.Tensor, b: int):
+    """Unsigned 32x32->64 multiply of int64 tensors holding u32 values."""
+    al, ah = a & 0xFFFF, a >> 16
+    bl, bh = b & 0xFFFF, b >> 16
+    ll = al * bl
+    lh = al * bh
+    hl = ah * bl
+    hh = ah * bh
+    mid = (ll >> 16) + (lh & 0xFFFF) + (hl & 0xFFFF)
+    lo = _u32((mid << 16) | (ll & 0xFFFF))
+    hi = _u32(hh + (lh >> 16) + (hl >> 16) + (mid >> 16))
+    return hi, lo
+
+
+def _ordered_bits(v: torch.Tensor) -> torch.Tensor:
+    u = v.float().view(torch.int32).long() & MASK32
+    neg = (u & 0x80000000) != 0
+    return torch.where(neg, _u32(~u), u | 0x80000000)
+
+
+def sample_keys(logits: torch.Tensor, temps: torch.Tensor, seeds: torch.Tensor, step: int, n_offset: int = 0):
+    """Packed argmax keys (int64 bit pattern of the kernel's u64) and token ids per row."""
+    M, N = logits.shape
+    gidx = torch.arange(N, device=logits.device, dtype=torch.int64) + n_offset
+    vals = logits.float().clone()
+    for m in range(M):
+        t = float(temps[m])
+        if t > 0:
+            seed = int(seeds[m]) & 0xFFFFFFFFFFFFFFFF
+            mixed = seed ^ ((step << 20) & 0xFFFFFFFFFFFFFFFF)
+            if mixed >= 1 << 63:
+                mixed -= 1 << 64
+            u = uniform01(torch.tensor(mixed, dtype=torch.int64), gidx).float()
+            vals[m] = vals[m] / t - torch.log(-torch.log(u))
+    ob = _ordered_bits(vals)
+    low = 0xFFFFFFFF - gidx
+    ids = torch.empty(M, dtype=torch.int64, device=logits.device)
+    keys = torch.empty(M, dtype=torch.int64, device=logits.device)
+    for m in range(M):
+        # max over (ob, low) lexicographic == max key
+        best = ob[m].max()
+        cand = torch.nonzero(ob[m] == best).flatten()
+        j = int(cand.min())  # smallest index wins ties (largest ~idx)
+        ids[m] = int(gidx[j])
+        key = (int(best) << 32) | int(low[j])
+        keys[m] = key - (1 << 64) if key >= 1 << 63 else key
+    return keys, ids
+
+
+def lm_head_sample(x, w, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset: int, logits=None) -> None:
+    lg = x.float() @ w.float().t()
+    if logits is not None:
+        logits.copy_(lg)
+    keys, ids = sample_keys(lg, temps, seeds, int(step.reshape(-1)[0]), n_offset)
+    M = x.shape[0]
+    out_keys[:M].copy_(keys)
+    out_ids[:M].copy_(ids.to(out_ids.dtype))
+
+
+def swiglu(gu, out) -> None:
+    g = linout_sum(gu)
+    F = out.shape[1]
+    y = torch.nn.functional.silu(g[:, :F]) * g[:, F:]
+    out.copy_(y.to(out.dtype))
+
+
+def rope_table(max_pos: int, head_dim: int, theta: float, scaling: dict | None = None,
+               device="cpu") -> torch.Tensor:
+    """``[max_pos, D]`` fp32 table ``[cos | sin]`` incl. Llama-3.1 NTK-by-parts scaling."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling and scaling.get("rope_type", scaling.get("type")) == "llama3":
+        factor = scaling["factor"]
+        lo, hi = scaling.get("low_freq_factor", 1.0), scaling.get("high_freq_factor", 4.0)
+        old = scaling.get("original_max_position_embeddings", 8192)
+        lo_wl, hi_wl = old / lo, old / hi
+        wl = 2 * math.pi / inv
+        smooth = (old / wl - lo) / (hi - lo)
+        scaled = torch.where(wl > lo_wl, inv / factor, inv)
+        mid = (wl <= lo_wl) & (wl >= hi_wl)
+        scaled = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+        inv = scaled
+    pos = torch.arange(max_pos, dtype=torch.float64)
+    ang = pos[:, None] * inv[None, :]
+    return torch.cat([ang.cos(), ang.sin()], dim=-1).float().to(device)
