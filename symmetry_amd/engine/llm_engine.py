@@ -1,0 +1,304 @@
+"""The native inference engine: model + paged KV cache + scheduler + streaming outputs.
+
+This replaces the external Ollama process that the reference proxies to
+(``src/provider.ts:206-214``): the provider submits chat requests here and
+receives one :class:`RequestOutput` per generated token.
+
+:class:`LLMEngine` is synchronous (``step()``); :class:`AsyncEngine` runs it
+on a dedicated thread and bridges outputs into asyncio with bounded
+per-request queues, so slow peers never stall the GPU loop (SURVEY.md §7.4
+item 6).
+"""
+from __future__ import annotations
+
+import asyncio
+import hashlib
+import os
+import queue
+import threading
+import time
+import traceback
+from dataclasses import dataclass, field
+
+import torch
+
+from ..models.config import ModelConfig, resolve
+from ..models.transformer import KVCache, TransformerLM
+from ..models.weights import ModelWeights, ShardSpec, load_hf_weights, random_weights
+from ..utils.metrics import EngineMetrics
+from .model_runner import ModelRunner
+from .scheduler import BlockManager, Scheduler, SchedulerConfig
+from .sequence import SamplingParams, Sequence, SeqStatus
+from .tokenizer import IncrementalDetokenizer, load_tokenizer
+
+
+@dataclass
+class EngineConfig:
+    model: str = "llama3:8b"
+    weights: str = "random"              # "random" or a HF safetensors directory
+    tokenizer: str | None = None
+    device: str = "auto"                 # "auto" | "cuda" | "cuda:N" | "cpu"
+    seed: int = 0
+    max_num_seqs: int = 64               # admission limit (maxConnections)
+    max_num_batched_tokens: int = 8192
+    max_model_len: int = 8192
+    block_size: int = 64
+    kv_cache_fraction: float = 0.85      # of the HBM left after weights + workspace
+    num_kv_blocks: int | None = None
+    use_graphs: bool = True
+    default_max_tokens: int = 256
+    tp_size: int = 1
+    tp_rank: int = 0
+    ep_size: int = 1
+    ep_rank: int = 0
+    weight_init: str = "auto"            # "full" | "shard" | "auto"
+    model_config: ModelConfig | None = None
+
+    @classmethod
+    def from_provider(cls, cfg: dict, **overrides) -> "EngineConfig":
+        """Map provider.yaml fields (REF schema + optional engine fields)."""
+        ec = cls(model=str(cfg.get("modelName", "llama3:8b")))
+        mc = cfg.get("maxConnections")
+        if mc:
+            ec.max_num_seqs = int(mc)
+        m = {"weights": "weights", "tokenizer": "tokenizer", "seed": "seed", "maxBatchTokens": "max_num_batched_tokens",
+             "maxModelLen": "max_model_len", "kvCacheFraction": "kv_cache_fraction", "blockSize": "block_size",
+             "maxTokens": "default_max_tokens", "tensorParallelSize": "tp_size", "device": "device",
+             "useGraphs": "use_graphs", "numKvBlocks": "num_kv_blocks"}
+        for k, attr in m.items():
+            if cfg.get(k) is not None:
+                setattr(ec, attr, type(getattr(ec, attr))(cfg[k]) if getattr(ec, attr) is not None else cfg[k])
+        for k, v in overrides.items():
+            setattr(ec, k, v)
+        return ec
+
+
+@dataclass
+class RequestOutput:
+    request_id: str
+    token_ids: list
+    text: str
+    finished: bool = False
+    finish_reason: str | None = None
+    error: str | None = None
+    seq: Sequence | None = field(default=None, repr=False)
+
+
+def _pick_device(spec: str) -> torch.device:
+    if spec == "auto":
+        return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    return torch.device(spec)
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, tp_comm=None, ep_comm=None, cpu_group=None):
+        self.cfg = cfg
+        self.device = _pick_device(cfg.device)
+        self.model_cfg = cfg.model_config or resolve(cfg.model)
+        mcfg = self.model_cfg
+        max_model_len = min(cfg.max_model_len, mcfg.max_position)
+        self.metrics = EngineMetrics()
+        shard = ShardSpec(cfg.tp_rank, cfg.tp_size, cfg.ep_rank, cfg.ep_size)
+        t0 = time.perf_counter()
+        if cfg.weights == "random":
+            mode = cfg.weight_init
+            if mode == "auto":
+                mode = "full" if mcfg.num_params() < 2e9 else "shard"
+            weights = random_weights(mcfg, shard, device=self.device, seed=cfg.seed, mode=mode)
+        else:
+            weights = load_hf_weights(cfg.weights, mcfg, shard, device=self.device)
+        self.weights: ModelWeights = weights
+        self.load_time = time.perf_counter() - t0
+        self.model = TransformerLM(weights, self.device, tp_comm=tp_comm, ep_comm=ep_comm,
+                                   max_decode_ctx=max_model_len)
+        self.tokenizer = load_tokenizer(mcfg, cfg.tokenizer or (cfg.weights if cfg.weights != "random" else None))
+        nb = cfg.num_kv_blocks or self._auto_blocks(max_model_len)
+        self.kv = KVCache(mcfg.num_layers, nb, mcfg.num_kv_heads // cfg.tp_size, mcfg.head_dim, cfg.block_size,
+                          self.device)
+        self.blocks = BlockManager(nb, cfg.block_size)
+        self.scheduler = Scheduler(
+            SchedulerConfig(max_num_seqs=min(cfg.max_num_seqs, 64 if self.device.type != "cpu" else cfg.max_num_seqs),
+                            max_num_batched_tokens=cfg.max_num_batched_tokens, max_model_len=max_model_len),
+            self.blocks)
+        self.runner = ModelRunner(self.model, self.kv, self.scheduler.cfg.max_num_seqs, max_model_len,
+                                  use_graphs=cfg.use_graphs and cfg.tp_size == 1 and cfg.ep_size == 1,
+                                  tp_rank=cfg.tp_rank, tp_size=cfg.tp_size, cpu_group=cpu_group)
+        self.requests: dict[str, tuple] = {}
+        self.lock = threading.Lock()
+
+    # ------------------------------------------------------------------------------------------
+    def _auto_blocks(self, max_model_len: int) -> int:
+        per_block = self.model_cfg.kv_bytes_per_token() // self.cfg.tp_size * self.cfg.block_size
+        if self.device.type == "cpu":
+            want = (self.cfg.max_num_seqs * max_model_len) // self.cfg.block_size + 8
+            return max(16, min(want, (1 << 30) // per_block))
+        free, total = torch.cuda.mem_get_info(self.device)
+        reserve = 6 << 30  # workspace, graphs, library GEMM scratch
+        budget = max(0, int((free - reserve) * self.cfg.kv_cache_fraction))
+        return max(16, budget // per_block)
+
+    def add_request(self, request_id: str, prompt_ids: list, params: SamplingParams | None = None,
+                    callback=None) -> Sequence:
+        params = params or SamplingParams(max_tokens=self.cfg.default_max_tokens)
+        seq = Sequence(request_id, list(prompt_ids), params, eos_ids=tuple(self.model_cfg.eos_token_ids))
+        if params.seed is not None:
+            seq.sampling_seed = int(params.seed)
+        else:
+            seq.sampling_seed = int.from_bytes(hashlib.blake2b(request_id.encode(), digest_size=8).digest(), "little")
+        with self.lock:
+            self.scheduler.add(seq)
+            self.requests[request_id] = (seq, IncrementalDetokenizer(self.tokenizer), callback)
+            self.metrics.on_arrival()
+        return seq
+
+    def add_chat_request(self, request_id: str, messages: list, params: SamplingParams | None = None,
+                         callback=None) -> Sequence:
+        return self.add_request(request_id, self.tokenizer.apply_chat_template(messages), params, callback)
+
+    def abort(self, request_id: str) -> None:
+        with self.lock:
+            seq = self.scheduler.abort(request_id)
+            entry = self.requests.pop(request_id, None)
+        if seq is not None and entry is not None:
+            self._emit(entry[2], RequestOutput(request_id, [], "", True, "abort", seq=seq))
+
+    def has_unfinished(self) -> bool:
+        return self.scheduler.has_work()
+
+    @staticmethod
+    def _emit(cb, out: RequestOutput) -> None:
+        if cb is not None:
+            cb(out)
+
+    # ------------------------------------------------------------------------------------------
+    def step(self) -> list[RequestOutput]:
+        with self.lock:
+            batch = self.scheduler.schedule()
+        if batch is None or not batch.seqs:
+            return []
+        t0 = time.perf_counter()
+        try:
+            ids = self.runner.execute(batch)
+        except Exception as exc:  # engine watchdog: fail the in-flight requests, keep serving
+            msg = f"{type(exc).__name__}: {exc}"
+            traceback.print_exc()
+            outs = []
+            with self.lock:
+                for seq in batch.seqs:
+                    self.scheduler.finish(seq, SeqStatus.FINISHED_ERROR)
+                    entry = self.requests.pop(seq.request_id, None)
+                    out = RequestOutput(seq.request_id, [], "", True, "error", error=msg, seq=seq)
+                    outs.append(out)
+                    if entry:
+                        self._emit(entry[2], out)
+            return outs
+        now = time.perf_counter()
+        self.metrics.on_step(batch.kind, len(batch.seqs), batch.num_tokens, now - t0, self.blocks.utilization(),
+                             len(self.scheduler.waiting))
+        outs = []
+        with self.lock:
+            for seq, n, keep, tok in zip(batch.seqs, batch.num_new_tokens, batch.sample, ids):
+                if seq.status.finished:
+                    continue
+                seq.num_computed += n
+                if not keep:
+                    continue
+                first = seq.first_token_time is None
+                seq.append(tok, now)
+                entry = self.requests.get(seq.request_id)
+                if entry is None:
+                    continue
+                _, detok, cb = entry
+                stop = seq.check_stop()
+                text = detok.add(tok)  # special / EOS ids decode to ''
+                if seq.params.stop and text:
+                    hit = min((i for i in (detok.text.find(s) for s in seq.params.stop) if i >= 0), default=-1)
+                    if hit >= 0:
+                        cut = len(detok.text) - hit
+                        text = text[:-cut] if cut <= len(text) else ""
+                        stop = SeqStatus.FINISHED_STOPPED
+                if first:
+                    self.metrics.on_first_token(seq.ttft)
+                else:
+                    self.metrics.on_token()
+                out = RequestOutput(seq.request_id, [tok], text, seq=seq)
+                if stop is not None:
+                    tail = detok.flush() if stop == SeqStatus.FINISHED_LENGTH else ""
+                    out.text += tail
+                    out.finished, out.finish_reason = True, stop.value
+                    seq.finish_time = now
+                    self.scheduler.finish(seq, stop)
+                    self.requests.pop(seq.request_id, None)
+                    self.metrics.on_finish(seq)
+                outs.append(out)
+                self._emit(cb, out)
+        return outs
+
+    def generate(self, prompt_ids: list, params: SamplingParams | None = None) -> list[int]:
+        """Blocking single-request helper (tests, smoke)."""
+        rid = f"gen-{time.monotonic_ns()}"
+        seq = self.add_request(rid, prompt_ids, params)
+        while not seq.status.finished:
+            self.step()
+        return list(seq.output_ids)
+
+    def shutdown(self) -> None:
+        self.runner.broadcast_stop()
+
+
+class AsyncEngine:
+    """Runs :class:`LLMEngine` on a dedicated thread; asyncio-facing ``generate``."""
+
+    def __init__(self, engine: LLMEngine, queue_limit: int = 4096):
+        self.engine = engine
+        self.queue_limit = queue_limit
+        self._wake = threading.Event()
+        self._stop = False
+        self._thread = threading.Thread(target=self._loop, name="symmetry-engine", daemon=True)
+        self._started = False
+
+    def start(self) -> None:
+        if not self._started:
+            self._started = True
+            self._thread.start()
+
+    def _loop(self) -> None:
+        while not self._stop:
+            if not self.engine.has_unfinished():
+                self._wake.wait(0.05)
+                self._wake.clear()
+                continue
+            self.engine.step()
+
+    def stop(self) -> None:
+        self._stop = True
+        self._wake.set()
+        if self._started:
+            self._thread.join(timeout=10)
+        self.engine.shutdown()
+
+    async def generate(self, request_id: str, messages: list | None = None, prompt_ids: list | None = None,
+                       params: SamplingParams | None = None):
+        """Async iterator of RequestOutput for one request; aborts the sequence if the consumer goes away."""
+        loop = asyncio.get_running_loop()
+        q: asyncio.Queue = asyncio.Queue(maxsize=self.queue_limit)
+
+        def cb(out: RequestOutput) -> None:
+            loop.call_soon_threadsafe(q.put_nowait, out)
+
+        if prompt_ids is None:
+            prompt_ids = self.engine.tokenizer.apply_chat_template(messages or [])
+        self.engine.add_request(request_id, prompt_ids, params, cb)
+        self.start()
+        self._wake.set()
+        finished = False
+        try:
+            while True:
+                out = await q.get()
+                yield out
+                if out.finished:
+                    finished = True
+                    return
+        finally:
+            if not finished:
+                self.engine.abort(request_id)

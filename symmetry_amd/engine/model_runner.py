@@ -1,0 +1,283 @@
+"""ModelRunner: scheduled batch -> device metadata -> forward -> sampled token ids.
+
+* All per-step host metadata (token ids, positions, slots, context lengths,
+  block tables, sampling params) is packed into ONE pinned int32 buffer and
+  moved with ONE async H2D copy.
+* Decode steps replay a hipGraph captured per batch-size bucket
+  (``torch.cuda.CUDAGraph`` is hipGraph on ROCm): the ~300 kernel launches of
+  a Llama-3-8B step become one graph launch (MI355X_MICROARCH.md rows
+  **boundary** / **graph-replay-floor**).  Padded rows write no cache
+  (slot -1) and read only the reserved block 0.
+* Tensor parallel: rank 0 runs the scheduler; :meth:`execute` broadcasts the
+  packed metadata to the other ranks (R4) which replay the
+  same forward via :meth:`worker_loop`.
+"""
+from __future__ import annotations
+
+import math
+import time
+
+import numpy as np
+import torch
+
+from ..models.transformer import ForwardBatch, KVCache, TransformerLM
+from .scheduler import ScheduledBatch
+
+DECODE_BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64)
+_SEED_MIX = 0x9E3779B97F4A7C15
+
+
+def _seq_seed(seed: int, n_out: int) -> int:
+    x = (seed * 0x100000001B3 + n_out * _SEED_MIX) & 0xFFFFFFFFFFFFFFFF
+    x ^= x >> 29
+    return x - (1 << 64) if x >= 1 << 63 else x
+
+
+class _Layout:
+    """Offsets of the packed int32 metadata buffer."""
+
+    def __init__(self, T: int, nseq: int, max_blocks: int, prefill: bool, ntiles: int = 0):
+        off = 0
+
+        def take(n):
+            nonlocal off
+            o = off
+            off += n
+            return o
+
+        self.T, self.nseq, self.max_blocks, self.ntiles = T, nseq, max_blocks, ntiles
+        self.ids = take(T)
+        self.pos = take(T)
+        self.slots = take(T)
+        self.ctx = take(nseq)
+        self.temps = take(nseq)
+        if off % 2:
+            take(1)
+        self.seeds = take(2 * nseq)
+        self.step = take(2)
+        self.bt = take(nseq * max_blocks)
+        self.prefill = prefill
+        if prefill:
+            self.cu = take(nseq + 1)
+            self.tiles = take(2 * ntiles)
+            if off % 2:
+                take(1)
+            self.last = take(2 * nseq)
+        self.size = off + (off % 2)
+
+    def views(self, buf: torch.Tensor) -> dict:
+        v = {
+            "input_ids": buf[self.ids:self.ids + self.T],
+            "positions": buf[self.pos:self.pos + self.T],
+            "slot_mapping": buf[self.slots:self.slots + self.T],
+            "ctx_lens": buf[self.ctx:self.ctx + self.nseq],
+            "temps": buf[self.temps:self.temps + self.nseq].view(torch.float32),
+            "seeds": buf[self.seeds:self.seeds + 2 * self.nseq].view(torch.int64),
+            "step": buf[self.step:self.step + 2].view(torch.int64),
+            "block_tables": buf[self.bt:self.bt + self.nseq * self.max_blocks].view(self.nseq, self.max_blocks),
+        }
+        if self.prefill:
+            v["cu_q"] = buf[self.cu:self.cu + self.nseq + 1]
+            v["tiles"] = buf[self.tiles:self.tiles + 2 * self.ntiles].view(self.ntiles, 2)
+            v["last_idx"] = buf[self.last:self.last + 2 * self.nseq].view(torch.int64)
+        return v
+
+
+class ModelRunner:
+    def __init__(self, model: TransformerLM, kv: KVCache, max_num_seqs: int, max_model_len: int,
+                 use_graphs: bool = True, tp_group=None, tp_rank: int = 0, tp_size: int = 1, cpu_group=None):
+        self.model = model
+        self.kv = kv
+        self.device = model.device
+        self.block_size = kv.block_size
+        self.max_blocks = math.ceil(max_model_len / kv.block_size)
+        self.max_num_seqs = max_num_seqs
+        self.buckets = [b for b in DECODE_BUCKETS if b < max_num_seqs] + [max_num_seqs]
+        self.buckets = sorted(set(b for b in self.buckets if b <= 64))
+        self.is_gpu = self.device.type != "cpu"
+        self.use_graphs = use_graphs and self.is_gpu
+        self.tp_size, self.tp_rank = tp_size, tp_rank
+        self.cpu_group = cpu_group
+        self.graphs: dict[int, tuple] = {}
+        self._graph_pool = None
+        self._pinned = {}
+        self.step_counter = 0
+        self.timing = {"h2d": 0.0, "forward": 0.0, "d2h": 0.0, "steps": 0}
+
+    # ------------------------------------------------------------------------------------------
+    def _host(self, n: int, key: str) -> torch.Tensor:
+        t = self._pinned.get(key)
+        if t is None or t.numel() < n:
+            t = torch.empty(max(n, 1024), dtype=torch.int32, pin_memory=self.is_gpu)
+            self._pinned[key] = t
+        return t[:n]
+
+    def _fill(self, lay: _Layout, host: np.ndarray, seqs, counts, pad_to: int | None = None) -> None:
+        BS = self.block_size
+        ids, pos, slots = [], [], []
+        ctx, temps, seeds = [], [], []
+        for seq, n in zip(seqs, counts):
+            start = seq.num_computed
+            toks = seq.token_ids[start:start + n]
+            p = np.arange(start, start + n, dtype=np.int64)
+            bt = np.asarray(seq.block_table, dtype=np.int64)
+            ids.extend(toks)
+            pos.append(p)
+            slots.append(bt[p // BS] * BS + p % BS)
+            ctx.append(start + n)
+            temps.append(seq.params.temperature)
+            seeds.append(_seq_seed(seq.sampling_seed, len(seq.output_ids)))
+        nreal = len(seqs)
+        T = lay.T
+        host[:] = 0
+        host[lay.ids:lay.ids + len(ids)] = ids
+        if pos:
+            host[lay.pos:lay.pos + len(ids)] = np.concatenate(pos)
+            host[lay.slots:lay.slots + len(ids)] = np.concatenate(slots)
+        host[lay.slots + len(ids):lay.slots + T] = -1
+        host[lay.ctx:lay.ctx + nreal] = ctx
+        host[lay.ctx + nreal:lay.ctx + lay.nseq] = 1
+        host[lay.temps:lay.temps + nreal] = np.asarray(temps, dtype=np.float32).view(np.int32)
+        host[lay.seeds:lay.seeds + 2 * nreal] = np.asarray(seeds, dtype=np.int64).view(np.int32)
+        btv = host[lay.bt:lay.bt + lay.nseq * lay.max_blocks].reshape(lay.nseq, lay.max_blocks)
+        for i, seq in enumerate(seqs):
+            btv[i, :len(seq.block_table)] = seq.block_table
+        if lay.prefill:
+            cu = np.zeros(lay.nseq + 1, dtype=np.int64)
+            cu[1:] = np.cumsum(counts)
+            host[lay.cu:lay.cu + lay.nseq + 1] = cu
+            tiles = []
+            for i, n in enumerate(counts):
+                tiles.extend((i, r) for r in range(0, n, 64))
+            host[lay.tiles:lay.tiles + 2 * len(tiles)] = np.asarray(tiles, dtype=np.int32).reshape(-1)
+            host[lay.last:lay.last + 2 * lay.nseq] = (cu[1:] - 1).astype(np.int64).view(np.int32)
+
+    def _forward_batch(self, kind: str, lay: _Layout, dev: torch.Tensor, nseq: int, need_logits=False):
+        v = lay.views(dev)
+        return ForwardBatch(kind=kind, num_seqs=nseq, need_logits=need_logits, **v)
+
+    # ------------------------------------------------------------------------------------------
+    def execute(self, batch: ScheduledBatch) -> list[int]:
+        """Rank-0 entry: run one scheduled step, return sampled ids (one per sequence)."""
+        seqs, counts = batch.seqs, batch.num_new_tokens
+        t0 = time.perf_counter()
+        if batch.kind == "decode":
+            nseq = len(seqs)
+            bucket = self._bucket(nseq)
+            lay = _Layout(bucket, bucket, self.max_blocks, prefill=False)
+        else:
+            nseq = len(seqs)
+            ntiles = sum((n + 63) // 64 for n in counts)
+            max_blocks = max(len(s.block_table) for s in seqs)
+            lay = _Layout(sum(counts), nseq, max_blocks, prefill=True, ntiles=ntiles)
+        host_t = self._host(lay.size, batch.kind)
+        host = host_t.numpy()
+        self._fill(lay, host, seqs, counts)
+        header = np.array([0 if batch.kind == "decode" else 1, lay.T, lay.nseq, lay.max_blocks, lay.ntiles, nseq],
+                          dtype=np.int32)
+        if self.tp_size > 1:
+            self._broadcast(header, host_t)
+        ids = self._run(header, host_t)
+        self.timing["steps"] += 1
+        self.timing["forward"] += time.perf_counter() - t0
+        return ids[:nseq]
+
+    def _bucket(self, n: int) -> int:
+        for b in self.buckets:
+            if b >= n:
+                return b
+        raise ValueError(f"decode batch {n} exceeds max_num_seqs {self.max_num_seqs}")
+
+    def _run(self, header: np.ndarray, host_t: torch.Tensor) -> list[int]:
+        kind = "decode" if header[0] == 0 else "prefill"
+        T, nseq_l, max_blocks, ntiles, nseq = (int(x) for x in header[1:6])
+        lay = _Layout(T, nseq_l, max_blocks, prefill=kind == "prefill", ntiles=ntiles)
+        if kind == "decode" and self.use_graphs:
+            g = self.graphs.get(T)
+            if g is None:
+                self._capture(T)
+                g = self.graphs[T]
+            graph, dev, out = g
+            dev.copy_(host_t[:lay.size], non_blocking=True)
+            graph.replay()
+            ids = out
+        else:
+            dev = self.model.ws.get("meta." + kind, (lay.size,), torch.int32, self.device)
+            dev.copy_(host_t[:lay.size], non_blocking=True)
+            fb = self._forward_batch(kind, lay, dev, nseq_l)
+            ids = self.model.forward(fb, self.kv)
+        if self.is_gpu:
+            out_host = self._host(ids.numel(), "ids_out")
+            out_host.copy_(ids, non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            return out_host.tolist()
+        return ids.tolist()
+
+    # ------------------------------------------------------------------------------------------
+    def _capture(self, bucket: int) -> None:
+        """Capture the decode forward for `bucket` rows (largest buckets first avoids buffer growth)."""
+        lay = _Layout(bucket, bucket, self.max_blocks, prefill=False)
+        dev = torch.zeros(lay.size, dtype=torch.int32, device=self.device)
+        host = self._host(lay.size, "capture")
+        hn = host.numpy()
+        self._fill(lay, hn, [], [])
+        dev.copy_(host[:lay.size])
+        fb = self._forward_batch("decode", lay, dev, bucket)
+        # eager warmup: allocates workspace and loads kernels outside the capture
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self.model.forward(fb, self.kv)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        if self._graph_pool is None:
+            self._graph_pool = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self._graph_pool):
+            out = self.model.forward(fb, self.kv)
+        torch.cuda.synchronize()
+        self.graphs[bucket] = (g, dev, out)
+
+    def capture_all(self) -> float:
+        t0 = time.perf_counter()
+        if self.use_graphs:
+            for b in sorted(self.buckets, reverse=True):
+                if b not in self.graphs:
+                    self._capture(b)
+        return time.perf_counter() - t0
+
+    # ------------------------------------------------------------------------------------------
+    # tensor-parallel metadata plane (R4)
+    def _broadcast(self, header: np.ndarray, host_t: torch.Tensor) -> None:
+        import torch.distributed as dist
+
+        h = torch.from_numpy(np.concatenate([header, [host_t.numel()]]).astype(np.int32))
+        dist.broadcast(h, src=0, group=self.cpu_group)
+        n = int(h[-1])
+        dist.broadcast(host_t[:n].contiguous() if n else torch.zeros(1, dtype=torch.int32), src=0,
+                       group=self.cpu_group)
+
+    def broadcast_stop(self) -> None:
+        if self.tp_size > 1:
+            import torch.distributed as dist
+
+            h = torch.tensor([-1, 0, 0, 0, 0, 0, 0], dtype=torch.int32)
+            dist.broadcast(h, src=0, group=self.cpu_group)
+
+    def worker_loop(self) -> None:
+        """Ranks 1..tp-1: mirror rank 0's steps until it broadcasts stop."""
+        import torch.distributed as dist
+
+        while True:
+            h = torch.zeros(7, dtype=torch.int32)
+            dist.broadcast(h, src=0, group=self.cpu_group)
+            header = h.numpy()
+            if header[0] < 0:
+                return
+            n = int(header[6])
+            host_t = self._host(max(n, 1), "worker")
+            buf = torch.zeros(max(n, 1), dtype=torch.int32)
+            dist.broadcast(buf, src=0, group=self.cpu_group)
+            host_t.copy_(buf)
+            self._run(header[:6], host_t)

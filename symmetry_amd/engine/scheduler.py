@@ -1,0 +1,189 @@
+"""Paged KV block manager and continuous-batching scheduler.
+
+REF: the reference has no scheduler -- every peer's ``data`` handler is an
+independent async task that fetches from Ollama (``src/provider.ts:174-192``)
+and ``maxConnections`` is passed to Hyperswarm and never enforced
+(``src/provider.ts:38-40``).  Here all active requests
+share one engine: each step is either a *prefill* batch (new prompts, chunked
+to a token budget, prefill-first for TTFT) or a *decode* batch (one token for
+every running sequence).  ``max_num_seqs`` is the admission limit (fed by
+``maxConnections``); KV blocks are allocated on demand and a sequence is
+preempted (recomputed later) when the cache runs out.
+"""
+from __future__ import annotations
+
+import collections
+from dataclasses import dataclass, field
+
+from .sequence import Sequence, SeqStatus
+
+
+class BlockManager:
+    def __init__(self, num_blocks: int, block_size: int, reserved: int = 1):
+        # block 0 is reserved as the scratch block of padded (graph) batch rows
+        self.block_size = block_size
+        self.num_blocks = num_blocks
+        self.free = collections.deque(range(reserved, num_blocks))
+        self.reserved = reserved
+
+    @property
+    def num_free(self) -> int:
+        return len(self.free)
+
+    def blocks_needed(self, seq: Sequence, num_tokens: int) -> int:
+        need = (num_tokens + self.block_size - 1) // self.block_size
+        return max(0, need - len(seq.block_table))
+
+    def can_grow(self, seq: Sequence, num_tokens: int) -> bool:
+        return self.blocks_needed(seq, num_tokens) <= self.num_free
+
+    def grow(self, seq: Sequence, num_tokens: int) -> None:
+        n = self.blocks_needed(seq, num_tokens)
+        if n > self.num_free:
+            raise MemoryError("out of KV blocks")
+        for _ in range(n):
+            seq.block_table.append(self.free.popleft())
+
+    def release(self, seq: Sequence) -> None:
+        self.free.extend(seq.block_table)
+        seq.block_table = []
+
+    def utilization(self) -> float:
+        usable = self.num_blocks - self.reserved
+        return 1.0 - self.num_free / max(1, usable)
+
+
+@dataclass
+class SchedulerConfig:
+    max_num_seqs: int = 64
+    max_num_batched_tokens: int = 8192
+    max_model_len: int = 8192
+    enable_chunked_prefill: bool = True
+
+
+@dataclass
+class ScheduledBatch:
+    kind: str                       # "prefill" | "decode"
+    seqs: list                      # sequences in batch order
+    num_new_tokens: list            # tokens computed this step per sequence
+    sample: list = field(default_factory=list)  # whether this step's sample is kept per sequence
+    preempted: list = field(default_factory=list)
+
+    @property
+    def num_tokens(self) -> int:
+        return sum(self.num_new_tokens)
+
+
+class Scheduler:
+    def __init__(self, cfg: SchedulerConfig, blocks: BlockManager):
+        self.cfg = cfg
+        self.blocks = blocks
+        self.waiting: collections.deque[Sequence] = collections.deque()
+        self.running: list[Sequence] = []
+
+    # ------------------------------------------------------------------------------------------
+    def add(self, seq: Sequence) -> None:
+        if seq.num_tokens + seq.params.max_tokens > self.cfg.max_model_len:
+            seq.params.max_tokens = max(1, self.cfg.max_model_len - seq.num_tokens)
+        if seq.num_tokens >= self.cfg.max_model_len:
+            raise ValueError(f"prompt of {seq.num_tokens} tokens exceeds max_model_len {self.cfg.max_model_len}")
+        seq.status = SeqStatus.WAITING
+        self.waiting.append(seq)
+
+    def finish(self, seq: Sequence, status: SeqStatus) -> None:
+        seq.status = status
+        self.blocks.release(seq)
+        if seq in self.running:
+            self.running.remove(seq)
+        else:
+            try:
+                self.waiting.remove(seq)
+            except ValueError:
+                pass
+
+    def abort(self, request_id: str) -> Sequence | None:
+        for seq in list(self.running) + list(self.waiting):
+            if seq.request_id == request_id:
+                self.finish(seq, SeqStatus.FINISHED_ABORTED)
+                return seq
+        return None
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    @property
+    def num_active(self) -> int:
+        return len(self.waiting) + len(self.running)
+
+    # ------------------------------------------------------------------------------------------
+    def schedule(self) -> ScheduledBatch | None:
+        batch = self._schedule_prefill()
+        if batch is not None:
+            return batch
+        return self._schedule_decode()
+
+    def _schedule_prefill(self) -> ScheduledBatch | None:
+        budget = self.cfg.max_num_batched_tokens
+        seqs, counts, sample = [], [], []
+
+        def take(seq: Sequence) -> bool:
+            nonlocal budget
+            remaining = seq.prefill_target - seq.num_computed
+            n = min(remaining, budget) if self.cfg.enable_chunked_prefill else remaining
+            if n <= 0 or n > budget:
+                return False
+            if not self.blocks.can_grow(seq, seq.num_computed + n):
+                return False
+            self.blocks.grow(seq, seq.num_computed + n)
+            seqs.append(seq)
+            counts.append(n)
+            # the final chunk of a fresh prompt samples the first output token
+            sample.append(seq.num_computed + n == seq.num_tokens and not seq.output_ids)
+            budget -= n
+            return True
+
+        # 1) continue partially prefilled running sequences
+        for seq in self.running:
+            if seq.in_prefill and budget > 0:
+                take(seq)
+        # 2) admit waiting sequences
+        while self.waiting and budget > 0 and len(self.running) < self.cfg.max_num_seqs:
+            seq = self.waiting[0]
+            if not take(seq):
+                break
+            self.waiting.popleft()
+            seq.status = SeqStatus.RUNNING
+            self.running.append(seq)
+        if not seqs:
+            return None
+        return ScheduledBatch("prefill", seqs, counts, sample)
+
+    def _schedule_decode(self) -> ScheduledBatch | None:
+        preempted = []
+        ready = [s for s in self.running if not s.in_prefill]
+        # ensure a cache slot for each decoding sequence; preempt the newest on exhaustion
+        ready.sort(key=lambda s: s.arrival_time)
+        out = []
+        while ready:
+            seq = ready.pop(0)
+            if self.blocks.can_grow(seq, seq.num_computed + 1):
+                self.blocks.grow(seq, seq.num_computed + 1)
+                out.append(seq)
+                continue
+            victim = ready.pop() if ready else seq
+            if victim is not seq:
+                ready.insert(0, seq)
+            self._preempt(victim)
+            preempted.append(victim)
+        if not out:
+            return ScheduledBatch("decode", [], [], [], preempted) if preempted else None
+        return ScheduledBatch("decode", out, [1] * len(out), [True] * len(out), preempted)
+
+    def _preempt(self, seq: Sequence) -> None:
+        self.blocks.release(seq)
+        seq.num_computed = 0
+        seq.num_preemptions += 1
+        seq.status = SeqStatus.WAITING
+        if seq in self.running:
+            self.running.remove(seq)
+        self.waiting.appendleft(seq)

@@ -78,15 +78,27 @@ class KVCache:
 
 @dataclass
 class Workspace:
+    """Named scratch buffers that only grow.
+
+    A replaced buffer is kept alive (``retired``): hipGraphs captured earlier
+    hold its raw address, so it must never return to the allocator.
+    """
+
     buffers: dict = field(default_factory=dict)
+    retired: list = field(default_factory=list)
 
     def get(self, name: str, shape, dtype, device) -> torch.Tensor:
         numel = math.prod(shape)
         buf = self.buffers.get((name, dtype))
         if buf is None or buf.numel() < numel:
+            if buf is not None:
+                self.retired.append(buf)
             buf = torch.empty(numel, dtype=dtype, device=device)
             self.buffers[(name, dtype)] = buf
         return buf[:numel].view(*shape)
+
+    def nbytes(self) -> int:
+        return sum(b.numel() * b.element_size() for b in list(self.buffers.values()) + self.retired)
 
 
 class TransformerLM:

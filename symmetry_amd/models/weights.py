@@ -35,6 +35,15 @@ import torch
 from .config import ModelConfig
 
 INIT_STD = 0.02
+# matrices are drawn with std = INIT_GAIN / sqrt(fan_in): 0.02 at d = 4096 (the Llama init),
+# and the same activation scale for the small test configs
+INIT_GAIN = 1.28
+
+
+def _std(name: str, shape) -> float:
+    if name == "embed":
+        return INIT_STD
+    return INIT_GAIN / (shape[-1] ** 0.5)
 
 
 @dataclass
@@ -170,7 +179,7 @@ def random_weights(cfg: ModelConfig, shard: ShardSpec | None = None, device="cpu
             if len(shape) == 1:
                 full[name] = torch.ones(shape, dtype=dtype)
             else:
-                full[name] = _randn(shape, _seed(seed, name), "cpu", dtype)
+                full[name] = _randn(shape, _seed(seed, name), "cpu", dtype, _std(name, shape))
         if cfg.tie_embeddings:
             full["lm_head"] = full["embed"]
         for name, t in shard_full(cfg, shard, full).items():
@@ -182,7 +191,7 @@ def random_weights(cfg: ModelConfig, shard: ShardSpec | None = None, device="cpu
                 tensors[name] = torch.ones(sshape, dtype=dtype, device=device)
             else:
                 rank = shard.tp_rank if name not in ("embed",) and not name.endswith("router") else -1
-                tensors[name] = _randn(sshape, _seed(seed, name, rank), device, dtype)
+                tensors[name] = _randn(sshape, _seed(seed, name, rank), device, dtype, _std(name, shape))
     else:
         raise ValueError(mode)
     return ModelWeights(cfg, shard, tensors)
