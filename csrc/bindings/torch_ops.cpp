@@ -208,7 +208,7 @@ void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                       (int)Hq, (int)Hkv, (int)k_cache.size(2), (int)block_tables.size(1), (float)scale, cur_stream(q));
 }
 
-void skinny_gemm(const Tensor& x, const Tensor& w, Tensor& y) {
+void skinny_gemm(const Tensor& x, const Tensor& w, Tensor& y, int64_t variant) {
   check_gpu(x, "x");
   check_gpu(w, "w");
   check_gpu(y, "y");
@@ -223,7 +223,9 @@ void skinny_gemm(const Tensor& x, const Tensor& w, Tensor& y) {
   TORCH_CHECK(S >= 1 && K % (S * 256) == 0, "skinny_gemm: K must be a multiple of 256 * nsplit");
   TORCH_CHECK(y.size(1) == M && y.size(2) == N, "skinny_gemm: y shape mismatch");
   const at::OptionalDeviceGuard g(x.device());
-  launch_skinny_gemm(ptr<bf16>(x), ptr<bf16>(w), ptr<float>(y), (int)M, (int)N, (int)K, (int)S, cur_stream(x));
+  TORCH_CHECK(variant != 3 || N % 32 == 0, "variant 3 needs N % 32 == 0");
+  launch_skinny_gemm(ptr<bf16>(x), ptr<bf16>(w), ptr<float>(y), (int)M, (int)N, (int)K, (int)S, cur_stream(x),
+                     (int)variant);
 }
 
 void lm_head_sample(const Tensor& x, const Tensor& w, const Tensor& temps, const Tensor& seeds, const Tensor& step,
@@ -298,7 +300,7 @@ TORCH_LIBRARY(symmetry_amd, m) {
       "attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, Tensor cu_q, "
       "Tensor tiles, Tensor(a!) out, float scale) -> ()",
       &attn_prefill);
-  m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) y) -> ()", &skinny_gemm);
+  m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) y, int variant=0) -> ()", &skinny_gemm);
   m.def(
       "lm_head_sample(Tensor x, Tensor w, Tensor temps, Tensor seeds, Tensor step, Tensor(a!) tile_keys, "
       "Tensor(b!) out_keys, Tensor(c!) out_ids, int n_offset, Tensor(d!)? logits) -> ()",

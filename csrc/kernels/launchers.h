@@ -28,7 +28,8 @@ void launch_attn_prefill(const bf16* q, const bf16* k_cache, const bf16* v_cache
                          int Hkv, int BS, int max_blocks, float scale, hipStream_t s);
 
 // skinny_gemm.hip
-void launch_skinny_gemm(const bf16* x, const bf16* W, float* y, int M, int N, int K, int S, hipStream_t s);
+void launch_skinny_gemm(const bf16* x, const bf16* W, float* y, int M, int N, int K, int S, hipStream_t s,
+                        int variant = 0);
 void launch_skinny_gemm_argmax(const bf16* x, const bf16* W, float* logits_or_null, int M, int N, int K,
                                const float* temps, const unsigned long long* seeds, const long long* step,
                                unsigned long long* tile_keys, int n_offset, hipStream_t s);

@@ -44,7 +44,11 @@ SYM_DEV unsigned long long pack_key(float v, uint32_t idx) {
   return ((unsigned long long)ordered_bits(v) << 32) | (unsigned long long)(0xFFFFFFFFu - idx);
 }
 
-template <int MT, int U, int EPI>
+// RT: 16-row weight tiles per wave (x fragments shared across them).
+// NAT: natural k order (lane group h reads k 8h..8h+7 of each 32-deep MFMA step: 64 contiguous
+//      bytes per row per instruction) vs the permuted order (32 contiguous bytes per lane).
+// NTL: non-temporal weight loads.
+template <int MT, int U, int EPI, int RT, bool NAT, bool NTL>
 __global__ __launch_bounds__(NT) void skinny_gemm_kernel(const bf16* __restrict__ x, const bf16* __restrict__ W,
                                                          float* __restrict__ y, int M, int N, int K, int kchunk,
                                                          const float* __restrict__ temps,
@@ -55,79 +59,108 @@ __global__ __launch_bounds__(NT) void skinny_gemm_kernel(const bf16* __restrict_
   const int tile = blockIdx.x, split = blockIdx.y;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r16 = lane & 15, h = lane >> 4;
-  const int n0 = tile * 16;
+  const int n0 = tile * 16 * RT;
   const int wk = kchunk / 4;  // k range of one wave
   const int kbeg = split * kchunk + wid * wk;
   const int nblk = wk / 64;
+  const int lo = NAT ? 8 * h : 16 * h;   // lane's offset inside a 64-deep k block, first MFMA
+  const int hi = NAT ? 32 : 8;           // offset of the second MFMA's slice
 
-  const bf16* wrow = W + (long long)(n0 + r16) * K + kbeg + 16 * h;
+  const bf16* wrow[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) wrow[rt] = W + (long long)(n0 + 16 * rt + r16) * K + kbeg + lo;
   const bf16* xrow[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int mrow = min(16 * mt + r16, M - 1);
-    xrow[mt] = x + (long long)mrow * K + kbeg + 16 * h;
+    xrow[mt] = x + (long long)mrow * K + kbeg + lo;
   }
-  f32x4 acc[MT];
+  f32x4 acc[RT][MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto wload = [&](const bf16* p) -> u32x4 {
+    if constexpr (NTL) return ld_nt16(p);
+    else return *reinterpret_cast<const u32x4*>(p);
+  };
 
   int b = 0;
   for (; b + U <= nblk; b += U) {
-    Pack8 wa[U][2], xa[U][MT][2];
+    Pack8 wa[U][RT][2], xa[U][MT][2];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int ko = (b + u) * 64;
-      wa[u][0].w = ld_nt16(wrow + ko);
-      wa[u][1].w = ld_nt16(wrow + ko + 8);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        wa[u][rt][0].w = wload(wrow[rt] + ko);
+        wa[u][rt][1].w = wload(wrow[rt] + ko + hi);
+      }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         xa[u][mt][0].u = *reinterpret_cast<const uint4*>(xrow[mt] + ko);
-        xa[u][mt][1].u = *reinterpret_cast<const uint4*>(xrow[mt] + ko + 8);
+        xa[u][mt][1].u = *reinterpret_cast<const uint4*>(xrow[mt] + ko + hi);
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        acc[mt] = mfma16(wa[u][0].v, xa[u][mt][0].v, acc[mt]);
-        acc[mt] = mfma16(wa[u][1].v, xa[u][mt][1].v, acc[mt]);
-      }
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          acc[rt][mt] = mfma16(wa[u][rt][0].v, xa[u][mt][0].v, acc[rt][mt]);
+          acc[rt][mt] = mfma16(wa[u][rt][1].v, xa[u][mt][1].v, acc[rt][mt]);
+        }
   }
   for (; b < nblk; ++b) {
     const int ko = b * 64;
-    Pack8 w0, w1;
-    w0.w = ld_nt16(wrow + ko);
-    w1.w = ld_nt16(wrow + ko + 8);
+    Pack8 w0[RT], w1[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      w0[rt].w = wload(wrow[rt] + ko);
+      w1[rt].w = wload(wrow[rt] + ko + hi);
+    }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       Pack8 x0, x1;
       x0.u = *reinterpret_cast<const uint4*>(xrow[mt] + ko);
-      x1.u = *reinterpret_cast<const uint4*>(xrow[mt] + ko + 8);
-      acc[mt] = mfma16(w0.v, x0.v, acc[mt]);
-      acc[mt] = mfma16(w1.v, x1.v, acc[mt]);
+      x1.u = *reinterpret_cast<const uint4*>(xrow[mt] + ko + hi);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        acc[rt][mt] = mfma16(w0[rt].v, x0.v, acc[rt][mt]);
+        acc[rt][mt] = mfma16(w1[rt].v, x1.v, acc[rt][mt]);
+      }
     }
   }
 
   // Sum the 4 waves' partial tiles through LDS.
-  __shared__ f32x4 red[4][MT][64];
+  __shared__ f32x4 red[4][RT * MT][64];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) red[wid][mt][lane] = acc[mt];
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) red[wid][rt * MT + mt][lane] = acc[rt][mt];
   __syncthreads();
   if (wid != 0) return;
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    acc[mt] = red[0][mt][lane] + red[1][mt][lane] + red[2][mt][lane] + red[3][mt][lane];
-  }
-  // lane (c = r16, h): rows n0 + 4h + i (i = 0..3), column m = 16 mt + c.
-  if constexpr (EPI == 0) {
+  for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const int m = 16 * mt + r16;
-      if (m < M) {
-        float* yp = y + ((long long)split * M + m) * N + n0 + 4 * h;
-        *reinterpret_cast<float4*>(yp) = make_float4(acc[mt][0], acc[mt][1], acc[mt][2], acc[mt][3]);
-      }
+      const int i = rt * MT + mt;
+      acc[rt][mt] = red[0][i][lane] + red[1][i][lane] + red[2][i][lane] + red[3][i][lane];
     }
+  // lane (c = r16, h): rows n0 + 16 rt + 4h + i (i = 0..3), column m = 16 mt + c.
+  if constexpr (EPI == 0) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = 16 * mt + r16;
+        if (m < M) {
+          float* yp = y + ((long long)split * M + m) * N + n0 + 16 * rt + 4 * h;
+          *reinterpret_cast<float4*>(yp) = make_float4(acc[rt][mt][0], acc[rt][mt][1], acc[rt][mt][2], acc[rt][mt][3]);
+        }
+      }
   } else {
     const long long step = step_ctr ? *step_ctr : 0;
 #pragma unroll
@@ -138,18 +171,21 @@ __global__ __launch_bounds__(NT) void skinny_gemm_kernel(const bf16* __restrict_
       const float t = temps ? temps[mm] : 0.f;
       unsigned long long best = 0;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int gidx = n_offset + n0 + 4 * h + i;
-        float v = acc[mt][i];
-        if (y && mok) y[(long long)m * N + n0 + 4 * h + i] = v;
-        if (t > 0.f) {
-          const unsigned long long seed = seeds ? seeds[mm] : 0ull;
-          const float u = uniform01(seed ^ ((unsigned long long)step << 20), (unsigned long long)gidx);
-          v = v / t - __logf(-__logf(u));
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int nl = n0 + 16 * rt + 4 * h + i;
+          const int gidx = n_offset + nl;
+          float v = acc[rt][mt][i];
+          if (y && mok) y[(long long)m * N + nl] = v;
+          if (t > 0.f) {
+            const unsigned long long seed = seeds ? seeds[mm] : 0ull;
+            const float u = uniform01(seed ^ ((unsigned long long)step << 20), (unsigned long long)gidx);
+            v = v / t - __logf(-__logf(u));
+          }
+          const unsigned long long kk = pack_key(v, (uint32_t)gidx);
+          best = kk > best ? kk : best;
         }
-        const unsigned long long kk = pack_key(v, (uint32_t)gidx);
-        best = kk > best ? kk : best;
-      }
       // reduce over the 4 lane groups (same column)
       unsigned long long o16 = __shfl_xor(best, 16, 64);
       best = o16 > best ? o16 : best;
@@ -182,41 +218,51 @@ __global__ __launch_bounds__(256) void argmax_reduce_kernel(const unsigned long 
   }
 }
 
-template <int MT, int EPI>
+template <int MT, int EPI, int RT, bool NAT, bool NTL>
 void launch_mt(const bf16* x, const bf16* W, float* y, int M, int N, int K, int S, const float* temps,
                const unsigned long long* seeds, const long long* step, unsigned long long* keys, int n_offset,
                hipStream_t s) {
-  const int ntiles = N / 16;
+  const int ntiles = N / (16 * RT);
   const int kchunk = K / S;
   dim3 grid(ntiles, S);
-  constexpr int U = MT == 1 ? 4 : (MT == 2 ? 2 : 1);
-  skinny_gemm_kernel<MT, U, EPI>
+  constexpr int U = MT == 1 ? (RT == 1 ? 4 : 2) : (MT == 2 ? 2 : 1);
+  skinny_gemm_kernel<MT, U, EPI, RT, NAT, NTL>
       <<<grid, NT, 0, s>>>(x, W, y, M, N, K, kchunk, temps, seeds, step, keys, n_offset, ntiles);
 }
 
-template <int EPI>
+template <int EPI, int RT, bool NAT, bool NTL>
 void launch_epi(const bf16* x, const bf16* W, float* y, int M, int N, int K, int S, const float* temps,
                 const unsigned long long* seeds, const long long* step, unsigned long long* keys, int n_offset,
                 hipStream_t s) {
   const int mt = (M + 15) / 16;
   switch (mt) {
-    case 1: launch_mt<1, EPI>(x, W, y, M, N, K, S, temps, seeds, step, keys, n_offset, s); break;
-    case 2: launch_mt<2, EPI>(x, W, y, M, N, K, S, temps, seeds, step, keys, n_offset, s); break;
-    case 3: launch_mt<3, EPI>(x, W, y, M, N, K, S, temps, seeds, step, keys, n_offset, s); break;
-    default: launch_mt<4, EPI>(x, W, y, M, N, K, S, temps, seeds, step, keys, n_offset, s); break;
+    case 1: launch_mt<1, EPI, RT, NAT, NTL>(x, W, y, M, N, K, S, temps, seeds, step, keys, n_offset, s); break;
+    case 2: launch_mt<2, EPI, RT, NAT, NTL>(x, W, y, M, N, K, S, temps, seeds, step, keys, n_offset, s); break;
+    case 3: launch_mt<3, EPI, RT, NAT, NTL>(x, W, y, M, N, K, S, temps, seeds, step, keys, n_offset, s); break;
+    default: launch_mt<4, EPI, RT, NAT, NTL>(x, W, y, M, N, K, S, temps, seeds, step, keys, n_offset, s); break;
   }
 }
 
 }  // namespace
 
-void launch_skinny_gemm(const bf16* x, const bf16* W, float* y, int M, int N, int K, int S, hipStream_t s) {
-  launch_epi<0>(x, W, y, M, N, K, S, nullptr, nullptr, nullptr, nullptr, 0, s);
+void launch_skinny_gemm(const bf16* x, const bf16* W, float* y, int M, int N, int K, int S, hipStream_t s,
+                        int variant) {
+  // variant 0 = auto: measured on MI355X (bench/kernels/bench_skinny.py, profiles/skinny_variants.md):
+  // plain loads beat non-temporal ones for these 33-235 MB weight streams, and two row tiles per wave
+  // (x fragments shared) win once M > 16.
+  if (variant == 0) variant = (M > 16 && N % 32 == 0) ? 3 : 2;
+  switch (variant) {
+    case 1: launch_epi<0, 1, false, true>(x, W, y, M, N, K, S, nullptr, nullptr, nullptr, nullptr, 0, s); break;
+    case 2: launch_epi<0, 1, true, false>(x, W, y, M, N, K, S, nullptr, nullptr, nullptr, nullptr, 0, s); break;
+    case 3: launch_epi<0, 2, true, false>(x, W, y, M, N, K, S, nullptr, nullptr, nullptr, nullptr, 0, s); break;
+    default: launch_epi<0, 1, true, true>(x, W, y, M, N, K, S, nullptr, nullptr, nullptr, nullptr, 0, s); break;
+  }
 }
 
 void launch_skinny_gemm_argmax(const bf16* x, const bf16* W, float* logits_or_null, int M, int N, int K,
                                const float* temps, const unsigned long long* seeds, const long long* step,
                                unsigned long long* tile_keys, int n_offset, hipStream_t s) {
-  launch_epi<1>(x, W, logits_or_null, M, N, K, 1, temps, seeds, step, tile_keys, n_offset, s);
+  launch_epi<1, 1, true, false>(x, W, logits_or_null, M, N, K, 1, temps, seeds, step, tile_keys, n_offset, s);
 }
 
 void launch_argmax_reduce(const unsigned long long* tile_keys, int M, int ntiles, unsigned long long* out_keys,

@@ -75,9 +75,9 @@ def attn_prefill(q, k_cache, v_cache, block_tables, ctx_lens, cu_q, tiles, out, 
     return reference.attn_prefill(q, k_cache, v_cache, block_tables, ctx_lens, cu_q, tiles, out, scale)
 
 
-def skinny_gemm(x, w, y):
+def skinny_gemm(x, w, y, variant: int = 0):
     if _gpu(x):
-        return _native.ops().skinny_gemm(x, w, y)
+        return _native.ops().skinny_gemm(x, w, y, int(variant))
     return reference.skinny_gemm(x, w, y)
 
 
