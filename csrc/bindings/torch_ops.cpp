@@ -281,6 +281,82 @@ void swiglu(const Tensor& gu, Tensor& out) {
   launch_swiglu(linout(gu, T, 2 * F, "gu"), ptr<bf16>(out), (int)T, (int)F, cur_stream(out));
 }
 
+// ---- MoE -----------------------------------------------------------------------------------------
+// Routing: logits LinOut [T][E] -> ids/w [T][k], counts [E] (zeroed here), offsets [E+1],
+// then rows scattered into expert segments of xs [T*k][d]; dst [T][k] row of each assignment.
+void moe_route_permute(const Tensor& logits, const Tensor& x, int64_t k, int64_t E_, Tensor& ids, Tensor& w,
+                       Tensor& counts, Tensor& offsets, Tensor& cursor, Tensor& xs, Tensor& dst) {
+  check_gpu(x, "x");
+  check_dtype(x, at::kBFloat16, "x");
+  const int64_t T = x.size(0), d = x.size(1);
+  const int64_t E = E_;
+  TORCH_CHECK(counts.numel() >= E, "moe: counts too small");
+  TORCH_CHECK(E >= 1 && E <= 64 && k >= 1 && k <= 8 && k <= E, "moe: need 1 <= k <= E <= 64, k <= 8");
+  TORCH_CHECK(d % 8 == 0, "moe: d % 8");
+  for (auto* t : {&ids, &counts, &offsets, &cursor, &dst}) {
+    check_gpu(*t, "index tensor");
+    check_dtype(*t, at::kInt, "index tensor");
+  }
+  check_gpu(w, "w");
+  check_dtype(w, at::kFloat, "w");
+  check_gpu(xs, "xs");
+  check_dtype(xs, at::kBFloat16, "xs");
+  TORCH_CHECK(ids.numel() >= T * k && w.numel() >= T * k && dst.numel() >= T * k, "moe: [T, k] outputs too small");
+  TORCH_CHECK(offsets.numel() >= E + 1 && cursor.numel() >= E, "moe: offsets/cursor too small");
+  TORCH_CHECK(xs.numel() >= T * k * d, "moe: xs too small");
+  const at::OptionalDeviceGuard g(x.device());
+  hipStream_t s = cur_stream(x);
+  hipMemsetAsync(counts.data_ptr(), 0, E * sizeof(int), s);
+  hipMemsetAsync(cursor.data_ptr(), 0, E * sizeof(int), s);
+  const int64_t ld = logits.size(logits.dim() - 1);
+  TORCH_CHECK(ld >= E, "moe: logits narrower than E");
+  launch_moe_route(linout(logits, T, ld, "logits"), (int)ld, (int)T, (int)E, (int)k, ptr<int>(ids), ptr<float>(w),
+                   ptr<int>(counts), s);
+  launch_moe_align(ptr<int>(counts), (int)E, ptr<int>(offsets), s);
+  launch_moe_scatter(ptr<bf16>(x), (int)T, (int)d, (int)k, ptr<int>(ids), ptr<int>(offsets), ptr<int>(cursor),
+                     ptr<bf16>(xs), ptr<int>(dst), nullptr, s);
+}
+
+void grouped_skinny(const Tensor& xs, const Tensor& W, const Tensor& offsets, int64_t e0, Tensor& y) {
+  check_gpu(xs, "xs");
+  check_gpu(W, "W");
+  check_gpu(offsets, "offsets");
+  check_gpu(y, "y");
+  check_dtype(xs, at::kBFloat16, "xs");
+  check_dtype(W, at::kBFloat16, "W");
+  check_dtype(offsets, at::kInt, "offsets");
+  check_dtype(y, at::kFloat, "y");
+  TORCH_CHECK(W.dim() == 3 && xs.dim() == 2 && y.dim() == 3, "grouped_skinny: W [E,N,K], xs [R,K], y [S,R,N]");
+  const int64_t E = W.size(0), N = W.size(1), K = W.size(2), R = xs.size(0), S = y.size(0);
+  TORCH_CHECK(xs.size(1) == K && y.size(1) == R && y.size(2) == N, "grouped_skinny: shape mismatch");
+  TORCH_CHECK(e0 >= 0 && offsets.numel() >= e0 + E + 1, "grouped_skinny: offsets must cover experts e0..e0+E");
+  TORCH_CHECK(N % 16 == 0 && K % (256 * S) == 0, "grouped_skinny: N % 16 and K % (256 S)");
+  TORCH_CHECK(R <= 64, "grouped_skinny: at most 64 routed rows on this path (larger batches use library GEMMs)");
+  const at::OptionalDeviceGuard g(xs.device());
+  launch_grouped_skinny(ptr<bf16>(xs), ptr<bf16>(W), ptr<int>(offsets), ptr<float>(y), (int)R, (int)E, (int)e0,
+                        (int)N, (int)K, (int)S, cur_stream(xs));
+}
+
+void moe_combine(const Tensor& y, const Tensor& dst, const Tensor& ids, int64_t e_lo, int64_t e_hi, const Tensor& w,
+                 int64_t k, Tensor& out, bool accumulate) {
+  check_gpu(out, "out");
+  check_dtype(out, at::kFloat, "out");
+  check_gpu(dst, "dst");
+  check_dtype(dst, at::kInt, "dst");
+  check_gpu(w, "w");
+  check_dtype(w, at::kFloat, "w");
+  TORCH_CHECK(out.dim() == 2, "out must be [T, d]");
+  const int64_t T = out.size(0), d = out.size(1);
+  const int64_t R = y.dim() == 3 ? y.size(1) : y.size(0);
+  check_gpu(ids, "ids");
+  check_dtype(ids, at::kInt, "ids");
+  TORCH_CHECK(dst.numel() >= T * k && w.numel() >= T * k && ids.numel() >= T * k, "moe_combine: dst/w too small");
+  TORCH_CHECK(d % 8 == 0, "moe_combine: d % 8");
+  const at::OptionalDeviceGuard g(out.device());
+  launch_moe_combine(linout(y, R, d, "y"), ptr<int>(dst), ptr<int>(ids), (int)e_lo, (int)e_hi, ptr<float>(w), (int)T,
+                     (int)k, (int)d, ptr<float>(out), accumulate ? 1 : 0, cur_stream(out));
+}
+
 }  // namespace
 
 TORCH_LIBRARY(symmetry_amd, m) {
@@ -306,4 +382,13 @@ TORCH_LIBRARY(symmetry_amd, m) {
       "Tensor(b!) out_keys, Tensor(c!) out_ids, int n_offset, Tensor(d!)? logits) -> ()",
       &lm_head_sample);
   m.def("swiglu(Tensor gu, Tensor(a!) out) -> ()", &swiglu);
+  m.def(
+      "moe_route_permute(Tensor logits, Tensor x, int k, int E, Tensor(a!) ids, Tensor(b!) w, Tensor(c!) counts, "
+      "Tensor(d!) offsets, Tensor(e!) cursor, Tensor(f!) xs, Tensor(g!) dst) -> ()",
+      &moe_route_permute);
+  m.def("grouped_skinny(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y) -> ()", &grouped_skinny);
+  m.def(
+      "moe_combine(Tensor y, Tensor dst, Tensor ids, int e_lo, int e_hi, Tensor w, int k, Tensor(a!) out, "
+      "bool accumulate) -> ()",
+      &moe_combine);
 }

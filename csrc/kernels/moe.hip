@@ -1,0 +1,207 @@
+// K10-K12: Mixture-of-Experts routing, permutation, grouped GEMM and combine (Mixtral 8x7B).
+//
+//   moe_route     router logits (LinOut [T][E]) -> top-k ids + softmax-renormalised weights,
+//                 per-expert counts (atomics; counts zeroed by the op with hipMemsetAsync)
+//   moe_align     exclusive prefix sum of counts -> expert segment offsets [E+1]
+//   moe_scatter   copy each (token, slot) row of x into its expert segment; dst[t][j] = row
+//   grouped_skinny  Y[rows of expert e] = Xs[rows of e] . W[e]^T on MFMA, one weight tile per
+//                 workgroup, reading the segment bounds from device memory (graph-capturable,
+//                 no host sync); fp32 split-K slabs like the dense skinny GEMM
+//   moe_combine   out[t] = sum_j w[t][j] * Y[dst[t][j]]  (fixed slot order -> deterministic)
+//
+// Rows inside an expert segment are placed by atomics (order varies run to run) but every row
+// is computed independently and the combine sums in slot order, so results are bitwise stable.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+SYM_DEV f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// One wave per token.  E <= 64 experts (lane e holds logit e), k <= 8.
+__global__ __launch_bounds__(256) void moe_route_kernel(LinOut logits, int ld, int T, int E, int k,
+                                                        int* __restrict__ ids, float* __restrict__ w,
+                                                        int* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T) return;
+  float v = lane < E ? linout_load1(logits, (long long)t * ld + lane) : -INFINITY;
+  float sel[8];
+  int seli[8];
+  for (int j = 0; j < k; ++j) {
+    float m = v;
+    int mi = lane;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(m, o, 64);
+      const int oi = __shfl_xor(mi, o, 64);
+      if (om > m || (om == m && oi < mi)) {
+        m = om;
+        mi = oi;
+      }
+    }
+    sel[j] = m;
+    seli[j] = mi;
+    if (lane == mi) v = -INFINITY;
+  }
+  if (lane == 0) {
+    float mx = sel[0], s = 0.f;
+    for (int j = 0; j < k; ++j) s += __expf(sel[j] - mx);
+    for (int j = 0; j < k; ++j) {
+      ids[t * k + j] = seli[j];
+      w[t * k + j] = __expf(sel[j] - mx) / s;
+      atomicAdd(&counts[seli[j]], 1);
+    }
+  }
+}
+
+__global__ void moe_align_kernel(const int* __restrict__ counts, int E, int* __restrict__ offsets) {
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int e = 0; e < E; ++e) {
+      offsets[e] = acc;
+      acc += counts[e];
+    }
+    offsets[E] = acc;
+  }
+}
+
+// one 256-thread block per (token, slot); cursor[E] zeroed by the op
+__global__ __launch_bounds__(256) void moe_scatter_kernel(const bf16* __restrict__ x, int d, int k,
+                                                          const int* __restrict__ ids, const int* __restrict__ offsets,
+                                                          int* __restrict__ cursor, bf16* __restrict__ xs,
+                                                          int* __restrict__ dst, int* __restrict__ src_tok) {
+  const int a = blockIdx.x;  // assignment t * k + j
+  const int t = a / k;
+  const int e = ids[a];
+  __shared__ int row;
+  if (threadIdx.x == 0) {
+    row = offsets[e] + atomicAdd(&cursor[e], 1);
+    dst[a] = row;
+    if (src_tok) src_tok[row] = t;
+  }
+  __syncthreads();
+  const uint4* s = reinterpret_cast<const uint4*>(x + (long long)t * d);
+  uint4* o = reinterpret_cast<uint4*>(xs + (long long)row * d);
+  for (int i = threadIdx.x; i < d / 8; i += 256) o[i] = s[i];
+}
+
+// Grouped skinny GEMM: grid (N/16, E, S).  W [E][N][K] holds experts e0 .. e0+E-1 of the global
+// numbering; rows of expert e: [off[e0+e], off[e0+e+1]) (absolute rows of xs / y).
+// Up to 64 rows per expert (4 MFMA column tiles); the prefill path uses library GEMMs instead.
+__global__ __launch_bounds__(256) void grouped_skinny_kernel(const bf16* __restrict__ xs, const bf16* __restrict__ W,
+                                                             const int* __restrict__ offsets, float* __restrict__ y,
+                                                             int R, int N, int K, int kchunk, int e0) {
+  const int tile = blockIdx.x, e = blockIdx.y, split = blockIdx.z;
+  const int r0 = offsets[e + e0], r1 = offsets[e + e0 + 1];
+  const int n_e = r1 - r0;
+  if (n_e <= 0) return;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, h = lane >> 4;
+  const int n0 = tile * 16;
+  const int wk = kchunk / 4;
+  const int kbeg = split * kchunk + wid * wk;
+  const int nblk = wk / 64;
+  const bf16* wrow = W + ((long long)e * N + n0 + r16) * K + kbeg + 8 * h;
+  const int MT = min(4, (n_e + 15) / 16);
+  const bf16* xrow[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const int m = r0 + min(16 * mt + r16, n_e - 1);
+    xrow[mt] = xs + (long long)m * K + kbeg + 8 * h;
+  }
+  f32x4 acc[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int b = 0; b < nblk; ++b) {
+    const int ko = b * 64;
+    Pack8 w0, w1;
+    w0.u = *reinterpret_cast<const uint4*>(wrow + ko);
+    w1.u = *reinterpret_cast<const uint4*>(wrow + ko + 32);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      if (mt < MT) {
+        Pack8 x0, x1;
+        x0.u = *reinterpret_cast<const uint4*>(xrow[mt] + ko);
+        x1.u = *reinterpret_cast<const uint4*>(xrow[mt] + ko + 32);
+        acc[mt] = mfma16(w0.v, x0.v, acc[mt]);
+        acc[mt] = mfma16(w1.v, x1.v, acc[mt]);
+      }
+    }
+  }
+  __shared__ f32x4 red[4][4][64];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) red[wid][mt][lane] = acc[mt];
+  __syncthreads();
+  if (wid != 0) return;
+  for (int mt = 0; mt < MT; ++mt) {
+    const f32x4 s = red[0][mt][lane] + red[1][mt][lane] + red[2][mt][lane] + red[3][mt][lane];
+    const int m = 16 * mt + r16;
+    if (m < n_e) {
+      float* yp = y + ((long long)split * R + r0 + m) * N + n0 + 4 * h;
+      *reinterpret_cast<float4*>(yp) = make_float4(s[0], s[1], s[2], s[3]);
+    }
+  }
+}
+
+// out[t] (fp32 [T][d]) = sum_j w[t][j] * y[dst[t][j]] over assignments whose expert is in
+// [e_lo, e_hi) (the experts this rank computed); y is a LinOut over R rows
+__global__ __launch_bounds__(256) void moe_combine_kernel(LinOut y, const int* __restrict__ dst,
+                                                          const int* __restrict__ ids, int e_lo, int e_hi,
+                                                          const float* __restrict__ w, int k, int d,
+                                                          float* __restrict__ out, int accumulate) {
+  const int t = blockIdx.x;
+  for (int i = threadIdx.x; i < d / 8; i += 256) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < k; ++j) {
+      const int row = dst[t * k + j];
+      const int ex = ids[t * k + j];
+      if (row < 0 || ex < e_lo || ex >= e_hi) continue;
+      const float wj = w[t * k + j];
+      float v[8];
+      linout_load8(y, (long long)row * d + i * 8, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += wj * v[q];
+    }
+    float* o = out + (long long)t * d + i * 8;
+    if (accumulate) {
+      float prev[8];
+      load8f(o, prev);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += prev[q];
+    }
+    store8f(o, acc);
+  }
+}
+
+}  // namespace
+
+void launch_moe_route(LinOut logits, int ld, int T, int E, int k, int* ids, float* w, int* counts, hipStream_t s) {
+  if (T == 0) return;
+  moe_route_kernel<<<(T + 3) / 4, 256, 0, s>>>(logits, ld, T, E, k, ids, w, counts);
+}
+
+void launch_moe_align(const int* counts, int E, int* offsets, hipStream_t s) {
+  moe_align_kernel<<<1, 64, 0, s>>>(counts, E, offsets);
+}
+
+void launch_moe_scatter(const bf16* x, int T, int d, int k, const int* ids, const int* offsets, int* cursor,
+                        bf16* xs, int* dst, int* src_tok, hipStream_t s) {
+  if (T == 0) return;
+  moe_scatter_kernel<<<T * k, 256, 0, s>>>(x, d, k, ids, offsets, cursor, xs, dst, src_tok);
+}
+
+void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, float* y, int R, int E, int e0, int N,
+                           int K, int S, hipStream_t s) {
+  if (R == 0) return;
+  dim3 grid(N / 16, E, S);
+  grouped_skinny_kernel<<<grid, 256, 0, s>>>(xs, W, offsets, y, R, N, K, K / S, e0);
+}
+
+void launch_moe_combine(LinOut y, const int* dst, const int* ids, int e_lo, int e_hi, const float* w, int T, int k,
+                        int d, float* out, int accumulate, hipStream_t s) {
+  if (T == 0) return;
+  moe_combine_kernel<<<T, 256, 0, s>>>(y, dst, ids, e_lo, e_hi, w, k, d, out, accumulate);
+}

@@ -103,22 +103,23 @@ def build_kernels(verbose: bool = False, force: bool = False) -> str:
         if force or _newer(obj, [src] + headers):
             cmd = [HIPCC, "-c", src, "-o", obj, "-I", kdir] + HIP_FLAGS
             jobs.append(cmd)
-    bsrc = os.path.join(CSRC, "bindings", "torch_ops.cpp")
-    bobj = os.path.join(OBJ, "torch_ops.cpp.o")
-    objs.append(bobj)
-    if force or _newer(bobj, [bsrc] + headers):
-        cmd = [HIPCC, "-c", bsrc, "-o", bobj, "-I", kdir, "-O2", "-std=c++17", "-fPIC",
-               "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
-               "-DTORCH_EXTENSION_NAME=_C", "-Wno-unused-result", "-Wno-deprecated-declarations"]
-        for i in tinc:
-            cmd += ["-isystem", i]
-        jobs.append(cmd)
+    for bsrc in sorted(glob.glob(os.path.join(CSRC, "bindings", "*.cpp"))):
+        bobj = os.path.join(OBJ, "bind_" + os.path.basename(bsrc) + ".o")
+        objs.append(bobj)
+        if force or _newer(bobj, [bsrc] + headers):
+            cmd = [HIPCC, "-c", bsrc, "-o", bobj, "-I", kdir, "-O2", "-std=c++17", "-fPIC",
+                   "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+                   "-DTORCH_EXTENSION_NAME=_C", "-Wno-unused-result", "-Wno-deprecated-declarations"]
+            for i in tinc:
+                cmd += ["-isystem", i]
+            jobs.append(cmd)
     if jobs:
         with cf.ThreadPoolExecutor(_jobs()) as ex:
             list(ex.map(lambda c: _run(c, verbose), jobs))
     if force or jobs or _newer(KERNEL_SO, objs):
         cmd = [HIPCC, "-shared", "-o", KERNEL_SO] + objs + [
             f"--offload-arch={ARCH}", "-L", tlib, "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch",
+            "-lrccl",
             f"-Wl,-rpath,{tlib}",
         ]
         _run(cmd, verbose)

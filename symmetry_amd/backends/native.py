@@ -1,0 +1,79 @@
+"""NativeBackend: the in-process MI355X engine replaces the upstream server.
+
+Every generated token becomes exactly one OpenAI ``chat.completion.chunk``
+SSE event, written to the peer as one swarm message:
+the first event carries ``role: assistant``, the last carries
+``finish_reason`` and is followed by ``data: [DONE]``.  Per-request sampling
+fields (``max_tokens``, ``temperature``, ``top_p``, ``seed``, ``stop``) are
+honoured when the inference request carries them; the reference sends none
+(``src/provider.ts:312-316``), so the default is greedy with a
+``maxTokens`` cap.  Closing the stream (peer gone) aborts the sequence and
+frees its KV blocks (item 10).
+"""
+from __future__ import annotations
+
+import asyncio
+import itertools
+import time
+
+from ..engine.llm_engine import AsyncEngine, EngineConfig, LLMEngine
+from ..engine.sequence import SamplingParams
+from ..protocol import sse
+from .base import Backend, BackendError, Chunk
+
+_ids = itertools.count()
+
+
+class NativeBackend(Backend):
+    name = "native"
+
+    def __init__(self, config: dict, engine: LLMEngine | None = None, **engine_overrides):
+        self.cfg = config
+        self._engine = engine
+        self._overrides = engine_overrides
+        self.aengine: AsyncEngine | None = None
+        self.model_name = str(config.get("modelName", "llama3:8b"))
+
+    @property
+    def engine(self) -> LLMEngine:
+        assert self.aengine is not None, "backend not started"
+        return self.aengine.engine
+
+    async def start(self) -> None:
+        if self.aengine is not None:
+            return
+        if self._engine is None:
+            ecfg = EngineConfig.from_provider(self.cfg, **self._overrides)
+            self._engine = await asyncio.to_thread(LLMEngine, ecfg)
+            if self._engine.runner.use_graphs:
+                await asyncio.to_thread(self._engine.runner.capture_all)
+        self.aengine = AsyncEngine(self._engine)
+        self.aengine.start()
+
+    async def stop(self) -> None:
+        if self.aengine is not None:
+            await asyncio.to_thread(self.aengine.stop)
+            self.aengine = None
+
+    async def stream(self, request: dict):
+        await self.start()
+        messages = request.get("messages") or []
+        if not isinstance(messages, list):
+            raise BackendError("messages must be a list")
+        params = SamplingParams.from_request(request, default_max_tokens=self.engine.cfg.default_max_tokens)
+        rid = f"chatcmpl-{next(_ids)}-{int(time.time() * 1000)}"
+        created = int(time.time())
+        first = True
+        async for out in self.aengine.generate(rid, messages=messages, params=params):
+            if out.error:
+                raise BackendError(out.error)
+            if out.text or first or out.finished:
+                ev = sse.chunk_event(rid, self.model_name, out.text, role="assistant" if first else None,
+                                     finish_reason=out.finish_reason if out.finished else None, created=created)
+                first = False
+                yield Chunk(ev.encode("utf-8"), out.text)
+            if out.finished:
+                yield Chunk(sse.done_event().encode("utf-8"), "")
+
+    def stats(self) -> dict:
+        return self.engine.metrics.summary() if self.aengine is not None else {}

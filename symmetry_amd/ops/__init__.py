@@ -24,6 +24,9 @@ __all__ = [
     "skinny_gemm",
     "lm_head_sample",
     "swiglu",
+    "moe_route_permute",
+    "grouped_skinny",
+    "moe_combine",
     "linear",
     "choose_splits",
 ]
@@ -92,6 +95,24 @@ def swiglu(gu, out):
     if _gpu(out):
         return _native.ops().swiglu(gu, out)
     return reference.swiglu(gu, out)
+
+
+def moe_route_permute(logits, x, k, E, ids, w, counts, offsets, cursor, xs, dst):
+    if _gpu(x):
+        return _native.ops().moe_route_permute(logits, x, int(k), int(E), ids, w, counts, offsets, cursor, xs, dst)
+    return reference.moe_route_permute(logits, x, k, E, ids, w, counts, offsets, cursor, xs, dst)
+
+
+def grouped_skinny(xs, W, offsets, e0, y):
+    if _gpu(xs):
+        return _native.ops().grouped_skinny(xs, W, offsets, int(e0), y)
+    return reference.grouped_skinny(xs, W, offsets, e0, y)
+
+
+def moe_combine(y, dst, ids, e_lo, e_hi, w, k, out, accumulate=False):
+    if _gpu(out):
+        return _native.ops().moe_combine(y, dst, ids, int(e_lo), int(e_hi), w, int(k), out, bool(accumulate))
+    return reference.moe_combine(y, dst, ids, e_lo, e_hi, w, k, out, accumulate)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

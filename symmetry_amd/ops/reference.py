@@ -230,3 +230,53 @@ def rope_table(max_pos: int, head_dim: int, theta: float, scaling: dict | None =
     pos = torch.arange(max_pos, dtype=torch.float64)
     ang = pos[:, None] * inv[None, :]
     return torch.cat([ang.cos(), ang.sin()], dim=-1).float().to(device)
+
+
+# ----- MoE ---------------------------------------------------------------------------------------
+def moe_route_permute(logits, x, k: int, E: int, ids, w, counts, offsets, cursor, xs, dst) -> None:
+    """Top-k routing (softmax over the selected logits), expert segments in token order."""
+    T = x.shape[0]
+    lg = linout_sum(logits)[:, :E]
+    topv, topi = torch.topk(lg, k, dim=-1)  # ties -> lower index first (same as the kernel)
+    wt = torch.softmax(topv, dim=-1)
+    ids[: T * k].copy_(topi.reshape(-1).to(ids.dtype))
+    w[: T * k].copy_(wt.reshape(-1))
+    flat = topi.reshape(-1)
+    cnt = torch.bincount(flat, minlength=E)[:E]
+    counts[:E].copy_(cnt.to(counts.dtype))
+    off = torch.zeros(E + 1, dtype=torch.int64)
+    off[1:] = torch.cumsum(cnt, 0)
+    offsets[: E + 1].copy_(off.to(offsets.dtype))
+    cur = off[:-1].clone()
+    rows = torch.empty(T * k, dtype=torch.int64)
+    for a in range(T * k):
+        e = int(flat[a])
+        rows[a] = cur[e]
+        cur[e] += 1
+    dst[: T * k].copy_(rows.to(dst.dtype))
+    xs[rows] = x[torch.arange(T * k) // k].to(xs.dtype)
+
+
+def grouped_skinny(xs, W, offsets, e0: int, y) -> None:
+    S = y.shape[0]
+    y.zero_()
+    for e in range(W.shape[0]):
+        a, b = int(offsets[e0 + e]), int(offsets[e0 + e + 1])
+        if b > a:
+            y[0, a:b] = xs[a:b].float() @ W[e].float().t()
+
+
+def moe_combine(y, dst, ids, e_lo: int, e_hi: int, w, k: int, out, accumulate: bool) -> None:
+    T, d = out.shape
+    yy = linout_sum(y)
+    res = torch.zeros(T, d, dtype=torch.float32)
+    for t in range(T):
+        for j in range(k):
+            a = t * k + j
+            e = int(ids[a])
+            if e_lo <= e < e_hi and int(dst[a]) >= 0:
+                res[t] += float(w[a]) * yy[int(dst[a])]
+    if accumulate:
+        out.add_(res)
+    else:
+        out.copy_(res)

@@ -1,0 +1,105 @@
+"""Collective communication for tensor / expert parallelism (R1-R4).
+
+Two interchangeable implementations of one small interface
+(``all_reduce``, ``all_gather``, ``all_to_all_rows``, ``broadcast``):
+
+* :class:`RcclComm` -- our C++ RCCL communicator (``csrc/bindings/rccl_comm.cpp``),
+  collectives enqueued on torch's current HIP stream so they are captured
+  into the decode hipGraph; rides xGMI on an MI355X node.
+* :class:`TorchComm` -- ``torch.distributed`` on a process group (gloo on the
+  CPU for the multi-process tests; RCCL through c10d on GPUs).
+
+xGMI is point-to-point (7 links x ~153 GB/s per GPU), so the per-layer
+decode all-reduce (16 KiB x batch for 70B) is latency-bound: the model
+issues exactly two per layer and keeps them inside the captured graph.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    rank: int = 0
+    world: int = 1
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> None:
+        raise NotImplementedError
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+    def all_to_all_rows(self, send: torch.Tensor, send_counts: list[int], recv_counts: list[int]) -> torch.Tensor:
+        raise NotImplementedError
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
+        raise NotImplementedError
+
+
+_OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+
+
+class TorchComm(Comm):
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    def all_reduce(self, t, op="sum"):
+        dist.all_reduce(t, op=_OPS[op], group=self.group)
+
+    def all_gather(self, t):
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t.contiguous(), group=self.group)
+        return torch.cat(out, 0)
+
+    def all_to_all_rows(self, send, send_counts, recv_counts):
+        recv = send.new_empty((sum(recv_counts),) + tuple(send.shape[1:]))
+        dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=list(recv_counts),
+                               input_split_sizes=list(send_counts), group=self.group)
+        return recv
+
+    def broadcast(self, t, src=0):
+        dist.broadcast(t, src=src, group=self.group)
+
+
+class RcclComm(Comm):
+    """Graph-capturable RCCL communicator over the ranks of ``group`` (bootstrapped through it)."""
+
+    def __init__(self, group=None, bootstrap_group=None):
+        from ..ops import _native
+
+        self.ops = _native.ops()
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        boot = bootstrap_group if bootstrap_group is not None else group
+        if self.rank == 0:
+            uid = self.ops.rccl_unique_id()
+        else:
+            uid = torch.zeros(128, dtype=torch.uint8)
+        if uid.numel() != 128:
+            buf = torch.zeros(max(128, uid.numel()), dtype=torch.uint8)
+            buf[: uid.numel()] = uid
+            uid = buf
+        dist.broadcast(uid, src=dist.get_global_rank(boot, 0) if boot is not None else 0, group=boot)
+        self.handle = int(self.ops.rccl_init(uid[:128].contiguous(), self.world, self.rank))
+
+    def all_reduce(self, t, op="sum"):
+        self.ops.rccl_all_reduce(t, self.handle, op)
+
+    def all_gather(self, t):
+        out = t.new_empty((self.world,) + tuple(t.shape))
+        self.ops.rccl_all_gather(t.contiguous(), out, self.handle)
+        return out.reshape((self.world * t.shape[0],) + tuple(t.shape[1:])) if t.dim() else out
+
+    def all_to_all_rows(self, send, send_counts, recv_counts):
+        row = int(send[0].numel()) if send.shape[0] else int(torch.tensor(send.shape[1:]).prod())
+        recv = send.new_empty((sum(recv_counts),) + tuple(send.shape[1:]))
+        self.ops.rccl_all_to_all(send.contiguous(), recv, list(send_counts), list(recv_counts), row, self.handle)
+        return recv
+
+    def broadcast(self, t, src=0):
+        self.ops.rccl_broadcast(t, src, self.handle)
+
+    def destroy(self):
+        self.ops.rccl_destroy(self.handle)

@@ -1,0 +1,51 @@
+"""Process-group setup for multi-GPU providers (one process per GPU).
+
+``init_tp_engine`` is called in every rank of a ``torchrun`` launch:
+* the default group uses the ``nccl`` backend (= RCCL on ROCm) on GPUs, gloo on CPU;
+* a gloo group carries the per-step metadata broadcast from rank 0 (R4);
+* the TP communicator is :class:`RcclComm` on GPUs (graph-capturable), or
+  :class:`TorchComm` over gloo on CPU (tests).
+Rank 0 owns the scheduler and the provider node; ranks 1..N-1 call
+``engine.runner.worker_loop()``.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+from .comm import RcclComm, TorchComm
+
+
+def init_distributed(backend: str | None = None) -> tuple[int, int, int]:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
+        backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
+        kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
+        dist.init_process_group(backend, **kw)
+    return rank, world, local
+
+
+def make_comms(on_gpu: bool):
+    cpu_group = dist.new_group(backend="gloo")
+    comm = RcclComm(bootstrap_group=cpu_group) if on_gpu else TorchComm(cpu_group)
+    return comm, cpu_group
+
+
+def init_tp_engine(ecfg):
+    """Build this rank's tensor-parallel engine shard; returns (engine, rank)."""
+    from ..engine.llm_engine import LLMEngine
+
+    rank, world, local = init_distributed()
+    on_gpu = torch.cuda.is_available() and ecfg.device != "cpu"
+    comm, cpu_group = make_comms(on_gpu)
+    ecfg.tp_size, ecfg.tp_rank = world, rank
+    if on_gpu:
+        ecfg.device = f"cuda:{local}"
+    engine = LLMEngine(ecfg, tp_comm=comm, cpu_group=cpu_group)
+    return engine, rank

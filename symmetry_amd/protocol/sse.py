@@ -3,9 +3,10 @@ the REF-compatible parsers used by the proxy backend.
 
 REF parsing (``src/utils.ts:16-52``):
 
-* :func:`safe_parse_stream_response` parses only the text after the FIRST
-  ``data:`` of a chunk -- a chunk carrying two events fails and yields None
-  (the reference's quirk).
+* :func:`safe_parse_stream_response` parses only the text between the first
+  two ``data:`` markers of a chunk -- a chunk carrying several events
+  contributes only its first event to the completion (the reference's quirk;
+  SURVEY.md §2.7 item 8).
 * :func:`get_chat_data_from_provider` extracts the content delta per upstream
   flavour: ollama/openwebui ``choices[0].delta.content or ''``; llamacpp
   ``content`` (None when absent); everything else ``choices[0].delta.content``.
