@@ -306,13 +306,10 @@ void moe_route_permute(const Tensor& logits, const Tensor& x, int64_t k, int64_t
   TORCH_CHECK(xs.numel() >= T * k * d, "moe: xs too small");
   const at::OptionalDeviceGuard g(x.device());
   hipStream_t s = cur_stream(x);
-  hipMemsetAsync(counts.data_ptr(), 0, E * sizeof(int), s);
-  hipMemsetAsync(cursor.data_ptr(), 0, E * sizeof(int), s);
   const int64_t ld = logits.size(logits.dim() - 1);
   TORCH_CHECK(ld >= E, "moe: logits narrower than E");
-  launch_moe_route(linout(logits, T, ld, "logits"), (int)ld, (int)T, (int)E, (int)k, ptr<int>(ids), ptr<float>(w),
-                   ptr<int>(counts), s);
-  launch_moe_align(ptr<int>(counts), (int)E, ptr<int>(offsets), s);
+  launch_moe_route(linout(logits, T, ld, "logits"), (int)ld, (int)T, (int)E, (int)k, ptr<int>(ids), ptr<float>(w), s);
+  launch_moe_align(ptr<int>(ids), (int)(T * k), (int)E, ptr<int>(counts), ptr<int>(offsets), ptr<int>(cursor), s);
   launch_moe_scatter(ptr<bf16>(x), (int)T, (int)d, (int)k, ptr<int>(ids), ptr<int>(offsets), ptr<int>(cursor),
                      ptr<bf16>(xs), ptr<int>(dst), nullptr, s);
 }
@@ -353,7 +350,7 @@ void moe_combine(const Tensor& y, const Tensor& dst, const Tensor& ids, int64_t 
   TORCH_CHECK(dst.numel() >= T * k && w.numel() >= T * k && ids.numel() >= T * k, "moe_combine: dst/w too small");
   TORCH_CHECK(d % 8 == 0, "moe_combine: d % 8");
   const at::OptionalDeviceGuard g(out.device());
-  launch_moe_combine(linout(y, R, d, "y"), ptr<int>(dst), ptr<int>(ids), (int)e_lo, (int)e_hi, ptr<float>(w), (int)T,
+  launch_moe_combine(linout(y, R, d, "y"), (int)R, ptr<int>(dst), ptr<int>(ids), (int)e_lo, (int)e_hi, ptr<float>(w), (int)T,
                      (int)k, (int)d, ptr<float>(out), accumulate ? 1 : 0, cur_stream(out));
 }
 

@@ -40,11 +40,11 @@ void launch_argmax_reduce(const unsigned long long* tile_keys, int M, int ntiles
 void launch_swiglu(LinOut gu, bf16* out, int T, int F, hipStream_t s);
 
 // moe.hip
-void launch_moe_route(LinOut logits, int ld, int T, int E, int k, int* ids, float* w, int* counts, hipStream_t s);
-void launch_moe_align(const int* counts, int E, int* offsets, hipStream_t s);
+void launch_moe_route(LinOut logits, int ld, int T, int E, int k, int* ids, float* w, hipStream_t s);
+void launch_moe_align(const int* ids, int n, int E, int* counts, int* offsets, int* cursor, hipStream_t s);
 void launch_moe_scatter(const bf16* x, int T, int d, int k, const int* ids, const int* offsets, int* cursor,
                         bf16* xs, int* dst, int* src_tok, hipStream_t s);
 void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, float* y, int R, int E, int e0, int N,
                            int K, int S, hipStream_t s);
-void launch_moe_combine(LinOut y, const int* dst, const int* ids, int e_lo, int e_hi, const float* w, int T, int k,
+void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_lo, int e_hi, const float* w, int T, int k,
                         int d, float* out, int accumulate, hipStream_t s);

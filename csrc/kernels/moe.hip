@@ -1,8 +1,7 @@
 // K10-K12: Mixture-of-Experts routing, permutation, grouped GEMM and combine (Mixtral 8x7B).
 //
-//   moe_route     router logits (LinOut [T][E]) -> top-k ids + softmax-renormalised weights,
-//                 per-expert counts (atomics; counts zeroed by the op with hipMemsetAsync)
-//   moe_align     exclusive prefix sum of counts -> expert segment offsets [E+1]
+//   moe_route     router logits (LinOut [T][E]) -> top-k ids + softmax-renormalised weights
+//   moe_align     one workgroup: expert histogram + exclusive prefix sum -> segment offsets [E+1]
 //   moe_scatter   copy each (token, slot) row of x into its expert segment; dst[t][j] = row
 //   grouped_skinny  Y[rows of expert e] = Xs[rows of e] . W[e]^T on MFMA, one weight tile per
 //                 workgroup, reading the segment bounds from device memory (graph-capturable,
@@ -22,12 +21,12 @@ SYM_DEV f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 
 // One wave per token.  E <= 64 experts (lane e holds logit e), k <= 8.
 __global__ __launch_bounds__(256) void moe_route_kernel(LinOut logits, int ld, int T, int E, int k,
-                                                        int* __restrict__ ids, float* __restrict__ w,
-                                                        int* __restrict__ counts) {
+                                                        int* __restrict__ ids, float* __restrict__ w) {
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= T) return;
   float v = lane < E ? linout_load1(logits, (long long)t * ld + lane) : -INFINITY;
+  if (v != v) v = -INFINITY;  // a NaN logit never wins (and never selects a lane >= E)
   float sel[8];
   int seli[8];
   for (int j = 0; j < k; ++j) {
@@ -42,34 +41,53 @@ __global__ __launch_bounds__(256) void moe_route_kernel(LinOut logits, int ld, i
         mi = oi;
       }
     }
+    if (mi >= E) mi = j;  // degenerate rows (all -inf): fall back to experts 0..k-1
     sel[j] = m;
     seli[j] = mi;
     if (lane == mi) v = -INFINITY;
   }
   if (lane == 0) {
     float mx = sel[0], s = 0.f;
+    if (mx == -INFINITY) {
+      for (int j = 0; j < k; ++j) sel[j] = 0.f;
+      mx = 0.f;
+    }
     for (int j = 0; j < k; ++j) s += __expf(sel[j] - mx);
     for (int j = 0; j < k; ++j) {
       ids[t * k + j] = seli[j];
       w[t * k + j] = __expf(sel[j] - mx) / s;
-      atomicAdd(&counts[seli[j]], 1);
     }
   }
 }
 
-__global__ void moe_align_kernel(const int* __restrict__ counts, int E, int* __restrict__ offsets) {
+// Single workgroup: histogram of the routed expert ids (LDS atomics), exclusive prefix sum ->
+// offsets[E+1], counts[E], and the scatter cursor zeroed.  Doing the zeroing here (instead of a
+// hipMemsetAsync node) keeps the whole MoE step a plain kernel chain under hipGraph replay.
+__global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__ ids, int n, int E,
+                                                         int* __restrict__ counts, int* __restrict__ offsets,
+                                                         int* __restrict__ cursor) {
+  __shared__ int hist[64];
+  if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int e = ids[i];
+    if (e >= 0 && e < E) atomicAdd(&hist[e], 1);
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     int acc = 0;
     for (int e = 0; e < E; ++e) {
       offsets[e] = acc;
-      acc += counts[e];
+      counts[e] = hist[e];
+      cursor[e] = 0;
+      acc += hist[e];
     }
     offsets[E] = acc;
   }
 }
 
 // one 256-thread block per (token, slot); cursor[E] zeroed by the op
-__global__ __launch_bounds__(256) void moe_scatter_kernel(const bf16* __restrict__ x, int d, int k,
+__global__ __launch_bounds__(256) void moe_scatter_kernel(const bf16* __restrict__ x, int d, int k, int R,
                                                           const int* __restrict__ ids, const int* __restrict__ offsets,
                                                           int* __restrict__ cursor, bf16* __restrict__ xs,
                                                           int* __restrict__ dst, int* __restrict__ src_tok) {
@@ -83,6 +101,7 @@ __global__ __launch_bounds__(256) void moe_scatter_kernel(const bf16* __restrict
     if (src_tok) src_tok[row] = t;
   }
   __syncthreads();
+  if (row < 0 || row >= R) return;
   const uint4* s = reinterpret_cast<const uint4*>(x + (long long)t * d);
   uint4* o = reinterpret_cast<uint4*>(xs + (long long)row * d);
   for (int i = threadIdx.x; i < d / 8; i += 256) o[i] = s[i];
@@ -95,9 +114,9 @@ __global__ __launch_bounds__(256) void grouped_skinny_kernel(const bf16* __restr
                                                              const int* __restrict__ offsets, float* __restrict__ y,
                                                              int R, int N, int K, int kchunk, int e0) {
   const int tile = blockIdx.x, e = blockIdx.y, split = blockIdx.z;
-  const int r0 = offsets[e + e0], r1 = offsets[e + e0 + 1];
+  const int r0 = offsets[e + e0], r1 = min(offsets[e + e0 + 1], R);
   const int n_e = r1 - r0;
-  if (n_e <= 0) return;
+  if (n_e <= 0 || r0 < 0) return;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r16 = lane & 15, h = lane >> 4;
   const int n0 = tile * 16;
@@ -148,7 +167,7 @@ __global__ __launch_bounds__(256) void grouped_skinny_kernel(const bf16* __restr
 
 // out[t] (fp32 [T][d]) = sum_j w[t][j] * y[dst[t][j]] over assignments whose expert is in
 // [e_lo, e_hi) (the experts this rank computed); y is a LinOut over R rows
-__global__ __launch_bounds__(256) void moe_combine_kernel(LinOut y, const int* __restrict__ dst,
+__global__ __launch_bounds__(256) void moe_combine_kernel(LinOut y, int R, const int* __restrict__ dst,
                                                           const int* __restrict__ ids, int e_lo, int e_hi,
                                                           const float* __restrict__ w, int k, int d,
                                                           float* __restrict__ out, int accumulate) {
@@ -158,7 +177,7 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(LinOut y, const int* _
     for (int j = 0; j < k; ++j) {
       const int row = dst[t * k + j];
       const int ex = ids[t * k + j];
-      if (row < 0 || ex < e_lo || ex >= e_hi) continue;
+      if (row < 0 || row >= R || ex < e_lo || ex >= e_hi) continue;
       const float wj = w[t * k + j];
       float v[8];
       linout_load8(y, (long long)row * d + i * 8, v);
@@ -178,19 +197,19 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(LinOut y, const int* _
 
 }  // namespace
 
-void launch_moe_route(LinOut logits, int ld, int T, int E, int k, int* ids, float* w, int* counts, hipStream_t s) {
+void launch_moe_route(LinOut logits, int ld, int T, int E, int k, int* ids, float* w, hipStream_t s) {
   if (T == 0) return;
-  moe_route_kernel<<<(T + 3) / 4, 256, 0, s>>>(logits, ld, T, E, k, ids, w, counts);
+  moe_route_kernel<<<(T + 3) / 4, 256, 0, s>>>(logits, ld, T, E, k, ids, w);
 }
 
-void launch_moe_align(const int* counts, int E, int* offsets, hipStream_t s) {
-  moe_align_kernel<<<1, 64, 0, s>>>(counts, E, offsets);
+void launch_moe_align(const int* ids, int n, int E, int* counts, int* offsets, int* cursor, hipStream_t s) {
+  moe_align_kernel<<<1, 1024, 0, s>>>(ids, n, E, counts, offsets, cursor);
 }
 
 void launch_moe_scatter(const bf16* x, int T, int d, int k, const int* ids, const int* offsets, int* cursor,
                         bf16* xs, int* dst, int* src_tok, hipStream_t s) {
   if (T == 0) return;
-  moe_scatter_kernel<<<T * k, 256, 0, s>>>(x, d, k, ids, offsets, cursor, xs, dst, src_tok);
+  moe_scatter_kernel<<<T * k, 256, 0, s>>>(x, d, k, T * k, ids, offsets, cursor, xs, dst, src_tok);
 }
 
 void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, float* y, int R, int E, int e0, int N,
@@ -200,8 +219,8 @@ void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, fl
   grouped_skinny_kernel<<<grid, 256, 0, s>>>(xs, W, offsets, y, R, N, K, K / S, e0);
 }
 
-void launch_moe_combine(LinOut y, const int* dst, const int* ids, int e_lo, int e_hi, const float* w, int T, int k,
+void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_lo, int e_hi, const float* w, int T, int k,
                         int d, float* out, int accumulate, hipStream_t s) {
   if (T == 0) return;
-  moe_combine_kernel<<<T, 256, 0, s>>>(y, dst, ids, e_lo, e_hi, w, k, d, out, accumulate);
+  moe_combine_kernel<<<T, 256, 0, s>>>(y, R, dst, ids, e_lo, e_hi, w, k, d, out, accumulate);
 }

@@ -1,0 +1,155 @@
+"""Tensor / expert parallelism on CPU with the gloo backend, world_size 2 (SURVEY.md §4.2 'Distributed').
+
+* TP=2 engine (rank 0 schedules, rank 1 mirrors through the metadata broadcast) generates the
+  same tokens as TP=1 on the same weights;
+* EP=2 MoE in both modes (all-reduce combine, all-to-all dispatch) equals the local MoE block;
+* the Comm primitives (all_reduce / all_gather / all_to_all_rows) are exact.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+
+
+def _run(fn, world=2):
+    port = _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    procs = [ctx.Process(target=_entry, args=(fn, r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get() for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    errs = [r for r in results if isinstance(r, str)]
+    assert not errs, errs[0]
+    return sorted(results, key=lambda r: r[0])
+
+
+def _entry(fn, rank, world, port, q):
+    import traceback
+
+    try:
+        _init(rank, world, port)
+        q.put((rank, fn(rank, world)))
+    except Exception:
+        q.put(traceback.format_exc())
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------------------------
+def _comm_worker(rank, world):
+    from symmetry_amd.parallel.comm import TorchComm
+
+    c = TorchComm()
+    t = torch.full((4,), float(rank + 1))
+    c.all_reduce(t)
+    m = torch.tensor([rank * 10], dtype=torch.int64)
+    c.all_reduce(m, op="max")
+    g = c.all_gather(torch.tensor([[rank, rank]]))
+    send = torch.arange(6, dtype=torch.float32).view(3, 2) + 100 * rank
+    sc = [1, 2] if rank == 0 else [2, 1]
+    rc = [1, 2] if rank == 0 else [2, 1]
+    r = c.all_to_all_rows(send, sc, rc)
+    return t.tolist(), int(m), g.tolist(), r.tolist()
+
+
+def test_comm_primitives():
+    (_, a), (_, b) = _run(_comm_worker)
+    assert a[0] == [3.0] * 4 and a[1] == 10
+    assert a[2] == [[0, 0], [1, 1]]
+    # rank 0 sends row0 -> r0, rows1-2 -> r1; rank 1 sends rows 0-1 -> r0, row2 -> r1
+    assert a[3] == [[0.0, 1.0], [100.0, 101.0], [102.0, 103.0]]
+    assert b[3] == [[2.0, 3.0], [4.0, 5.0], [104.0, 105.0]]
+
+
+def _tp_worker(rank, world):
+    from symmetry_amd.engine.llm_engine import EngineConfig
+    from symmetry_amd.engine.sequence import SamplingParams
+    from symmetry_amd.parallel.launch import init_tp_engine
+
+    ecfg = EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=4, max_model_len=256, block_size=32,
+                        weight_init="full")
+    eng, r = init_tp_engine(ecfg)
+    if r != 0:
+        eng.runner.worker_loop()
+        return None
+    prompts = [list(range(5, 40)), list(range(100, 120)), list(range(7, 9))]
+    seqs = [eng.add_request(f"q{i}", p, SamplingParams(max_tokens=8, ignore_eos=True)) for i, p in enumerate(prompts)]
+    while eng.has_unfinished():
+        eng.step()
+    eng.shutdown()
+    return [s.output_ids for s in seqs]
+
+
+def test_tp2_matches_tp1():
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+    from symmetry_amd.models import reference_model as rm
+
+    res = _run(_tp_worker)
+    tp_out = res[0][1]
+    eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=4, max_model_len=256, block_size=32,
+                                 weight_init="full"))
+    prompts = [list(range(5, 40)), list(range(100, 120)), list(range(7, 9))]
+    for p, out in zip(prompts, tp_out):
+        # TP partial sums reduce in a different order: check against the fp32 oracle (near-ties may flip)
+        lg = rm.forward_logits(eng.weights, p + out[:-1])
+        for j, t in enumerate(out):
+            row = lg[len(p) - 1 + j]
+            assert float(row.max() - row[t]) <= 0.05
+
+
+def _ep_worker(rank, world):
+    from symmetry_amd.models.config import TINY_MIXTRAL
+    from symmetry_amd.models.moe import MoEBlock
+    from symmetry_amd.models.transformer import TransformerLM
+    from symmetry_amd.models.weights import ShardSpec, random_weights
+    from symmetry_amd.parallel.comm import TorchComm
+
+    comm = TorchComm()
+    outs = {}
+    g = torch.Generator().manual_seed(11)
+    x_all = torch.randn(2, 6, TINY_MIXTRAL.hidden_size, generator=g).bfloat16()  # per-rank token sets
+    full = random_weights(TINY_MIXTRAL, ShardSpec(), seed=3)
+    ref_model = TransformerLM(full, "cpu")
+    ep_w = random_weights(TINY_MIXTRAL, ShardSpec(0, 1, rank, world), seed=3)
+    ep_model = TransformerLM(ep_w, "cpu", ep_comm=comm)
+    # all-reduce mode: identical tokens on both ranks
+    ref = ref_model.moe.forward(0, x_all[0]).clone()
+    ep_model.moe.mode = "allreduce"
+    outs["allreduce"] = torch.allclose(ep_model.moe.forward(0, x_all[0]), ref, atol=1e-4)
+    # all-to-all mode: each rank routes its own tokens
+    ref_r = ref_model.moe.forward(1, x_all[rank]).clone()
+    ep_model.moe.mode = "a2a"
+    got = ep_model.moe.forward(1, x_all[rank])
+    outs["a2a"] = torch.allclose(got, ref_r, atol=1e-4)
+    outs["a2a_err"] = float((got - ref_r).abs().max())
+    return outs
+
+
+def test_expert_parallel_modes_match_local_moe():
+    res = _run(_ep_worker)
+    for _, r in res:
+        assert r["allreduce"], r
+        assert r["a2a"], r
