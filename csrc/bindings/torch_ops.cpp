@@ -113,7 +113,7 @@ void embed_rms_norm(const Tensor& ids, const Tensor& table, Tensor& residual, co
 }
 
 void rope_cache(const Tensor& qkv, const Tensor& positions, const Tensor& slots, const Tensor& cos_sin,
-                Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t Hq, int64_t Hkv) {
+                Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t Hq, int64_t Hkv, bool perm) {
   check_gpu(positions, "positions");
   check_gpu(slots, "slots");
   check_gpu(cos_sin, "cos_sin");
@@ -140,7 +140,7 @@ void rope_cache(const Tensor& qkv, const Tensor& positions, const Tensor& slots,
   const at::OptionalDeviceGuard g(positions.device());
   launch_rope_cache(linout(qkv, T, (Hq + 2 * Hkv) * D, "qkv"), ptr<int>(positions), ptr<int>(slots),
                     ptr<float>(cos_sin), ptr<bf16>(q_out), ptr<bf16>(k_cache), ptr<bf16>(v_cache), (int)T, (int)Hq,
-                    (int)Hkv, (int)D, (int)BS, cur_stream(positions));
+                    (int)Hkv, (int)D, (int)BS, cur_stream(positions), perm ? 1 : 0);
 }
 
 void check_cache(const Tensor& k_cache, const Tensor& v_cache) {
@@ -271,14 +271,15 @@ void lm_head_sample(const Tensor& x, const Tensor& w, const Tensor& temps, const
                        ptr<int>(out_ids), s);
 }
 
-void swiglu(const Tensor& gu, Tensor& out) {
+void swiglu(const Tensor& gu, Tensor& out, bool interleaved) {
   check_gpu(out, "out");
   check_dtype(out, at::kBFloat16, "out");
   TORCH_CHECK(out.dim() == 2, "out must be [T, F]");
   const int64_t T = out.size(0), F = out.size(1);
   TORCH_CHECK(F % 8 == 0, "swiglu: F must be a multiple of 8");
   const at::OptionalDeviceGuard g(out.device());
-  launch_swiglu(linout(gu, T, 2 * F, "gu"), ptr<bf16>(out), (int)T, (int)F, cur_stream(out));
+  TORCH_CHECK(!interleaved || F % 8 == 0, "swiglu: interleaved layout needs F % 8");
+  launch_swiglu(linout(gu, T, 2 * F, "gu"), ptr<bf16>(out), (int)T, (int)F, cur_stream(out), interleaved ? 1 : 0);
 }
 
 // ---- MoE -----------------------------------------------------------------------------------------
@@ -354,6 +355,202 @@ void moe_combine(const Tensor& y, const Tensor& dst, const Tensor& ids, int64_t 
                      (int)k, (int)d, ptr<float>(out), accumulate ? 1 : 0, cur_stream(out));
 }
 
+// ---- fused decode projections (decode_gemm.hip) ----------------------------------------------------
+struct DGShape {
+  int64_t M, N, K;
+};
+
+DGShape dg_check(const Tensor& x, const Tensor& W) {
+  check_gpu(x, "x");
+  check_gpu(W, "W");
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(W, at::kBFloat16, "W");
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && x.size(1) == W.size(1), "decode_gemm: x [M,K], W [N,K]");
+  const int64_t M = x.size(0), K = x.size(1), N = W.size(0);
+  TORCH_CHECK(M >= 1 && M <= 64, "decode_gemm: M must be in [1, 64]");
+  TORCH_CHECK(N % 16 == 0, "decode_gemm: N % 16");
+  TORCH_CHECK(K % 256 == 0, "decode_gemm: K must be a multiple of 256 (4 waves x 64)");
+  return {M, N, K};
+}
+
+void dg_norm_in(DecodeEpi& e, const c10::optional<Tensor>& ss_in, int64_t M, int64_t K, double eps) {
+  if (!ss_in.has_value()) return;
+  check_gpu(*ss_in, "ss_in");
+  check_dtype(*ss_in, at::kFloat, "ss_in");
+  TORCH_CHECK(ss_in->dim() == 2 && ss_in->size(0) >= M, "ss_in must be [>=M, tiles]");
+  e.ss_in = ptr<float>(*ss_in);
+  e.ss_tiles = (int)ss_in->size(1);
+  e.inv_d = 1.f / (float)K;
+  e.eps = (float)eps;
+}
+
+void dg_f32(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, Tensor& y) {
+  auto sh = dg_check(x, W);
+  check_gpu(y, "y");
+  check_dtype(y, at::kFloat, "y");
+  TORCH_CHECK(y.numel() == sh.M * sh.N, "dg_f32: y must be [M, N]");
+  DecodeEpi e;
+  dg_norm_in(e, ss_in, sh.M, sh.K, eps);
+  e.y = ptr<float>(y);
+  const at::OptionalDeviceGuard g(x.device());
+  launch_decode_gemm(DECODE_EPI_F32, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, e, cur_stream(x));
+}
+
+void dg_qkv(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, const Tensor& positions,
+            const Tensor& slots, const Tensor& cos_sin, Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t Hq,
+            int64_t Hkv) {
+  auto sh = dg_check(x, W);
+  for (auto* t : {&positions, &slots}) {
+    check_gpu(*t, "index tensor");
+    check_dtype(*t, at::kInt, "index tensor");
+  }
+  check_gpu(cos_sin, "cos_sin");
+  check_dtype(cos_sin, at::kFloat, "cos_sin");
+  check_cache(k_cache, v_cache);
+  check_gpu(q_out, "q_out");
+  check_dtype(q_out, at::kBFloat16, "q_out");
+  TORCH_CHECK(sh.N == (Hq + 2 * Hkv) * 128, "dg_qkv: N must be (Hq + 2 Hkv) * 128");
+  TORCH_CHECK(k_cache.size(1) == Hkv, "dg_qkv: cache head count");
+  TORCH_CHECK(positions.numel() >= sh.M && slots.numel() >= sh.M, "dg_qkv: positions/slots too short");
+  TORCH_CHECK(q_out.numel() >= sh.M * Hq * 128, "dg_qkv: q_out too small");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == 128, "dg_qkv: cos_sin [max_pos, 128]");
+  DecodeEpi e;
+  dg_norm_in(e, ss_in, sh.M, sh.K, eps);
+  e.positions = ptr<int>(positions);
+  e.slots = ptr<int>(slots);
+  e.cos_sin = ptr<float>(cos_sin);
+  e.q_out = ptr<bf16>(q_out);
+  e.k_cache = ptr<bf16>(k_cache);
+  e.v_cache = ptr<bf16>(v_cache);
+  e.Hq = (int)Hq;
+  e.Hkv = (int)Hkv;
+  e.BS = (int)k_cache.size(2);
+  const at::OptionalDeviceGuard g(x.device());
+  launch_decode_gemm(DECODE_EPI_QKV, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, e, cur_stream(x));
+}
+
+void dg_resid(const Tensor& x, const Tensor& W, Tensor& resid, const Tensor& w_next, Tensor& xw_out, Tensor& ss_out) {
+  auto sh = dg_check(x, W);
+  check_gpu(resid, "resid");
+  check_dtype(resid, at::kFloat, "resid");
+  check_gpu(w_next, "w_next");
+  check_dtype(w_next, at::kBFloat16, "w_next");
+  check_gpu(xw_out, "xw_out");
+  check_dtype(xw_out, at::kBFloat16, "xw_out");
+  check_gpu(ss_out, "ss_out");
+  check_dtype(ss_out, at::kFloat, "ss_out");
+  TORCH_CHECK(resid.numel() == sh.M * sh.N && xw_out.numel() == sh.M * sh.N && w_next.numel() == sh.N,
+              "dg_resid: shape mismatch");
+  TORCH_CHECK(ss_out.dim() == 2 && ss_out.size(0) >= sh.M && ss_out.size(1) == sh.N / 16, "dg_resid: ss_out [M, N/16]");
+  DecodeEpi e;
+  e.resid = ptr<float>(resid);
+  e.w_next = ptr<bf16>(w_next);
+  e.xw_out = ptr<bf16>(xw_out);
+  e.ss_out = ptr<float>(ss_out);
+  const at::OptionalDeviceGuard g(x.device());
+  launch_decode_gemm(DECODE_EPI_RESID, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, e, cur_stream(x));
+}
+
+void dg_swiglu(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, Tensor& act) {
+  auto sh = dg_check(x, W);
+  check_gpu(act, "act");
+  check_dtype(act, at::kBFloat16, "act");
+  TORCH_CHECK(act.numel() == sh.M * sh.N / 2, "dg_swiglu: act must be [M, N/2]");
+  DecodeEpi e;
+  dg_norm_in(e, ss_in, sh.M, sh.K, eps);
+  e.act = ptr<bf16>(act);
+  const at::OptionalDeviceGuard g(x.device());
+  launch_decode_gemm(DECODE_EPI_SWIGLU, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, e,
+                     cur_stream(x));
+}
+
+void dg_argmax(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, const Tensor& temps,
+               const Tensor& seeds, const Tensor& step, Tensor& tile_keys, Tensor& out_keys, Tensor& out_ids,
+               int64_t n_offset, const c10::optional<Tensor>& logits) {
+  auto sh = dg_check(x, W);
+  check_gpu(temps, "temps");
+  check_dtype(temps, at::kFloat, "temps");
+  check_gpu(seeds, "seeds");
+  check_dtype(seeds, at::kLong, "seeds");
+  check_gpu(step, "step");
+  check_dtype(step, at::kLong, "step");
+  check_gpu(tile_keys, "tile_keys");
+  check_dtype(tile_keys, at::kLong, "tile_keys");
+  check_gpu(out_keys, "out_keys");
+  check_dtype(out_keys, at::kLong, "out_keys");
+  check_gpu(out_ids, "out_ids");
+  check_dtype(out_ids, at::kInt, "out_ids");
+  TORCH_CHECK(temps.numel() >= sh.M && seeds.numel() >= sh.M, "dg_argmax: sampling params");
+  TORCH_CHECK(tile_keys.numel() >= sh.M * (sh.N / 16), "dg_argmax: tile_keys too small");
+  TORCH_CHECK(out_keys.numel() >= sh.M && out_ids.numel() >= sh.M, "dg_argmax: outputs too small");
+  DecodeEpi e;
+  dg_norm_in(e, ss_in, sh.M, sh.K, eps);
+  if (logits.has_value()) {
+    check_gpu(*logits, "logits");
+    check_dtype(*logits, at::kFloat, "logits");
+    TORCH_CHECK(logits->numel() == sh.M * sh.N, "dg_argmax: logits [M, N]");
+    e.y = ptr<float>(*logits);
+  }
+  e.temps = ptr<float>(temps);
+  e.seeds = reinterpret_cast<const unsigned long long*>(seeds.data_ptr());
+  e.step = reinterpret_cast<const long long*>(step.data_ptr());
+  e.keys = reinterpret_cast<unsigned long long*>(tile_keys.data_ptr());
+  e.n_offset = (int)n_offset;
+  const at::OptionalDeviceGuard g(x.device());
+  hipStream_t s = cur_stream(x);
+  launch_decode_gemm(DECODE_EPI_ARGMAX, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, e, s);
+  launch_argmax_reduce(e.keys, (int)sh.M, (int)(sh.N / 16), reinterpret_cast<unsigned long long*>(out_keys.data_ptr()),
+                       ptr<int>(out_ids), s);
+}
+
+void embed_prep(const Tensor& ids, const Tensor& table, Tensor& resid, const Tensor& w, Tensor& xw, Tensor& ss) {
+  check_gpu(ids, "ids");
+  check_dtype(ids, at::kInt, "ids");
+  check_gpu(table, "table");
+  check_dtype(table, at::kBFloat16, "table");
+  const int64_t T = ids.numel(), d = table.size(1);
+  check_gpu(resid, "resid");
+  check_dtype(resid, at::kFloat, "resid");
+  check_gpu(xw, "xw");
+  check_dtype(xw, at::kBFloat16, "xw");
+  check_gpu(ss, "ss");
+  check_dtype(ss, at::kFloat, "ss");
+  TORCH_CHECK(resid.numel() == T * d && xw.numel() == T * d && w.numel() == d && ss.numel() >= T && d % 8 == 0,
+              "embed_prep: shape mismatch");
+  const at::OptionalDeviceGuard g(ids.device());
+  launch_embed_prep(ptr<int>(ids), ptr<bf16>(table), ptr<float>(resid), ptr<bf16>(w), ptr<bf16>(xw), ptr<float>(ss),
+                    (int)T, (int)d, cur_stream(ids));
+}
+
+void add_prep(const Tensor& delta, Tensor& resid, const Tensor& w, Tensor& xw, Tensor& ss) {
+  check_gpu(resid, "resid");
+  check_dtype(resid, at::kFloat, "resid");
+  TORCH_CHECK(resid.dim() == 2, "add_prep: resid [T, d]");
+  const int64_t T = resid.size(0), d = resid.size(1);
+  check_gpu(xw, "xw");
+  check_dtype(xw, at::kBFloat16, "xw");
+  check_gpu(ss, "ss");
+  check_dtype(ss, at::kFloat, "ss");
+  TORCH_CHECK(xw.numel() == T * d && w.numel() == d && ss.numel() >= T && d % 8 == 0, "add_prep: shape mismatch");
+  const at::OptionalDeviceGuard g(resid.device());
+  launch_add_prep(linout(delta, T, d, "delta"), ptr<float>(resid), ptr<bf16>(w), ptr<bf16>(xw), ptr<float>(ss), (int)T,
+                  (int)d, cur_stream(resid));
+}
+
+void rownorm(const Tensor& xw, const Tensor& ss, double eps, Tensor& out) {
+  check_gpu(xw, "xw");
+  check_dtype(xw, at::kBFloat16, "xw");
+  check_gpu(ss, "ss");
+  check_dtype(ss, at::kFloat, "ss");
+  check_gpu(out, "out");
+  check_dtype(out, at::kBFloat16, "out");
+  TORCH_CHECK(xw.dim() == 2 && ss.dim() == 2 && ss.size(0) >= xw.size(0) && out.numel() == xw.numel(),
+              "rownorm: shape mismatch");
+  const at::OptionalDeviceGuard g(xw.device());
+  launch_rownorm(ptr<bf16>(xw), ptr<float>(ss), (int)ss.size(1), (float)eps, ptr<bf16>(out), (int)xw.size(0),
+                 (int)xw.size(1), cur_stream(xw));
+}
+
 }  // namespace
 
 TORCH_LIBRARY(symmetry_amd, m) {
@@ -363,7 +560,7 @@ TORCH_LIBRARY(symmetry_amd, m) {
         &embed_rms_norm);
   m.def(
       "rope_cache(Tensor qkv, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(a!) q_out, Tensor(b!) k_cache, "
-      "Tensor(c!) v_cache, int Hq, int Hkv) -> ()",
+      "Tensor(c!) v_cache, int Hq, int Hkv, bool perm=False) -> ()",
       &rope_cache);
   m.def(
       "attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, Tensor(a!) out, "
@@ -378,11 +575,27 @@ TORCH_LIBRARY(symmetry_amd, m) {
       "lm_head_sample(Tensor x, Tensor w, Tensor temps, Tensor seeds, Tensor step, Tensor(a!) tile_keys, "
       "Tensor(b!) out_keys, Tensor(c!) out_ids, int n_offset, Tensor(d!)? logits) -> ()",
       &lm_head_sample);
-  m.def("swiglu(Tensor gu, Tensor(a!) out) -> ()", &swiglu);
+  m.def("swiglu(Tensor gu, Tensor(a!) out, bool interleaved=False) -> ()", &swiglu);
   m.def(
       "moe_route_permute(Tensor logits, Tensor x, int k, int E, Tensor(a!) ids, Tensor(b!) w, Tensor(c!) counts, "
       "Tensor(d!) offsets, Tensor(e!) cursor, Tensor(f!) xs, Tensor(g!) dst) -> ()",
       &moe_route_permute);
+  m.def("dg_f32(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor(a!) y) -> ()", &dg_f32);
+  m.def(
+      "dg_qkv(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor positions, Tensor slots, Tensor cos_sin, "
+      "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv) -> ()",
+      &dg_qkv);
+  m.def("dg_resid(Tensor x, Tensor W, Tensor(a!) resid, Tensor w_next, Tensor(b!) xw_out, Tensor(c!) ss_out) -> ()",
+        &dg_resid);
+  m.def("dg_swiglu(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor(a!) act) -> ()", &dg_swiglu);
+  m.def(
+      "dg_argmax(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor temps, Tensor seeds, Tensor step, "
+      "Tensor(a!) tile_keys, Tensor(b!) out_keys, Tensor(c!) out_ids, int n_offset, Tensor(d!)? logits) -> ()",
+      &dg_argmax);
+  m.def("embed_prep(Tensor ids, Tensor table, Tensor(a!) resid, Tensor w, Tensor(b!) xw, Tensor(c!) ss) -> ()",
+        &embed_prep);
+  m.def("add_prep(Tensor delta, Tensor(a!) resid, Tensor w, Tensor(b!) xw, Tensor(c!) ss) -> ()", &add_prep);
+  m.def("rownorm(Tensor xw, Tensor ss, float eps, Tensor(a!) out) -> ()", &rownorm);
   m.def("grouped_skinny(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y) -> ()", &grouped_skinny);
   m.def(
       "moe_combine(Tensor y, Tensor dst, Tensor ids, int e_lo, int e_hi, Tensor w, int k, Tensor(a!) out, "

@@ -1,0 +1,323 @@
+// Fused decode projections: one weight-streaming MFMA GEMM per projection with the neighbouring
+// elementwise / normalisation work folded into its prologue and epilogue.
+//
+// Per Llama layer the decode step becomes
+//   QKV  (+ RMSNorm row scale, RoPE, paged K/V cache write, q out)
+//   attention (+ split-KV reduce)
+//   O    (+ residual add, next-norm prep)
+//   gate_up (+ RMSNorm row scale, SwiGLU)
+//   down (+ residual add, next-norm prep)
+// instead of ten launches (profiles/r1_baseline: the small kernels cost ~1 ms per step).
+//
+// Deferred RMSNorm.  RMSNorm(r) * w = rsqrt(mean(r^2) + eps) * (r * w): the producer of the
+// residual r (O / down epilogue, embed_prep, add_prep) stores xw = bf16(r * w) plus per-(row, tile)
+// partial sums of r^2 (plain stores, fixed summation order: bitwise reproducible); the consumer GEMM
+// sums the partials of its rows in the prologue and scales its accumulators by rsqrt(.) in the
+// epilogue.  No norm kernel, no cross-workgroup synchronisation.
+//
+// Layout contracts (applied once at load by symmetry_amd.models.layout):
+//   * q/k head rows are permuted so a 16-row tile j of a head holds dims 8j..8j+7 and
+//     64+8j..64+8j+7: both halves of each rotate-half pair land in one MFMA tile, lanes l and
+//     l^32 (one __shfl_xor) -- RoPE happens in registers;
+//   * gate_up rows are interleaved per tile: rows 0-7 gate f = 8j.., rows 8-15 up f = 8j.. .
+//
+// Decomposition: one workgroup per 16-row weight tile, NW waves splitting K (no split-K across
+// workgroups, so every epilogue sees final values), U 64-deep k blocks in flight per wave, partial
+// accumulators summed through LDS.  MFMA v_mfma_f32_16x16x32_bf16, natural k order (each load
+// instruction reads 16 rows x 64 contiguous bytes).
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+SYM_DEV f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+SYM_DEV uint32_t ordered_bits(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+SYM_DEV unsigned long long pack_key(float v, uint32_t idx) {
+  return ((unsigned long long)ordered_bits(v) << 32) | (unsigned long long)(0xFFFFFFFFu - idx);
+}
+
+SYM_DEV void store4bf(bf16* p, float a, float b, float c, float d) {
+  bf16x4 v;
+  v[0] = (bf16)a;
+  v[1] = (bf16)b;
+  v[2] = (bf16)c;
+  v[3] = (bf16)d;
+  *reinterpret_cast<bf16x4*>(p) = v;
+}
+
+template <int MT, int NW, int U, int EPI>
+__global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __restrict__ x,
+                                                              const bf16* __restrict__ W, int M, int N, int K,
+                                                              DecodeEpi e) {
+  const int tile = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, h = lane >> 4;
+  const int n0 = tile * 16;
+  const int wk = K / NW;
+  const int kbeg = wid * wk;
+  const int nblk = wk / 64;
+
+  const bf16* wrow = W + (long long)(n0 + r16) * K + kbeg + 8 * h;
+  const bf16* xrow[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) xrow[mt] = x + (long long)min(16 * mt + r16, M - 1) * K + kbeg + 8 * h;
+
+  __shared__ f32x4 red[NW][MT][64];
+  __shared__ float rn_s[64];
+
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int b = 0;
+  bool rn_done = false;
+  for (; b + U <= nblk; b += U) {
+    Pack8 wa[U][2], xa[U][MT][2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ko = (b + u) * 64;
+      wa[u][0].u = *reinterpret_cast<const uint4*>(wrow + ko);
+      wa[u][1].u = *reinterpret_cast<const uint4*>(wrow + ko + 32);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        xa[u][mt][0].u = *reinterpret_cast<const uint4*>(xrow[mt] + ko);
+        xa[u][mt][1].u = *reinterpret_cast<const uint4*>(xrow[mt] + ko + 32);
+      }
+    }
+    if (!rn_done) {
+      // RMSNorm row scales of the input rows, computed while the first weight batch is in flight.
+      rn_done = true;
+      if (e.ss_in) {
+        for (int m = wid; m < M; m += NW) {
+          float s = 0.f;
+          for (int i = lane; i < e.ss_tiles; i += 64) s += e.ss_in[(long long)m * e.ss_tiles + i];
+          s = wave_sum(s);
+          if (lane == 0) rn_s[m] = rsqrtf(s * e.inv_d + e.eps);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        acc[mt] = mfma16(wa[u][0].v, xa[u][mt][0].v, acc[mt]);
+        acc[mt] = mfma16(wa[u][1].v, xa[u][mt][1].v, acc[mt]);
+      }
+  }
+  for (; b < nblk; ++b) {
+    const int ko = b * 64;
+    Pack8 w0, w1;
+    w0.u = *reinterpret_cast<const uint4*>(wrow + ko);
+    w1.u = *reinterpret_cast<const uint4*>(wrow + ko + 32);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      Pack8 x0, x1;
+      x0.u = *reinterpret_cast<const uint4*>(xrow[mt] + ko);
+      x1.u = *reinterpret_cast<const uint4*>(xrow[mt] + ko + 32);
+      acc[mt] = mfma16(w0.v, x0.v, acc[mt]);
+      acc[mt] = mfma16(w1.v, x1.v, acc[mt]);
+    }
+  }
+  if (!rn_done && e.ss_in) {
+    for (int m = wid; m < M; m += NW) {
+      float s = 0.f;
+      for (int i = lane; i < e.ss_tiles; i += 64) s += e.ss_in[(long long)m * e.ss_tiles + i];
+      s = wave_sum(s);
+      if (lane == 0) rn_s[m] = rsqrtf(s * e.inv_d + e.eps);
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) red[wid][mt][lane] = acc[mt];
+  __syncthreads();
+  if (wid >= MT) return;
+  // wave `wid` finishes column tile mt = wid (parallel epilogue across waves)
+  const int mt = wid;
+  f32x4 v = red[0][mt][lane];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) v += red[w][mt][lane];
+  const int m = 16 * mt + r16;
+  const bool mok = m < M;
+  const float sc = (e.ss_in && mok) ? rn_s[m] : 1.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] *= sc;
+
+  if constexpr (EPI == DECODE_EPI_F32) {
+    if (mok) *reinterpret_cast<float4*>(e.y + (long long)m * N + n0 + 4 * h) = make_float4(v[0], v[1], v[2], v[3]);
+  } else if constexpr (EPI == DECODE_EPI_QKV) {
+    const int D = 128;
+    const int head = n0 / D, jj = (n0 % D) / 16;
+    float p[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p[i] = __shfl_xor(v[i], 32, 64);
+    if (!mok) return;
+    const int pos = e.positions[m];
+    const int slot = e.slots[m];
+    const float* cs = e.cos_sin + (long long)pos * D;
+    if (head < e.Hq + e.Hkv) {
+      const bool lo = h < 2;
+      const int dh = 8 * jj + 4 * (h & 1);  // dim within the half (0..63)
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float c = cs[dh + i], s = cs[64 + dh + i];
+        o[i] = lo ? (v[i] * c - p[i] * s) : (v[i] * c + p[i] * s);
+      }
+      const int d = (lo ? 0 : 64) + dh;
+      if (head < e.Hq) {
+        store4bf(e.q_out + ((long long)m * e.Hq + head) * D + d, o[0], o[1], o[2], o[3]);
+      } else if (slot >= 0) {
+        const long long blk = slot / e.BS, off = slot % e.BS;
+        store4bf(e.k_cache + ((blk * e.Hkv + (head - e.Hq)) * e.BS + off) * D + d, o[0], o[1], o[2], o[3]);
+      }
+    } else if (slot >= 0) {
+      const int vh = head - e.Hq - e.Hkv;
+      const int d = 16 * jj + 4 * h;
+      const long long blk = slot / e.BS, off = slot % e.BS;
+      bf16* vp = e.v_cache + ((blk * e.Hkv + vh) * D + d) * e.BS + off;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) vp[(long long)i * e.BS] = (bf16)v[i];
+    }
+  } else if constexpr (EPI == DECODE_EPI_RESID) {
+    float sq = 0.f;
+    if (mok) {
+      float* rp = e.resid + (long long)m * N + n0 + 4 * h;
+      const float4 r = *reinterpret_cast<const float4*>(rp);
+      const float rr[4] = {r.x + v[0], r.y + v[1], r.z + v[2], r.w + v[3]};
+      *reinterpret_cast<float4*>(rp) = make_float4(rr[0], rr[1], rr[2], rr[3]);
+      float wn[4];
+      Pack8 wp;  // 4 bf16 of the next norm weight
+      const uint2 raw = *reinterpret_cast<const uint2*>(e.w_next + n0 + 4 * h);
+      wp.u = make_uint4(raw.x, raw.y, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        wn[i] = (float)wp.h[i];
+        sq += rr[i] * rr[i];
+      }
+      store4bf(e.xw_out + (long long)m * N + n0 + 4 * h, rr[0] * wn[0], rr[1] * wn[1], rr[2] * wn[2], rr[3] * wn[3]);
+    }
+    sq += __shfl_xor(sq, 16, 64);
+    sq += __shfl_xor(sq, 32, 64);
+    if (mok && h == 0) e.ss_out[(long long)m * gridDim.x + tile] = sq;
+  } else if constexpr (EPI == DECODE_EPI_SWIGLU) {
+    float u[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) u[i] = __shfl_xor(v[i], 32, 64);
+    if (mok && h < 2) {
+      const int f = 8 * tile + 4 * h;
+      store4bf(e.act + (long long)m * (N / 2) + f, silu(v[0]) * u[0], silu(v[1]) * u[1], silu(v[2]) * u[2],
+               silu(v[3]) * u[3]);
+    }
+  } else {  // DECODE_EPI_ARGMAX
+    const int mm = mok ? m : 0;
+    const float t = e.temps ? e.temps[mm] : 0.f;
+    const long long step = e.step ? *e.step : 0;
+    unsigned long long best = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int nl = n0 + 4 * h + i;
+      const int gidx = e.n_offset + nl;
+      float val = v[i];
+      if (e.y && mok) e.y[(long long)m * N + nl] = val;
+      if (t > 0.f) {
+        const unsigned long long seed = e.seeds ? e.seeds[mm] : 0ull;
+        const float uu = uniform01(seed ^ ((unsigned long long)step << 20), (unsigned long long)gidx);
+        val = val / t - __logf(-__logf(uu));
+      }
+      const unsigned long long kk = pack_key(val, (uint32_t)gidx);
+      best = kk > best ? kk : best;
+    }
+    unsigned long long o16 = __shfl_xor(best, 16, 64);
+    best = o16 > best ? o16 : best;
+    unsigned long long o32 = __shfl_xor(best, 32, 64);
+    best = o32 > best ? o32 : best;
+    if (h == 0 && mok) e.keys[(long long)m * gridDim.x + tile] = best;
+  }
+}
+
+// ---- residual producers without a GEMM ----------------------------------------------------------
+// embed_prep: resid = table[ids]; xw = bf16(resid * w); ss[m][0] = sum(resid^2)
+// add_prep:   resid += delta (LinOut); xw = bf16(resid * w); ss[m][0] = sum(resid^2)
+template <int MODE>
+__global__ __launch_bounds__(256) void prep_kernel(LinOut delta, const int* __restrict__ ids,
+                                                   const bf16* __restrict__ table, float* __restrict__ resid,
+                                                   const bf16* __restrict__ w, bf16* __restrict__ xw,
+                                                   float* __restrict__ ss, int d) {
+  __shared__ float scratch[4];
+  const int row = blockIdx.x;
+  const long long rb = (long long)row * d;
+  float acc = 0.f;
+  for (int vi = threadIdx.x; vi < d / 8; vi += 256) {
+    float r[8], g[8];
+    if constexpr (MODE == 0) {
+      load8(table + (long long)ids[row] * d + vi * 8, r);
+    } else {
+      float dd[8];
+      load8f(resid + rb + vi * 8, r);
+      linout_load8(delta, rb + vi * 8, dd);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] += dd[i];
+    }
+    store8f(resid + rb + vi * 8, r);
+    load8(w + vi * 8, g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      acc += r[i] * r[i];
+      g[i] *= r[i];
+    }
+    store8(xw + rb + vi * 8, g);
+  }
+  acc = block_sum<256>(acc, scratch);
+  if (threadIdx.x == 0) ss[row] = acc;
+}
+
+template <int MT, int EPI>
+void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, hipStream_t s) {
+  constexpr int U = MT == 1 ? 4 : (MT == 2 ? 2 : 1);
+  // 8 waves split K when K % 512 == 0, else 4 (e.g. Llama-3-8B down_proj under TP=8: K = 1792)
+  if (K % 512 == 0)
+    decode_gemm_kernel<MT, 8, U, EPI><<<N / 16, 8 * 64, 0, s>>>(x, W, M, N, K, e);
+  else
+    decode_gemm_kernel<MT, 4, U, EPI><<<N / 16, 4 * 64, 0, s>>>(x, W, M, N, K, e);
+}
+
+template <int EPI>
+void launch_epi(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, hipStream_t s) {
+  switch ((M + 15) / 16) {
+    case 1: launch_mt<1, EPI>(x, W, M, N, K, e, s); break;
+    case 2: launch_mt<2, EPI>(x, W, M, N, K, e, s); break;
+    case 3: launch_mt<3, EPI>(x, W, M, N, K, e, s); break;
+    default: launch_mt<4, EPI>(x, W, M, N, K, e, s); break;
+  }
+}
+
+}  // namespace
+
+void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e,
+                        hipStream_t s) {
+  switch (epi) {
+    case DECODE_EPI_F32: launch_epi<DECODE_EPI_F32>(x, W, M, N, K, e, s); break;
+    case DECODE_EPI_QKV: launch_epi<DECODE_EPI_QKV>(x, W, M, N, K, e, s); break;
+    case DECODE_EPI_RESID: launch_epi<DECODE_EPI_RESID>(x, W, M, N, K, e, s); break;
+    case DECODE_EPI_SWIGLU: launch_epi<DECODE_EPI_SWIGLU>(x, W, M, N, K, e, s); break;
+    default: launch_epi<DECODE_EPI_ARGMAX>(x, W, M, N, K, e, s); break;
+  }
+}
+
+void launch_embed_prep(const int* ids, const bf16* table, float* resid, const bf16* w, bf16* xw, float* ss, int T,
+                       int d, hipStream_t s) {
+  if (T == 0) return;
+  LinOut none{nullptr, 0, 1, 0};
+  prep_kernel<0><<<T, 256, 0, s>>>(none, ids, table, resid, w, xw, ss, d);
+}
+
+void launch_add_prep(LinOut delta, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d, hipStream_t s) {
+  if (T == 0) return;
+  prep_kernel<1><<<T, 256, 0, s>>>(delta, nullptr, nullptr, resid, w, xw, ss, d);
+}

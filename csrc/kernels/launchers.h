@@ -8,6 +8,43 @@
 #include <algorithm>
 #include "common.h"
 
+// decode_gemm.hip -- fused decode projections (see the file header)
+enum { DECODE_EPI_F32 = 0, DECODE_EPI_QKV = 1, DECODE_EPI_RESID = 2, DECODE_EPI_SWIGLU = 3, DECODE_EPI_ARGMAX = 4 };
+struct DecodeEpi {
+  // prologue: RMSNorm row scale rsqrt(sum(ss_in[m][0..ss_tiles)) * inv_d + eps); ss_in == nullptr -> 1
+  const float* ss_in = nullptr;
+  int ss_tiles = 0;
+  float inv_d = 0.f, eps = 0.f;
+  float* y = nullptr;  // F32 output / ARGMAX optional logits
+  // QKV: RoPE + paged cache write + q out
+  const int* positions = nullptr;
+  const int* slots = nullptr;
+  const float* cos_sin = nullptr;
+  bf16* q_out = nullptr;
+  bf16* k_cache = nullptr;
+  bf16* v_cache = nullptr;
+  int Hq = 0, Hkv = 0, BS = 0;
+  // RESID: resid += y; xw_out = bf16(resid * w_next); ss_out[m][tile] = sum(resid^2)
+  float* resid = nullptr;
+  const bf16* w_next = nullptr;
+  bf16* xw_out = nullptr;
+  float* ss_out = nullptr;
+  // SWIGLU
+  bf16* act = nullptr;
+  // ARGMAX (fused sampling)
+  const float* temps = nullptr;
+  const unsigned long long* seeds = nullptr;
+  const long long* step = nullptr;
+  unsigned long long* keys = nullptr;
+  int n_offset = 0;
+};
+void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e,
+                        hipStream_t s);
+void launch_embed_prep(const int* ids, const bf16* table, float* resid, const bf16* w, bf16* xw, float* ss, int T,
+                       int d, hipStream_t s);
+void launch_add_prep(LinOut delta, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d, hipStream_t s);
+void launch_rownorm(const bf16* xw, const float* ss, int ss_tiles, float eps, bf16* out, int T, int d, hipStream_t s);
+
 // norm.hip
 void launch_rms_norm(LinOut x, const bf16* w, bf16* out, int T, int d, float eps, hipStream_t s);
 void launch_add_rms_norm(LinOut delta, float* residual, const bf16* w, bf16* out, int T, int d, float eps,
@@ -17,7 +54,8 @@ void launch_embed_rms_norm(const int* ids, const bf16* table, float* residual, c
 
 // rope_cache.hip
 void launch_rope_cache(LinOut qkv, const int* positions, const int* slots, const float* cos_sin, bf16* q_out,
-                       bf16* k_cache, bf16* v_cache, int T, int Hq, int Hkv, int D, int BS, hipStream_t s);
+                       bf16* k_cache, bf16* v_cache, int T, int Hq, int Hkv, int D, int BS, hipStream_t s,
+                       int perm = 0);
 
 // attention.hip
 void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,
@@ -37,7 +75,7 @@ void launch_argmax_reduce(const unsigned long long* tile_keys, int M, int ntiles
                           int* out_ids, hipStream_t s);
 
 // activation.hip
-void launch_swiglu(LinOut gu, bf16* out, int T, int F, hipStream_t s);
+void launch_swiglu(LinOut gu, bf16* out, int T, int F, hipStream_t s, int interleaved = 0);
 
 // moe.hip
 void launch_moe_route(LinOut logits, int ld, int T, int E, int k, int* ids, float* w, hipStream_t s);

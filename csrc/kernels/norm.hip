@@ -96,3 +96,29 @@ void launch_embed_rms_norm(const int* ids, const bf16* table, float* residual, c
   LinOut none{nullptr, 0, 1, 0};
   launch_mode<2>(none, ids, table, residual, w, out, T, d, eps, s);
 }
+
+// rownorm: out = xw * rsqrt(sum(ss[m][:]) / d + eps)  -- materialises a normalised activation from the
+// deferred-RMSNorm residual state (xw, ss) for consumers that are not fused decode GEMMs (MoE).
+namespace {
+__global__ __launch_bounds__(256) void rownorm_kernel(const bf16* __restrict__ xw, const float* __restrict__ ss,
+                                                      int ss_tiles, float eps, bf16* __restrict__ out, int d) {
+  __shared__ float scratch[4];
+  const int row = blockIdx.x;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < ss_tiles; i += 256) s += ss[(long long)row * ss_tiles + i];
+  s = block_sum<256>(s, scratch);
+  const float r = rsqrtf(s / (float)d + eps);
+  for (int vi = threadIdx.x; vi < d / 8; vi += 256) {
+    float v[8];
+    load8(xw + (long long)row * d + vi * 8, v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] *= r;
+    store8(out + (long long)row * d + vi * 8, v);
+  }
+}
+}  // namespace
+
+void launch_rownorm(const bf16* xw, const float* ss, int ss_tiles, float eps, bf16* out, int T, int d, hipStream_t s) {
+  if (T == 0) return;
+  rownorm_kernel<<<T, 256, 0, s>>>(xw, ss, ss_tiles, eps, out, d);
+}

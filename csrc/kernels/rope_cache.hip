@@ -22,7 +22,7 @@ __global__ __launch_bounds__(NT) void rope_cache_kernel(LinOut qkv, const int* _
                                                         const float* __restrict__ cos_sin,
                                                         bf16* __restrict__ q_out, bf16* __restrict__ k_cache,
                                                         bf16* __restrict__ v_cache, int Hq, int Hkv, int D,
-                                                        int BS) {
+                                                        int BS, int perm) {
   const int t = blockIdx.x;
   const int N = (Hq + 2 * Hkv) * D;
   const long long row = (long long)t * N;
@@ -38,8 +38,11 @@ __global__ __launch_bounds__(NT) void rope_cache_kernel(LinOut qkv, const int* _
       const int h = it / gpr;          // 0..Hq+Hkv-1 (q heads then k heads)
       const int i0 = (it % gpr) * 8;   // pair index within the half
       float x1[8], x2[8], c[8], s[8];
-      linout_load8(qkv, row + (long long)h * D + i0, x1);
-      linout_load8(qkv, row + (long long)h * D + half + i0, x2);
+      // perm: rows of a q/k head are stored tile-interleaved (decode layout, decode_gemm.hip):
+      // dims i0..i0+7 at 2*i0, dims half+i0.. at 2*i0 + 8
+      const int p1 = perm ? 2 * i0 : i0, p2 = perm ? 2 * i0 + 8 : half + i0;
+      linout_load8(qkv, row + (long long)h * D + p1, x1);
+      linout_load8(qkv, row + (long long)h * D + p2, x2);
       load8f(cs + i0, c);
       load8f(cs + half + i0, s);
       float o1[8], o2[8];
@@ -76,7 +79,7 @@ __global__ __launch_bounds__(NT) void rope_cache_kernel(LinOut qkv, const int* _
 }  // namespace
 
 void launch_rope_cache(LinOut qkv, const int* positions, const int* slots, const float* cos_sin, bf16* q_out,
-                       bf16* k_cache, bf16* v_cache, int T, int Hq, int Hkv, int D, int BS, hipStream_t s) {
+                       bf16* k_cache, bf16* v_cache, int T, int Hq, int Hkv, int D, int BS, hipStream_t s, int perm) {
   if (T == 0) return;
-  rope_cache_kernel<<<T, NT, 0, s>>>(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D, BS);
+  rope_cache_kernel<<<T, NT, 0, s>>>(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D, BS, perm);
 }

@@ -36,6 +36,10 @@ def _moe(cfg, w, i, h):
 @torch.no_grad()
 def forward_logits(w: ModelWeights, ids: list[int]) -> torch.Tensor:
     """Logits [len(ids), V] for a single sequence (tp=1 weights)."""
+    from .layout import natural_tensors
+
+    if getattr(w, "layout", "natural") != "natural":
+        w = ModelWeights(w.cfg, w.shard, natural_tensors(w))
     cfg = w.cfg
     T = len(ids)
     D, Hq, Hkv = cfg.head_dim, cfg.num_heads, cfg.num_kv_heads

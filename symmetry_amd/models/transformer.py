@@ -7,12 +7,21 @@ Per layer (SURVEY.md §3.6)::
     -> O proj -> [R1 all-reduce] -> K1 add+RMSNorm -> gate_up proj -> K7 SwiGLU
     -> down proj -> [R1 all-reduce]            (Mixtral: K10-K12 MoE block, R3 all-to-all)
 
-Projections with <= 64 rows (every decode step, short prefills) run the
-skinny MFMA GEMM and hand fp32 split-K slabs straight to the next fused
-kernel; larger ones run the library GEMM (hipBLASLt through torch.matmul).
-The final norm + lm_head + sampling use the fused lm_head_sample kernel on the
-last row of each sequence only.  All intermediates live in a preallocated
-:class:`Workspace`, so the decode forward is hipGraph-capturable.
+Two paths over the same weights (stored in the decode layout, models/layout.py):
+
+* fused (<= 64 rows: every decode step, short prefills) -- five launches per dense layer::
+
+      dg_qkv (norm scale + RoPE + KV write) -> attention -> dg_resid (O, residual add, ln2 prep)
+      -> dg_swiglu (norm scale + SwiGLU) -> dg_resid (down, residual add, next-ln1 prep)
+
+  with RMSNorm deferred into the consuming GEMM (csrc/kernels/decode_gemm.hip) and the final
+  norm + lm_head + sampling in dg_argmax.  Under TP the row-parallel projections write fp32,
+  are all-reduced, and add_prep does the residual + norm prep.
+* general (long prefills): library GEMM (hipBLASLt through torch.matmul) + fused elementwise
+  kernels, with the layout flags on rope_cache / swiglu.
+
+All intermediates live in a preallocated :class:`Workspace`, so the decode forward is
+hipGraph-capturable.
 """
 from __future__ import annotations
 
@@ -24,6 +33,7 @@ import torch
 from .. import ops
 from ..ops import reference
 from .config import ModelConfig
+from .layout import apply_decode_layout
 from .weights import ModelWeights
 
 SKINNY_MAX_M = 64
@@ -125,6 +135,17 @@ class TransformerLM:
             from .moe import MoEBlock
 
             self.moe = MoEBlock(self, ep_comm)
+        apply_decode_layout(weights)
+        self.fused = self._fused_supported()
+
+    def _fused_supported(self) -> bool:
+        """Shape contract of the fused decode GEMMs: D == 128, every K % 256 == 0, every N % 16 == 0."""
+        cfg = self.cfg
+        ks = [cfg.hidden_size, self.hq * self.D]
+        if not cfg.is_moe:
+            ks.append(self.w.layer(0, "w_gu").shape[0] // 2)
+        return (self.D == 128 and all(k % 256 == 0 for k in ks) and cfg.hidden_size % 16 == 0
+                and self.vocab_shard % 16 == 0)
 
     # ------------------------------------------------------------------------------------------
     def _buf(self, name, shape, dtype):
@@ -146,9 +167,80 @@ class TransformerLM:
         return y
 
     # ------------------------------------------------------------------------------------------
+    def _attention(self, b: ForwardBatch, kv: KVCache, i: int, q: torch.Tensor, attn: torch.Tensor) -> None:
+        if b.kind == "decode":
+            max_parts = (b.block_tables.shape[1] * kv.block_size + 255) // 256
+            tmp_o = self._buf("tmp_o", (b.num_seqs, self.hq, max_parts, self.D), torch.float32)
+            tmp_ml = self._buf("tmp_ml", (b.num_seqs, self.hq, max_parts, 2), torch.float32)
+            ops.attn_decode(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, attn, tmp_o, tmp_ml, self.scale)
+        else:
+            ops.attn_prefill(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, b.cu_q, b.tiles, attn, self.scale)
+
     @torch.no_grad()
     def forward(self, b: ForwardBatch, kv: KVCache) -> torch.Tensor:
         """Run one step; returns sampled token ids [num_seqs] int32 (device)."""
+        if self.fused and b.num_tokens <= SKINNY_MAX_M:
+            return self._forward_fused(b, kv)
+        return self._forward_general(b, kv)
+
+    # ------------------------------------------------------------------------------------------
+    def _tp_active(self) -> bool:
+        return self.tp is not None and self.tp_size > 1
+
+    def _resid_proj(self, name, x, W, resid, w_next, xw, ss_t, ss_1) -> torch.Tensor:
+        """Row-parallel projection + residual add + next-norm prep; returns the ss partials to use."""
+        if self._tp_active():
+            y = self._buf(name + ".f32", (x.shape[0], W.shape[0]), torch.float32)
+            ops.dg_f32(x, W, None, 0.0, y)
+            self.tp.all_reduce(y)
+            ops.add_prep(y, resid, w_next, xw, ss_1)
+            return ss_1
+        ops.dg_resid(x, W, resid, w_next, xw, ss_t)
+        return ss_t
+
+    def _forward_fused(self, b: ForwardBatch, kv: KVCache) -> torch.Tensor:
+        cfg, w = self.cfg, self.w
+        T, d, eps = b.num_tokens, cfg.hidden_size, cfg.rms_eps
+        resid = self._buf("resid", (T, d), torch.float32)
+        xw = self._buf("xw", (T, d), torch.bfloat16)
+        ss_t = self._buf("ss_t", (T, d // 16), torch.float32)
+        ss_1 = self._buf("ss_1", (T, 1), torch.float32)
+        q = self._buf("q", (T, self.hq, self.D), torch.bfloat16)
+        attn = self._buf("attn", (T, self.hq, self.D), torch.bfloat16)
+        ops.embed_prep(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), xw, ss_1)
+        ss = ss_1
+        for i in range(cfg.num_layers):
+            ops.dg_qkv(xw, w.layer(i, "wqkv"), ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i],
+                       kv.v[i], self.hq, self.hkv)
+            self._attention(b, kv, i, q, attn)
+            ss = self._resid_proj("o", attn.view(T, self.hq * self.D), w.layer(i, "wo"), resid, w.layer(i, "ln2"),
+                                  xw, ss_t, ss_1)
+            nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
+            if cfg.is_moe:
+                xn = self._buf("x", (T, d), torch.bfloat16)
+                ops.rownorm(xw, ss, eps, xn)
+                ops.add_prep(self.moe.forward(i, xn), resid, nxt, xw, ss_1)
+                ss = ss_1
+            else:
+                w_gu = w.layer(i, "w_gu")
+                act = self._buf("act", (T, w_gu.shape[0] // 2), torch.bfloat16)
+                ops.dg_swiglu(xw, w_gu, ss, eps, act)
+                ss = self._resid_proj("down", act, w.layer(i, "w_down"), resid, nxt, xw, ss_t, ss_1)
+        n = b.num_seqs
+        if b.kind == "decode":
+            xl, sl = xw, ss
+        else:
+            xl, sl = xw.index_select(0, b.last_idx), ss.index_select(0, b.last_idx)
+        ids = self._buf("ids", (n,), torch.int32)
+        keys = self._buf("keys", (n,), torch.int64)
+        tk = self._buf("tile_keys", (n * (self.vocab_shard // 16),), torch.int64)
+        logits = self._buf("logits", (n, self.vocab_shard), torch.float32) if b.need_logits else None
+        ops.dg_argmax(xl, w["lm_head"], sl, eps, b.temps, b.seeds, b.step, tk, keys, ids,
+                      self.tp_rank * self.vocab_shard, logits)
+        return self._combine_tp(ids, keys, logits)
+
+    # ------------------------------------------------------------------------------------------
+    def _forward_general(self, b: ForwardBatch, kv: KVCache) -> torch.Tensor:
         cfg, w = self.cfg, self.w
         T = b.num_tokens
         d = cfg.hidden_size
@@ -160,14 +252,9 @@ class TransformerLM:
         ops.embed_rms_norm(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), eps, x)
         for i in range(cfg.num_layers):
             qkv = self._linear("qkv", x, w.layer(i, "wqkv"))
-            ops.rope_cache(qkv, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq, self.hkv)
-            if b.kind == "decode":
-                max_parts = (b.block_tables.shape[1] * kv.block_size + 255) // 256
-                tmp_o = self._buf("tmp_o", (b.num_seqs, self.hq, max_parts, self.D), torch.float32)
-                tmp_ml = self._buf("tmp_ml", (b.num_seqs, self.hq, max_parts, 2), torch.float32)
-                ops.attn_decode(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, attn, tmp_o, tmp_ml, self.scale)
-            else:
-                ops.attn_prefill(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, b.cu_q, b.tiles, attn, self.scale)
+            ops.rope_cache(qkv, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq, self.hkv,
+                           perm=True)
+            self._attention(b, kv, i, q, attn)
             o = self._linear("o", attn.view(T, self.hq * self.D), w.layer(i, "wo"), reduce=True)
             ops.add_rms_norm(o, resid, w.layer(i, "ln2"), eps, x)
             if cfg.is_moe:
@@ -176,7 +263,7 @@ class TransformerLM:
                 gu = self._linear("gu", x, w.layer(i, "w_gu"))
                 F = gu.shape[-1] // 2
                 act = self._buf("act", (T, F), torch.bfloat16)
-                ops.swiglu(gu, act)
+                ops.swiglu(gu, act, interleaved=True)
                 mlp = self._linear("down", act, w.layer(i, "w_down"), reduce=True)
             nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
             ops.add_rms_norm(mlp, resid, nxt, eps, x)
@@ -196,7 +283,10 @@ class TransformerLM:
             ops.lm_head_sample(xl[m0:m1].contiguous() if m0 or m1 < n else xl, self.w["lm_head"],
                                b.temps[m0:m1], b.seeds[m0:m1], b.step, tk, keys[m0:m1], ids[m0:m1],
                                self.tp_rank * self.vocab_shard, logits[m0:m1] if logits is not None else None)
-        if self.tp is not None and self.tp_size > 1:
+        return self._combine_tp(ids, keys, logits)
+
+    def _combine_tp(self, ids, keys, logits) -> torch.Tensor:
+        if self._tp_active():
             # keys are u64 (order-preserving); flip the sign bit so signed MAX == unsigned max
             keys.bitwise_xor_(SIGN64)
             self.tp.all_reduce(keys, op="max")

@@ -70,6 +70,7 @@ class ModelWeights:
     cfg: ModelConfig
     shard: ShardSpec
     tensors: dict = field(default_factory=dict)
+    layout: str = "natural"  # "decode" after models.layout.apply_decode_layout
 
     def __getitem__(self, k):
         return self.tensors[k]
@@ -258,8 +259,10 @@ def save_hf_weights(weights: ModelWeights, path: str) -> None:
     """Write full (tp=1) fused weights back out in HF naming (used to test the loader)."""
     from safetensors.torch import save_file
 
+    from .layout import natural_tensors
+
     cfg = weights.cfg
-    t = weights.tensors
+    t = natural_tensors(weights)
     out = {"model.embed_tokens.weight": t["embed"], "model.norm.weight": t["norm"], "lm_head.weight": t["lm_head"]}
     q, kv, F = cfg.q_size, cfg.kv_size, cfg.intermediate_size
     for i in range(cfg.num_layers):

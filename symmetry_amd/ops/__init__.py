@@ -27,6 +27,14 @@ __all__ = [
     "moe_route_permute",
     "grouped_skinny",
     "moe_combine",
+    "dg_f32",
+    "dg_qkv",
+    "dg_resid",
+    "dg_swiglu",
+    "dg_argmax",
+    "embed_prep",
+    "add_prep",
+    "rownorm",
     "linear",
     "choose_splits",
 ]
@@ -58,10 +66,11 @@ def embed_rms_norm(ids, table, residual, w, eps, out):
     return reference.embed_rms_norm(ids, table, residual, w, eps, out)
 
 
-def rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv):
+def rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, perm=False):
     if _gpu(q_out):
-        return _native.ops().rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, int(Hq), int(Hkv))
-    return reference.rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv)
+        return _native.ops().rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, int(Hq), int(Hkv),
+                                        bool(perm))
+    return reference.rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, perm)
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, scale):
@@ -91,10 +100,62 @@ def lm_head_sample(x, w, temps, seeds, step, tile_keys, out_keys, out_ids, n_off
     return reference.lm_head_sample(x, w, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset, logits)
 
 
-def swiglu(gu, out):
+def swiglu(gu, out, interleaved=False):
     if _gpu(out):
-        return _native.ops().swiglu(gu, out)
-    return reference.swiglu(gu, out)
+        return _native.ops().swiglu(gu, out, bool(interleaved))
+    return reference.swiglu(gu, out, interleaved)
+
+
+# ---- fused decode GEMMs: M <= 64 rows, weights in the decode layout (models/layout.py) ----------
+# ss_in: per-(row, tile) sums of squares of the residual [>=M, tiles] (deferred RMSNorm) or None.
+def dg_f32(x, W, ss_in, eps, y):
+    if _gpu(x):
+        return _native.ops().dg_f32(x, W, ss_in, float(eps), y)
+    return reference.dg_f32(x, W, ss_in, eps, y)
+
+
+def dg_qkv(x, W, ss_in, eps, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv):
+    if _gpu(x):
+        return _native.ops().dg_qkv(x, W, ss_in, float(eps), positions, slots, cos_sin, q_out, k_cache, v_cache,
+                                    int(Hq), int(Hkv))
+    return reference.dg_qkv(x, W, ss_in, eps, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv)
+
+
+def dg_resid(x, W, resid, w_next, xw_out, ss_out):
+    if _gpu(x):
+        return _native.ops().dg_resid(x, W, resid, w_next, xw_out, ss_out)
+    return reference.dg_resid(x, W, resid, w_next, xw_out, ss_out)
+
+
+def dg_swiglu(x, W, ss_in, eps, act):
+    if _gpu(x):
+        return _native.ops().dg_swiglu(x, W, ss_in, float(eps), act)
+    return reference.dg_swiglu(x, W, ss_in, eps, act)
+
+
+def dg_argmax(x, W, ss_in, eps, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset=0, logits=None):
+    if _gpu(x):
+        return _native.ops().dg_argmax(x, W, ss_in, float(eps), temps, seeds, step, tile_keys, out_keys, out_ids,
+                                       int(n_offset), logits)
+    return reference.dg_argmax(x, W, ss_in, eps, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset, logits)
+
+
+def embed_prep(ids, table, resid, w, xw, ss):
+    if _gpu(resid):
+        return _native.ops().embed_prep(ids, table, resid, w, xw, ss)
+    return reference.embed_prep(ids, table, resid, w, xw, ss)
+
+
+def add_prep(delta, resid, w, xw, ss):
+    if _gpu(resid):
+        return _native.ops().add_prep(delta, resid, w, xw, ss)
+    return reference.add_prep(delta, resid, w, xw, ss)
+
+
+def rownorm(xw, ss, eps, out):
+    if _gpu(out):
+        return _native.ops().rownorm(xw, ss, float(eps), out)
+    return reference.rownorm(xw, ss, eps, out)
 
 
 def moe_route_permute(logits, x, k, E, ids, w, counts, offsets, cursor, xs, dst):

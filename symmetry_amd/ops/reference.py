@@ -44,11 +44,24 @@ def embed_rms_norm(ids, table, residual, w, eps, out) -> None:
     rms_norm(residual, w, eps, out)
 
 
-def rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq: int, Hkv: int) -> None:
+def _unperm_qk(x: torch.Tensor, nqk: int, D: int) -> torch.Tensor:
+    """Undo the decode layout (models/layout.py) of the first ``nqk`` heads of x [T, H, D]."""
+    from ..models.layout import _pair_perm
+
+    inv = torch.empty(D, dtype=torch.long)
+    inv[_pair_perm(D // 2)] = torch.arange(D)
+    x = x.clone()
+    x[:, :nqk] = x[:, :nqk].index_select(-1, inv.to(x.device))
+    return x
+
+
+def rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq: int, Hkv: int, perm: bool = False) -> None:
     T = positions.numel()
     D = k_cache.shape[3]
     BS = k_cache.shape[2]
     x = linout_sum(qkv).view(T, Hq + 2 * Hkv, D)
+    if perm:
+        x = _unperm_qk(x, Hq + Hkv, D)
     cs = cos_sin[positions.long()]  # [T, D]
     half = D // 2
     cos, sin = cs[:, None, :half], cs[:, None, half:]
@@ -205,11 +218,81 @@ def lm_head_sample(x, w, temps, seeds, step, tile_keys, out_keys, out_ids, n_off
     out_ids[:M].copy_(ids.to(out_ids.dtype))
 
 
-def swiglu(gu, out) -> None:
+def swiglu(gu, out, interleaved: bool = False) -> None:
     g = linout_sum(gu)
     F = out.shape[1]
+    if interleaved:
+        from ..models.layout import _inverse, gu_perm
+
+        g = g.index_select(-1, _inverse(gu_perm(F)).to(g.device))
     y = torch.nn.functional.silu(g[:, :F]) * g[:, F:]
     out.copy_(y.to(out.dtype))
+
+
+# ----- fused decode GEMMs (csrc/kernels/decode_gemm.hip) -----------------------------------------
+def _row_scale(ss_in, eps: float, K: int, M: int):
+    if ss_in is None:
+        return None
+    return torch.rsqrt(ss_in[:M].float().sum(-1, keepdim=True) / K + eps)
+
+
+def _dg(x, W, ss_in, eps):
+    y = x.float() @ W.float().t()
+    rn = _row_scale(ss_in, eps, x.shape[1], x.shape[0])
+    return y if rn is None else y * rn
+
+
+def dg_f32(x, W, ss_in, eps, y) -> None:
+    y[: x.shape[0]].copy_(_dg(x, W, ss_in, eps))
+
+
+def dg_qkv(x, W, ss_in, eps, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq: int, Hkv: int) -> None:
+    rope_cache(_dg(x, W, ss_in, eps), positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, perm=True)
+
+
+def dg_resid(x, W, resid, w_next, xw_out, ss_out) -> None:
+    M = x.shape[0]
+    r = resid[:M]
+    r.add_(x.float() @ W.float().t())
+    xw_out[:M].copy_((r * w_next.float()).to(xw_out.dtype))
+    ss_out[:M].copy_(r.pow(2).view(M, -1, 16).sum(-1))
+
+
+def dg_swiglu(x, W, ss_in, eps, act) -> None:
+    swiglu(_dg(x, W, ss_in, eps), act[: x.shape[0]], interleaved=True)
+
+
+def dg_argmax(x, W, ss_in, eps, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset: int, logits=None) -> None:
+    lg = _dg(x, W, ss_in, eps)
+    if logits is not None:
+        logits[: x.shape[0]].copy_(lg)
+    keys, ids = sample_keys(lg, temps, seeds, int(step.reshape(-1)[0]), n_offset)
+    M = x.shape[0]
+    out_keys[:M].copy_(keys)
+    out_ids[:M].copy_(ids.to(out_ids.dtype))
+
+
+def embed_prep(ids, table, resid, w, xw, ss) -> None:
+    T = ids.numel()
+    r = table[ids.long()].float()
+    resid[:T].copy_(r)
+    xw[:T].copy_((r * w.float()).to(xw.dtype))
+    ss.view(-1)[:T].copy_(r.pow(2).sum(-1))  # ss: [>=T] or [>=T, 1] (one tile per row)
+
+
+def add_prep(delta, resid, w, xw, ss) -> None:
+    d = linout_sum(delta)
+    T = d.shape[0]
+    r = resid[:T]
+    r.add_(d)
+    xw[:T].copy_((r * w.float()).to(xw.dtype))
+    ss.view(-1)[:T].copy_(r.pow(2).sum(-1))  # ss: [>=T] or [>=T, 1] (one tile per row)
+
+
+def rownorm(xw, ss, eps, out) -> None:
+    T, d = out.shape
+    rn = torch.rsqrt(ss[:T].float().sum(-1, keepdim=True) / d + eps)
+    out.copy_((xw[:T].float() * rn).to(out.dtype))
 
 
 def rope_table(max_pos: int, head_dim: int, theta: float, scaling: dict | None = None,

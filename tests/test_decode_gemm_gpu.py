@@ -1,0 +1,172 @@
+"""Fused decode GEMMs (csrc/kernels/decode_gemm.hip) against the fp32 references.
+
+Shapes cover the 8-wave (K % 512 == 0) and 4-wave (K = 256, K = 1792: Llama-3-8B down_proj at
+TP=8) decompositions and 1..4 column tiles (M = 1, 7, 16, 33, 64).
+"""
+import pytest
+import torch
+
+from symmetry_amd import ops
+from symmetry_amd.models.layout import gu_perm, qkv_perm
+from symmetry_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+MS = [1, 7, 16, 33, 64]
+
+
+def _close(a, b, atol, rtol=0.0):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    assert torch.isfinite(a).all(), "non-finite output"
+    assert (err <= atol + rtol * b.abs()).all(), f"max err {err.max().item():.4g}"
+
+
+def _inputs(gpu, M, N, K, seed=0, ss=True):
+    g = torch.Generator(device=gpu).manual_seed(seed)
+    x = torch.randn(M, K, device=gpu, generator=g).bfloat16()
+    W = (torch.randn(N, K, device=gpu, generator=g) / K ** 0.5).bfloat16()
+    s = (torch.rand(M, K // 16, device=gpu, generator=g) * 16 + 1) if ss else None
+    return x, W, s
+
+
+@pytest.mark.parametrize("M", MS)
+@pytest.mark.parametrize("N,K", [(4096, 4096), (512, 256), (4096, 1792)])
+def test_dg_f32(gpu, M, N, K):
+    x, W, s = _inputs(gpu, M, N, K)
+    y = torch.empty(M, N, device=gpu)
+    ops.dg_f32(x, W, s, 1e-5, y)
+    y_ref = torch.empty(M, N)
+    ref.dg_f32(x.cpu(), W.cpu(), s.cpu(), 1e-5, y_ref)
+    _close(y, y_ref, atol=2e-3, rtol=1e-2)
+    ops.dg_f32(x, W, None, 0.0, y)
+    ref.dg_f32(x.cpu(), W.cpu(), None, 0.0, y_ref)
+    _close(y, y_ref, atol=2e-3, rtol=1e-2)
+
+
+@pytest.mark.parametrize("M", MS)
+@pytest.mark.parametrize("N,K", [(4096, 4096), (1024, 1792)])
+def test_dg_resid(gpu, M, N, K):
+    x, W, _ = _inputs(gpu, M, N, K, seed=1)
+    g = torch.Generator(device=gpu).manual_seed(2)
+    resid = torch.randn(M, N, device=gpu, generator=g)
+    wn = (torch.randn(N, device=gpu, generator=g) * 0.1 + 1).bfloat16()
+    xw = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    ss = torch.empty(M, N // 16, device=gpu)
+    r_ref, xw_ref, ss_ref = resid.cpu().clone(), torch.empty(M, N, dtype=torch.bfloat16), torch.empty(M, N // 16)
+    ops.dg_resid(x, W, resid, wn, xw, ss)
+    ref.dg_resid(x.cpu(), W.cpu(), r_ref, wn.cpu(), xw_ref, ss_ref)
+    _close(resid, r_ref, atol=2e-3, rtol=1e-3)
+    _close(xw, xw_ref, atol=2e-2, rtol=1e-2)
+    _close(ss, ss_ref, atol=1e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("M", MS)
+@pytest.mark.parametrize("F,K", [(1792, 4096), (512, 256)])
+def test_dg_swiglu(gpu, M, F, K):
+    x, W, s = _inputs(gpu, M, 2 * F, K, seed=3)
+    W = W[gu_perm(F).to(gpu)].contiguous()
+    act = torch.empty(M, F, device=gpu, dtype=torch.bfloat16)
+    ops.dg_swiglu(x, W, s, 1e-5, act)
+    act_ref = torch.empty(M, F, dtype=torch.bfloat16)
+    ref.dg_swiglu(x.cpu(), W.cpu(), s.cpu(), 1e-5, act_ref)
+    _close(act, act_ref, atol=1e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", MS)
+@pytest.mark.parametrize("Hq,Hkv,K", [(32, 8, 4096), (4, 1, 512), (2, 1, 256)])
+def test_dg_qkv(gpu, M, Hq, Hkv, K):
+    D, BS, NB = 128, 32, 8
+    N = (Hq + 2 * Hkv) * D
+    x, W, s = _inputs(gpu, M, N, K, seed=4)
+    W = W[qkv_perm(Hq, Hkv, D).to(gpu)].contiguous()
+    cs = ref.rope_table(1024, D, 500000.0, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(5)
+    pos = torch.randint(0, 1024, (M,), device=gpu, generator=g, dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device=gpu, generator=g)[:M].int()
+    slots[0] = -1  # a row without a cache write
+    q = torch.empty(M, Hq, D, device=gpu, dtype=torch.bfloat16)
+    kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=torch.bfloat16)
+    vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=torch.bfloat16)
+    ops.dg_qkv(x, W, s, 1e-5, pos, slots, cs, q, kc, vc, Hq, Hkv)
+    q_r, kc_r, vc_r = torch.empty(M, Hq, D, dtype=torch.bfloat16), torch.zeros_like(kc.cpu()), torch.zeros_like(vc.cpu())
+    ref.dg_qkv(x.cpu(), W.cpu(), s.cpu(), 1e-5, pos.cpu(), slots.cpu(), cs.cpu(), q_r, kc_r, vc_r, Hq, Hkv)
+    _close(q, q_r, atol=2e-2, rtol=2e-2)
+    _close(kc, kc_r, atol=2e-2, rtol=2e-2)
+    _close(vc, vc_r, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", MS)
+def test_dg_argmax(gpu, M):
+    N, K = 16032, 4096  # Llama-3 vocab shard at TP=8
+    x, W, s = _inputs(gpu, M, N, K, seed=6)
+    g = torch.Generator(device=gpu).manual_seed(7)
+    temps = torch.where(torch.arange(M, device=gpu) % 2 == 0, 0.0, 0.8).float()
+    seeds = torch.randint(0, 1 << 62, (M,), device=gpu, generator=g)
+    step = torch.tensor([3], device=gpu, dtype=torch.int64)
+    tk = torch.empty(M * (N // 16), device=gpu, dtype=torch.int64)
+    keys = torch.empty(M, device=gpu, dtype=torch.int64)
+    ids = torch.empty(M, device=gpu, dtype=torch.int32)
+    logits = torch.empty(M, N, device=gpu)
+    ops.dg_argmax(x, W, s, 1e-5, temps, seeds, step, tk, keys, ids, 100, logits)
+    lg_ref = torch.empty(M, N)
+    ref.dg_f32(x.cpu(), W.cpu(), s.cpu(), 1e-5, lg_ref)
+    _close(logits, lg_ref, atol=2e-3, rtol=1e-2)
+    # sample from the kernel's own logits (ties at fp32 rounding are not a kernel property)
+    k_ref, i_ref = ref.sample_keys(logits.cpu(), temps.cpu(), seeds.cpu(), 3, 100)
+    assert torch.equal(ids.cpu().long(), i_ref)
+    assert torch.equal(keys.cpu(), k_ref)
+
+
+@pytest.mark.parametrize("T,d", [(1, 4096), (13, 4096), (5, 256)])
+def test_prep_and_rownorm(gpu, T, d):
+    g = torch.Generator(device=gpu).manual_seed(8)
+    table = torch.randn(300, d, device=gpu, generator=g).bfloat16()
+    ids = torch.randint(0, 300, (T,), device=gpu, generator=g, dtype=torch.int32)
+    w = (torch.randn(d, device=gpu, generator=g) * 0.1 + 1).bfloat16()
+    resid = torch.empty(T, d, device=gpu)
+    xw = torch.empty(T, d, device=gpu, dtype=torch.bfloat16)
+    ss = torch.empty(T, 1, device=gpu)
+    ops.embed_prep(ids, table, resid, w, xw, ss)
+    r_ref, xw_ref, ss_ref = torch.empty(T, d), torch.empty(T, d, dtype=torch.bfloat16), torch.empty(T, 1)
+    ref.embed_prep(ids.cpu(), table.cpu(), r_ref, w.cpu(), xw_ref, ss_ref)
+    _close(resid, r_ref, atol=0)
+    _close(xw, xw_ref, atol=1e-2, rtol=1e-2)
+    _close(ss, ss_ref, atol=1e-2, rtol=1e-4)
+    delta = torch.randn(T, d, device=gpu, generator=g).bfloat16()
+    ops.add_prep(delta, resid, w, xw, ss)
+    ref.add_prep(delta.cpu(), r_ref, w.cpu(), xw_ref, ss_ref)
+    _close(resid, r_ref, atol=1e-5)
+    _close(xw, xw_ref, atol=1e-2, rtol=1e-2)
+    _close(ss, ss_ref, atol=1e-2, rtol=1e-4)
+    out = torch.empty(T, d, device=gpu, dtype=torch.bfloat16)
+    ops.rownorm(xw, ss, 1e-5, out)
+    out_ref = torch.empty(T, d, dtype=torch.bfloat16)
+    ref.rownorm(xw_ref, ss_ref, 1e-5, out_ref)
+    _close(out, out_ref, atol=2e-2, rtol=2e-2)
+
+
+def test_rope_cache_perm_and_swiglu_interleaved(gpu):
+    """Library-GEMM path consumers of the decode layout."""
+    T, Hq, Hkv, D, BS = 9, 4, 2, 128, 32
+    g = torch.Generator(device=gpu).manual_seed(9)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=gpu, generator=g).bfloat16()
+    cs = ref.rope_table(64, D, 500000.0, device=gpu)
+    pos = torch.arange(T, device=gpu, dtype=torch.int32)
+    slots = torch.arange(T, device=gpu, dtype=torch.int32)
+    q = torch.empty(T, Hq, D, device=gpu, dtype=torch.bfloat16)
+    kc = torch.zeros(1, Hkv, BS, D, device=gpu, dtype=torch.bfloat16)
+    vc = torch.zeros(1, Hkv, D, BS, device=gpu, dtype=torch.bfloat16)
+    ops.rope_cache(qkv, pos, slots, cs, q, kc, vc, Hq, Hkv, perm=True)
+    q_r, kc_r, vc_r = torch.empty(T, Hq, D, dtype=torch.bfloat16), torch.zeros_like(kc.cpu()), torch.zeros_like(vc.cpu())
+    ref.rope_cache(qkv.cpu(), pos.cpu(), slots.cpu(), cs.cpu(), q_r, kc_r, vc_r, Hq, Hkv, perm=True)
+    _close(q, q_r, atol=2e-2, rtol=1e-2)
+    _close(kc, kc_r, atol=2e-2, rtol=1e-2)
+    _close(vc, vc_r, atol=0)
+    F = 256
+    gu = torch.randn(T, 2 * F, device=gpu, generator=g).bfloat16()
+    a = torch.empty(T, F, device=gpu, dtype=torch.bfloat16)
+    ops.swiglu(gu, a, interleaved=True)
+    a_r = torch.empty(T, F, dtype=torch.bfloat16)
+    ref.swiglu(gu.cpu(), a_r, interleaved=True)
+    _close(a, a_r, atol=2e-2, rtol=1e-2)
