@@ -72,6 +72,10 @@ class ModelWeights:
     tensors: dict = field(default_factory=dict)
     layout: str = "natural"  # "decode" after models.layout.apply_decode_layout
 
+    def to(self, device) -> "ModelWeights":
+        """Copy on ``device`` (keeps the layout tag)."""
+        return ModelWeights(self.cfg, self.shard, {k: v.to(device) for k, v in self.tensors.items()}, self.layout)
+
     def __getitem__(self, k):
         return self.tensors[k]
 

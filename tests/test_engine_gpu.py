@@ -15,7 +15,7 @@ def _agree(weights, prompt, out, tol):
     from symmetry_amd.models import reference_model as rm
     from symmetry_amd.models.weights import ModelWeights
 
-    cpu = ModelWeights(weights.cfg, weights.shard, {k: v.cpu() for k, v in weights.tensors.items()})
+    cpu = weights.to("cpu")
     lg = rm.forward_logits(cpu, prompt + out[:-1])
     for j, t in enumerate(out):
         row = lg[len(prompt) - 1 + j]

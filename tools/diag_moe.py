@@ -8,7 +8,7 @@ from symmetry_amd.models.transformer import TransformerLM
 
 w = random_weights(TINY_MIXTRAL, ShardSpec(), seed=0)
 cpu = TransformerLM(w, "cpu")
-wg = ModelWeights(w.cfg, w.shard, {k: v.cuda() for k, v in w.tensors.items()})
+wg = w.to("cuda")
 gpu = TransformerLM(wg, "cuda")
 for T in (1, 5, 8, 20, 33, 40, 100):
     x = torch.randn(T, 256, generator=torch.Generator().manual_seed(T)).bfloat16()

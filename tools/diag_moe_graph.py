@@ -7,7 +7,7 @@ from symmetry_amd.models.weights import random_weights, ShardSpec, ModelWeights
 from symmetry_amd.models.transformer import TransformerLM
 
 w = random_weights(TINY_MIXTRAL, ShardSpec(), seed=0)
-wg = ModelWeights(w.cfg, w.shard, {k: v.cuda() for k, v in w.tensors.items()})
+wg = w.to("cuda")
 gpu = TransformerLM(wg, "cuda")
 T = 8
 x = torch.randn(T, 256, generator=torch.Generator().manual_seed(1)).bfloat16().cuda()
