@@ -217,8 +217,9 @@ class TransformerLM:
                                   xw, ss_t, ss_1)
             nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
             if cfg.is_moe:
+                # router + experts are not decode GEMMs: materialise RMSNorm(resid) (one bf16 rounding)
                 xn = self._buf("x", (T, d), torch.bfloat16)
-                ops.rownorm(xw, ss, eps, xn)
+                ops.rms_norm(resid, w.layer(i, "ln2"), eps, xn)
                 ops.add_prep(self.moe.forward(i, xn), resid, nxt, xw, ss_1)
                 ss = ss_1
             else:
