@@ -596,6 +596,7 @@ TORCH_LIBRARY(symmetry_amd, m) {
         &embed_prep);
   m.def("add_prep(Tensor delta, Tensor(a!) resid, Tensor w, Tensor(b!) xw, Tensor(c!) ss) -> ()", &add_prep);
   m.def("rownorm(Tensor xw, Tensor ss, float eps, Tensor(a!) out) -> ()", &rownorm);
+  m.def("decode_gemm_variant(int v) -> ()", [](int64_t v) { set_decode_gemm_variant((int)v); });
   m.def("grouped_skinny(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y) -> ()", &grouped_skinny);
   m.def(
       "moe_combine(Tensor y, Tensor dst, Tensor ids, int e_lo, int e_hi, Tensor w, int k, Tensor(a!) out, "

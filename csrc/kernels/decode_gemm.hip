@@ -52,102 +52,11 @@ SYM_DEV void store4bf(bf16* p, float a, float b, float c, float d) {
   *reinterpret_cast<bf16x4*>(p) = v;
 }
 
-template <int MT, int NW, int U, int EPI>
-__global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __restrict__ x,
-                                                              const bf16* __restrict__ W, int M, int N, int K,
-                                                              DecodeEpi e) {
-  const int tile = blockIdx.x;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int r16 = lane & 15, h = lane >> 4;
+// Epilogue of one finished 16x16 accumulator tile (rows n0.., columns = token rows 16*mt..).
+// Lane (r16, h) holds rows n0 + 4h .. n0 + 4h + 3 of token row m = 16 * mt + r16.
+template <int EPI>
+SYM_DEV void epilogue(const DecodeEpi& e, f32x4 v, int tile, int m, bool mok, int h, int N) {
   const int n0 = tile * 16;
-  const int wk = K / NW;
-  const int kbeg = wid * wk;
-  const int nblk = wk / 64;
-
-  const bf16* wrow = W + (long long)(n0 + r16) * K + kbeg + 8 * h;
-  const bf16* xrow[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) xrow[mt] = x + (long long)min(16 * mt + r16, M - 1) * K + kbeg + 8 * h;
-
-  __shared__ f32x4 red[NW][MT][64];
-  __shared__ float rn_s[64];
-
-  f32x4 acc[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  int b = 0;
-  bool rn_done = false;
-  for (; b + U <= nblk; b += U) {
-    Pack8 wa[U][2], xa[U][MT][2];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int ko = (b + u) * 64;
-      wa[u][0].u = *reinterpret_cast<const uint4*>(wrow + ko);
-      wa[u][1].u = *reinterpret_cast<const uint4*>(wrow + ko + 32);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        xa[u][mt][0].u = *reinterpret_cast<const uint4*>(xrow[mt] + ko);
-        xa[u][mt][1].u = *reinterpret_cast<const uint4*>(xrow[mt] + ko + 32);
-      }
-    }
-    if (!rn_done) {
-      // RMSNorm row scales of the input rows, computed while the first weight batch is in flight.
-      rn_done = true;
-      if (e.ss_in) {
-        for (int m = wid; m < M; m += NW) {
-          float s = 0.f;
-          for (int i = lane; i < e.ss_tiles; i += 64) s += e.ss_in[(long long)m * e.ss_tiles + i];
-          s = wave_sum(s);
-          if (lane == 0) rn_s[m] = rsqrtf(s * e.inv_d + e.eps);
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        acc[mt] = mfma16(wa[u][0].v, xa[u][mt][0].v, acc[mt]);
-        acc[mt] = mfma16(wa[u][1].v, xa[u][mt][1].v, acc[mt]);
-      }
-  }
-  for (; b < nblk; ++b) {
-    const int ko = b * 64;
-    Pack8 w0, w1;
-    w0.u = *reinterpret_cast<const uint4*>(wrow + ko);
-    w1.u = *reinterpret_cast<const uint4*>(wrow + ko + 32);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      Pack8 x0, x1;
-      x0.u = *reinterpret_cast<const uint4*>(xrow[mt] + ko);
-      x1.u = *reinterpret_cast<const uint4*>(xrow[mt] + ko + 32);
-      acc[mt] = mfma16(w0.v, x0.v, acc[mt]);
-      acc[mt] = mfma16(w1.v, x1.v, acc[mt]);
-    }
-  }
-  if (!rn_done && e.ss_in) {
-    for (int m = wid; m < M; m += NW) {
-      float s = 0.f;
-      for (int i = lane; i < e.ss_tiles; i += 64) s += e.ss_in[(long long)m * e.ss_tiles + i];
-      s = wave_sum(s);
-      if (lane == 0) rn_s[m] = rsqrtf(s * e.inv_d + e.eps);
-    }
-  }
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) red[wid][mt][lane] = acc[mt];
-  __syncthreads();
-  if (wid >= MT) return;
-  // wave `wid` finishes column tile mt = wid (parallel epilogue across waves)
-  const int mt = wid;
-  f32x4 v = red[0][mt][lane];
-#pragma unroll
-  for (int w = 1; w < NW; ++w) v += red[w][mt][lane];
-  const int m = 16 * mt + r16;
-  const bool mok = m < M;
-  const float sc = (e.ss_in && mok) ? rn_s[m] : 1.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] *= sc;
-
   if constexpr (EPI == DECODE_EPI_F32) {
     if (mok) *reinterpret_cast<float4*>(e.y + (long long)m * N + n0 + 4 * h) = make_float4(v[0], v[1], v[2], v[3]);
   } else if constexpr (EPI == DECODE_EPI_QKV) {
@@ -204,7 +113,7 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __rest
     }
     sq += __shfl_xor(sq, 16, 64);
     sq += __shfl_xor(sq, 32, 64);
-    if (mok && h == 0) e.ss_out[(long long)m * gridDim.x + tile] = sq;
+    if (mok && h == 0) e.ss_out[(long long)m * (N / 16) + tile] = sq;
   } else if constexpr (EPI == DECODE_EPI_SWIGLU) {
     float u[4];
 #pragma unroll
@@ -237,7 +146,119 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __rest
     best = o16 > best ? o16 : best;
     unsigned long long o32 = __shfl_xor(best, 32, 64);
     best = o32 > best ? o32 : best;
-    if (h == 0 && mok) e.keys[(long long)m * gridDim.x + tile] = best;
+    if (h == 0 && mok) e.keys[(long long)m * (N / 16) + tile] = best;
+  }
+}
+
+template <int MT, int NW, int U, int RT, int EPI>
+__global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __restrict__ x,
+                                                              const bf16* __restrict__ W, int M, int N, int K,
+                                                              DecodeEpi e) {
+  const int tile0 = blockIdx.x * RT;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, h = lane >> 4;
+  const int wk = K / NW;
+  const int kbeg = wid * wk;
+  const int nblk = wk / 64;
+
+  const bf16* wrow[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) wrow[rt] = W + (long long)(16 * (tile0 + rt) + r16) * K + kbeg + 8 * h;
+  const bf16* xrow[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) xrow[mt] = x + (long long)min(16 * mt + r16, M - 1) * K + kbeg + 8 * h;
+
+  __shared__ f32x4 red[NW][RT * MT][64];
+  __shared__ float rn_s[64];
+
+  f32x4 acc[RT][MT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto row_scales = [&]() {
+    // RMSNorm row scales of the input rows (deferred norm), overlapped with the weight loads in flight.
+    if (e.ss_in) {
+      for (int m = wid; m < M; m += NW) {
+        float s = 0.f;
+        for (int i = lane; i < e.ss_tiles; i += 64) s += e.ss_in[(long long)m * e.ss_tiles + i];
+        s = wave_sum(s);
+        if (lane == 0) rn_s[m] = rsqrtf(s * e.inv_d + e.eps);
+      }
+    }
+  };
+
+  int b = 0;
+  bool rn_done = false;
+  for (; b + U <= nblk; b += U) {
+    Pack8 wa[U][RT][2], xa[U][MT][2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ko = (b + u) * 64;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        wa[u][rt][0].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko);
+        wa[u][rt][1].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko + 32);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        xa[u][mt][0].u = *reinterpret_cast<const uint4*>(xrow[mt] + ko);
+        xa[u][mt][1].u = *reinterpret_cast<const uint4*>(xrow[mt] + ko + 32);
+      }
+    }
+    if (!rn_done) {
+      rn_done = true;
+      row_scales();
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          acc[rt][mt] = mfma16(wa[u][rt][0].v, xa[u][mt][0].v, acc[rt][mt]);
+          acc[rt][mt] = mfma16(wa[u][rt][1].v, xa[u][mt][1].v, acc[rt][mt]);
+        }
+  }
+  for (; b < nblk; ++b) {
+    const int ko = b * 64;
+    Pack8 w0[RT], w1[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      w0[rt].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko);
+      w1[rt].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko + 32);
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      Pack8 x0, x1;
+      x0.u = *reinterpret_cast<const uint4*>(xrow[mt] + ko);
+      x1.u = *reinterpret_cast<const uint4*>(xrow[mt] + ko + 32);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        acc[rt][mt] = mfma16(w0[rt].v, x0.v, acc[rt][mt]);
+        acc[rt][mt] = mfma16(w1[rt].v, x1.v, acc[rt][mt]);
+      }
+    }
+  }
+  if (!rn_done) row_scales();
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) red[wid][rt * MT + mt][lane] = acc[rt][mt];
+  __syncthreads();
+  // parallel epilogue: wave `wid` finishes accumulator tiles job = wid, wid + NW, ...
+  for (int job = wid; job < RT * MT; job += NW) {
+    const int rt = job / MT, mt = job % MT;
+    f32x4 v = red[0][job][lane];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) v += red[w][job][lane];
+    const int m = 16 * mt + r16;
+    const bool mok = m < M;
+    const float sc = (e.ss_in && mok) ? rn_s[m] : 1.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] *= sc;
+    epilogue<EPI>(e, v, tile0 + rt, m, mok, h, N);
   }
 }
 
@@ -277,14 +298,35 @@ __global__ __launch_bounds__(256) void prep_kernel(LinOut delta, const int* __re
   if (threadIdx.x == 0) ss[row] = acc;
 }
 
+// Decomposition variants (A/B: bench/kernels/bench_decode_gemm.py; chosen by decode_gemm_variant()):
+//   0  8 waves split K, 1 row tile, U = 4 / 2 / 1 k-blocks in flight for 1 / 2 / 3-4 column tiles
+//   1  8 waves, 1 row tile, deeper: U = 8 / 4 / 2
+//   2 16 waves (K % 1024 == 0), 1 row tile
+//   3  8 waves, 2 row tiles per workgroup (x fragments shared by both)
+//   4  4 waves, 1 row tile
+int g_variant = -1;
+
+template <int MT, int NW, int U, int RT, int EPI>
+void go(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, hipStream_t s) {
+  decode_gemm_kernel<MT, NW, U, RT, EPI><<<N / (16 * RT), NW * 64, 0, s>>>(x, W, M, N, K, e);
+}
+
 template <int MT, int EPI>
 void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, hipStream_t s) {
-  constexpr int U = MT == 1 ? 4 : (MT == 2 ? 2 : 1);
-  // 8 waves split K when K % 512 == 0, else 4 (e.g. Llama-3-8B down_proj under TP=8: K = 1792)
-  if (K % 512 == 0)
-    decode_gemm_kernel<MT, 8, U, EPI><<<N / 16, 8 * 64, 0, s>>>(x, W, M, N, K, e);
-  else
-    decode_gemm_kernel<MT, 4, U, EPI><<<N / 16, 4 * 64, 0, s>>>(x, W, M, N, K, e);
+  constexpr int U0 = MT == 1 ? 4 : (MT == 2 ? 2 : 1);
+  constexpr int U1 = MT == 1 ? 8 : (MT == 2 ? 4 : 2);
+  int v = g_variant;
+  if (v < 0) v = 0;
+  if (v == 2 && K % 1024) v = 0;
+  if (v == 3 && N % 32) v = 0;
+  if (K % 512) v = 4;  // e.g. Llama-3-8B down_proj under TP=8: K = 1792
+  switch (v) {
+    case 1: go<MT, 8, U1, 1, EPI>(x, W, M, N, K, e, s); break;
+    case 2: go<MT, 16, U0, 1, EPI>(x, W, M, N, K, e, s); break;
+    case 3: go<MT, 8, (U0 > 1 ? U0 / 2 : 1), 2, EPI>(x, W, M, N, K, e, s); break;
+    case 4: go<MT, 4, U0, 1, EPI>(x, W, M, N, K, e, s); break;
+    default: go<MT, 8, U0, 1, EPI>(x, W, M, N, K, e, s); break;
+  }
 }
 
 template <int EPI>
@@ -309,6 +351,8 @@ void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int
     default: launch_epi<DECODE_EPI_ARGMAX>(x, W, M, N, K, e, s); break;
   }
 }
+
+void set_decode_gemm_variant(int v) { g_variant = v; }
 
 void launch_embed_prep(const int* ids, const bf16* table, float* resid, const bf16* w, bf16* xw, float* ss, int T,
                        int d, hipStream_t s) {

@@ -38,6 +38,7 @@ struct DecodeEpi {
   unsigned long long* keys = nullptr;
   int n_offset = 0;
 };
+void set_decode_gemm_variant(int v);  // -1: default heuristic
 void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e,
                         hipStream_t s);
 void launch_embed_prep(const int* ids, const bf16* table, float* resid, const bf16* w, bf16* xw, float* ss, int T,
