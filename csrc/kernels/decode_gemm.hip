@@ -164,9 +164,17 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __rest
   const bf16* wrow[RT];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) wrow[rt] = W + (long long)(16 * (tile0 + rt) + r16) * K + kbeg + 8 * h;
+  // x fragments of rows >= M are never fetched (masked lanes load nothing; MFMA sees zeros).
   const bf16* xrow[MT];
+  bool xok[MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) xrow[mt] = x + (long long)min(16 * mt + r16, M - 1) * K + kbeg + 8 * h;
+  for (int mt = 0; mt < MT; ++mt) {
+    xok[mt] = 16 * mt + r16 < M;
+    xrow[mt] = x + (long long)min(16 * mt + r16, M - 1) * K + kbeg + 8 * h;
+  }
+  auto ldx = [&](int mt, int ko) -> uint4 {
+    return xok[mt] ? *reinterpret_cast<const uint4*>(xrow[mt] + ko) : make_uint4(0, 0, 0, 0);
+  };
 
   __shared__ f32x4 red[NW][RT * MT][64];
   __shared__ float rn_s[64];
@@ -203,8 +211,8 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __rest
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        xa[u][mt][0].u = *reinterpret_cast<const uint4*>(xrow[mt] + ko);
-        xa[u][mt][1].u = *reinterpret_cast<const uint4*>(xrow[mt] + ko + 32);
+        xa[u][mt][0].u = ldx(mt, ko);
+        xa[u][mt][1].u = ldx(mt, ko + 32);
       }
     }
     if (!rn_done) {
@@ -232,8 +240,8 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __rest
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       Pack8 x0, x1;
-      x0.u = *reinterpret_cast<const uint4*>(xrow[mt] + ko);
-      x1.u = *reinterpret_cast<const uint4*>(xrow[mt] + ko + 32);
+      x0.u = ldx(mt, ko);
+      x1.u = ldx(mt, ko + 32);
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
         acc[rt][mt] = mfma16(w0[rt].v, x0.v, acc[rt][mt]);
@@ -304,6 +312,9 @@ __global__ __launch_bounds__(256) void prep_kernel(LinOut delta, const int* __re
 //   2 16 waves (K % 1024 == 0), 1 row tile
 //   3  8 waves, 2 row tiles per workgroup (x fragments shared by both)
 //   4  4 waves, 1 row tile
+//   5  8 waves, 4 row tiles (1 column tile only; else as 3)
+//   6  4 waves, 2 row tiles
+//   7  4 waves, 4 row tiles (1 column tile only; else as 6)
 int g_variant = -1;
 
 template <int MT, int NW, int U, int RT, int EPI>
@@ -316,15 +327,31 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
   constexpr int U0 = MT == 1 ? 4 : (MT == 2 ? 2 : 1);
   constexpr int U1 = MT == 1 ? 8 : (MT == 2 ? 4 : 2);
   int v = g_variant;
-  if (v < 0) v = 0;
+  if (v < 0) {
+    // Measured on MI355X (profiles/decode_gemm_variants_r1.jsonl): the x fragments (re-read from L2 by
+    // every workgroup) dominate the L1/TA traffic once M > 4, so wide-N projections share them over
+    // 4 (2 for M > 16) row tiles per workgroup; the 4096-wide ones keep 256 workgroups and split K
+    // over 4 waves; small TP shards keep the 8-wave split.
+    if (M <= 4) v = 0;
+    else if (N >= 12288) v = 7;
+    else if (N >= 6144 && K >= 4096) v = 3;
+    else if (N <= 4096 && K >= 4096) v = 4;
+    else v = 0;
+  }
   if (v == 2 && K % 1024) v = 0;
-  if (v == 3 && N % 32) v = 0;
-  if (K % 512) v = 4;  // e.g. Llama-3-8B down_proj under TP=8: K = 1792
+  if ((v == 5 || v == 7) && (MT > 1 || N % 64)) v = v == 5 ? 3 : 6;
+  if ((v == 3 || v == 6) && N % 32) v = 0;
+  if (K % 512) v = (v == 6 || v == 7) ? 6 : 4;  // e.g. Llama-3-8B down_proj under TP=8: K = 1792
+  if (v == 6 && N % 32) v = 4;
+  constexpr int UH = U0 > 1 ? U0 / 2 : 1;
   switch (v) {
     case 1: go<MT, 8, U1, 1, EPI>(x, W, M, N, K, e, s); break;
     case 2: go<MT, 16, U0, 1, EPI>(x, W, M, N, K, e, s); break;
-    case 3: go<MT, 8, (U0 > 1 ? U0 / 2 : 1), 2, EPI>(x, W, M, N, K, e, s); break;
+    case 3: go<MT, 8, UH, 2, EPI>(x, W, M, N, K, e, s); break;
     case 4: go<MT, 4, U0, 1, EPI>(x, W, M, N, K, e, s); break;
+    case 5: if constexpr (MT == 1) go<1, 8, 1, 4, EPI>(x, W, M, N, K, e, s); break;
+    case 6: go<MT, 4, UH, 2, EPI>(x, W, M, N, K, e, s); break;
+    case 7: if constexpr (MT == 1) go<1, 4, 2, 4, EPI>(x, W, M, N, K, e, s); break;
     default: go<MT, 8, U0, 1, EPI>(x, W, M, N, K, e, s); break;
   }
 }
