@@ -155,7 +155,7 @@ void check_cache(const Tensor& k_cache, const Tensor& v_cache) {
 }
 
 void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
-                 const Tensor& ctx_lens, Tensor& out, Tensor& tmp_o, Tensor& tmp_ml, double scale) {
+                 const Tensor& ctx_lens, Tensor& out, Tensor& tmp_o, Tensor& tmp_ml, Tensor& counters, double scale) {
   check_gpu(q, "q");
   check_dtype(q, at::kBFloat16, "q");
   check_cache(k_cache, v_cache);
@@ -179,10 +179,13 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, 
   TORCH_CHECK(tmp_ml.numel() >= S * Hq * max_parts * 2, "tmp_ml too small");
   const int64_t BS = k_cache.size(2), max_blocks = block_tables.size(1);
   TORCH_CHECK(max_parts * 256 >= max_blocks * BS, "tmp_o has too few partitions for the block table span");
+  check_gpu(counters, "counters");
+  check_dtype(counters, at::kInt, "counters");
+  TORCH_CHECK(counters.numel() >= S * Hkv, "counters must hold num_seqs * Hkv zero-initialised ints");
   const at::OptionalDeviceGuard g(q.device());
   launch_attn_decode(ptr<bf16>(q), ptr<bf16>(k_cache), ptr<bf16>(v_cache), ptr<int>(block_tables), ptr<int>(ctx_lens),
-                     ptr<bf16>(out), ptr<float>(tmp_o), ptr<float>(tmp_ml), (int)S, (int)Hq, (int)Hkv, (int)BS,
-                     (int)max_blocks, (int)max_parts, (float)scale, cur_stream(q));
+                     ptr<bf16>(out), ptr<float>(tmp_o), ptr<float>(tmp_ml), ptr<int>(counters), (int)S, (int)Hq,
+                     (int)Hkv, (int)BS, (int)max_blocks, (int)max_parts, (float)scale, cur_stream(q));
 }
 
 void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
@@ -564,7 +567,7 @@ TORCH_LIBRARY(symmetry_amd, m) {
       &rope_cache);
   m.def(
       "attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, Tensor(a!) out, "
-      "Tensor(b!) tmp_o, Tensor(c!) tmp_ml, float scale) -> ()",
+      "Tensor(b!) tmp_o, Tensor(c!) tmp_ml, Tensor(d!) counters, float scale) -> ()",
       &attn_decode);
   m.def(
       "attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, Tensor cu_q, "

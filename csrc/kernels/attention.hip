@@ -20,7 +20,8 @@
 // Decode (K5): grid (seq, kv_head, partition); 4 waves x 64 tokens = 256
 // tokens per partition; the G = Hq/Hkv query heads of a kv head are the MFMA
 // columns (K/V are read once per kv head).  Multi-partition sequences write
-// fp32 partials reduced by attn_decode_reduce (split-KV, flash-decoding).
+// fp32 partials that the last-arriving partition combines (split-KV,
+// flash-decoding, one launch).
 // The grid is sized for the max context so the launch is hipGraph-capturable;
 // partitions past a sequence's context exit at once.
 //
@@ -113,8 +114,8 @@ SYM_DEV void attend_group(const bf16* __restrict__ kb, const bf16* __restrict__ 
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
     const int* __restrict__ block_tables, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
-    float* __restrict__ tmp_o, float* __restrict__ tmp_ml, int Hq, int Hkv, int BS, int max_blocks, int max_parts,
-    float scale_log2) {
+    float* __restrict__ tmp_o, float* __restrict__ tmp_ml, int* __restrict__ counters, int Hq, int Hkv, int BS,
+    int max_blocks, int max_parts, float scale_log2) {
   const int seq = blockIdx.x, kvh = blockIdx.y, part = blockIdx.z;
   const int ctx = ctx_lens[seq];
   if (part * PART >= ctx) return;
@@ -164,62 +165,81 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     for (int r = 0; r < 4; ++r) sm_o[wid][c][16 * dt + 4 * h + r] = o[dt][r];
   __syncthreads();
 
+  // Combine the 4 waves' partial softmax states: thread (qq, d0) owns 8 dims of query column qq.
   const int qq = threadIdx.x >> 4;        // 0..15 query column
   const int d0 = (threadIdx.x & 15) * 8;  // 8 dims per thread
-  if (qq >= G) return;
-  float M = -INFINITY;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) M = fmaxf(M, sm_m[w][qq]);
-  float L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const float mw = sm_m[w][qq];
-    const float f = (mw == -INFINITY) ? 0.f : exp2f(mw - M);
-    L += sm_l[w][qq] * f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += sm_o[w][qq][d0 + j] * f;
-  }
+  const bool active = qq < G;
   const int head = kvh * G + qq;
   const int nparts = (ctx + PART - 1) / PART;
-  if (nparts == 1) {
+  float M = -INFINITY, L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (active) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm_m[w][qq]);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float mw = sm_m[w][qq];
+      const float f = (mw == -INFINITY) ? 0.f : exp2f(mw - M);
+      L += sm_l[w][qq] * f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += sm_o[w][qq][d0 + j] * f;
+    }
+  }
+  if (nparts == 1) {  // uniform over the workgroup
+    if (active) {
+      const float inv = 1.f / L;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] *= inv;
+      store8(out + ((long long)seq * Hq + head) * D + d0, acc);
+    }
+    return;
+  }
+  // Split-KV combine in the same launch (no reduce kernel): every partition publishes its partial
+  // state with write-through (sc1) stores, drains them (vmcnt(0)), then bumps the (seq, kv head)
+  // arrival counter; the workgroup whose add returns nparts - 1 reads all partials back with sc1
+  // loads and writes the output, then re-arms the counter to 0 (graph-replay safe, no memset).
+  // MI355X_MICROARCH.md hand-off table: sc1 stores + agent atomic add + sc1 loads, hipMalloc memory.
+  const long long base = ((long long)seq * Hq + head) * max_parts;
+  if (active) {
+    float* po = tmp_o + (base + part) * D + d0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) __hip_atomic_store(po + j, acc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d0 == 0) {
+      __hip_atomic_store(tmp_ml + (base + part) * 2, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(tmp_ml + (base + part) * 2 + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __shared__ int s_last;
+  __syncthreads();
+  int* cnt = counters + (long long)seq * Hkv + kvh;
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == nparts - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (active) {
+    M = -INFINITY;
+    for (int p = 0; p < nparts; ++p)
+      M = fmaxf(M, __hip_atomic_load(tmp_ml + (base + p) * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    L = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int p = 0; p < nparts; ++p) {
+      const float mp = __hip_atomic_load(tmp_ml + (base + p) * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float lp = __hip_atomic_load(tmp_ml + (base + p) * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float f = exp2f(mp - M);
+      L += lp * f;
+      const float* po = tmp_o + (base + p) * D + d0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += __hip_atomic_load(po + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * f;
+    }
     const float inv = 1.f / L;
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] *= inv;
     store8(out + ((long long)seq * Hq + head) * D + d0, acc);
-  } else {
-    const long long pbase = ((long long)seq * Hq + head) * max_parts + part;
-    store8f(tmp_o + pbase * D + d0, acc);
-    if (d0 == 0) {
-      tmp_ml[pbase * 2] = M;
-      tmp_ml[pbase * 2 + 1] = L;
-    }
   }
-}
-
-__global__ __launch_bounds__(64) void attn_decode_reduce_kernel(const float* __restrict__ tmp_o,
-                                                              const float* __restrict__ tmp_ml,
-                                                              const int* __restrict__ ctx_lens, bf16* __restrict__ out,
-                                                              int Hq, int max_parts) {
-  const int seq = blockIdx.x, head = blockIdx.y;
-  const int ctx = ctx_lens[seq];
-  const int nparts = (ctx + PART - 1) / PART;
-  if (nparts <= 1) return;
-  const long long base = ((long long)seq * Hq + head) * max_parts;
-  float M = -INFINITY;
-  for (int p = 0; p < nparts; ++p) M = fmaxf(M, tmp_ml[(base + p) * 2]);
-  const int d = threadIdx.x * 2;
-  float L = 0.f, a0 = 0.f, a1 = 0.f;
-  for (int p = 0; p < nparts; ++p) {
-    const float f = exp2f(tmp_ml[(base + p) * 2] - M);
-    L += tmp_ml[(base + p) * 2 + 1] * f;
-    const float2 v = *reinterpret_cast<const float2*>(tmp_o + (base + p) * D + d);
-    a0 += v.x * f;
-    a1 += v.y * f;
-  }
-  const float inv = 1.f / L;
-  bf16* op = out + ((long long)seq * Hq + head) * D + d;
-  op[0] = (bf16)(a0 * inv);
-  op[1] = (bf16)(a1 * inv);
+  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -291,16 +311,13 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(
 }  // namespace
 
 void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,
-                        const int* ctx_lens, bf16* out, float* tmp_o, float* tmp_ml, int num_seqs, int Hq, int Hkv,
-                        int BS, int max_blocks, int max_parts, float scale, hipStream_t s) {
+                        const int* ctx_lens, bf16* out, float* tmp_o, float* tmp_ml, int* counters, int num_seqs,
+                        int Hq, int Hkv, int BS, int max_blocks, int max_parts, float scale, hipStream_t s) {
   if (num_seqs == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(num_seqs, Hkv, max_parts);
-  attn_decode_kernel<<<grid, 256, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, Hq, Hkv,
-                                          BS, max_blocks, max_parts, scale_log2);
-  if (max_parts > 1) {
-    attn_decode_reduce_kernel<<<dim3(num_seqs, Hq), 64, 0, s>>>(tmp_o, tmp_ml, ctx_lens, out, Hq, max_parts);
-  }
+  attn_decode_kernel<<<grid, 256, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters,
+                                          Hq, Hkv, BS, max_blocks, max_parts, scale_log2);
 }
 
 void launch_attn_prefill(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,

@@ -3,11 +3,13 @@
 * All per-step host metadata (token ids, positions, slots, context lengths,
   block tables, sampling params) is packed into ONE pinned int32 buffer and
   moved with ONE async H2D copy.
-* Decode steps replay a hipGraph captured per batch-size bucket
-  (``torch.cuda.CUDAGraph`` is hipGraph on ROCm): the ~300 kernel launches of
-  a Llama-3-8B step become one graph launch (MI355X_MICROARCH.md rows
-  **boundary** / **graph-replay-floor**).  Padded rows write no cache
-  (slot -1) and read only the reserved block 0.
+* Decode steps replay a hipGraph captured per (batch-size bucket, context
+  bucket) (``torch.cuda.CUDAGraph`` is hipGraph on ROCm): the ~200 kernel
+  launches of a Llama-3-8B step become one graph launch (MI355X_MICROARCH.md
+  rows **boundary** / **graph-replay-floor**).  The context bucket bounds the
+  block-table width and therefore the split-KV grid of decode attention, so
+  short chats do not launch thousands of empty partition workgroups.  Padded
+  rows write no cache (slot -1) and read only the reserved block 0.
 * Tensor parallel: rank 0 runs the scheduler; :meth:`execute` broadcasts the
   packed metadata to the other ranks (R4) which replay the
   same forward via :meth:`worker_loop`.
@@ -24,6 +26,7 @@ from ..models.transformer import ForwardBatch, KVCache, TransformerLM
 from .scheduler import ScheduledBatch
 
 DECODE_BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64)
+CTX_BUCKETS = (256, 1024, 4096, 16384, 65536, 131072)  # tokens
 _SEED_MIX = 0x9E3779B97F4A7C15
 
 
@@ -94,11 +97,14 @@ class ModelRunner:
         self.max_num_seqs = max_num_seqs
         self.buckets = [b for b in DECODE_BUCKETS if b < max_num_seqs] + [max_num_seqs]
         self.buckets = sorted(set(b for b in self.buckets if b <= 64))
+        bs = kv.block_size
+        self.ctx_blocks = sorted({math.ceil(min(c, max_model_len) / bs) for c in CTX_BUCKETS} | {self.max_blocks})
+        self.ctx_blocks = [b for b in self.ctx_blocks if b <= self.max_blocks]
         self.is_gpu = self.device.type != "cpu"
         self.use_graphs = use_graphs and self.is_gpu
         self.tp_size, self.tp_rank = tp_size, tp_rank
         self.cpu_group = cpu_group
-        self.graphs: dict[int, tuple] = {}
+        self.graphs: dict[tuple, tuple] = {}
         self._graph_pool = None
         self._pinned = {}
         self.step_counter = 0
@@ -164,7 +170,8 @@ class ModelRunner:
         if batch.kind == "decode":
             nseq = len(seqs)
             bucket = self._bucket(nseq)
-            lay = _Layout(bucket, bucket, self.max_blocks, prefill=False)
+            need = max(len(s.block_table) for s in seqs)
+            lay = _Layout(bucket, bucket, self._ctx_bucket(need), prefill=False)
         else:
             nseq = len(seqs)
             ntiles = sum((n + 63) // 64 for n in counts)
@@ -188,15 +195,21 @@ class ModelRunner:
                 return b
         raise ValueError(f"decode batch {n} exceeds max_num_seqs {self.max_num_seqs}")
 
+    def _ctx_bucket(self, nblocks: int) -> int:
+        for b in self.ctx_blocks:
+            if b >= nblocks:
+                return b
+        raise ValueError(f"sequence needs {nblocks} blocks > max {self.max_blocks}")
+
     def _run(self, header: np.ndarray, host_t: torch.Tensor) -> list[int]:
         kind = "decode" if header[0] == 0 else "prefill"
         T, nseq_l, max_blocks, ntiles, nseq = (int(x) for x in header[1:6])
         lay = _Layout(T, nseq_l, max_blocks, prefill=kind == "prefill", ntiles=ntiles)
         if kind == "decode" and self.use_graphs:
-            g = self.graphs.get(T)
+            g = self.graphs.get((T, max_blocks))
             if g is None:
-                self._capture(T)
-                g = self.graphs[T]
+                self._capture(T, max_blocks)
+                g = self.graphs[(T, max_blocks)]
             graph, dev, out = g
             dev.copy_(host_t[:lay.size], non_blocking=True)
             graph.replay()
@@ -214,9 +227,10 @@ class ModelRunner:
         return ids.tolist()
 
     # ------------------------------------------------------------------------------------------
-    def _capture(self, bucket: int) -> None:
-        """Capture the decode forward for `bucket` rows (largest buckets first avoids buffer growth)."""
-        lay = _Layout(bucket, bucket, self.max_blocks, prefill=False)
+    def _capture(self, bucket: int, max_blocks: int) -> None:
+        """Capture the decode forward for `bucket` rows and a `max_blocks`-wide block table
+        (largest first avoids workspace growth)."""
+        lay = _Layout(bucket, bucket, max_blocks, prefill=False)
         dev = torch.zeros(lay.size, dtype=torch.int32, device=self.device)
         host = self._host(lay.size, "capture")
         hn = host.numpy()
@@ -237,14 +251,15 @@ class ModelRunner:
         with torch.cuda.graph(g, pool=self._graph_pool):
             out = self.model.forward(fb, self.kv)
         torch.cuda.synchronize()
-        self.graphs[bucket] = (g, dev, out)
+        self.graphs[(bucket, max_blocks)] = (g, dev, out)
 
     def capture_all(self) -> float:
         t0 = time.perf_counter()
         if self.use_graphs:
-            for b in sorted(self.buckets, reverse=True):
-                if b not in self.graphs:
-                    self._capture(b)
+            for mb in sorted(self.ctx_blocks, reverse=True):
+                for b in sorted(self.buckets, reverse=True):
+                    if (b, mb) not in self.graphs:
+                        self._capture(b, mb)
         return time.perf_counter() - t0
 
     # ------------------------------------------------------------------------------------------

@@ -97,13 +97,14 @@ class Workspace:
     buffers: dict = field(default_factory=dict)
     retired: list = field(default_factory=list)
 
-    def get(self, name: str, shape, dtype, device) -> torch.Tensor:
+    def get(self, name: str, shape, dtype, device, zeros: bool = False) -> torch.Tensor:
+        """``zeros``: zero-fill on (re)allocation only -- for state the kernels keep re-armed themselves."""
         numel = math.prod(shape)
         buf = self.buffers.get((name, dtype))
         if buf is None or buf.numel() < numel:
             if buf is not None:
                 self.retired.append(buf)
-            buf = torch.empty(numel, dtype=dtype, device=device)
+            buf = (torch.zeros if zeros else torch.empty)(numel, dtype=dtype, device=device)
             self.buffers[(name, dtype)] = buf
         return buf[:numel].view(*shape)
 
@@ -172,7 +173,8 @@ class TransformerLM:
             max_parts = (b.block_tables.shape[1] * kv.block_size + 255) // 256
             tmp_o = self._buf("tmp_o", (b.num_seqs, self.hq, max_parts, self.D), torch.float32)
             tmp_ml = self._buf("tmp_ml", (b.num_seqs, self.hq, max_parts, 2), torch.float32)
-            ops.attn_decode(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, attn, tmp_o, tmp_ml, self.scale)
+            cnt = self.ws.get("attn_counters", (b.num_seqs * self.hkv,), torch.int32, self.device, zeros=True)
+            ops.attn_decode(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, attn, tmp_o, tmp_ml, cnt, self.scale)
         else:
             ops.attn_prefill(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, b.cu_q, b.tiles, attn, self.scale)
 

@@ -73,9 +73,11 @@ def rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv,
     return reference.rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, perm)
 
 
-def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, scale):
+def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters, scale):
+    """Split-KV paged decode attention.  ``counters``: int32 [>= num_seqs * Hkv], zero-initialised once;
+    the kernel re-arms it (graph-replay safe)."""
     if _gpu(q):
-        return _native.ops().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml,
+        return _native.ops().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters,
                                          float(scale))
     return reference.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, scale)
 

@@ -118,11 +118,17 @@ def test_attn_decode(gpu, Hq, Hkv, BS):
     tmp_o = torch.empty(S, Hq, max_parts, 128, device=gpu)
     tmp_ml = torch.empty(S, Hq, max_parts, 2, device=gpu)
     out = torch.empty(S, Hq, 128, device=gpu, dtype=torch.bfloat16)
+    cnt = torch.zeros(S * Hkv, device=gpu, dtype=torch.int32)
     scale = 1 / math.sqrt(128)
-    ops.attn_decode(q, kc, vc, bt, ctx, out, tmp_o, tmp_ml, scale)
+    ops.attn_decode(q, kc, vc, bt, ctx, out, tmp_o, tmp_ml, cnt, scale)
     out_r = torch.empty(S, Hq, 128, dtype=torch.bfloat16)
     ref.attn_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), ctx.cpu(), out_r, scale=scale)
     _close(out, out_r, atol=2e-2, rtol=2e-2)
+    # the in-kernel split-KV combine re-arms its arrival counters: a second call is identical
+    assert int(cnt.abs().sum()) == 0
+    out2 = torch.empty_like(out)
+    ops.attn_decode(q, kc, vc, bt, ctx, out2, tmp_o, tmp_ml, cnt, scale)
+    assert torch.equal(out, out2)
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 8)])
