@@ -45,8 +45,9 @@ class NativeBackend(Backend):
         if self._engine is None:
             ecfg = EngineConfig.from_provider(self.cfg, **self._overrides)
             self._engine = await asyncio.to_thread(LLMEngine, ecfg)
-            if self._engine.runner.use_graphs:
-                await asyncio.to_thread(self._engine.runner.capture_all)
+            if self._engine.device.type != "cpu":
+                # start-up warmup (prefill size classes + decode hipGraphs) before the first client
+                await asyncio.to_thread(self._engine.warmup)
         self.aengine = AsyncEngine(self._engine)
         self.aengine.start()
 

@@ -234,6 +234,22 @@ class LLMEngine:
                 self._emit(cb, out)
         return outs
 
+    def warmup(self, prompt_lens=None) -> float:
+        """Provider start-up pass: one prefill per size class (library GEMM heuristics and code objects
+        load here, not in the first client's TTFT), then capture the decode hipGraphs.  Returns seconds."""
+        t0 = time.perf_counter()
+        limit = min(self.scheduler.cfg.max_num_batched_tokens, self.scheduler.cfg.max_model_len - 4)
+        lens = prompt_lens or [n for n in (1, 16, 64, 128, 256, 512, 1024, 2048, 4096, 8192) if n <= limit]
+        vocab = self.model_cfg.vocab_size
+        for n in lens:
+            ids = [(7 * i + 3) % (vocab - 1) + 1 for i in range(n)]
+            seq = self.add_request(f"__warmup-{n}", ids, SamplingParams(max_tokens=2, ignore_eos=True))
+            while not seq.status.finished:
+                self.step()
+        self.runner.capture_all()
+        self.metrics = EngineMetrics()
+        return time.perf_counter() - t0
+
     def generate(self, prompt_ids: list, params: SamplingParams | None = None) -> list[int]:
         """Blocking single-request helper (tests, smoke)."""
         rid = f"gen-{time.monotonic_ns()}"
