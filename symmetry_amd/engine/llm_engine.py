@@ -63,7 +63,8 @@ class EngineConfig:
             ec.max_num_seqs = int(mc)
         m = {"weights": "weights", "tokenizer": "tokenizer", "seed": "seed", "maxBatchTokens": "max_num_batched_tokens",
              "maxModelLen": "max_model_len", "kvCacheFraction": "kv_cache_fraction", "blockSize": "block_size",
-             "maxTokens": "default_max_tokens", "tensorParallelSize": "tp_size", "device": "device",
+             "maxTokens": "default_max_tokens", "tensorParallelSize": "tp_size", "expertParallelSize": "ep_size",
+             "device": "device",
              "useGraphs": "use_graphs", "numKvBlocks": "num_kv_blocks"}
         for k, attr in m.items():
             if cfg.get(k) is not None:
@@ -121,12 +122,24 @@ class LLMEngine:
                             max_num_batched_tokens=cfg.max_num_batched_tokens, max_model_len=max_model_len),
             self.blocks)
         self.runner = ModelRunner(self.model, self.kv, self.scheduler.cfg.max_num_seqs, max_model_len,
-                                  use_graphs=cfg.use_graphs and cfg.tp_size == 1 and cfg.ep_size == 1,
+                                  use_graphs=cfg.use_graphs and self._graph_safe(tp_comm, ep_comm),
                                   tp_rank=cfg.tp_rank, tp_size=cfg.tp_size, cpu_group=cpu_group)
         self.requests: dict[str, tuple] = {}
         self.lock = threading.Lock()
 
     # ------------------------------------------------------------------------------------------
+    def _graph_safe(self, tp_comm, ep_comm) -> bool:
+        """Decode hipGraphs need every collective to be capturable (our RCCL communicator) and no
+        host-side data-dependent shapes (all-to-all expert dispatch reads counts on the host)."""
+        from ..parallel.comm import RcclComm
+
+        for c in (tp_comm, ep_comm):
+            if c is not None and getattr(c, "world", 1) > 1 and not isinstance(c, RcclComm):
+                return False
+        if self.model.moe is not None and self.model.moe.ep > 1 and self.model.moe.mode != "allreduce":
+            return False
+        return True
+
     def _auto_blocks(self, max_model_len: int) -> int:
         per_block = self.model_cfg.kv_bytes_per_token() // self.cfg.tp_size * self.cfg.block_size
         if self.device.type == "cpu":

@@ -27,6 +27,7 @@ from .scheduler import ScheduledBatch
 
 DECODE_BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64)
 CTX_BUCKETS = (256, 1024, 4096, 16384, 65536, 131072)  # tokens
+CMD_STOP, CMD_CAPTURE = -1, 2  # control headers of the rank-0 -> worker metadata plane
 _SEED_MIX = 0x9E3779B97F4A7C15
 
 
@@ -254,11 +255,16 @@ class ModelRunner:
         self.graphs[(bucket, max_blocks)] = (g, dev, out)
 
     def capture_all(self) -> float:
+        """Rank 0: capture every (batch, context) decode graph; under TP each capture is mirrored by the
+        workers (the graphs contain RCCL collectives, so all ranks must capture together)."""
         t0 = time.perf_counter()
         if self.use_graphs:
             for mb in sorted(self.ctx_blocks, reverse=True):
                 for b in sorted(self.buckets, reverse=True):
                     if (b, mb) not in self.graphs:
+                        if self.tp_size > 1:
+                            self._broadcast(np.array([CMD_CAPTURE, b, b, mb, 0, b], dtype=np.int32),
+                                            torch.zeros(0, dtype=torch.int32))
                         self._capture(b, mb)
         return time.perf_counter() - t0
 
@@ -277,7 +283,7 @@ class ModelRunner:
         if self.tp_size > 1:
             import torch.distributed as dist
 
-            h = torch.tensor([-1, 0, 0, 0, 0, 0, 0], dtype=torch.int32)
+            h = torch.tensor([CMD_STOP, 0, 0, 0, 0, 0, 0], dtype=torch.int32)
             dist.broadcast(h, src=0, group=self.cpu_group)
 
     def worker_loop(self) -> None:
@@ -288,11 +294,14 @@ class ModelRunner:
             h = torch.zeros(7, dtype=torch.int32)
             dist.broadcast(h, src=0, group=self.cpu_group)
             header = h.numpy()
-            if header[0] < 0:
+            if header[0] == CMD_STOP:
                 return
             n = int(header[6])
             host_t = self._host(max(n, 1), "worker")
             buf = torch.zeros(max(n, 1), dtype=torch.int32)
             dist.broadcast(buf, src=0, group=self.cpu_group)
             host_t.copy_(buf)
+            if header[0] == CMD_CAPTURE:
+                self._capture(int(header[1]), int(header[3]))
+                continue
             self._run(header[:6], host_t)

@@ -38,14 +38,28 @@ def make_comms(on_gpu: bool):
 
 
 def init_tp_engine(ecfg):
-    """Build this rank's tensor-parallel engine shard; returns (engine, rank)."""
+    """Build this rank's engine shard; returns (engine, rank).
+
+    Dense models: tensor parallel over all ranks.  MoE models (Mixtral, BASELINE config 5): attention
+    tensor parallel over all ranks and the experts expert-parallel over the same ranks (E / world experts
+    per GPU), sharing one communicator; the expert outputs are combined by all-reduce (tokens are
+    replicated by the TP attention) or all-to-all dispatch (``moe.mode = "a2a"``).
+    """
     from ..engine.llm_engine import LLMEngine
+    from ..models.config import resolve
 
     rank, world, local = init_distributed()
     on_gpu = torch.cuda.is_available() and ecfg.device != "cpu"
     comm, cpu_group = make_comms(on_gpu)
     ecfg.tp_size, ecfg.tp_rank = world, rank
+    mcfg = ecfg.model_config or resolve(ecfg.model)
+    ep_comm = None
+    if mcfg.is_moe and world > 1:
+        if mcfg.num_experts % world:
+            raise ValueError(f"{mcfg.num_experts} experts do not shard over {world} ranks")
+        ecfg.ep_size, ecfg.ep_rank = world, rank
+        ep_comm = comm
     if on_gpu:
         ecfg.device = f"cuda:{local}"
-    engine = LLMEngine(ecfg, tp_comm=comm, cpu_group=cpu_group)
+    engine = LLMEngine(ecfg, tp_comm=comm, ep_comm=ep_comm, cpu_group=cpu_group)
     return engine, rank

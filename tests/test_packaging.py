@@ -29,7 +29,7 @@ def test_install_scripts_parse():
     assert "symmetry_amd.cli --init" in ps1
 
 
-def test_cli_version_and_init(tmp_path):
+def test_cli_init_writes_install_defaults(tmp_path):
     out = subprocess.run([sys.executable, "-m", "symmetry_amd.cli", "--version"], capture_output=True, text=True,
                          cwd=ROOT, check=True)
     assert out.stdout.strip() == "1.0.0"  # reference src/symmetry.ts:11

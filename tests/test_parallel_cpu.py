@@ -83,12 +83,12 @@ def test_comm_primitives():
     assert b[3] == [[2.0, 3.0], [4.0, 5.0], [104.0, 105.0]]
 
 
-def _tp_worker(rank, world):
+def _tp_worker(rank, world, model="tiny-llama"):
     from symmetry_amd.engine.llm_engine import EngineConfig
     from symmetry_amd.engine.sequence import SamplingParams
     from symmetry_amd.parallel.launch import init_tp_engine
 
-    ecfg = EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=4, max_model_len=256, block_size=32,
+    ecfg = EngineConfig(model=model, device="cpu", max_num_seqs=4, max_model_len=256, block_size=32,
                         weight_init="full")
     eng, r = init_tp_engine(ecfg)
     if r != 0:
@@ -102,14 +102,19 @@ def _tp_worker(rank, world):
     return [s.output_ids for s in seqs]
 
 
-def test_tp2_matches_tp1():
+def _tp_ep_worker(rank, world):
+    return _tp_worker(rank, world, model="tiny-mixtral")
+
+
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-mixtral"])
+def test_tp2_matches_tp1(model):
+    """tiny-llama: TP=2.  tiny-mixtral: attention TP=2 + experts EP=2 (BASELINE config 5 layout)."""
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
-    from symmetry_amd.engine.sequence import SamplingParams
     from symmetry_amd.models import reference_model as rm
 
-    res = _run(_tp_worker)
+    res = _run(_tp_worker if model == "tiny-llama" else _tp_ep_worker)
     tp_out = res[0][1]
-    eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=4, max_model_len=256, block_size=32,
+    eng = LLMEngine(EngineConfig(model=model, device="cpu", max_num_seqs=4, max_model_len=256, block_size=32,
                                  weight_init="full"))
     prompts = [list(range(5, 40)), list(range(100, 120)), list(range(7, 9))]
     for p, out in zip(prompts, tp_out):
@@ -153,3 +158,34 @@ def test_expert_parallel_modes_match_local_moe():
     for _, r in res:
         assert r["allreduce"], r
         assert r["a2a"], r
+
+
+def _capture_worker(rank, world):
+    from symmetry_amd.engine.llm_engine import EngineConfig
+    from symmetry_amd.parallel.launch import init_tp_engine
+
+    ecfg = EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=4, max_model_len=1024, block_size=32,
+                        weight_init="full")
+    eng, r = init_tp_engine(ecfg)
+    runner = eng.runner
+    seen = []
+
+    def fake_capture(bucket, max_blocks):  # records what a GPU rank would capture (graphs need a GPU)
+        seen.append((bucket, max_blocks))
+        runner.graphs[(bucket, max_blocks)] = None
+
+    runner._capture = fake_capture
+    runner.use_graphs = True
+    if r != 0:
+        runner.worker_loop()
+        return seen
+    runner.capture_all()
+    eng.shutdown()
+    return seen
+
+
+def test_tp_graph_capture_is_mirrored_on_every_rank():
+    """Decode graphs hold RCCL collectives: every rank must capture the same (batch, context) graphs in
+    the same order, driven by rank 0's capture commands on the metadata plane."""
+    (_, a), (_, b) = _run(_capture_worker)
+    assert a == b and len(a) == len(set(a)) > 4
