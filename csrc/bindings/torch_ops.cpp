@@ -540,6 +540,29 @@ void add_prep(const Tensor& delta, Tensor& resid, const Tensor& w, Tensor& xw, T
                   (int)d, cur_stream(resid));
 }
 
+void sample_filtered(const Tensor& logits, const Tensor& temps, const Tensor& top_k, const Tensor& top_p,
+                     const Tensor& seeds, const Tensor& step, Tensor& out_ids) {
+  check_gpu(logits, "logits");
+  check_dtype(logits, at::kFloat, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "sample_filtered: logits [B, V] contiguous");
+  const int64_t B = logits.size(0), V = logits.size(1);
+  for (const Tensor* t : {&temps, &top_k, &top_p, &seeds, &step, static_cast<const Tensor*>(&out_ids)})
+    check_gpu(*t, "sampling tensor");
+  check_dtype(temps, at::kFloat, "temps");
+  check_dtype(top_k, at::kInt, "top_k");
+  check_dtype(top_p, at::kFloat, "top_p");
+  check_dtype(seeds, at::kLong, "seeds");
+  check_dtype(step, at::kLong, "step");
+  check_dtype(out_ids, at::kInt, "out_ids");
+  TORCH_CHECK(temps.numel() >= B && top_k.numel() >= B && top_p.numel() >= B && seeds.numel() >= B &&
+                  out_ids.numel() >= B && step.numel() >= 1,
+              "sample_filtered: per-row tensors too short");
+  const at::OptionalDeviceGuard g(logits.device());
+  launch_sample_filtered(ptr<float>(logits), (int)B, (int)V, ptr<float>(temps), ptr<int>(top_k), ptr<float>(top_p),
+                         reinterpret_cast<const long long*>(seeds.data_ptr()),
+                         reinterpret_cast<const long long*>(step.data_ptr()), ptr<int>(out_ids), cur_stream(logits));
+}
+
 void rownorm(const Tensor& xw, const Tensor& ss, double eps, Tensor& out) {
   check_gpu(xw, "xw");
   check_dtype(xw, at::kBFloat16, "xw");
@@ -599,6 +622,10 @@ TORCH_LIBRARY(symmetry_amd, m) {
         &embed_prep);
   m.def("add_prep(Tensor delta, Tensor(a!) resid, Tensor w, Tensor(b!) xw, Tensor(c!) ss) -> ()", &add_prep);
   m.def("rownorm(Tensor xw, Tensor ss, float eps, Tensor(a!) out) -> ()", &rownorm);
+  m.def(
+      "sample_filtered(Tensor logits, Tensor temps, Tensor top_k, Tensor top_p, Tensor seeds, Tensor step, "
+      "Tensor(a!) out_ids) -> ()",
+      &sample_filtered);
   m.def("decode_gemm_variant(int v) -> ()", [](int64_t v) { set_decode_gemm_variant((int)v); });
   m.def("grouped_skinny(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y) -> ()", &grouped_skinny);
   m.def(

@@ -75,6 +75,11 @@ void launch_skinny_gemm_argmax(const bf16* x, const bf16* W, float* logits_or_nu
 void launch_argmax_reduce(const unsigned long long* tile_keys, int M, int ntiles, unsigned long long* out_keys,
                           int* out_ids, hipStream_t s);
 
+// sampling.hip: temperature + top-k + top-p over full-vocab fp32 logits [B, V]; rows without a
+// filter (or greedy) keep out_ids untouched
+void launch_sample_filtered(const float* logits, int B, int V, const float* temps, const int* top_k, const float* top_p,
+                            const long long* seeds, const long long* step, int* out_ids, hipStream_t s);
+
 // activation.hip
 void launch_swiglu(LinOut gu, bf16* out, int T, int F, hipStream_t s, int interleaved = 0);
 

@@ -107,7 +107,7 @@ def build_kernels(verbose: bool = False, force: bool = False) -> str:
         bobj = os.path.join(OBJ, "bind_" + os.path.basename(bsrc) + ".o")
         objs.append(bobj)
         if force or _newer(bobj, [bsrc] + headers):
-            cmd = [HIPCC, "-c", bsrc, "-o", bobj, "-I", kdir, "-O2", "-std=c++17", "-fPIC",
+            cmd = [HIPCC, "-c", bsrc, "-o", bobj, "-I", kdir, "-O2", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
                    "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
                    "-DTORCH_EXTENSION_NAME=_C", "-Wno-unused-result", "-Wno-deprecated-declarations"]
             for i in tinc:

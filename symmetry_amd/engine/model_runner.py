@@ -28,6 +28,7 @@ from .scheduler import ScheduledBatch
 DECODE_BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64)
 CTX_BUCKETS = (256, 1024, 4096, 16384, 65536, 131072)  # tokens
 CMD_STOP, CMD_CAPTURE = -1, 2  # control headers of the rank-0 -> worker metadata plane
+HEADER_LEN = 7  # kind, T, rows, max_blocks, prefill tiles, real seqs, filtered-sampling flag
 _SEED_MIX = 0x9E3779B97F4A7C15
 
 
@@ -55,6 +56,8 @@ class _Layout:
         self.slots = take(T)
         self.ctx = take(nseq)
         self.temps = take(nseq)
+        self.topk = take(nseq)
+        self.topp = take(nseq)
         if off % 2:
             take(1)
         self.seeds = take(2 * nseq)
@@ -76,6 +79,8 @@ class _Layout:
             "slot_mapping": buf[self.slots:self.slots + self.T],
             "ctx_lens": buf[self.ctx:self.ctx + self.nseq],
             "temps": buf[self.temps:self.temps + self.nseq].view(torch.float32),
+            "top_k": buf[self.topk:self.topk + self.nseq],
+            "top_p": buf[self.topp:self.topp + self.nseq].view(torch.float32),
             "seeds": buf[self.seeds:self.seeds + 2 * self.nseq].view(torch.int64),
             "step": buf[self.step:self.step + 2].view(torch.int64),
             "block_tables": buf[self.bt:self.bt + self.nseq * self.max_blocks].view(self.nseq, self.max_blocks),
@@ -122,7 +127,7 @@ class ModelRunner:
     def _fill(self, lay: _Layout, host: np.ndarray, seqs, counts, pad_to: int | None = None) -> None:
         BS = self.block_size
         ids, pos, slots = [], [], []
-        ctx, temps, seeds = [], [], []
+        ctx, temps, seeds, topk, topp = [], [], [], [], []
         for seq, n in zip(seqs, counts):
             start = seq.num_computed
             toks = seq.token_ids[start:start + n]
@@ -133,6 +138,8 @@ class ModelRunner:
             slots.append(bt[p // BS] * BS + p % BS)
             ctx.append(start + n)
             temps.append(seq.params.temperature)
+            topk.append(seq.params.top_k)
+            topp.append(seq.params.top_p)
             seeds.append(_seq_seed(seq.sampling_seed, len(seq.output_ids)))
         nreal = len(seqs)
         T = lay.T
@@ -145,6 +152,9 @@ class ModelRunner:
         host[lay.ctx:lay.ctx + nreal] = ctx
         host[lay.ctx + nreal:lay.ctx + lay.nseq] = 1
         host[lay.temps:lay.temps + nreal] = np.asarray(temps, dtype=np.float32).view(np.int32)
+        host[lay.topk:lay.topk + nreal] = topk
+        host[lay.topp:lay.topp + lay.nseq] = np.ones(lay.nseq, dtype=np.float32).view(np.int32)
+        host[lay.topp:lay.topp + nreal] = np.asarray(topp, dtype=np.float32).view(np.int32)
         host[lay.seeds:lay.seeds + 2 * nreal] = np.asarray(seeds, dtype=np.int64).view(np.int32)
         btv = host[lay.bt:lay.bt + lay.nseq * lay.max_blocks].reshape(lay.nseq, lay.max_blocks)
         for i, seq in enumerate(seqs):
@@ -159,9 +169,15 @@ class ModelRunner:
             host[lay.tiles:lay.tiles + 2 * len(tiles)] = np.asarray(tiles, dtype=np.int32).reshape(-1)
             host[lay.last:lay.last + 2 * lay.nseq] = (cu[1:] - 1).astype(np.int64).view(np.int32)
 
-    def _forward_batch(self, kind: str, lay: _Layout, dev: torch.Tensor, nseq: int, need_logits=False):
+    def _forward_batch(self, kind: str, lay: _Layout, dev: torch.Tensor, nseq: int, need_logits=False,
+                       filtered=False):
         v = lay.views(dev)
-        return ForwardBatch(kind=kind, num_seqs=nseq, need_logits=need_logits, **v)
+        return ForwardBatch(kind=kind, num_seqs=nseq, need_logits=need_logits, filtered=filtered, **v)
+
+    @staticmethod
+    def _filtered(seqs) -> bool:
+        """Does any row need the full-vocab top-k / top-p sampler (temperature > 0 and a filter)?"""
+        return any(s.params.temperature > 0 and (s.params.top_k > 0 or s.params.top_p < 1.0) for s in seqs)
 
     # ------------------------------------------------------------------------------------------
     def execute(self, batch: ScheduledBatch) -> list[int]:
@@ -181,8 +197,8 @@ class ModelRunner:
         host_t = self._host(lay.size, batch.kind)
         host = host_t.numpy()
         self._fill(lay, host, seqs, counts)
-        header = np.array([0 if batch.kind == "decode" else 1, lay.T, lay.nseq, lay.max_blocks, lay.ntiles, nseq],
-                          dtype=np.int32)
+        header = np.array([0 if batch.kind == "decode" else 1, lay.T, lay.nseq, lay.max_blocks, lay.ntiles, nseq,
+                           int(self._filtered(seqs))], dtype=np.int32)
         if self.tp_size > 1:
             self._broadcast(header, host_t)
         ids = self._run(header, host_t)
@@ -204,13 +220,14 @@ class ModelRunner:
 
     def _run(self, header: np.ndarray, host_t: torch.Tensor) -> list[int]:
         kind = "decode" if header[0] == 0 else "prefill"
-        T, nseq_l, max_blocks, ntiles, nseq = (int(x) for x in header[1:6])
+        T, nseq_l, max_blocks, ntiles, nseq, filt = (int(x) for x in header[1:HEADER_LEN])
         lay = _Layout(T, nseq_l, max_blocks, prefill=kind == "prefill", ntiles=ntiles)
         if kind == "decode" and self.use_graphs:
-            g = self.graphs.get((T, max_blocks))
+            key = (T, max_blocks, bool(filt))
+            g = self.graphs.get(key)
             if g is None:
-                self._capture(T, max_blocks)
-                g = self.graphs[(T, max_blocks)]
+                self._capture(T, max_blocks, bool(filt))
+                g = self.graphs[key]
             graph, dev, out = g
             dev.copy_(host_t[:lay.size], non_blocking=True)
             graph.replay()
@@ -218,7 +235,7 @@ class ModelRunner:
         else:
             dev = self.model.ws.get("meta." + kind, (lay.size,), torch.int32, self.device)
             dev.copy_(host_t[:lay.size], non_blocking=True)
-            fb = self._forward_batch(kind, lay, dev, nseq_l)
+            fb = self._forward_batch(kind, lay, dev, nseq_l, filtered=bool(filt))
             ids = self.model.forward(fb, self.kv)
         if self.is_gpu:
             out_host = self._host(ids.numel(), "ids_out")
@@ -228,16 +245,16 @@ class ModelRunner:
         return ids.tolist()
 
     # ------------------------------------------------------------------------------------------
-    def _capture(self, bucket: int, max_blocks: int) -> None:
-        """Capture the decode forward for `bucket` rows and a `max_blocks`-wide block table
-        (largest first avoids workspace growth)."""
+    def _capture(self, bucket: int, max_blocks: int, filtered: bool = False) -> None:
+        """Capture the decode forward for `bucket` rows and a `max_blocks`-wide block table, with or
+        without the top-k / top-p resampler (largest first avoids workspace growth)."""
         lay = _Layout(bucket, bucket, max_blocks, prefill=False)
         dev = torch.zeros(lay.size, dtype=torch.int32, device=self.device)
         host = self._host(lay.size, "capture")
         hn = host.numpy()
         self._fill(lay, hn, [], [])
         dev.copy_(host[:lay.size])
-        fb = self._forward_batch("decode", lay, dev, bucket)
+        fb = self._forward_batch("decode", lay, dev, bucket, filtered=filtered)
         # eager warmup: allocates workspace and loads kernels outside the capture
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -252,7 +269,7 @@ class ModelRunner:
         with torch.cuda.graph(g, pool=self._graph_pool):
             out = self.model.forward(fb, self.kv)
         torch.cuda.synchronize()
-        self.graphs[(bucket, max_blocks)] = (g, dev, out)
+        self.graphs[(bucket, max_blocks, filtered)] = (g, dev, out)
 
     def capture_all(self) -> float:
         """Rank 0: capture every (batch, context) decode graph; under TP each capture is mirrored by the
@@ -261,9 +278,9 @@ class ModelRunner:
         if self.use_graphs:
             for mb in sorted(self.ctx_blocks, reverse=True):
                 for b in sorted(self.buckets, reverse=True):
-                    if (b, mb) not in self.graphs:
+                    if (b, mb, False) not in self.graphs:
                         if self.tp_size > 1:
-                            self._broadcast(np.array([CMD_CAPTURE, b, b, mb, 0, b], dtype=np.int32),
+                            self._broadcast(np.array([CMD_CAPTURE, b, b, mb, 0, b, 0], dtype=np.int32),
                                             torch.zeros(0, dtype=torch.int32))
                         self._capture(b, mb)
         return time.perf_counter() - t0
@@ -283,7 +300,7 @@ class ModelRunner:
         if self.tp_size > 1:
             import torch.distributed as dist
 
-            h = torch.tensor([CMD_STOP, 0, 0, 0, 0, 0, 0], dtype=torch.int32)
+            h = torch.tensor([CMD_STOP] + [0] * HEADER_LEN, dtype=torch.int32)
             dist.broadcast(h, src=0, group=self.cpu_group)
 
     def worker_loop(self) -> None:
@@ -291,17 +308,17 @@ class ModelRunner:
         import torch.distributed as dist
 
         while True:
-            h = torch.zeros(7, dtype=torch.int32)
+            h = torch.zeros(HEADER_LEN + 1, dtype=torch.int32)
             dist.broadcast(h, src=0, group=self.cpu_group)
             header = h.numpy()
             if header[0] == CMD_STOP:
                 return
-            n = int(header[6])
+            n = int(header[HEADER_LEN])
             host_t = self._host(max(n, 1), "worker")
             buf = torch.zeros(max(n, 1), dtype=torch.int32)
             dist.broadcast(buf, src=0, group=self.cpu_group)
             host_t.copy_(buf)
             if header[0] == CMD_CAPTURE:
-                self._capture(int(header[1]), int(header[3]))
+                self._capture(int(header[1]), int(header[3]), bool(header[6]))
                 continue
-            self._run(header[:6], host_t)
+            self._run(header[:HEADER_LEN], host_t)

@@ -63,6 +63,9 @@ class ForwardBatch:
     tiles: torch.Tensor | None = None       # [n_tiles, 2] int32
     last_idx: torch.Tensor | None = None    # [num_seqs] int64 row of each sequence's last token
     need_logits: bool = False
+    top_k: torch.Tensor | None = None       # [num_seqs] int32 (0 = off)
+    top_p: torch.Tensor | None = None       # [num_seqs] f32 (1 = off)
+    filtered: bool = False                  # some row needs the top-k / top-p resampler
 
     @property
     def num_tokens(self) -> int:
@@ -237,10 +240,10 @@ class TransformerLM:
         ids = self._buf("ids", (n,), torch.int32)
         keys = self._buf("keys", (n,), torch.int64)
         tk = self._buf("tile_keys", (n * (self.vocab_shard // 16),), torch.int64)
-        logits = self._buf("logits", (n, self.vocab_shard), torch.float32) if b.need_logits else None
+        logits = self._buf("logits", (n, self.vocab_shard), torch.float32) if b.need_logits or b.filtered else None
         ops.dg_argmax(xl, w["lm_head"], sl, eps, b.temps, b.seeds, b.step, tk, keys, ids,
                       self.tp_rank * self.vocab_shard, logits)
-        return self._combine_tp(ids, keys, logits)
+        return self._finish_sampling(b, ids, keys, logits)
 
     # ------------------------------------------------------------------------------------------
     def _forward_general(self, b: ForwardBatch, kv: KVCache) -> torch.Tensor:
@@ -279,14 +282,25 @@ class TransformerLM:
         ids = self._buf("ids", (n,), torch.int32)
         keys = self._buf("keys", (n,), torch.int64)
         ntiles = self.vocab_shard // 16
-        logits = self._buf("logits", (n, self.vocab_shard), torch.float32) if b.need_logits else None
+        logits = self._buf("logits", (n, self.vocab_shard), torch.float32) if b.need_logits or b.filtered else None
         for m0 in range(0, n, SKINNY_MAX_M):
             m1 = min(n, m0 + SKINNY_MAX_M)
             tk = self._buf("tile_keys", ((m1 - m0) * ntiles,), torch.int64)
             ops.lm_head_sample(xl[m0:m1].contiguous() if m0 or m1 < n else xl, self.w["lm_head"],
                                b.temps[m0:m1], b.seeds[m0:m1], b.step, tk, keys[m0:m1], ids[m0:m1],
                                self.tp_rank * self.vocab_shard, logits[m0:m1] if logits is not None else None)
-        return self._combine_tp(ids, keys, logits)
+        return self._finish_sampling(b, ids, keys, logits)
+
+    def _finish_sampling(self, b: ForwardBatch, ids, keys, logits) -> torch.Tensor:
+        """TP combine of the fused sampler's keys, then the top-k / top-p resampler for rows that ask."""
+        ids = self._combine_tp(ids, keys, logits)
+        if b.filtered:
+            full = logits
+            if self._tp_active():
+                g = self.tp.all_gather(logits)  # [tp * n, V / tp]
+                full = g.view(self.tp_size, logits.shape[0], -1).permute(1, 0, 2).reshape(logits.shape[0], -1)
+            ops.sample_filtered(full, b.temps, b.top_k, b.top_p, b.seeds, b.step, ids)
+        return ids
 
     def _combine_tp(self, ids, keys, logits) -> torch.Tensor:
         if self._tp_active():

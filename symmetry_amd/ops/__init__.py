@@ -35,6 +35,7 @@ __all__ = [
     "embed_prep",
     "add_prep",
     "rownorm",
+    "sample_filtered",
     "linear",
     "choose_splits",
 ]
@@ -176,6 +177,13 @@ def moe_combine(y, dst, ids, e_lo, e_hi, w, k, out, accumulate=False):
     if _gpu(out):
         return _native.ops().moe_combine(y, dst, ids, int(e_lo), int(e_hi), w, int(k), out, bool(accumulate))
     return reference.moe_combine(y, dst, ids, e_lo, e_hi, w, k, out, accumulate)
+
+
+def sample_filtered(logits, temps, top_k, top_p, seeds, step, out_ids):
+    """Resample rows that request top-k / top-p (temperature > 0) from full-vocab fp32 logits."""
+    if _gpu(logits):
+        return _native.ops().sample_filtered(logits, temps, top_k, top_p, seeds, step, out_ids)
+    return reference.sample_filtered(logits, temps, top_k, top_p, seeds, step, out_ids)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

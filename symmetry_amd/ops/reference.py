@@ -363,3 +363,36 @@ def moe_combine(y, dst, ids, e_lo: int, e_hi: int, w, k: int, out, accumulate: b
         out.add_(res)
     else:
         out.copy_(res)
+
+
+def sample_filtered(logits, temps, top_k, top_p, seeds, step, out_ids) -> None:
+    """Temperature + top-k + top-p (nucleus) resampling of full-vocab rows (csrc/kernels/sampling.hip).
+
+    Kept set = {tokens whose logit >= the k-th largest} intersected with the smallest descending prefix
+    whose probability mass reaches top_p (ties at the threshold are kept).  Rows with t == 0 or without a
+    filter are left untouched.  Same RNG stream as the fused lm_head sampler."""
+    st = int(step.reshape(-1)[0])
+    B, V = logits.shape
+    for r in range(B):
+        t, k, p = float(temps[r]), int(top_k[r]), float(top_p[r])
+        use_k, use_p = 0 < k < V, p < 1.0
+        if t <= 0 or not (use_k or use_p):
+            continue
+        l = logits[r].float()
+        thr = -float("inf")
+        srt = torch.sort(l, descending=True).values
+        if use_k:
+            thr = max(thr, float(srt[k - 1]))
+        if use_p:
+            w = torch.exp((srt - srt[0]) / t)
+            cum = torch.cumsum(w, 0)
+            j = int(torch.searchsorted(cum, max(p, 0.0) * float(w.sum())).clamp(max=V - 1))
+            thr = max(thr, float(srt[j]))
+        seed = int(seeds[r]) & 0xFFFFFFFFFFFFFFFF
+        mixed = seed ^ ((st << 20) & 0xFFFFFFFFFFFFFFFF)
+        if mixed >= 1 << 63:
+            mixed -= 1 << 64
+        u = uniform01(torch.tensor(mixed, dtype=torch.int64), torch.arange(V, dtype=torch.int64)).float()
+        v = l / t - torch.log(-torch.log(u.to(l.device)))
+        v = torch.where(l >= thr, v, torch.full_like(v, -float("inf")))
+        out_ids[r] = int(torch.argmax(v))

@@ -135,3 +135,21 @@ def test_rccl_single_rank_allreduce_and_capture(gpu):
     assert float(buf[0]) == 2.0
     comm.destroy()
     dist.destroy_process_group()
+
+
+def test_top_k_one_in_graph_equals_greedy(gpu):
+    """The filtered-sampling decode graph variant (full logits + sample_filtered kernel) with top_k=1
+    reproduces greedy decoding; a seeded top-p request is reproducible."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+
+    eng = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", max_num_seqs=4, max_model_len=512,
+                                 num_kv_blocks=32, use_graphs=True))
+    prompt = list(range(200, 237))
+    greedy = eng.generate(prompt, SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True))
+    k1 = eng.generate(prompt, SamplingParams(max_tokens=10, temperature=1.0, top_k=1, ignore_eos=True))
+    assert k1 == greedy
+    a = eng.generate(prompt, SamplingParams(max_tokens=10, temperature=0.9, top_p=0.8, seed=3, ignore_eos=True))
+    b = eng.generate(prompt, SamplingParams(max_tokens=10, temperature=0.9, top_p=0.8, seed=3, ignore_eos=True))
+    assert a == b
+    assert any(k[2] for k in eng.runner.graphs)  # the filtered graph variant was captured and used

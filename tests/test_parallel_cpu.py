@@ -170,9 +170,9 @@ def _capture_worker(rank, world):
     runner = eng.runner
     seen = []
 
-    def fake_capture(bucket, max_blocks):  # records what a GPU rank would capture (graphs need a GPU)
-        seen.append((bucket, max_blocks))
-        runner.graphs[(bucket, max_blocks)] = None
+    def fake_capture(bucket, max_blocks, filtered=False):  # records what a GPU rank would capture
+        seen.append((bucket, max_blocks, filtered))
+        runner.graphs[(bucket, max_blocks, filtered)] = None
 
     runner._capture = fake_capture
     runner.use_graphs = True
