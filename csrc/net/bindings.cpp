@@ -219,6 +219,8 @@ PYBIND11_MODULE(_native, m) {
              return t.write(id, std::move(d));
            })
       .def("end", &Transport::end, py::call_guard<py::gil_scoped_release>())
+      .def("inject_fault",
+           [](Transport& t, uint64_t id, int mode, py::bytes data) { t.inject_fault(id, mode, std::string(data)); })
       .def("destroy", &Transport::destroy, py::call_guard<py::gil_scoped_release>())
       .def("queued", &Transport::queued)
       .def("fileno", &Transport::fileno)

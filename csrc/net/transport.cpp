@@ -1,6 +1,7 @@
 // epoll-driven encrypted transport (see transport.h).
 #include "transport.h"
 
+#include <stdexcept>
 #include <arpa/inet.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -20,7 +21,7 @@ namespace symnet {
 namespace {
 constexpr uint64_t kListenTag = 1ull << 62;
 constexpr uint64_t kCmdTag = 1ull << 63;
-constexpr size_t kMaxFrame = (1u << 24) - 1;
+constexpr size_t kMaxFrame = 8u << 20;  // bytes of one encrypted frame (message + 17-byte AEAD overhead)
 
 int64_t now_ms() {
   return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
@@ -160,6 +161,14 @@ uint64_t Transport::connect(const std::string& host, int port) {
   }
   wake();
   return id;
+}
+
+void Transport::inject_fault(uint64_t id, int mode, std::string data) {
+  {
+    std::lock_guard<std::mutex> g(cmd_mu_);
+    cmds_.push_back(Cmd{Cmd::FAULT, id, std::move(data), {}, mode});
+  }
+  wake();
 }
 
 bool Transport::write(uint64_t id, std::string data) {
@@ -320,6 +329,15 @@ void Transport::handle_cmds() {
       c->shared->queued -= f.size() + 3;  // re-added by send_frame, released by flush as bytes leave
       send_frame(c, f.data(), f.size());
       c->shared->bytes_out += cmd.data.size();
+    } else if (cmd.kind == Cmd::FAULT) {
+      if (cmd.port == 0) {
+        c->wbuf.append(cmd.data);
+        if (c->shared) c->shared->queued += cmd.data.size();
+      } else if (c->phase == Conn::OPEN) {
+        Bytes f = c->tx.push((const uint8_t*)cmd.data.data(), cmd.data.size());
+        f[f.size() / 2] ^= 0x40;
+        send_frame(c, f.data(), f.size());
+      }
     } else if (cmd.kind == Cmd::END) {
       c->ending = true;
     } else if (cmd.kind == Cmd::DESTROY) {
@@ -471,6 +489,10 @@ void Transport::process_frames(Conn* c) {
     if (avail < 3) break;
     const uint8_t* p = (const uint8_t*)c->rbuf.data() + c->roff;
     const size_t n = p[0] | (p[1] << 8) | ((size_t)p[2] << 16);
+    if (n > kMaxFrame) {  // a peer announcing an oversized frame is broken or hostile: do not buffer it
+      close_conn(c, "protocol error: frame too large");
+      return;
+    }
     if (avail < 3 + n) break;
     c->roff += 3 + n;
     try {

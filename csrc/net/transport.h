@@ -59,6 +59,9 @@ class Transport {
   bool write(uint64_t id, std::string data);  // false: above the high watermark (message still queued)
   void end(uint64_t id);                     // flush queued messages, then close
   void destroy(uint64_t id);                 // close now
+  // Fault injection (tests): mode 0 appends `data` raw to the socket stream (bypassing
+  // framing and encryption); mode 1 frames + encrypts `data`, then flips one ciphertext bit.
+  void inject_fault(uint64_t id, int mode, std::string data);
   int fileno() const { return event_fd_; }
   std::vector<Event> poll();
   void close();
@@ -68,7 +71,7 @@ class Transport {
  private:
   struct Conn;
   struct Cmd {
-    enum Kind { CONNECT, WRITE, END, DESTROY } kind;
+    enum Kind { CONNECT, WRITE, END, DESTROY, FAULT } kind;
     uint64_t id;
     std::string data;
     std::string host;

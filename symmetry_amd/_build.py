@@ -135,7 +135,7 @@ def build_net(verbose: bool = False, force: bool = False) -> str:
     os.makedirs(OBJ, exist_ok=True)
     ndir = os.path.join(CSRC, "net")
     headers = glob.glob(os.path.join(ndir, "*.h"))
-    sources = sorted(glob.glob(os.path.join(ndir, "*.cpp")))
+    sources = sorted(s for s in glob.glob(os.path.join(ndir, "*.cpp")) if not s.endswith("selftest.cpp"))
     pyinc = sysconfig.get_paths()["include"]
     cxx = shutil.which("g++") or "c++"
     flags = ["-O2", "-g", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-fvisibility=hidden"]
@@ -155,6 +155,24 @@ def build_net(verbose: bool = False, force: bool = False) -> str:
     return NET_SO
 
 
+SELFTEST = os.path.join(ROOT, "build", "net_selftest_asan")
+
+
+def build_selftest(verbose: bool = False, force: bool = False) -> str:
+    """Host-only AddressSanitizer + UBSan build of the P2P plane and its self-test driver
+    (csrc/net/selftest.cpp).  GPU sanitizers are not used: this is CPU code."""
+    ndir = os.path.join(CSRC, "net")
+    srcs = [os.path.join(ndir, f) for f in ("crypto.cpp", "noise.cpp", "transport.cpp", "selftest.cpp")]
+    headers = glob.glob(os.path.join(ndir, "*.h"))
+    os.makedirs(os.path.dirname(SELFTEST), exist_ok=True)
+    if force or _newer(SELFTEST, srcs + headers):
+        cxx = shutil.which("g++") or "c++"
+        _run([cxx, "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+              "-fno-sanitize-recover=undefined", "-I", ndir] + srcs + ["-o", SELFTEST, "-lcrypto", "-lpthread"],
+             verbose)
+    return SELFTEST
+
+
 def build_all(verbose: bool = False, force: bool = False):
     net = build_net(verbose, force)
     ker = build_kernels(verbose, force)
@@ -169,3 +187,5 @@ if __name__ == "__main__":
         print(build_net(verbose, force))
     if not what or "kernels" in what:
         print(build_kernels(verbose, force))
+    if "selftest" in what:
+        print(build_selftest(verbose, force))

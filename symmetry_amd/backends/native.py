@@ -48,7 +48,7 @@ class NativeBackend(Backend):
             if self._engine.device.type != "cpu":
                 # start-up warmup (prefill size classes + decode hipGraphs) before the first client
                 await asyncio.to_thread(self._engine.warmup)
-        self.aengine = AsyncEngine(self._engine)
+        self.aengine = AsyncEngine(self._engine, queue_limit=int(self.cfg.get("maxBacklog") or 4096))
         self.aengine.start()
 
     async def stop(self) -> None:

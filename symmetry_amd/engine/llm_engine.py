@@ -308,12 +308,28 @@ class AsyncEngine:
 
     async def generate(self, request_id: str, messages: list | None = None, prompt_ids: list | None = None,
                        params: SamplingParams | None = None):
-        """Async iterator of RequestOutput for one request; aborts the sequence if the consumer goes away."""
+        """Async iterator of RequestOutput for one request; aborts the sequence if the consumer goes away.
+
+        The engine thread never blocks on a consumer: outputs are buffered, and a consumer that falls
+        more than ``queue_limit`` outputs behind (a stalled / slow reader) has its request aborted with
+        an error output, so its KV blocks return to the pool (SURVEY.md §7.4 risk 6)."""
         loop = asyncio.get_running_loop()
-        q: asyncio.Queue = asyncio.Queue(maxsize=self.queue_limit)
+        q: asyncio.Queue = asyncio.Queue()
+        state = {"overflow": False}
+
+        def deliver(out: RequestOutput) -> None:
+            if state["overflow"]:
+                return
+            if not out.finished and q.qsize() >= self.queue_limit:
+                state["overflow"] = True
+                self.engine.abort(request_id)
+                q.put_nowait(RequestOutput(request_id, [], "", True, "error",
+                                           error=f"client too slow: more than {self.queue_limit} outputs behind"))
+                return
+            q.put_nowait(out)
 
         def cb(out: RequestOutput) -> None:
-            loop.call_soon_threadsafe(q.put_nowait, out)
+            loop.call_soon_threadsafe(deliver, out)
 
         if prompt_ids is None:
             prompt_ids = self.engine.tokenizer.apply_chat_template(messages or [])

@@ -119,6 +119,11 @@ class Connection(EventEmitter):
         self._drain_waiters.append(fut)
         await fut
 
+    def inject_fault(self, kind: str, data: bytes = b"\x00" * 16) -> None:
+        """Fault injection for tests: ``"raw"`` writes unframed bytes into the encrypted
+        stream, ``"corrupt"`` sends a message whose ciphertext fails authentication at the peer."""
+        self.swarm._transport.inject_fault(self.id, {"raw": 0, "corrupt": 1}[kind], bytes(data))
+
     def end(self) -> None:
         if self._open:
             self.swarm._transport.end(self.id)
