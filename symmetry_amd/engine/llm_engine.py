@@ -91,6 +91,9 @@ def _pick_device(spec: str) -> torch.device:
     return torch.device(spec)
 
 
+_PROFILE_DIR = os.environ.get("SYMMETRY_PROFILE")
+
+
 class LLMEngine:
     def __init__(self, cfg: EngineConfig, tp_comm=None, ep_comm=None, cpu_group=None):
         self.cfg = cfg
@@ -126,6 +129,9 @@ class LLMEngine:
                                   tp_rank=cfg.tp_rank, tp_size=cfg.tp_size, cpu_group=cpu_group)
         self.requests: dict[str, tuple] = {}
         self.lock = threading.Lock()
+        self._profiler = None
+        self._profile_left = int(os.environ.get("SYMMETRY_PROFILE_STEPS", "20"))
+        self.profile_trace: str | None = None
 
     # ------------------------------------------------------------------------------------------
     def _graph_safe(self, tp_comm, ep_comm) -> bool:
@@ -172,6 +178,8 @@ class LLMEngine:
         with self.lock:
             seq = self.scheduler.abort(request_id)
             entry = self.requests.pop(request_id, None)
+        if seq is not None:
+            self.metrics.on_abort()
         if seq is not None and entry is not None:
             self._emit(entry[2], RequestOutput(request_id, [], "", True, "abort", seq=seq))
 
@@ -185,10 +193,13 @@ class LLMEngine:
 
     # ------------------------------------------------------------------------------------------
     def step(self) -> list[RequestOutput]:
+        t_sched = time.perf_counter()
         with self.lock:
             batch = self.scheduler.schedule()
         if batch is None or not batch.seqs:
             return []
+        if self._profiler is None and _PROFILE_DIR and self._profile_left > 0:
+            self._start_profiler()
         t0 = time.perf_counter()
         try:
             ids = self.runner.execute(batch)
@@ -198,6 +209,7 @@ class LLMEngine:
             outs = []
             with self.lock:
                 for seq in batch.seqs:
+                    self.metrics.on_abort(error=True)
                     self.scheduler.finish(seq, SeqStatus.FINISHED_ERROR)
                     entry = self.requests.pop(seq.request_id, None)
                     out = RequestOutput(seq.request_id, [], "", True, "error", error=msg, seq=seq)
@@ -245,7 +257,29 @@ class LLMEngine:
                     self.metrics.on_finish(seq)
                 outs.append(out)
                 self._emit(cb, out)
+        self.metrics.on_phase(t0 - t_sched, now - t0, time.perf_counter() - now)
+        if self._profiler is not None:
+            self._profiler.step()
+            self._profile_left -= 1
+            if self._profile_left <= 0:
+                self._stop_profiler()
         return outs
+
+    # ---- torch.profiler hook: SYMMETRY_PROFILE=<dir> [SYMMETRY_PROFILE_STEPS=N] ----------
+    def _start_profiler(self) -> None:
+        from torch.profiler import ProfilerActivity, profile
+
+        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if self.device.type != "cpu" else [])
+        self._profiler = profile(activities=acts, record_shapes=False)
+        self._profiler.__enter__()
+
+    def _stop_profiler(self) -> None:
+        prof, self._profiler = self._profiler, None
+        prof.__exit__(None, None, None)
+        os.makedirs(_PROFILE_DIR, exist_ok=True)
+        path = os.path.join(_PROFILE_DIR, f"engine_trace_rank{self.cfg.tp_rank}_{os.getpid()}.json")
+        prof.export_chrome_trace(path)
+        self.profile_trace = path
 
     def warmup(self, prompt_lens=None) -> float:
         """Provider start-up pass: one prefill per size class (library GEMM heuristics and code objects

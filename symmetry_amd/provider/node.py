@@ -40,6 +40,7 @@ from ..net.swarm import Swarm
 from ..protocol import sse
 from ..protocol.codec import buffer_json, create_message, emitter_header, safe_parse_json
 from ..protocol.keys import NATIVE_PROVIDER, Keys
+from ..utils.metrics import MetricsReporter
 from .datacollect import save_completion
 
 DEFAULT_BOOTSTRAP = "127.0.0.1:49737"
@@ -123,6 +124,10 @@ class SymmetryProvider:
             logger.info(f"🔑 Server key: {cfg.get('serverKey')}")
             logger.info("🔗 Joining server, please wait.")
             await self.join_server()
+        self.metrics_reporter = MetricsReporter(
+            self.stats, interval_s=float(cfg.get("metricsInterval", 60) or 0),
+            path=cfg.get("metricsFile"), log=lambda line: logger.info(f"📊 {line}"))
+        self.metrics_reporter.start()
         if self.install_signal_handlers:
             loop = asyncio.get_running_loop()
             for sig in (signal.SIGINT, signal.SIGTERM):
@@ -262,7 +267,16 @@ class SymmetryProvider:
             await gen.aclose()
 
     # ------------------------------------------------------------------------------------------
+    def stats(self) -> dict:
+        """Backend (engine) metrics merged with the provider's own counters."""
+        d = dict(self.backend.stats())
+        d.update(active_peers=self.active_peers, completed=self.completed,
+                 conversations=self._conversation_index, server_verified=self._server_verified)
+        return d
+
     async def destroy(self) -> None:
+        if getattr(self, "metrics_reporter", None) is not None:
+            self.metrics_reporter.stop()
         for t in list(self._tasks):
             t.cancel()
         if self._provider_swarm is not None:

@@ -38,6 +38,9 @@ class EngineMetrics:
         self.kv_util = 0.0
         self.queue_depth = 0
         self.active_peers = 0
+        self.phase = {"schedule": 0.0, "execute": 0.0, "postprocess": 0.0}  # engine step timer (seconds)
+        self.aborted = 0
+        self.errors = 0
 
     def on_arrival(self):
         with self.lock:
@@ -67,6 +70,19 @@ class EngineMetrics:
         with self.lock:
             self.finished += 1
 
+    def on_phase(self, schedule: float, execute: float, postprocess: float):
+        with self.lock:
+            self.phase["schedule"] += schedule
+            self.phase["execute"] += execute
+            self.phase["postprocess"] += postprocess
+
+    def on_abort(self, error: bool = False):
+        with self.lock:
+            if error:
+                self.errors += 1
+            else:
+                self.aborted += 1
+
     def summary(self) -> dict:
         with self.lock:
             el = time.perf_counter() - self.t_start
@@ -84,4 +100,55 @@ class EngineMetrics:
                 "kv_utilization": round(self.kv_util, 4),
                 "queue_depth": self.queue_depth,
                 "active_peers": self.active_peers,
+                "aborted": self.aborted,
+                "errors": self.errors,
+                "step_phase_ms": {k: round(1e3 * v / max(1, sum(self.steps.values())), 4)
+                                  for k, v in self.phase.items()},
             }
+
+
+class MetricsReporter:
+    """Periodic metrics: one ``📊`` log line and (optionally) a JSON snapshot file every ``interval_s``.
+
+    ``source`` returns the dict to report (engine summary merged with provider counters)."""
+
+    def __init__(self, source, interval_s: float = 60.0, path: str | None = None, log=None):
+        self.source, self.interval_s, self.path, self.log = source, interval_s, path, log
+        self._task = None
+
+    def snapshot(self) -> dict:
+        snap = dict(self.source())
+        snap["ts"] = time.time()
+        if self.path:
+            import json
+            import os
+
+            tmp = self.path + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump(snap, f)
+            os.replace(tmp, self.path)
+        if self.log is not None:
+            keys = ("tokens_per_s", "p50_ttft_ms", "p50_itl_ms", "mean_decode_batch", "kv_utilization",
+                    "queue_depth", "active_peers")
+            self.log(" ".join(f"{k}={snap[k]:.4g}" if isinstance(snap.get(k), float) else f"{k}={snap.get(k)}"
+                              for k in keys if k in snap))
+        return snap
+
+    def start(self) -> None:
+        import asyncio
+
+        async def loop():
+            while True:
+                await asyncio.sleep(self.interval_s)
+                try:
+                    self.snapshot()
+                except Exception:  # metrics must never take the provider down
+                    pass
+
+        if self.interval_s and self.interval_s > 0:
+            self._task = asyncio.ensure_future(loop())
+
+    def stop(self) -> None:
+        if self._task is not None:
+            self._task.cancel()
+            self._task = None

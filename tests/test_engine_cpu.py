@@ -157,3 +157,25 @@ def test_chat_templates():
     mtok = ByteTokenizer(resolve("mixtral:8x7b"))
     mids = mtok.apply_chat_template([{"role": "system", "content": "be brief"}, {"role": "user", "content": "hi"}])
     assert mids[0] == 1 and bytes(mids[1:]).decode() == "[INST] be brief\n\nhi [/INST]"
+
+
+def test_metrics_reporter_and_profiler_hook(tmp_path, monkeypatch):
+    """step-phase timer, JSON metrics snapshot, torch.profiler chrome trace."""
+    import json
+
+    from symmetry_amd.engine import llm_engine as le
+    from symmetry_amd.utils.metrics import MetricsReporter
+
+    monkeypatch.setattr(le, "_PROFILE_DIR", str(tmp_path / "prof"))
+    monkeypatch.setenv("SYMMETRY_PROFILE_STEPS", "3")
+    eng = le.LLMEngine(le.EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=2, max_model_len=128,
+                                       num_kv_blocks=16, block_size=16, use_graphs=False))
+    eng.generate([1, 2, 3], le.SamplingParams(max_tokens=5, ignore_eos=True))
+    assert eng.profile_trace and json.load(open(eng.profile_trace))["traceEvents"]
+    lines = []
+    rep = MetricsReporter(eng.metrics.summary, path=str(tmp_path / "m.json"), log=lines.append)
+    snap = rep.snapshot()
+    assert snap["tokens"] == 5 and snap["decode_steps"] >= 4
+    assert set(snap["step_phase_ms"]) == {"schedule", "execute", "postprocess"}
+    assert json.load(open(tmp_path / "m.json"))["tokens"] == 5
+    assert lines and "tokens_per_s=" in lines[0]
