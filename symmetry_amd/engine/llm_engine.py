@@ -137,8 +137,11 @@ class LLMEngine:
     def _graph_safe(self, tp_comm, ep_comm) -> bool:
         """Decode hipGraphs need every collective to be capturable (our RCCL communicator) and no
         host-side data-dependent shapes (all-to-all expert dispatch reads counts on the host)."""
+        from .. import ops
         from ..parallel.comm import RcclComm
 
+        if ops.torch_mode():  # eager torch baseline: host-synchronising reference ops
+            return False
         for c in (tp_comm, ep_comm):
             if c is not None and getattr(c, "world", 1) > 1 and not isinstance(c, RcclComm):
                 return False

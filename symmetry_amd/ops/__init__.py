@@ -3,15 +3,26 @@
 Dispatch rule (no silent fallback): a GPU tensor always runs the CDNA4 HIP
 kernel from ``_C.so`` (``torch.ops.symmetry_amd.*``) and raises if the
 library is not built/loadable; a CPU tensor runs the fp32 torch reference
-(:mod:`symmetry_amd.ops.reference`).  All ops write into caller-provided
+(:mod:`symmetry_amd.ops.reference`).  The only exception is the explicit
+``SYMMETRY_OPS=torch`` switch: the "unoptimised native" baseline B1
+ that runs the torch reference ops, eagerly, on the GPU.  All ops write into caller-provided
 outputs and allocate nothing on the GPU path, so the model runner can capture
 them in a hipGraph.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _native, reference
+
+_TORCH_MODE = os.environ.get("SYMMETRY_OPS", "native").lower() == "torch"
+
+
+def torch_mode() -> bool:
+    """True under SYMMETRY_OPS=torch (eager torch ops on the GPU: baseline B1, no hipGraphs)."""
+    return _TORCH_MODE
 
 __all__ = [
     "native_available",
@@ -46,7 +57,7 @@ def native_available() -> bool:
 
 
 def _gpu(t: torch.Tensor) -> bool:
-    return t.device.type != "cpu"
+    return t.device.type != "cpu" and not _TORCH_MODE
 
 
 def rms_norm(x, w, eps, out):

@@ -21,6 +21,15 @@ import torch
 MASK32 = 0xFFFFFFFF
 
 
+def _mm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """x @ w.T in fp32.  On the CPU (the numerics oracle) both operands are upcast; on a GPU (only in the
+    SYMMETRY_OPS=torch eager baseline) the product runs as a bf16 library GEMM with fp32 output, so the
+    baseline never materialises fp32 copies of the weights."""
+    if x.device.type == "cpu":
+        return x.float() @ w.float().t()
+    return (x.to(w.dtype) @ w.t()).float()
+
+
 def linout_sum(x: torch.Tensor) -> torch.Tensor:
     """Collapse a LinOut to fp32 ``[T, N]``."""
     if x.dtype == torch.float32 and x.dim() == 3:
@@ -134,7 +143,7 @@ def skinny_gemm(x, w, y) -> None:
     K = x.shape[1]
     kc = K // S
     for s in range(S):
-        y[s] = x[:, s * kc : (s + 1) * kc].float() @ w[:, s * kc : (s + 1) * kc].float().t()
+        y[s] = _mm(x[:, s * kc : (s + 1) * kc], w[:, s * kc : (s + 1) * kc])
 
 
 # ----- sampling: same counter-based RNG and packed keys as the kernel ----------------------------
@@ -191,7 +200,7 @@ def sample_keys(logits: torch.Tensor, temps: torch.Tensor, seeds: torch.Tensor, 
             mixed = seed ^ ((step << 20) & 0xFFFFFFFFFFFFFFFF)
             if mixed >= 1 << 63:
                 mixed -= 1 << 64
-            u = uniform01(torch.tensor(mixed, dtype=torch.int64), gidx).float()
+            u = uniform01(torch.tensor(mixed, dtype=torch.int64, device=gidx.device), gidx).float()
             vals[m] = vals[m] / t - torch.log(-torch.log(u))
     ob = _ordered_bits(vals)
     low = 0xFFFFFFFF - gidx
@@ -209,7 +218,7 @@ def sample_keys(logits: torch.Tensor, temps: torch.Tensor, seeds: torch.Tensor, 
 
 
 def lm_head_sample(x, w, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset: int, logits=None) -> None:
-    lg = x.float() @ w.float().t()
+    lg = _mm(x, w)
     if logits is not None:
         logits.copy_(lg)
     keys, ids = sample_keys(lg, temps, seeds, int(step.reshape(-1)[0]), n_offset)
@@ -237,7 +246,7 @@ def _row_scale(ss_in, eps: float, K: int, M: int):
 
 
 def _dg(x, W, ss_in, eps):
-    y = x.float() @ W.float().t()
+    y = _mm(x, W)
     rn = _row_scale(ss_in, eps, x.shape[1], x.shape[0])
     return y if rn is None else y * rn
 
@@ -253,7 +262,7 @@ def dg_qkv(x, W, ss_in, eps, positions, slots, cos_sin, q_out, k_cache, v_cache,
 def dg_resid(x, W, resid, w_next, xw_out, ss_out) -> None:
     M = x.shape[0]
     r = resid[:M]
-    r.add_(x.float() @ W.float().t())
+    r.add_(_mm(x, W))
     xw_out[:M].copy_((r * w_next.float()).to(xw_out.dtype))
     ss_out[:M].copy_(r.pow(2).view(M, -1, 16).sum(-1))
 
@@ -346,7 +355,7 @@ def grouped_skinny(xs, W, offsets, e0: int, y) -> None:
     for e in range(W.shape[0]):
         a, b = int(offsets[e0 + e]), int(offsets[e0 + e + 1])
         if b > a:
-            y[0, a:b] = xs[a:b].float() @ W[e].float().t()
+            y[0, a:b] = _mm(xs[a:b], W[e])
 
 
 def moe_combine(y, dst, ids, e_lo: int, e_hi: int, w, k: int, out, accumulate: bool) -> None:
