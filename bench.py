@@ -157,7 +157,8 @@ def main() -> int:
             "data": "synthetic prompts, random-init weights (real Llama-3-8B architecture)",
             "config": {"model": args.model, "global_batch": world * C, "seq_len": P,
                        "parallelism": f"dp{world}", "clients_per_gpu": C, "max_model_len": args.max_model_len,
-                       "decode": "greedy", "hipgraphs": not args.no_graphs},
+                       "decode": "greedy", "hipgraphs": bool(eng.runner.use_graphs),
+                       "ops": "torch-eager (baseline B1)" if ops.torch_mode() else "native gfx950 HIP"},
             "per_client_tokens_per_s": round(per_client, 2),
             "p50_ttft_ms": round(p50_ttft, 2),
             "load_s": round(t_load, 1),
