@@ -506,7 +506,8 @@ void dg_argmax(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss
                        ptr<int>(out_ids), s);
 }
 
-void embed_prep(const Tensor& ids, const Tensor& table, Tensor& resid, const Tensor& w, Tensor& xw, Tensor& ss) {
+void embed_prep(const Tensor& ids, const Tensor& table, Tensor& resid, const Tensor& w, Tensor& xw, Tensor& ss,
+                const c10::optional<Tensor>& src, const c10::optional<Tensor>& prev) {
   check_gpu(ids, "ids");
   check_dtype(ids, at::kInt, "ids");
   check_gpu(table, "table");
@@ -520,9 +521,21 @@ void embed_prep(const Tensor& ids, const Tensor& table, Tensor& resid, const Ten
   check_dtype(ss, at::kFloat, "ss");
   TORCH_CHECK(resid.numel() == T * d && xw.numel() == T * d && w.numel() == d && ss.numel() >= T && d % 8 == 0,
               "embed_prep: shape mismatch");
+  const int* sp = nullptr;
+  const int* pp = nullptr;
+  TORCH_CHECK(src.has_value() == prev.has_value(), "embed_prep: src and prev go together");
+  if (src.has_value()) {
+    check_gpu(*src, "src");
+    check_gpu(*prev, "prev");
+    check_dtype(*src, at::kInt, "src");
+    check_dtype(*prev, at::kInt, "prev");
+    TORCH_CHECK(src->numel() >= T, "embed_prep: src must have one entry per row");
+    sp = ptr<int>(*src);
+    pp = ptr<int>(*prev);
+  }
   const at::OptionalDeviceGuard g(ids.device());
-  launch_embed_prep(ptr<int>(ids), ptr<bf16>(table), ptr<float>(resid), ptr<bf16>(w), ptr<bf16>(xw), ptr<float>(ss),
-                    (int)T, (int)d, cur_stream(ids));
+  launch_embed_prep(ptr<int>(ids), sp, pp, ptr<bf16>(table), ptr<float>(resid), ptr<bf16>(w), ptr<bf16>(xw),
+                    ptr<float>(ss), (int)T, (int)d, cur_stream(ids));
 }
 
 void add_prep(const Tensor& delta, Tensor& resid, const Tensor& w, Tensor& xw, Tensor& ss) {
@@ -618,7 +631,8 @@ TORCH_LIBRARY(symmetry_amd, m) {
       "dg_argmax(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor temps, Tensor seeds, Tensor step, "
       "Tensor(a!) tile_keys, Tensor(b!) out_keys, Tensor(c!) out_ids, int n_offset, Tensor(d!)? logits) -> ()",
       &dg_argmax);
-  m.def("embed_prep(Tensor ids, Tensor table, Tensor(a!) resid, Tensor w, Tensor(b!) xw, Tensor(c!) ss) -> ()",
+  m.def("embed_prep(Tensor ids, Tensor table, Tensor(a!) resid, Tensor w, Tensor(b!) xw, Tensor(c!) ss, "
+        "Tensor? src=None, Tensor? prev=None) -> ()",
         &embed_prep);
   m.def("add_prep(Tensor delta, Tensor(a!) resid, Tensor w, Tensor(b!) xw, Tensor(c!) ss) -> ()", &add_prep);
   m.def("rownorm(Tensor xw, Tensor ss, float eps, Tensor(a!) out) -> ()", &rownorm);

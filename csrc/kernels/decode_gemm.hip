@@ -271,10 +271,13 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __rest
 }
 
 // ---- residual producers without a GEMM ----------------------------------------------------------
-// embed_prep: resid = table[ids]; xw = bf16(resid * w); ss[m][0] = sum(resid^2)
+// embed_prep: resid = table[tok]; xw = bf16(resid * w); ss[m][0] = sum(resid^2), where
+//   tok = src[m] >= 0 ? prev[src[m]] : ids[m]  -- src/prev (optional) feed the previous step's sampled ids
+//   straight from device memory (pipelined decode: the host has not seen them yet)
 // add_prep:   resid += delta (LinOut); xw = bf16(resid * w); ss[m][0] = sum(resid^2)
 template <int MODE>
 __global__ __launch_bounds__(256) void prep_kernel(LinOut delta, const int* __restrict__ ids,
+                                                   const int* __restrict__ src, const int* __restrict__ prev,
                                                    const bf16* __restrict__ table, float* __restrict__ resid,
                                                    const bf16* __restrict__ w, bf16* __restrict__ xw,
                                                    float* __restrict__ ss, int d) {
@@ -282,10 +285,15 @@ __global__ __launch_bounds__(256) void prep_kernel(LinOut delta, const int* __re
   const int row = blockIdx.x;
   const long long rb = (long long)row * d;
   float acc = 0.f;
+  long long tok = 0;
+  if constexpr (MODE == 0) {
+    const int sr = src ? src[row] : -1;
+    tok = sr >= 0 ? prev[sr] : ids[row];
+  }
   for (int vi = threadIdx.x; vi < d / 8; vi += 256) {
     float r[8], g[8];
     if constexpr (MODE == 0) {
-      load8(table + (long long)ids[row] * d + vi * 8, r);
+      load8(table + tok * d + vi * 8, r);
     } else {
       float dd[8];
       load8f(resid + rb + vi * 8, r);
@@ -381,14 +389,14 @@ void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int
 
 void set_decode_gemm_variant(int v) { g_variant = v; }
 
-void launch_embed_prep(const int* ids, const bf16* table, float* resid, const bf16* w, bf16* xw, float* ss, int T,
-                       int d, hipStream_t s) {
+void launch_embed_prep(const int* ids, const int* src, const int* prev, const bf16* table, float* resid, const bf16* w,
+                       bf16* xw, float* ss, int T, int d, hipStream_t s) {
   if (T == 0) return;
   LinOut none{nullptr, 0, 1, 0};
-  prep_kernel<0><<<T, 256, 0, s>>>(none, ids, table, resid, w, xw, ss, d);
+  prep_kernel<0><<<T, 256, 0, s>>>(none, ids, src, prev, table, resid, w, xw, ss, d);
 }
 
 void launch_add_prep(LinOut delta, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d, hipStream_t s) {
   if (T == 0) return;
-  prep_kernel<1><<<T, 256, 0, s>>>(delta, nullptr, nullptr, resid, w, xw, ss, d);
+  prep_kernel<1><<<T, 256, 0, s>>>(delta, nullptr, nullptr, nullptr, nullptr, resid, w, xw, ss, d);
 }

@@ -52,6 +52,7 @@ class EngineConfig:
     ep_size: int = 1
     ep_rank: int = 0
     weight_init: str = "auto"            # "full" | "shard" | "auto"
+    pipeline: bool = True                # enqueue decode step N+1 before step N's tokens reach the host
     model_config: ModelConfig | None = None
 
     @classmethod
@@ -129,6 +130,8 @@ class LLMEngine:
                                   tp_rank=cfg.tp_rank, tp_size=cfg.tp_size, cpu_group=cpu_group)
         self.requests: dict[str, tuple] = {}
         self.lock = threading.Lock()
+        self._inflight: dict | None = None
+        self.pipeline = cfg.pipeline and cfg.tp_size == 1
         self._profiler = None
         self._profile_left = int(os.environ.get("SYMMETRY_PROFILE_STEPS", "20"))
         self.profile_trace: str | None = None
@@ -187,7 +190,9 @@ class LLMEngine:
             self._emit(entry[2], RequestOutput(request_id, [], "", True, "abort", seq=seq))
 
     def has_unfinished(self) -> bool:
-        return self.scheduler.has_work()
+        fl = self._inflight
+        live = fl is not None and any(not s.status.finished for s in fl["batch"].seqs)
+        return self.scheduler.has_work() or live
 
     @staticmethod
     def _emit(cb, out: RequestOutput) -> None:
@@ -196,40 +201,88 @@ class LLMEngine:
 
     # ------------------------------------------------------------------------------------------
     def step(self) -> list[RequestOutput]:
+        """One engine iteration; returns the outputs that completed in it.
+
+        Pipelined decode (single-GPU engines): step N+1 is scheduled and enqueued on the GPU before
+        step N's sampled ids are copied back -- its pending input tokens are gathered on the device
+        from step N's output buffer -- and only then does the host wait for, detokenize and stream
+        step N.  Host scheduling, detokenization and the provider's socket writes thus overlap the GPU,
+        which never idles between decode steps.  A sequence that stops at step N has already been
+        given one extra step; that token is discarded (its KV blocks are released in stream order)."""
         t_sched = time.perf_counter()
+        prev = self._inflight
+        if prev is not None:
+            with self.lock:
+                nxt = self.scheduler.schedule_lookahead()
+            self._inflight = None
+            if nxt is not None:
+                self._inflight = self._launch(nxt, prev)
+            return self._complete(prev, t_sched)
         with self.lock:
             batch = self.scheduler.schedule()
         if batch is None or not batch.seqs:
             return []
+        fl = self._launch(batch, None)
+        if fl is None or "failed" in fl:
+            return fl["failed"] if fl else []
+        if self.pipeline and batch.kind == "decode":
+            self._inflight = fl
+            return []
+        return self._complete(fl, t_sched)
+
+    def has_in_flight(self) -> bool:
+        return self._inflight is not None
+
+    def _fail(self, batch, exc) -> list[RequestOutput]:
+        """Engine watchdog: fail the requests of a step that raised, keep serving the others."""
+        msg = f"{type(exc).__name__}: {exc}"
+        traceback.print_exc()
+        outs = []
+        with self.lock:
+            for seq in batch.seqs:
+                if seq.status.finished:
+                    continue
+                self.metrics.on_abort(error=True)
+                self.scheduler.finish(seq, SeqStatus.FINISHED_ERROR)
+                entry = self.requests.pop(seq.request_id, None)
+                out = RequestOutput(seq.request_id, [], "", True, "error", error=msg, seq=seq)
+                outs.append(out)
+                if entry:
+                    self._emit(entry[2], out)
+        return outs
+
+    def _launch(self, batch, prev) -> dict:
         if self._profiler is None and _PROFILE_DIR and self._profile_left > 0:
             self._start_profiler()
         t0 = time.perf_counter()
+        prev_rows = None
+        if prev is not None:
+            prev_rows = {s.seq_id: i for i, s in enumerate(prev["batch"].seqs)}
         try:
-            ids = self.runner.execute(batch)
-        except Exception as exc:  # engine watchdog: fail the in-flight requests, keep serving
-            msg = f"{type(exc).__name__}: {exc}"
-            traceback.print_exc()
-            outs = []
-            with self.lock:
-                for seq in batch.seqs:
-                    self.metrics.on_abort(error=True)
-                    self.scheduler.finish(seq, SeqStatus.FINISHED_ERROR)
-                    entry = self.requests.pop(seq.request_id, None)
-                    out = RequestOutput(seq.request_id, [], "", True, "error", error=msg, seq=seq)
-                    outs.append(out)
-                    if entry:
-                        self._emit(entry[2], out)
-            return outs
+            handle = self.runner.launch(batch, prev_rows)
+        except Exception as exc:
+            return {"failed": self._fail(batch, exc)}
+        with self.lock:
+            for seq, n, keep in zip(batch.seqs, batch.num_new_tokens, batch.sample):
+                seq.num_computed += n
+                seq.num_pending += int(keep)
+        return {"batch": batch, "handle": handle, "t0": t0}
+
+    def _complete(self, fl: dict, t_sched: float) -> list[RequestOutput]:
+        batch, t0 = fl["batch"], fl["t0"]
+        try:
+            ids = self.runner.wait(fl["handle"])
+        except Exception as exc:
+            return self._fail(batch, exc)
         now = time.perf_counter()
         self.metrics.on_step(batch.kind, len(batch.seqs), batch.num_tokens, now - t0, self.blocks.utilization(),
                              len(self.scheduler.waiting))
         outs = []
         with self.lock:
-            for seq, n, keep, tok in zip(batch.seqs, batch.num_new_tokens, batch.sample, ids):
-                if seq.status.finished:
-                    continue
-                seq.num_computed += n
-                if not keep:
+            for seq, keep, tok in zip(batch.seqs, batch.sample, ids):
+                if keep:
+                    seq.num_pending -= 1
+                if seq.status.finished or not keep:
                     continue
                 first = seq.first_token_time is None
                 seq.append(tok, now)

@@ -52,6 +52,7 @@ class _Layout:
 
         self.T, self.nseq, self.max_blocks, self.ntiles = T, nseq, max_blocks, ntiles
         self.ids = take(T)
+        self.src = take(T)
         self.pos = take(T)
         self.slots = take(T)
         self.ctx = take(nseq)
@@ -75,6 +76,7 @@ class _Layout:
     def views(self, buf: torch.Tensor) -> dict:
         v = {
             "input_ids": buf[self.ids:self.ids + self.T],
+            "src": buf[self.src:self.src + self.T],
             "positions": buf[self.pos:self.pos + self.T],
             "slot_mapping": buf[self.slots:self.slots + self.T],
             "ctx_lens": buf[self.ctx:self.ctx + self.nseq],
@@ -114,6 +116,7 @@ class ModelRunner:
         self._graph_pool = None
         self._pinned = {}
         self.step_counter = 0
+        self._parity = 0
         self.timing = {"h2d": 0.0, "forward": 0.0, "d2h": 0.0, "steps": 0}
 
     # ------------------------------------------------------------------------------------------
@@ -124,13 +127,21 @@ class ModelRunner:
             self._pinned[key] = t
         return t[:n]
 
-    def _fill(self, lay: _Layout, host: np.ndarray, seqs, counts, pad_to: int | None = None) -> None:
+    def _fill(self, lay: _Layout, host: np.ndarray, seqs, counts, prev_rows: dict | None = None) -> None:
+        """Pack one step's metadata.  A decode row whose input token is still in flight (sampled by the
+        previous, not yet completed step: pipelined decode) gets id 0 and src = that step's output row;
+        the embedding kernel then reads the token from device memory."""
         BS = self.block_size
-        ids, pos, slots = [], [], []
+        ids, pos, slots, src = [], [], [], []
         ctx, temps, seeds, topk, topp = [], [], [], [], []
         for seq, n in zip(seqs, counts):
             start = seq.num_computed
             toks = seq.token_ids[start:start + n]
+            if len(toks) < n:  # pending token (pipelined decode): resolved on the device
+                toks = toks + [0] * (n - len(toks))
+                src.extend([-1] * (n - 1) + [prev_rows[seq.seq_id]])
+            else:
+                src.extend([-1] * n)
             p = np.arange(start, start + n, dtype=np.int64)
             bt = np.asarray(seq.block_table, dtype=np.int64)
             ids.extend(toks)
@@ -145,6 +156,8 @@ class ModelRunner:
         T = lay.T
         host[:] = 0
         host[lay.ids:lay.ids + len(ids)] = ids
+        host[lay.src:lay.src + T] = -1
+        host[lay.src:lay.src + len(src)] = src
         if pos:
             host[lay.pos:lay.pos + len(ids)] = np.concatenate(pos)
             host[lay.slots:lay.slots + len(ids)] = np.concatenate(slots)
@@ -182,6 +195,12 @@ class ModelRunner:
     # ------------------------------------------------------------------------------------------
     def execute(self, batch: ScheduledBatch) -> list[int]:
         """Rank-0 entry: run one scheduled step, return sampled ids (one per sequence)."""
+        return self.wait(self.launch(batch))
+
+    def launch(self, batch: ScheduledBatch, prev_rows: dict | None = None) -> dict:
+        """Enqueue one step on the GPU without waiting for it; ``wait(handle)`` returns its sampled ids.
+        ``prev_rows`` maps seq_id -> output row of the in-flight previous step, for rows whose input
+        token is that step's (not yet host-visible) sample."""
         seqs, counts = batch.seqs, batch.num_new_tokens
         t0 = time.perf_counter()
         if batch.kind == "decode":
@@ -194,17 +213,35 @@ class ModelRunner:
             ntiles = sum((n + 63) // 64 for n in counts)
             max_blocks = max(len(s.block_table) for s in seqs)
             lay = _Layout(sum(counts), nseq, max_blocks, prefill=True, ntiles=ntiles)
-        host_t = self._host(lay.size, batch.kind)
-        host = host_t.numpy()
-        self._fill(lay, host, seqs, counts)
+        self._parity ^= 1
+        host_t = self._host(lay.size, f"{batch.kind}{self._parity}")  # double-buffered: the previous
+        host = host_t.numpy()                                          # step's H2D may still be queued
+        self._fill(lay, host, seqs, counts, prev_rows)
         header = np.array([0 if batch.kind == "decode" else 1, lay.T, lay.nseq, lay.max_blocks, lay.ntiles, nseq,
                            int(self._filtered(seqs))], dtype=np.int32)
         if self.tp_size > 1:
             self._broadcast(header, host_t)
         ids = self._run(header, host_t)
+        handle = {"nseq": nseq, "t0": t0}
+        if self.is_gpu:
+            pin = self._host(max(ids.numel(), 1), f"ids_out{self._parity}")[:ids.numel()]
+            pin.copy_(ids, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            handle.update(pin=pin, event=ev)
+        else:
+            handle["ids"] = ids.tolist()
         self.timing["steps"] += 1
-        self.timing["forward"] += time.perf_counter() - t0
-        return ids[:nseq]
+        return handle
+
+    def wait(self, handle: dict) -> list[int]:
+        if "event" in handle:
+            handle["event"].synchronize()
+            ids = handle["pin"].tolist()
+        else:
+            ids = handle["ids"]
+        self.timing["forward"] += time.perf_counter() - handle["t0"]
+        return ids[:handle["nseq"]]
 
     def _bucket(self, n: int) -> int:
         for b in self.buckets:
@@ -218,7 +255,7 @@ class ModelRunner:
                 return b
         raise ValueError(f"sequence needs {nblocks} blocks > max {self.max_blocks}")
 
-    def _run(self, header: np.ndarray, host_t: torch.Tensor) -> list[int]:
+    def _run(self, header: np.ndarray, host_t: torch.Tensor) -> torch.Tensor:
         kind = "decode" if header[0] == 0 else "prefill"
         T, nseq_l, max_blocks, ntiles, nseq, filt = (int(x) for x in header[1:HEADER_LEN])
         lay = _Layout(T, nseq_l, max_blocks, prefill=kind == "prefill", ntiles=ntiles)
@@ -237,12 +274,7 @@ class ModelRunner:
             dev.copy_(host_t[:lay.size], non_blocking=True)
             fb = self._forward_batch(kind, lay, dev, nseq_l, filtered=bool(filt))
             ids = self.model.forward(fb, self.kv)
-        if self.is_gpu:
-            out_host = self._host(ids.numel(), "ids_out")
-            out_host.copy_(ids, non_blocking=True)
-            torch.cuda.current_stream().synchronize()
-            return out_host.tolist()
-        return ids.tolist()
+        return ids
 
     # ------------------------------------------------------------------------------------------
     def _capture(self, bucket: int, max_blocks: int, filtered: bool = False) -> None:
@@ -322,3 +354,5 @@ class ModelRunner:
                 self._capture(int(header[1]), int(header[3]), bool(header[6]))
                 continue
             self._run(header[:HEADER_LEN], host_t)
+            if self.is_gpu:
+                torch.cuda.current_stream().synchronize()

@@ -160,7 +160,8 @@ class Scheduler:
 
     def _schedule_decode(self) -> ScheduledBatch | None:
         preempted = []
-        ready = [s for s in self.running if not s.in_prefill]
+        # a sequence whose in-flight tokens already reach max_tokens needs no further step
+        ready = [s for s in self.running if not s.in_prefill and len(s.output_ids) + s.num_pending < s.params.max_tokens]
         # ensure a cache slot for each decoding sequence; preempt the newest on exhaustion
         ready.sort(key=lambda s: s.arrival_time)
         out = []
@@ -178,6 +179,14 @@ class Scheduler:
         if not out:
             return ScheduledBatch("decode", [], [], [], preempted) if preempted else None
         return ScheduledBatch("decode", out, [1] * len(out), [True] * len(out), preempted)
+
+    def schedule_lookahead(self) -> ScheduledBatch | None:
+        """Next decode step while the previous one is still in flight (pipelined decode).  Only a pure
+        decode continuation qualifies: new arrivals and prefill chunks wait until the pipeline drains."""
+        if self.waiting or any(s.in_prefill for s in self.running):
+            return None
+        b = self._schedule_decode()
+        return b if b is not None and b.seqs else None
 
     def _preempt(self, seq: Sequence) -> None:
         self.blocks.release(seq)

@@ -73,7 +73,8 @@ class Sequence:
     output_ids: list = field(default_factory=list)
     status: SeqStatus = SeqStatus.WAITING
     block_table: list = field(default_factory=list)
-    num_computed: int = 0          # tokens whose KV is in the cache
+    num_computed: int = 0          # tokens whose KV is in the cache (or enqueued to be written)
+    num_pending: int = 0           # sampled tokens launched on the GPU but not yet seen by the host
     arrival_time: float = field(default_factory=time.perf_counter)
     first_token_time: float | None = None
     last_token_time: float | None = None

@@ -37,6 +37,7 @@ from .layout import apply_decode_layout
 from .weights import ModelWeights
 
 SKINNY_MAX_M = 64
+MAX_STEP_SEQS = 4096  # sequences per step (rows of last_ids)
 SIGN64 = -(1 << 63)
 
 
@@ -63,6 +64,7 @@ class ForwardBatch:
     tiles: torch.Tensor | None = None       # [n_tiles, 2] int32
     last_idx: torch.Tensor | None = None    # [num_seqs] int64 row of each sequence's last token
     need_logits: bool = False
+    src: torch.Tensor | None = None         # [T] int32: >= 0 -> token = previous step's sample in that row
     top_k: torch.Tensor | None = None       # [num_seqs] int32 (0 = off)
     top_p: torch.Tensor | None = None       # [num_seqs] f32 (1 = off)
     filtered: bool = False                  # some row needs the top-k / top-p resampler
@@ -141,6 +143,10 @@ class TransformerLM:
             self.moe = MoEBlock(self, ep_comm)
         apply_decode_layout(weights)
         self.fused = self._fused_supported()
+        # Sampled ids of the most recent step live at a fixed device address: every step writes its
+        # samples here and the next step's embedding reads pending input tokens from here (src map),
+        # so the host can enqueue step N+1 before it has seen step N's tokens (pipelined decode).
+        self.last_ids = torch.zeros(MAX_STEP_SEQS, dtype=torch.int32, device=self.device)
 
     def _fused_supported(self) -> bool:
         """Shape contract of the fused decode GEMMs: D == 128, every K % 256 == 0, every N % 16 == 0."""
@@ -212,7 +218,7 @@ class TransformerLM:
         ss_1 = self._buf("ss_1", (T, 1), torch.float32)
         q = self._buf("q", (T, self.hq, self.D), torch.bfloat16)
         attn = self._buf("attn", (T, self.hq, self.D), torch.bfloat16)
-        ops.embed_prep(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), xw, ss_1)
+        ops.embed_prep(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), xw, ss_1, b.src, self.last_ids)
         ss = ss_1
         for i in range(cfg.num_layers):
             ops.dg_qkv(xw, w.layer(i, "wqkv"), ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i],
@@ -237,7 +243,7 @@ class TransformerLM:
             xl, sl = xw, ss
         else:
             xl, sl = xw.index_select(0, b.last_idx), ss.index_select(0, b.last_idx)
-        ids = self._buf("ids", (n,), torch.int32)
+        ids = self.last_ids[:n]
         keys = self._buf("keys", (n,), torch.int64)
         tk = self._buf("tile_keys", (n * (self.vocab_shard // 16),), torch.int64)
         logits = self._buf("logits", (n, self.vocab_shard), torch.float32) if b.need_logits or b.filtered else None
@@ -255,7 +261,10 @@ class TransformerLM:
         x = self._buf("x", (T, d), torch.bfloat16)
         q = self._buf("q", (T, self.hq, self.D), torch.bfloat16)
         attn = self._buf("attn", (T, self.hq, self.D), torch.bfloat16)
-        ops.embed_rms_norm(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), eps, x)
+        tok = b.input_ids
+        if b.src is not None and b.kind == "decode":  # pipelined decode rows (prefill never has pending ids)
+            tok = reference.resolve_ids(b.input_ids, b.src, self.last_ids).to(torch.int32)
+        ops.embed_rms_norm(tok, w["embed"], resid, w.layer(0, "ln1"), eps, x)
         for i in range(cfg.num_layers):
             qkv = self._linear("qkv", x, w.layer(i, "wqkv"))
             ops.rope_cache(qkv, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq, self.hkv,
@@ -279,7 +288,7 @@ class TransformerLM:
         """Fused lm_head + greedy/Gumbel sampling on each sequence's last row."""
         n = b.num_seqs
         xl = x if b.kind == "decode" else x.index_select(0, b.last_idx)
-        ids = self._buf("ids", (n,), torch.int32)
+        ids = self.last_ids[:n]
         keys = self._buf("keys", (n,), torch.int64)
         ntiles = self.vocab_shard // 16
         logits = self._buf("logits", (n, self.vocab_shard), torch.float32) if b.need_logits or b.filtered else None

@@ -154,10 +154,12 @@ def dg_argmax(x, W, ss_in, eps, temps, seeds, step, tile_keys, out_keys, out_ids
     return reference.dg_argmax(x, W, ss_in, eps, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset, logits)
 
 
-def embed_prep(ids, table, resid, w, xw, ss):
+def embed_prep(ids, table, resid, w, xw, ss, src=None, prev=None):
+    """Embedding gather + deferred-norm prep; with ``src``/``prev`` a row whose src >= 0 takes its token
+    from ``prev[src]`` (the previous step's device-resident samples: pipelined decode)."""
     if _gpu(resid):
-        return _native.ops().embed_prep(ids, table, resid, w, xw, ss)
-    return reference.embed_prep(ids, table, resid, w, xw, ss)
+        return _native.ops().embed_prep(ids, table, resid, w, xw, ss, src, prev)
+    return reference.embed_prep(ids, table, resid, w, xw, ss, src, prev)
 
 
 def add_prep(delta, resid, w, xw, ss):

@@ -281,9 +281,17 @@ def dg_argmax(x, W, ss_in, eps, temps, seeds, step, tile_keys, out_keys, out_ids
     out_ids[:M].copy_(ids.to(out_ids.dtype))
 
 
-def embed_prep(ids, table, resid, w, xw, ss) -> None:
+def resolve_ids(ids, src=None, prev=None):
+    """Token per row: prev[src] where src >= 0 (previous step's on-device samples), else ids."""
+    if src is None:
+        return ids.long()
+    s = src[: ids.numel()].long()
+    return torch.where(s >= 0, prev.long()[s.clamp(min=0)], ids.long())
+
+
+def embed_prep(ids, table, resid, w, xw, ss, src=None, prev=None) -> None:
     T = ids.numel()
-    r = table[ids.long()].float()
+    r = table[resolve_ids(ids, src, prev)].float()
     resid[:T].copy_(r)
     xw[:T].copy_((r * w.float()).to(xw.dtype))
     ss.view(-1)[:T].copy_(r.pow(2).sum(-1))  # ss: [>=T] or [>=T, 1] (one tile per row)

@@ -179,3 +179,35 @@ def test_metrics_reporter_and_profiler_hook(tmp_path, monkeypatch):
     assert set(snap["step_phase_ms"]) == {"schedule", "execute", "postprocess"}
     assert json.load(open(tmp_path / "m.json"))["tokens"] == 5
     assert lines and "tokens_per_s=" in lines[0]
+
+
+def test_pipelined_decode_matches_synchronous_engine():
+    """Pipelined decode (step N+1 enqueued before step N's tokens reach the host, pending input ids
+    gathered on the device) produces exactly the synchronous engine's tokens under staggered arrivals,
+    EOS / max_tokens stops and KV preemption."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+
+    def run(pipeline):
+        eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=4, max_model_len=256,
+                                     num_kv_blocks=12, block_size=16, use_graphs=False, pipeline=pipeline))
+        assert eng.pipeline == pipeline
+        seqs, launched_ahead = [], 0
+        plan = {0: [list(range(3, 30))], 3: [list(range(50, 61)), [7, 8, 9]], 9: [list(range(100, 140))]}
+        step = 0
+        while step < 400:
+            for p in plan.get(step, []):
+                i = len(seqs)
+                stop = (5,) if i == 1 else ()
+                seqs.append(eng.add_request(f"r{i}", p, SamplingParams(max_tokens=10 + 7 * i, ignore_eos=True,
+                                                                      stop_token_ids=stop)))
+            if step > max(plan) and not eng.has_unfinished():
+                break
+            eng.step()
+            launched_ahead += eng.has_in_flight()
+            step += 1
+        return [s.output_ids for s in seqs], launched_ahead
+
+    sync, n0 = run(False)
+    pipe, n1 = run(True)
+    assert pipe == sync
+    assert n0 == 0 and n1 > 10
