@@ -131,6 +131,7 @@ class LLMEngine:
         self.requests: dict[str, tuple] = {}
         self.lock = threading.Lock()
         self._inflight: dict | None = None
+        self._last_done = 0.0
         self.pipeline = cfg.pipeline and cfg.tp_size == 1
         self._profiler = None
         self._profile_left = int(os.environ.get("SYMMETRY_PROFILE_STEPS", "20"))
@@ -216,19 +217,21 @@ class LLMEngine:
                 nxt = self.scheduler.schedule_lookahead()
             self._inflight = None
             if nxt is not None:
-                self._inflight = self._launch(nxt, prev)
-            return self._complete(prev, t_sched)
+                fl = self._launch(nxt, prev)
+                if "failed" not in fl:
+                    self._inflight = fl
+            return self._complete(prev, time.perf_counter() - t_sched)
         with self.lock:
             batch = self.scheduler.schedule()
         if batch is None or not batch.seqs:
             return []
         fl = self._launch(batch, None)
-        if fl is None or "failed" in fl:
-            return fl["failed"] if fl else []
+        if "failed" in fl:
+            return fl["failed"]
         if self.pipeline and batch.kind == "decode":
             self._inflight = fl
             return []
-        return self._complete(fl, t_sched)
+        return self._complete(fl, time.perf_counter() - t_sched)
 
     def has_in_flight(self) -> bool:
         return self._inflight is not None
@@ -268,14 +271,20 @@ class LLMEngine:
                 seq.num_pending += int(keep)
         return {"batch": batch, "handle": handle, "t0": t0}
 
-    def _complete(self, fl: dict, t_sched: float) -> list[RequestOutput]:
+    def _complete(self, fl: dict, t_launch: float) -> list[RequestOutput]:
+        """Wait for a launched step and stream its tokens.  ``t_launch``: host seconds this iteration spent
+        scheduling + enqueueing (metrics phases: launch / wait on the GPU / postprocess)."""
         batch, t0 = fl["batch"], fl["t0"]
+        t_wait = time.perf_counter()
         try:
             ids = self.runner.wait(fl["handle"])
         except Exception as exc:
             return self._fail(batch, exc)
         now = time.perf_counter()
-        self.metrics.on_step(batch.kind, len(batch.seqs), batch.num_tokens, now - t0, self.blocks.utilization(),
+        # step latency: completion-to-completion while the pipeline is full, launch-to-completion otherwise
+        dt = now - max(t0, self._last_done)
+        self._last_done = now
+        self.metrics.on_step(batch.kind, len(batch.seqs), batch.num_tokens, dt, self.blocks.utilization(),
                              len(self.scheduler.waiting))
         outs = []
         with self.lock:
@@ -313,7 +322,7 @@ class LLMEngine:
                     self.metrics.on_finish(seq)
                 outs.append(out)
                 self._emit(cb, out)
-        self.metrics.on_phase(t0 - t_sched, now - t0, time.perf_counter() - now)
+        self.metrics.on_phase(t_launch, now - t_wait, time.perf_counter() - now)
         if self._profiler is not None:
             self._profiler.step()
             self._profile_left -= 1

@@ -38,7 +38,8 @@ class EngineMetrics:
         self.kv_util = 0.0
         self.queue_depth = 0
         self.active_peers = 0
-        self.phase = {"schedule": 0.0, "execute": 0.0, "postprocess": 0.0}  # engine step timer (seconds)
+        # engine step timer (seconds): host scheduling + enqueue, host blocked on the GPU, streaming out
+        self.phase = {"launch": 0.0, "wait": 0.0, "postprocess": 0.0}
         self.aborted = 0
         self.errors = 0
 
@@ -70,10 +71,10 @@ class EngineMetrics:
         with self.lock:
             self.finished += 1
 
-    def on_phase(self, schedule: float, execute: float, postprocess: float):
+    def on_phase(self, launch: float, wait: float, postprocess: float):
         with self.lock:
-            self.phase["schedule"] += schedule
-            self.phase["execute"] += execute
+            self.phase["launch"] += launch
+            self.phase["wait"] += wait
             self.phase["postprocess"] += postprocess
 
     def on_abort(self, error: bool = False):

@@ -176,7 +176,7 @@ def test_metrics_reporter_and_profiler_hook(tmp_path, monkeypatch):
     rep = MetricsReporter(eng.metrics.summary, path=str(tmp_path / "m.json"), log=lines.append)
     snap = rep.snapshot()
     assert snap["tokens"] == 5 and snap["decode_steps"] >= 4
-    assert set(snap["step_phase_ms"]) == {"schedule", "execute", "postprocess"}
+    assert set(snap["step_phase_ms"]) == {"launch", "wait", "postprocess"}
     assert json.load(open(tmp_path / "m.json"))["tokens"] == 5
     assert lines and "tokens_per_s=" in lines[0]
 
