@@ -27,20 +27,20 @@ SHAPES = {
 }
 
 
-def make_call(epi, x, W, M, N, K, dev):
+def make_call(epi, x, W, M, N, K, dev, sh=False):
     ss = torch.rand(M, K // 16, device=dev) + 0.5
     if epi == "f32":
         y = torch.empty(M, N, device=dev)
-        return lambda w: ops.dg_f32(x, w, ss, 1e-5, y)
+        return lambda w: ops.dg_f32(x, w, ss, 1e-5, y, wshuf=sh)
     if epi == "resid":
         resid = torch.zeros(M, N, device=dev)
         wn = torch.ones(N, device=dev, dtype=torch.bfloat16)
         xw = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         sso = torch.empty(M, N // 16, device=dev)
-        return lambda w: ops.dg_resid(x, w, resid, wn, xw, sso)
+        return lambda w: ops.dg_resid(x, w, resid, wn, xw, sso, wshuf=sh)
     if epi == "swiglu":
         act = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
-        return lambda w: ops.dg_swiglu(x, w, ss, 1e-5, act)
+        return lambda w: ops.dg_swiglu(x, w, ss, 1e-5, act, wshuf=sh)
     if epi == "qkv":
         hkv = N // 128 // 6
         hq = 4 * hkv
@@ -50,14 +50,14 @@ def make_call(epi, x, W, M, N, K, dev):
         q = torch.empty(M, hq, 128, device=dev, dtype=torch.bfloat16)
         kc = torch.zeros(4, hkv, 64, 128, device=dev, dtype=torch.bfloat16)
         vc = torch.zeros(4, hkv, 128, 64, device=dev, dtype=torch.bfloat16)
-        return lambda w: ops.dg_qkv(x, w, ss, 1e-5, pos, slots, cs, q, kc, vc, hq, hkv)
+        return lambda w: ops.dg_qkv(x, w, ss, 1e-5, pos, slots, cs, q, kc, vc, hq, hkv, wshuf=sh)
     temps = torch.zeros(M, device=dev)
     seeds = torch.zeros(M, device=dev, dtype=torch.int64)
     step = torch.zeros(1, device=dev, dtype=torch.int64)
     tk = torch.empty(M * (N // 16), device=dev, dtype=torch.int64)
     keys = torch.empty(M, device=dev, dtype=torch.int64)
     ids = torch.empty(M, device=dev, dtype=torch.int32)
-    return lambda w: ops.dg_argmax(x, w, ss, 1e-5, temps, seeds, step, tk, keys, ids, 0, None)
+    return lambda w: ops.dg_argmax(x, w, ss, 1e-5, temps, seeds, step, tk, keys, ids, 0, None, wshuf=sh)
 
 
 def main():
@@ -68,6 +68,8 @@ def main():
     ap.add_argument("--chain", type=int, default=16)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--warm", action="store_true", help="one weight copy: measures Infinity-Cache-resident weights")
+    ap.add_argument("--layouts", nargs="+", default=["row"], choices=["row", "shuf"],
+                    help="weight stream layout(s): row-major and/or MFMA-preshuffled")
     args = ap.parse_args()
     dev = torch.device("cuda")
     lib = _native.ops()
@@ -78,20 +80,21 @@ def main():
         ws = [(torch.randn(N, K, device=dev) * 0.02).bfloat16() for _ in range(copies)]
         for M in args.m:
             x = torch.randn(M, K, device=dev).bfloat16()
-            call = make_call(epi, x, ws[0], M, N, K, dev)
             graphs = {}
-            for v in args.variants:
-                lib.decode_gemm_variant(v)
-                for c in range(2):
-                    call(ws[c % copies])
-                torch.cuda.synchronize()
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    for c in range(args.chain):
+            for lay in args.layouts:
+                call = make_call(epi, x, ws[0], M, N, K, dev, sh=lay == "shuf")
+                for v in args.variants:
+                    lib.decode_gemm_variant(v)
+                    for c in range(2):
                         call(ws[c % copies])
-                graphs[v] = g
+                    torch.cuda.synchronize()
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        for c in range(args.chain):
+                            call(ws[c % copies])
+                    graphs[(lay, v)] = g
             lib.decode_gemm_variant(-1)
-            times = {v: [] for v in args.variants}
+            times = {k: [] for k in graphs}
             for it in range(args.iters):
                 for v, g in graphs.items():
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -101,11 +104,11 @@ def main():
                     torch.cuda.synchronize()
                     if it:
                         times[v].append(e0.elapsed_time(e1) * 1e3 / args.chain)
-            for v, t in times.items():
+            for (lay, v), t in times.items():
                 t.sort()
                 us = t[len(t) // 2]
-                print(json.dumps({"shape": name, "N": N, "K": K, "M": M, "variant": v, "us": round(us, 2),
-                                  "TBps": round(nbytes / us / 1e6, 3)}), flush=True)
+                print(json.dumps({"shape": name, "N": N, "K": K, "M": M, "layout": lay, "variant": v,
+                                  "us": round(us, 2), "TBps": round(nbytes / us / 1e6, 3)}), flush=True)
             del graphs
         del ws
         torch.cuda.empty_cache()

@@ -387,12 +387,13 @@ void dg_norm_in(DecodeEpi& e, const c10::optional<Tensor>& ss_in, int64_t M, int
   e.eps = (float)eps;
 }
 
-void dg_f32(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, Tensor& y) {
+void dg_f32(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, Tensor& y, bool wshuf) {
   auto sh = dg_check(x, W);
   check_gpu(y, "y");
   check_dtype(y, at::kFloat, "y");
   TORCH_CHECK(y.numel() == sh.M * sh.N, "dg_f32: y must be [M, N]");
   DecodeEpi e;
+  e.wshuf = wshuf ? 1 : 0;
   dg_norm_in(e, ss_in, sh.M, sh.K, eps);
   e.y = ptr<float>(y);
   const at::OptionalDeviceGuard g(x.device());
@@ -401,7 +402,7 @@ void dg_f32(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in
 
 void dg_qkv(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, const Tensor& positions,
             const Tensor& slots, const Tensor& cos_sin, Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t Hq,
-            int64_t Hkv) {
+            int64_t Hkv, bool wshuf) {
   auto sh = dg_check(x, W);
   for (auto* t : {&positions, &slots}) {
     check_gpu(*t, "index tensor");
@@ -418,6 +419,7 @@ void dg_qkv(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in
   TORCH_CHECK(q_out.numel() >= sh.M * Hq * 128, "dg_qkv: q_out too small");
   TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == 128, "dg_qkv: cos_sin [max_pos, 128]");
   DecodeEpi e;
+  e.wshuf = wshuf ? 1 : 0;
   dg_norm_in(e, ss_in, sh.M, sh.K, eps);
   e.positions = ptr<int>(positions);
   e.slots = ptr<int>(slots);
@@ -432,7 +434,7 @@ void dg_qkv(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in
   launch_decode_gemm(DECODE_EPI_QKV, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, e, cur_stream(x));
 }
 
-void dg_resid(const Tensor& x, const Tensor& W, Tensor& resid, const Tensor& w_next, Tensor& xw_out, Tensor& ss_out) {
+void dg_resid(const Tensor& x, const Tensor& W, Tensor& resid, const Tensor& w_next, Tensor& xw_out, Tensor& ss_out, bool wshuf) {
   auto sh = dg_check(x, W);
   check_gpu(resid, "resid");
   check_dtype(resid, at::kFloat, "resid");
@@ -446,6 +448,7 @@ void dg_resid(const Tensor& x, const Tensor& W, Tensor& resid, const Tensor& w_n
               "dg_resid: shape mismatch");
   TORCH_CHECK(ss_out.dim() == 2 && ss_out.size(0) >= sh.M && ss_out.size(1) == sh.N / 16, "dg_resid: ss_out [M, N/16]");
   DecodeEpi e;
+  e.wshuf = wshuf ? 1 : 0;
   e.resid = ptr<float>(resid);
   e.w_next = ptr<bf16>(w_next);
   e.xw_out = ptr<bf16>(xw_out);
@@ -454,12 +457,13 @@ void dg_resid(const Tensor& x, const Tensor& W, Tensor& resid, const Tensor& w_n
   launch_decode_gemm(DECODE_EPI_RESID, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, e, cur_stream(x));
 }
 
-void dg_swiglu(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, Tensor& act) {
+void dg_swiglu(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, Tensor& act, bool wshuf) {
   auto sh = dg_check(x, W);
   check_gpu(act, "act");
   check_dtype(act, at::kBFloat16, "act");
   TORCH_CHECK(act.numel() == sh.M * sh.N / 2, "dg_swiglu: act must be [M, N/2]");
   DecodeEpi e;
+  e.wshuf = wshuf ? 1 : 0;
   dg_norm_in(e, ss_in, sh.M, sh.K, eps);
   e.act = ptr<bf16>(act);
   const at::OptionalDeviceGuard g(x.device());
@@ -469,7 +473,7 @@ void dg_swiglu(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss
 
 void dg_argmax(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, const Tensor& temps,
                const Tensor& seeds, const Tensor& step, Tensor& tile_keys, Tensor& out_keys, Tensor& out_ids,
-               int64_t n_offset, const c10::optional<Tensor>& logits) {
+               int64_t n_offset, const c10::optional<Tensor>& logits, bool wshuf) {
   auto sh = dg_check(x, W);
   check_gpu(temps, "temps");
   check_dtype(temps, at::kFloat, "temps");
@@ -487,6 +491,7 @@ void dg_argmax(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss
   TORCH_CHECK(tile_keys.numel() >= sh.M * (sh.N / 16), "dg_argmax: tile_keys too small");
   TORCH_CHECK(out_keys.numel() >= sh.M && out_ids.numel() >= sh.M, "dg_argmax: outputs too small");
   DecodeEpi e;
+  e.wshuf = wshuf ? 1 : 0;
   dg_norm_in(e, ss_in, sh.M, sh.K, eps);
   if (logits.has_value()) {
     check_gpu(*logits, "logits");
@@ -619,17 +624,17 @@ TORCH_LIBRARY(symmetry_amd, m) {
       "moe_route_permute(Tensor logits, Tensor x, int k, int E, Tensor(a!) ids, Tensor(b!) w, Tensor(c!) counts, "
       "Tensor(d!) offsets, Tensor(e!) cursor, Tensor(f!) xs, Tensor(g!) dst) -> ()",
       &moe_route_permute);
-  m.def("dg_f32(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor(a!) y) -> ()", &dg_f32);
+  m.def("dg_f32(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor(a!) y, bool wshuf=False) -> ()", &dg_f32);
   m.def(
       "dg_qkv(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor positions, Tensor slots, Tensor cos_sin, "
-      "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv) -> ()",
+      "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, bool wshuf=False) -> ()",
       &dg_qkv);
-  m.def("dg_resid(Tensor x, Tensor W, Tensor(a!) resid, Tensor w_next, Tensor(b!) xw_out, Tensor(c!) ss_out) -> ()",
+  m.def("dg_resid(Tensor x, Tensor W, Tensor(a!) resid, Tensor w_next, Tensor(b!) xw_out, Tensor(c!) ss_out, bool wshuf=False) -> ()",
         &dg_resid);
-  m.def("dg_swiglu(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor(a!) act) -> ()", &dg_swiglu);
+  m.def("dg_swiglu(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor(a!) act, bool wshuf=False) -> ()", &dg_swiglu);
   m.def(
       "dg_argmax(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor temps, Tensor seeds, Tensor step, "
-      "Tensor(a!) tile_keys, Tensor(b!) out_keys, Tensor(c!) out_ids, int n_offset, Tensor(d!)? logits) -> ()",
+      "Tensor(a!) tile_keys, Tensor(b!) out_keys, Tensor(c!) out_ids, int n_offset, Tensor(d!)? logits, bool wshuf=False) -> ()",
       &dg_argmax);
   m.def("embed_prep(Tensor ids, Tensor table, Tensor(a!) resid, Tensor w, Tensor(b!) xw, Tensor(c!) ss, "
         "Tensor? src=None, Tensor? prev=None) -> ()",

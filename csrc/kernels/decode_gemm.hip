@@ -161,9 +161,13 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __rest
   const int kbeg = wid * wk;
   const int nblk = wk / 64;
 
+  // weight stream: row-major (16 rows x 64 B per load) or preshuffled (1 KB contiguous per load)
   const bf16* wrow[RT];
+  const int wmul = e.wshuf ? 16 : 1, wsec = e.wshuf ? 512 : 32;
 #pragma unroll
-  for (int rt = 0; rt < RT; ++rt) wrow[rt] = W + (long long)(16 * (tile0 + rt) + r16) * K + kbeg + 8 * h;
+  for (int rt = 0; rt < RT; ++rt)
+    wrow[rt] = e.wshuf ? W + ((long long)(tile0 + rt) * (K / 32) + kbeg / 32) * 512 + lane * 8
+                       : W + (long long)(16 * (tile0 + rt) + r16) * K + kbeg + 8 * h;
   // x fragments of rows >= M are never fetched (masked lanes load nothing; MFMA sees zeros).
   const bf16* xrow[MT];
   bool xok[MT];
@@ -206,8 +210,8 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __rest
       const int ko = (b + u) * 64;
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
-        wa[u][rt][0].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko);
-        wa[u][rt][1].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko + 32);
+        wa[u][rt][0].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko * wmul);
+        wa[u][rt][1].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko * wmul + wsec);
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
@@ -234,8 +238,8 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __rest
     Pack8 w0[RT], w1[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
-      w0[rt].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko);
-      w1[rt].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko + 32);
+      w0[rt].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko * wmul);
+      w1[rt].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko * wmul + wsec);
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {

@@ -11,6 +11,10 @@
 // decode_gemm.hip -- fused decode projections (see the file header)
 enum { DECODE_EPI_F32 = 0, DECODE_EPI_QKV = 1, DECODE_EPI_RESID = 2, DECODE_EPI_SWIGLU = 3, DECODE_EPI_ARGMAX = 4 };
 struct DecodeEpi {
+  // weight layout: 0 = row-major [N][K]; 1 = MFMA-preshuffled (models/layout.py::preshuffle): each
+  // 16-row x 32-k block is 1 KB contiguous in lane order, so one load instruction reads 1 KB and a
+  // wave's k-slice of a row tile is one contiguous stream
+  int wshuf = 0;
   // prologue: RMSNorm row scale rsqrt(sum(ss_in[m][0..ss_tiles)) * inv_d + eps); ss_in == nullptr -> 1
   const float* ss_in = nullptr;
   int ss_tiles = 0;

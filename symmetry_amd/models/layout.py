@@ -72,3 +72,17 @@ def natural_tensors(w: ModelWeights) -> dict:
             t = out[k]
             out[k] = t.index_select(0, _inverse(gu_perm(t.shape[0] // 2)).to(t.device))
     return out
+
+
+# ---- MFMA-preshuffled weight stream (csrc/kernels/decode_gemm.hip, DecodeEpi::wshuf) -----------------
+def preshuffle(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] row-major -> the same elements ordered [N/16][K/32][lane 64][8]: block (t, kb) holds rows
+    16t.. and k 32kb.. with lane l = 16 * (k8 group) + row, i.e. exactly the MFMA 16x16x32 A-fragment
+    order, so one wave load instruction reads 1 KB contiguous.  Returned with the original [N, K] shape."""
+    N, K = w.shape
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N, K)
+
+
+def unshuffle(w: torch.Tensor) -> torch.Tensor:
+    N, K = w.shape
+    return w.reshape(N // 16, K // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).contiguous().view(N, K)

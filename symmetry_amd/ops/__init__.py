@@ -122,36 +122,39 @@ def swiglu(gu, out, interleaved=False):
 
 # ---- fused decode GEMMs: M <= 64 rows, weights in the decode layout (models/layout.py) ----------
 # ss_in: per-(row, tile) sums of squares of the residual [>=M, tiles] (deferred RMSNorm) or None.
-def dg_f32(x, W, ss_in, eps, y):
+def dg_f32(x, W, ss_in, eps, y, wshuf=False):
     if _gpu(x):
-        return _native.ops().dg_f32(x, W, ss_in, float(eps), y)
-    return reference.dg_f32(x, W, ss_in, eps, y)
+        return _native.ops().dg_f32(x, W, ss_in, float(eps), y, bool(wshuf))
+    return reference.dg_f32(x, reference.unshuffled(W, wshuf), ss_in, eps, y)
 
 
-def dg_qkv(x, W, ss_in, eps, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv):
+def dg_qkv(x, W, ss_in, eps, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, wshuf=False):
     if _gpu(x):
         return _native.ops().dg_qkv(x, W, ss_in, float(eps), positions, slots, cos_sin, q_out, k_cache, v_cache,
-                                    int(Hq), int(Hkv))
-    return reference.dg_qkv(x, W, ss_in, eps, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv)
+                                    int(Hq), int(Hkv), bool(wshuf))
+    return reference.dg_qkv(x, reference.unshuffled(W, wshuf), ss_in, eps, positions, slots, cos_sin, q_out,
+                            k_cache, v_cache, Hq, Hkv)
 
 
-def dg_resid(x, W, resid, w_next, xw_out, ss_out):
+def dg_resid(x, W, resid, w_next, xw_out, ss_out, wshuf=False):
     if _gpu(x):
-        return _native.ops().dg_resid(x, W, resid, w_next, xw_out, ss_out)
-    return reference.dg_resid(x, W, resid, w_next, xw_out, ss_out)
+        return _native.ops().dg_resid(x, W, resid, w_next, xw_out, ss_out, bool(wshuf))
+    return reference.dg_resid(x, reference.unshuffled(W, wshuf), resid, w_next, xw_out, ss_out)
 
 
-def dg_swiglu(x, W, ss_in, eps, act):
+def dg_swiglu(x, W, ss_in, eps, act, wshuf=False):
     if _gpu(x):
-        return _native.ops().dg_swiglu(x, W, ss_in, float(eps), act)
-    return reference.dg_swiglu(x, W, ss_in, eps, act)
+        return _native.ops().dg_swiglu(x, W, ss_in, float(eps), act, bool(wshuf))
+    return reference.dg_swiglu(x, reference.unshuffled(W, wshuf), ss_in, eps, act)
 
 
-def dg_argmax(x, W, ss_in, eps, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset=0, logits=None):
+def dg_argmax(x, W, ss_in, eps, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset=0, logits=None,
+              wshuf=False):
     if _gpu(x):
         return _native.ops().dg_argmax(x, W, ss_in, float(eps), temps, seeds, step, tile_keys, out_keys, out_ids,
-                                       int(n_offset), logits)
-    return reference.dg_argmax(x, W, ss_in, eps, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset, logits)
+                                       int(n_offset), logits, bool(wshuf))
+    return reference.dg_argmax(x, reference.unshuffled(W, wshuf), ss_in, eps, temps, seeds, step, tile_keys,
+                               out_keys, out_ids, n_offset, logits)
 
 
 def embed_prep(ids, table, resid, w, xw, ss, src=None, prev=None):

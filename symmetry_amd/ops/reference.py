@@ -239,6 +239,15 @@ def swiglu(gu, out, interleaved: bool = False) -> None:
 
 
 # ----- fused decode GEMMs (csrc/kernels/decode_gemm.hip) -----------------------------------------
+def unshuffled(W, wshuf: bool):
+    """Row-major view of a decode weight stored MFMA-preshuffled (models/layout.py::preshuffle)."""
+    if not wshuf:
+        return W
+    from ..models.layout import unshuffle
+
+    return unshuffle(W)
+
+
 def _row_scale(ss_in, eps: float, K: int, M: int):
     if ss_in is None:
         return None

@@ -171,3 +171,17 @@ def test_rope_cache_perm_and_swiglu_interleaved(gpu):
     a_r = torch.empty(T, F, dtype=torch.bfloat16)
     ref.swiglu(gu.cpu(), a_r, interleaved=True)
     _close(a, a_r, atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("M", [1, 10, 33])
+def test_preshuffled_weight_stream(gpu, M):
+    """MFMA-preshuffled weights (1 KB contiguous per wave load) give the row-major result exactly."""
+    from symmetry_amd.models.layout import preshuffle
+
+    for N, K in ((4096, 4096), (28672, 4096), (4096, 1792)):
+        x, W, s = _inputs(gpu, M, N, K, seed=12)
+        y0 = torch.empty(M, N, device=gpu)
+        y1 = torch.empty(M, N, device=gpu)
+        ops.dg_f32(x, W, s, 1e-5, y0)
+        ops.dg_f32(x, preshuffle(W), s, 1e-5, y1, wshuf=True)
+        assert torch.equal(y0, y1), (N, K)

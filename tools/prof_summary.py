@@ -1,7 +1,9 @@
 """Summarise a rocprofv3 kernel-trace database (rocpd SQLite) into a per-kernel CSV.
 
-usage: python tools/prof_summary.py gpurun_out/prof/run_results.db [out.csv] [--top N]
-Kernel names are shortened to the template head (argument lists dropped).
+usage: python tools/prof_summary.py gpurun_out/prof/run_results.db [out.csv] [--top N] [--last-ms T]
+Kernel names are shortened to the template head (argument lists dropped).  ``--last-ms T`` keeps only
+dispatches that start in the final T ms of the trace (steady-state decode after ``bench.py
+--profile-steps``) and also prints the GPU-busy fraction of that window.
 """
 import csv
 import re
@@ -28,9 +30,28 @@ def main():
     db = sys.argv[1]
     out = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("--") else None
     top = int(sys.argv[sys.argv.index("--top") + 1]) if "--top" in sys.argv else 40
+    last_ms = float(sys.argv[sys.argv.index("--last-ms") + 1]) if "--last-ms" in sys.argv else None
     c = sqlite3.connect(db)
+    rows_all = list(c.execute("select name, duration, grid_x, workgroup_x, start, end from kernels order by start"))
+    if last_ms is not None and rows_all:
+        t_end = max(r[5] for r in rows_all)
+        t_lo = t_end - last_ms * 1e6
+        rows_all = [r for r in rows_all if r[4] >= t_lo]
+        busy, cur_s, cur_e = 0, None, None
+        for r in rows_all:
+            if cur_e is None or r[4] > cur_e:
+                if cur_e is not None:
+                    busy += cur_e - cur_s
+                cur_s, cur_e = r[4], r[5]
+            else:
+                cur_e = max(cur_e, r[5])
+        if cur_e is not None:
+            busy += cur_e - cur_s
+        span = t_end - rows_all[0][4] if rows_all else 1
+        print(f"# window {span / 1e6:.2f} ms, {len(rows_all)} dispatches, GPU busy {100 * busy / span:.1f}%",
+              file=sys.stderr)
     agg = defaultdict(lambda: [0, 0, 1 << 62, 0, ""])
-    for name, dur, gx, wx in c.execute("select name, duration, grid_x, workgroup_x from kernels"):
+    for name, dur, gx, wx, _, _ in rows_all:
         k = short(name)
         a = agg[k]
         a[0] += 1
