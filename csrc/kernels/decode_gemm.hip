@@ -344,11 +344,23 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
     // every workgroup) dominate the L1/TA traffic once M > 4, so wide-N projections share them over
     // 4 (2 for M > 16) row tiles per workgroup; the 4096-wide ones keep 256 workgroups and split K
     // over 4 waves; small TP shards keep the 8-wave split.
-    if (M <= 4) v = 0;
-    else if (N >= 12288) v = 7;
-    else if (N >= 6144 && K >= 4096) v = 3;
-    else if (N <= 4096 && K >= 4096) v = 4;
-    else v = 0;
+    if (e.wshuf) {
+      // preshuffled stream (profiles/decode_gemm_preshuffle_r1.jsonl): 1 KB loads make the x-fragment
+      // sharing of multi-tile workgroups unnecessary; wide N prefers 4 waves per tile
+      if (M <= 4) v = 0;
+      else if (N >= 12288) v = M > 16 ? 3 : 4;
+      else v = 0;
+    } else if (M <= 4) {
+      v = 0;
+    } else if (N >= 12288) {
+      v = 7;
+    } else if (N >= 6144 && K >= 4096) {
+      v = 3;
+    } else if (N <= 4096 && K >= 4096) {
+      v = 4;
+    } else {
+      v = 0;
+    }
   }
   if (v == 2 && K % 1024) v = 0;
   if ((v == 5 || v == 7) && (MT > 1 || N % 64)) v = v == 5 ? 3 : 6;

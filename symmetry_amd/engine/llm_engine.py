@@ -53,6 +53,7 @@ class EngineConfig:
     ep_rank: int = 0
     weight_init: str = "auto"            # "full" | "shard" | "auto"
     pipeline: bool = True                # enqueue decode step N+1 before step N's tokens reach the host
+    decode_weights: str = "auto"         # "preshuffled" | "shared" | "auto": extra MFMA-ordered decode copies
     model_config: ModelConfig | None = None
 
     @classmethod
@@ -66,7 +67,7 @@ class EngineConfig:
              "maxModelLen": "max_model_len", "kvCacheFraction": "kv_cache_fraction", "blockSize": "block_size",
              "maxTokens": "default_max_tokens", "tensorParallelSize": "tp_size", "expertParallelSize": "ep_size",
              "device": "device",
-             "useGraphs": "use_graphs", "numKvBlocks": "num_kv_blocks"}
+             "useGraphs": "use_graphs", "numKvBlocks": "num_kv_blocks", "decodeWeights": "decode_weights"}
         for k, attr in m.items():
             if cfg.get(k) is not None:
                 setattr(ec, attr, type(getattr(ec, attr))(cfg[k]) if getattr(ec, attr) is not None else cfg[k])
@@ -115,7 +116,7 @@ class LLMEngine:
         self.weights: ModelWeights = weights
         self.load_time = time.perf_counter() - t0
         self.model = TransformerLM(weights, self.device, tp_comm=tp_comm, ep_comm=ep_comm,
-                                   max_decode_ctx=max_model_len)
+                                   max_decode_ctx=max_model_len, decode_weights=cfg.decode_weights)
         self.tokenizer = load_tokenizer(mcfg, cfg.tokenizer or (cfg.weights if cfg.weights != "random" else None))
         nb = cfg.num_kv_blocks or self._auto_blocks(max_model_len)
         self.kv = KVCache(mcfg.num_layers, nb, mcfg.num_kv_heads // cfg.tp_size, mcfg.head_dim, cfg.block_size,

@@ -118,7 +118,8 @@ class Workspace:
 
 
 class TransformerLM:
-    def __init__(self, weights: ModelWeights, device, tp_comm=None, ep_comm=None, max_decode_ctx: int | None = None):
+    def __init__(self, weights: ModelWeights, device, tp_comm=None, ep_comm=None, max_decode_ctx: int | None = None,
+                 decode_weights: str = "auto"):
         self.cfg: ModelConfig = weights.cfg
         self.w = weights
         self.device = torch.device(device)
@@ -147,6 +148,33 @@ class TransformerLM:
         # samples here and the next step's embedding reads pending input tokens from here (src map),
         # so the host can enqueue step N+1 before it has seen step N's tokens (pipelined decode).
         self.last_ids = torch.zeros(MAX_STEP_SEQS, dtype=torch.int32, device=self.device)
+        self.dgw = self._decode_copies(decode_weights)
+
+    def _decode_copies(self, mode: str) -> dict:
+        """MFMA-preshuffled copies of the decode-GEMM weights (1 KB contiguous per wave load:
+        profiles/decode_gemm_preshuffle_r1.jsonl, -9 % per layer).  The row-major tensors stay for the
+        hipBLASLt prefill GEMMs, so this costs one extra copy of the layer weights: on by default when it
+        fits comfortably in HBM (8B: +14.5 GB of 288 GB), off for e.g. 70B on one GPU."""
+        if not self.fused or self.device.type == "cpu" or mode == "shared":
+            return {}
+        names = ["wqkv", "wo"] + ([] if self.cfg.is_moe else ["w_gu", "w_down"])
+        extra = sum(self.w.layer(i, n).numel() * 2 for i in range(self.cfg.num_layers) for n in names)
+        if mode == "auto":
+            free, total = torch.cuda.mem_get_info(self.device)
+            if extra > 0.4 * free:
+                return {}
+        from .layout import preshuffle
+
+        out = {}
+        for i in range(self.cfg.num_layers):
+            for n in names:
+                out[(i, n)] = preshuffle(self.w.layer(i, n))
+        return out
+
+    def _dgw(self, i: int, name: str):
+        """(weight, wshuf) for decode GEMM `name` of layer i."""
+        t = self.dgw.get((i, name))
+        return (t, True) if t is not None else (self.w.layer(i, name), False)
 
     def _fused_supported(self) -> bool:
         """Shape contract of the fused decode GEMMs: D == 128, every K % 256 == 0, every N % 16 == 0."""
@@ -198,15 +226,16 @@ class TransformerLM:
     def _tp_active(self) -> bool:
         return self.tp is not None and self.tp_size > 1
 
-    def _resid_proj(self, name, x, W, resid, w_next, xw, ss_t, ss_1) -> torch.Tensor:
+    def _resid_proj(self, name, x, Wsh, resid, w_next, xw, ss_t, ss_1) -> torch.Tensor:
         """Row-parallel projection + residual add + next-norm prep; returns the ss partials to use."""
+        W, sh = Wsh
         if self._tp_active():
             y = self._buf(name + ".f32", (x.shape[0], W.shape[0]), torch.float32)
-            ops.dg_f32(x, W, None, 0.0, y)
+            ops.dg_f32(x, W, None, 0.0, y, wshuf=sh)
             self.tp.all_reduce(y)
             ops.add_prep(y, resid, w_next, xw, ss_1)
             return ss_1
-        ops.dg_resid(x, W, resid, w_next, xw, ss_t)
+        ops.dg_resid(x, W, resid, w_next, xw, ss_t, wshuf=sh)
         return ss_t
 
     def _forward_fused(self, b: ForwardBatch, kv: KVCache) -> torch.Tensor:
@@ -221,10 +250,11 @@ class TransformerLM:
         ops.embed_prep(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), xw, ss_1, b.src, self.last_ids)
         ss = ss_1
         for i in range(cfg.num_layers):
-            ops.dg_qkv(xw, w.layer(i, "wqkv"), ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i],
-                       kv.v[i], self.hq, self.hkv)
+            wq, shq = self._dgw(i, "wqkv")
+            ops.dg_qkv(xw, wq, ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq,
+                       self.hkv, wshuf=shq)
             self._attention(b, kv, i, q, attn)
-            ss = self._resid_proj("o", attn.view(T, self.hq * self.D), w.layer(i, "wo"), resid, w.layer(i, "ln2"),
+            ss = self._resid_proj("o", attn.view(T, self.hq * self.D), self._dgw(i, "wo"), resid, w.layer(i, "ln2"),
                                   xw, ss_t, ss_1)
             nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
             if cfg.is_moe:
@@ -234,10 +264,10 @@ class TransformerLM:
                 ops.add_prep(self.moe.forward(i, xn), resid, nxt, xw, ss_1)
                 ss = ss_1
             else:
-                w_gu = w.layer(i, "w_gu")
+                w_gu, shg = self._dgw(i, "w_gu")
                 act = self._buf("act", (T, w_gu.shape[0] // 2), torch.bfloat16)
-                ops.dg_swiglu(xw, w_gu, ss, eps, act)
-                ss = self._resid_proj("down", act, w.layer(i, "w_down"), resid, nxt, xw, ss_t, ss_1)
+                ops.dg_swiglu(xw, w_gu, ss, eps, act, wshuf=shg)
+                ss = self._resid_proj("down", act, self._dgw(i, "w_down"), resid, nxt, xw, ss_t, ss_1)
         n = b.num_seqs
         if b.kind == "decode":
             xl, sl = xw, ss
