@@ -177,11 +177,18 @@ def test_rope_cache_perm_and_swiglu_interleaved(gpu):
 def test_preshuffled_weight_stream(gpu, M):
     """MFMA-preshuffled weights (1 KB contiguous per wave load) give the row-major result exactly."""
     from symmetry_amd.models.layout import preshuffle
+    from symmetry_amd.ops import _native
 
-    for N, K in ((4096, 4096), (28672, 4096), (4096, 1792)):
-        x, W, s = _inputs(gpu, M, N, K, seed=12)
-        y0 = torch.empty(M, N, device=gpu)
-        y1 = torch.empty(M, N, device=gpu)
-        ops.dg_f32(x, W, s, 1e-5, y0)
-        ops.dg_f32(x, preshuffle(W), s, 1e-5, y1, wshuf=True)
-        assert torch.equal(y0, y1), (N, K)
+    lib = _native.ops()
+    try:
+        for v in (0, 3, 4, 7):  # same decomposition on both layouts -> same summation order -> bitwise equal
+            lib.decode_gemm_variant(v)
+            for N, K in ((4096, 4096), (28672, 4096), (4096, 1792)):
+                x, W, s = _inputs(gpu, M, N, K, seed=12)
+                y0 = torch.empty(M, N, device=gpu)
+                y1 = torch.empty(M, N, device=gpu)
+                ops.dg_f32(x, W, s, 1e-5, y0)
+                ops.dg_f32(x, preshuffle(W), s, 1e-5, y1, wshuf=True)
+                assert torch.equal(y0, y1), (v, N, K)
+    finally:
+        lib.decode_gemm_variant(-1)
