@@ -53,29 +53,39 @@ SYM_DEV bf16x8 zero8() {
 }
 
 // One 32-token group: S^T for two 16-token tiles, online softmax update, P.V.
-// `valid(a, r)` tells whether token (8h + 4a + r) of the group is visible to this lane's query column.
-template <typename ValidFn>
-SYM_DEV void attend_group(const bf16* __restrict__ kb, const bf16* __restrict__ vb, int BS, const bf16x8 (&qf)[4],
-                          float scale_log2, ValidFn valid, f32x4 (&o)[8], float& m, float& lsum) {
+// Split into a load phase (K and V fragments of the group to registers) and a compute phase so that
+// callers can have the next group's loads in flight while computing the current one.
+struct KVFrag {
+  bf16x8 k[2][4];  // two 16-token S^T tiles x 4 D-slices
+  bf16x8 v[8];     // 8 dim tiles of V^T
+};
+
+SYM_DEV void load_group(const bf16* __restrict__ kb, const bf16* __restrict__ vb, int BS, KVFrag& f) {
   const int lane = threadIdx.x & 63;
   const int r16 = lane & 15, h = lane >> 4;
-  f32x4 s[2];
 #pragma unroll
   for (int a = 0; a < 2; ++a) {
     const int trow = (r16 >> 2) * 8 + 4 * a + (r16 & 3);
     const bf16* kr = kb + (long long)trow * D + 32 * h;
-    bf16x8 kf[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) kf[i] = ld16(kr + 8 * i);
+    for (int i = 0; i < 4; ++i) f.k[a][i] = ld16(kr + 8 * i);
+  }
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) f.v[dt] = ld16(vb + (long long)(16 * dt + r16) * BS + 8 * h);
+}
+
+// `valid(a, r)` tells whether token (8h + 4a + r) of the group is visible to this lane's query column.
+template <typename ValidFn>
+SYM_DEV void compute_group(const KVFrag& f, const bf16x8 (&qf)[4], float scale_log2, ValidFn valid, f32x4 (&o)[8],
+                           float& m, float& lsum) {
+  f32x4 s[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc = mfma16(kf[i], qf[i], acc);
+    for (int i = 0; i < 4; ++i) acc = mfma16(f.k[a][i], qf[i], acc);
     s[a] = acc;
   }
-  bf16x8 vf[8];
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) vf[dt] = ld16(vb + (long long)(16 * dt + r16) * BS + 8 * h);
-
   float x[8];
   float gmax = -INFINITY;
 #pragma unroll
@@ -104,7 +114,7 @@ SYM_DEV void attend_group(const bf16* __restrict__ kb, const bf16* __restrict__ 
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) {
     o[dt] *= alpha;
-    o[dt] = mfma16(vf[dt], pf.v, o[dt]);
+    o[dt] = mfma16(f.v[dt], pf.v, o[dt]);
   }
 }
 
@@ -137,18 +147,29 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, lsum = 0.f;
 
+  // Both 32-token groups of this wave are loaded before either is computed: one memory round trip
+  // (block table -> K/V) instead of one per group.
   const int* bt = block_tables + (long long)seq * max_blocks;
   const int tok0 = part * PART + wid * 64;
+  KVFrag f[2];
+  const int ngroups = tok0 >= ctx ? 0 : (tok0 + 32 >= ctx ? 1 : 2);
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
-    const int tbase = tok0 + 32 * g;
-    if (tbase >= ctx) break;
-    const long long blk = bt[tbase / BS];
-    const int boff = tbase % BS;
-    const bf16* kb = k_cache + ((blk * Hkv + kvh) * BS + boff) * D;
-    const bf16* vb = v_cache + (blk * Hkv + kvh) * (long long)D * BS + boff;
-    attend_group(kb, vb, BS, qf, scale_log2,
-                 [&](int a, int r) { return tbase + 8 * h + 4 * a + r < ctx; }, o, m, lsum);
+    if (g < ngroups) {
+      const int tbase = tok0 + 32 * g;
+      const long long blk = bt[tbase / BS];
+      const int boff = tbase % BS;
+      load_group(k_cache + ((blk * Hkv + kvh) * BS + boff) * D, v_cache + (blk * Hkv + kvh) * (long long)D * BS + boff,
+                 BS, f[g]);
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    if (g < ngroups) {
+      const int tbase = tok0 + 32 * g;
+      compute_group(f[g], qf, scale_log2, [&](int a, int r) { return tbase + 8 * h + 4 * a + r < ctx; }, o, m,
+                    lsum);
+    }
   }
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
@@ -282,17 +303,32 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(
   const int* bt = block_tables + (long long)seq * max_blocks;
   // last key any row of this wave may see
   const int kend = min(ctx, pos0 + min(row0 + 16, qlen));
-  for (int tbase = 0; tbase < kend; tbase += 32) {
+  // software pipeline: group g+1's K/V loads are in flight while group g is computed
+  auto kv_ptrs = [&](int tbase, const bf16*& kb, const bf16*& vb) {
     const long long blk = bt[tbase / BS];
     const int boff = tbase % BS;
-    const bf16* kb = k_cache + ((blk * Hkv + kvh) * BS + boff) * D;
-    const bf16* vb = v_cache + (blk * Hkv + kvh) * (long long)D * BS + boff;
-    attend_group(kb, vb, BS, qf, scale_log2,
-                 [&](int a, int r) {
-                   const int t = tbase + 8 * h + 4 * a + r;
-                   return row_ok && t <= mypos && t < ctx;
-                 },
-                 o, m, lsum);
+    kb = k_cache + ((blk * Hkv + kvh) * BS + boff) * D;
+    vb = v_cache + (blk * Hkv + kvh) * (long long)D * BS + boff;
+  };
+  KVFrag cur, nxt;
+  if (kend > 0) {
+    const bf16 *kb, *vb;
+    kv_ptrs(0, kb, vb);
+    load_group(kb, vb, BS, cur);
+  }
+  for (int tbase = 0; tbase < kend; tbase += 32) {
+    if (tbase + 32 < kend) {
+      const bf16 *kb, *vb;
+      kv_ptrs(tbase + 32, kb, vb);
+      load_group(kb, vb, BS, nxt);
+    }
+    compute_group(cur, qf, scale_log2,
+                  [&](int a, int r) {
+                    const int t = tbase + 8 * h + 4 * a + r;
+                    return row_ok && t <= mypos && t < ctx;
+                  },
+                  o, m, lsum);
+    cur = nxt;
   }
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
