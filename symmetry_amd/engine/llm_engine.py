@@ -100,7 +100,7 @@ class LLMEngine:
     def __init__(self, cfg: EngineConfig, tp_comm=None, ep_comm=None, cpu_group=None):
         self.cfg = cfg
         self.device = _pick_device(cfg.device)
-        self.model_cfg = cfg.model_config or resolve(cfg.model)
+        self.model_cfg = cfg.model_config or self._model_config(cfg)
         mcfg = self.model_cfg
         max_model_len = min(cfg.max_model_len, mcfg.max_position)
         self.metrics = EngineMetrics()
@@ -139,6 +139,20 @@ class LLMEngine:
         self.profile_trace: str | None = None
 
     # ------------------------------------------------------------------------------------------
+    @staticmethod
+    def _model_config(cfg: "EngineConfig") -> ModelConfig:
+        """A HF checkpoint directory's config.json wins over the registry (any Llama / Mixtral size)."""
+        if cfg.weights != "random":
+            path = os.path.join(cfg.weights, "config.json")
+            if os.path.exists(path):
+                import json
+
+                from ..models.config import from_hf_config
+
+                with open(path) as f:
+                    return from_hf_config(json.load(f), name=cfg.model)
+        return resolve(cfg.model)
+
     def _graph_safe(self, tp_comm, ep_comm) -> bool:
         """Decode hipGraphs need every collective to be capturable (our RCCL communicator) and no
         host-side data-dependent shapes (all-to-all expert dispatch reads counts on the host)."""
