@@ -53,6 +53,7 @@ class EngineConfig:
     ep_rank: int = 0
     weight_init: str = "auto"            # "full" | "shard" | "auto"
     pipeline: bool = True                # enqueue decode step N+1 before step N's tokens reach the host
+    mixed_prefill_tokens: int = 512      # prompt-chunk budget of steps that also carry decodes
     decode_weights: str = "auto"         # "preshuffled" | "shared" | "auto": extra MFMA-ordered decode copies
     model_config: ModelConfig | None = None
 
@@ -67,7 +68,8 @@ class EngineConfig:
              "maxModelLen": "max_model_len", "kvCacheFraction": "kv_cache_fraction", "blockSize": "block_size",
              "maxTokens": "default_max_tokens", "tensorParallelSize": "tp_size", "expertParallelSize": "ep_size",
              "device": "device",
-             "useGraphs": "use_graphs", "numKvBlocks": "num_kv_blocks", "decodeWeights": "decode_weights"}
+             "useGraphs": "use_graphs", "numKvBlocks": "num_kv_blocks", "decodeWeights": "decode_weights",
+             "prefillChunk": "mixed_prefill_tokens"}
         for k, attr in m.items():
             if cfg.get(k) is not None:
                 setattr(ec, attr, type(getattr(ec, attr))(cfg[k]) if getattr(ec, attr) is not None else cfg[k])
@@ -124,7 +126,8 @@ class LLMEngine:
         self.blocks = BlockManager(nb, cfg.block_size)
         self.scheduler = Scheduler(
             SchedulerConfig(max_num_seqs=min(cfg.max_num_seqs, 64 if self.device.type != "cpu" else cfg.max_num_seqs),
-                            max_num_batched_tokens=cfg.max_num_batched_tokens, max_model_len=max_model_len),
+                            max_num_batched_tokens=cfg.max_num_batched_tokens, max_model_len=max_model_len,
+                            mixed_prefill_tokens=cfg.mixed_prefill_tokens),
             self.blocks)
         self.runner = ModelRunner(self.model, self.kv, self.scheduler.cfg.max_num_seqs, max_model_len,
                                   use_graphs=cfg.use_graphs and self._graph_safe(tp_comm, ep_comm),

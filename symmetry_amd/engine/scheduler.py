@@ -59,6 +59,9 @@ class SchedulerConfig:
     max_num_batched_tokens: int = 8192
     max_model_len: int = 8192
     enable_chunked_prefill: bool = True
+    # prompt tokens per step while other sequences are decoding: mixed steps keep every running
+    # sequence streaming (one token per step) while long prompts prefill in chunks
+    mixed_prefill_tokens: int = 512
 
 
 @dataclass
@@ -117,13 +120,27 @@ class Scheduler:
 
     # ------------------------------------------------------------------------------------------
     def schedule(self) -> ScheduledBatch | None:
-        batch = self._schedule_prefill()
-        if batch is not None:
-            return batch
-        return self._schedule_decode()
+        """Pure prefill when nothing is decoding (best TTFT for simultaneous arrivals), pure decode when
+        no prompt work is pending, otherwise a mixed step: one token for every decoding sequence plus
+        prompt chunks up to ``mixed_prefill_tokens`` (decodes never stall behind a long prompt)."""
+        prompt_work = bool(self.waiting) or any(s.in_prefill for s in self.running)
+        decoding = any(not s.in_prefill for s in self.running)
+        if not prompt_work:
+            return self._schedule_decode()
+        if not decoding:
+            return self._schedule_prefill()
+        d = self._schedule_decode()
+        nd = len(d.seqs) if d is not None else 0
+        p = self._schedule_prefill(max(self.cfg.mixed_prefill_tokens - nd, 1))
+        if d is None or not d.seqs:
+            return p if p is not None else d
+        if p is None:
+            return d
+        return ScheduledBatch("prefill", d.seqs + p.seqs, d.num_new_tokens + p.num_new_tokens, d.sample + p.sample,
+                              d.preempted)
 
-    def _schedule_prefill(self) -> ScheduledBatch | None:
-        budget = self.cfg.max_num_batched_tokens
+    def _schedule_prefill(self, budget: int | None = None) -> ScheduledBatch | None:
+        budget = self.cfg.max_num_batched_tokens if budget is None else budget
         seqs, counts, sample = [], [], []
 
         def take(seq: Sequence) -> bool:
