@@ -347,8 +347,8 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
     if (e.wshuf) {
       // preshuffled stream (profiles/decode_gemm_preshuffle_r1.jsonl): 1 KB loads make the x-fragment
       // sharing of multi-tile workgroups unnecessary; wide N prefers 4 waves per tile
-      if (M <= 4) v = 0;
-      else if (N >= 12288) v = M > 16 ? 3 : 4;
+      if (N >= 12288) v = M > 16 ? 3 : (M <= 4 ? 0 : 4);
+      else if (N <= 4096 && K % 1024 == 0) v = 2;  // few row tiles: split K over 16 waves
       else v = 0;
     } else if (M <= 4) {
       v = 0;
