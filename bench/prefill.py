@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""TTFT / prefill throughput of the native engine: C prompts of L tokens arriving together.
+
+Reports the wall time of the prefill step(s) that produce every first token (= TTFT of the last client),
+prefill tokens/s and achieved TFLOP/s (2 x params x tokens + attention), after the engine's start-up warmup.
+
+  python bench/prefill.py --model llama3:8b --clients 10 --prompt-len 128 --reps 5
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3:8b")
+    ap.add_argument("--clients", type=int, default=10)
+    ap.add_argument("--prompt-len", type=int, default=128)
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+
+    C, L = args.clients, args.prompt_len
+    eng = LLMEngine(EngineConfig(model=args.model, max_num_seqs=max(C, 1), max_model_len=max(2048, L + 64),
+                                 max_num_batched_tokens=max(8192, C * L)))
+    eng.warmup([16, 128, 512, C * L] if C * L > 512 else None)
+    cfg = eng.model_cfg
+    times = []
+    for r in range(args.reps):
+        seqs = [eng.add_request(f"p{r}-{i}", [(97 * i + 13 * k + r) % 30000 + 300 for k in range(L)],
+                                SamplingParams(max_tokens=1, ignore_eos=True)) for i in range(C)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        while not all(s.output_ids for s in seqs):
+            eng.step()
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+        while eng.has_unfinished():
+            eng.step()
+    times.sort()
+    t = times[len(times) // 2]
+    toks = C * L
+    vd = cfg.vocab_size * cfg.hidden_size
+    body = cfg.num_params() - vd - (0 if cfg.tie_embeddings else vd)  # layers only: embedding is a gather
+    flops = 2 * body * toks + 2 * vd * C + 4 * cfg.num_layers * cfg.num_heads * cfg.head_dim * C * L * L / 2
+    print(json.dumps({"model": args.model, "clients": C, "prompt_len": L, "ttft_ms": round(t * 1e3, 2),
+                      "prefill_tokens_per_s": round(toks / t), "tflops": round(flops / t / 1e12, 1)}))
+
+
+if __name__ == "__main__":
+    main()
