@@ -368,13 +368,20 @@ class LLMEngine:
         """Provider start-up pass: one prefill per size class (library GEMM heuristics and code objects
         load here, not in the first client's TTFT), then capture the decode hipGraphs.  Returns seconds."""
         t0 = time.perf_counter()
-        limit = min(self.scheduler.cfg.max_num_batched_tokens, self.scheduler.cfg.max_model_len - 4)
-        lens = prompt_lens or [n for n in (1, 16, 64, 128, 256, 512, 1024, 2048, 4096, 8192) if n <= limit]
+        budget = self.scheduler.cfg.max_num_batched_tokens
+        seq_cap = self.scheduler.cfg.max_model_len - 4
+        lens = prompt_lens or [n for n in (1, 16, 64, 128, 256, 512, 1024, 2048, 4096, 8192) if n <= budget]
         vocab = self.model_cfg.vocab_size
         for n in lens:
-            ids = [(7 * i + 3) % (vocab - 1) + 1 for i in range(n)]
-            seq = self.add_request(f"__warmup-{n}", ids, SamplingParams(max_tokens=2, ignore_eos=True))
-            while not seq.status.finished:
+            n = min(n, budget)
+            # a size class larger than one sequence may hold is warmed as several prompts in one step
+            k = max(1, -(-n // seq_cap))
+            seqs = []
+            for j in range(k):
+                m = n // k + (1 if j < n % k else 0)
+                ids = [(7 * i + 3 * j) % (vocab - 1) + 1 for i in range(m)]
+                seqs.append(self.add_request(f"__warmup-{n}-{j}", ids, SamplingParams(max_tokens=2, ignore_eos=True)))
+            while not all(s.status.finished for s in seqs):
                 self.step()
         self.runner.capture_all()
         self.metrics = EngineMetrics()
