@@ -131,12 +131,12 @@ def test_attn_decode(gpu, Hq, Hkv, BS):
     assert torch.equal(out, out2)
 
 
-@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 8)])
-def test_attn_prefill(gpu, Hq, Hkv):
-    BS = 64
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 8), (64, 8), (16, 8)])
+@pytest.mark.parametrize("BS", [32, 64])
+def test_attn_prefill(gpu, Hq, Hkv, BS):
     g = torch.Generator(device=gpu).manual_seed(4)
     # (new tokens, total context): fresh prompts and chunked continuations
-    specs = [(5, 5), (64, 64), (100, 100), (37, 300), (130, 130), (1, 77)]
+    specs = [(5, 5), (64, 64), (100, 100), (37, 300), (130, 130), (1, 77), (200, 457)]
     ctx_lens = [c for _, c in specs]
     kc, vc, bt = _random_paged(gpu, ctx_lens, Hkv, BS, g)
     qlens = [n for n, _ in specs]
