@@ -158,7 +158,8 @@ def main() -> int:
             "config": {"model": args.model, "global_batch": world * C, "seq_len": P,
                        "parallelism": f"dp{world}", "clients_per_gpu": C, "max_model_len": args.max_model_len,
                        "decode": "greedy", "hipgraphs": bool(eng.runner.use_graphs),
-                       "ops": "torch-eager (baseline B1)" if ops.torch_mode() else "native gfx950 HIP"},
+                       "ops": ("torch-eager (baseline B1)" if ops.torch_mode() else
+                               "native gfx950 HIP" if torch.cuda.is_available() else "torch reference (CPU)")},
             "per_client_tokens_per_s": round(per_client, 2),
             "p50_ttft_ms": round(p50_ttft, 2),
             "load_s": round(t_load, 1),
