@@ -17,7 +17,7 @@
 // contiguous bytes.  Softmax is online (running max / sum per query column),
 // in base 2 with the 1/sqrt(D)*log2(e) scale folded into one multiply.
 //
-// Decode (K5): grid (seq, kv_head, partition); 4 waves x 64 tokens = 256
+// Decode (K5): grid (seq, kv_head, partition); 8 waves x 64 tokens = 512
 // tokens per partition; the G = Hq/Hkv query heads of a kv head are the MFMA
 // columns (K/V are read once per kv head).  Multi-partition sequences write
 // fp32 partials that the last-arriving partition combines (split-KV,
@@ -34,7 +34,8 @@
 namespace {
 
 constexpr int D = 128;
-constexpr int PART = 256;  // tokens per decode partition (4 waves x 64)
+constexpr int DWAVES = 8;            // waves per decode workgroup
+constexpr int PART = DWAVES * 64;    // tokens per decode partition: contexts <= 512 need no combine
 
 SYM_DEV f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -121,7 +122,7 @@ SYM_DEV void compute_group(const KVFrag& f, const bf16x8 (&qf)[4], float scale_l
 // ---------------------------------------------------------------------------------------------
 // Decode
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void attn_decode_kernel(
+__global__ __launch_bounds__(DWAVES * 64) void attn_decode_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
     const int* __restrict__ block_tables, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
     float* __restrict__ tmp_o, float* __restrict__ tmp_ml, int* __restrict__ counters, int Hq, int Hkv, int BS,
@@ -174,8 +175,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
 
-  __shared__ float sm_m[4][16], sm_l[4][16];
-  __shared__ float sm_o[4][16][D + 4];
+  __shared__ float sm_m[DWAVES][16], sm_l[DWAVES][16];
+  __shared__ float sm_o[DWAVES][16][D + 4];
   if (h == 0) {
     sm_m[wid][c] = m;
     sm_l[wid][c] = lsum;
@@ -186,7 +187,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     for (int r = 0; r < 4; ++r) sm_o[wid][c][16 * dt + 4 * h + r] = o[dt][r];
   __syncthreads();
 
-  // Combine the 4 waves' partial softmax states: thread (qq, d0) owns 8 dims of query column qq.
+  // Combine the waves' partial softmax states: thread (qq, d0) owns 8 dims of query column qq.
   const int qq = threadIdx.x >> 4;        // 0..15 query column
   const int d0 = (threadIdx.x & 15) * 8;  // 8 dims per thread
   const bool active = qq < G;
@@ -195,9 +196,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   float M = -INFINITY, L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (active) {
 #pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm_m[w][qq]);
+    for (int w = 0; w < DWAVES; ++w) M = fmaxf(M, sm_m[w][qq]);
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < DWAVES; ++w) {
       const float mw = sm_m[w][qq];
       const float f = (mw == -INFINITY) ? 0.f : exp2f(mw - M);
       L += sm_l[w][qq] * f;
@@ -499,7 +500,7 @@ void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache,
   if (num_seqs == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(num_seqs, Hkv, max_parts);
-  attn_decode_kernel<<<grid, 256, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters,
+  attn_decode_kernel<<<grid, DWAVES * 64, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters,
                                           Hq, Hkv, BS, max_blocks, max_parts, scale_log2);
 }
 

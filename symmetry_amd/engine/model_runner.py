@@ -26,7 +26,7 @@ from ..models.transformer import ForwardBatch, KVCache, TransformerLM
 from .scheduler import ScheduledBatch
 
 DECODE_BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64)
-CTX_BUCKETS = (256, 1024, 4096, 16384, 65536, 131072)  # tokens
+CTX_BUCKETS = (512, 2048, 8192, 32768, 131072)  # tokens (multiples of the 512-token attention partition)
 CMD_STOP, CMD_CAPTURE = -1, 2  # control headers of the rank-0 -> worker metadata plane
 HEADER_LEN = 7  # kind, T, rows, max_blocks, prefill tiles, real seqs, filtered-sampling flag
 _SEED_MIX = 0x9E3779B97F4A7C15

@@ -207,7 +207,8 @@ class TransformerLM:
     # ------------------------------------------------------------------------------------------
     def _attention(self, b: ForwardBatch, kv: KVCache, i: int, q: torch.Tensor, attn: torch.Tensor) -> None:
         if b.kind == "decode":
-            max_parts = (b.block_tables.shape[1] * kv.block_size + 255) // 256
+            span = b.block_tables.shape[1] * kv.block_size
+            max_parts = (span + ops.ATTN_DECODE_PART - 1) // ops.ATTN_DECODE_PART
             tmp_o = self._buf("tmp_o", (b.num_seqs, self.hq, max_parts, self.D), torch.float32)
             tmp_ml = self._buf("tmp_ml", (b.num_seqs, self.hq, max_parts, 2), torch.float32)
             cnt = self.ws.get("attn_counters", (b.num_seqs * self.hkv,), torch.int32, self.device, zeros=True)

@@ -85,6 +85,9 @@ def rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv,
     return reference.rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, perm)
 
 
+ATTN_DECODE_PART = 512  # context tokens per split-KV partition of attn_decode (csrc/kernels/attention.hip)
+
+
 def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters, scale):
     """Split-KV paged decode attention.  ``counters``: int32 [>= num_seqs * Hkv], zero-initialised once;
     the kernel re-arms it (graph-replay safe)."""

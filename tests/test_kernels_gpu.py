@@ -109,12 +109,12 @@ def _random_paged(gpu, ctx_lens, Hkv, BS, g, extra_blocks=3):
 @pytest.mark.parametrize("BS", [32, 64])
 def test_attn_decode(gpu, Hq, Hkv, BS):
     g = torch.Generator(device=gpu).manual_seed(3)
-    ctx_lens = [1, 17, 64, 255, 256, 257, 1000, 2049]
+    ctx_lens = [1, 17, 64, 255, 256, 257, 511, 512, 513, 1000, 2049, 4100]
     kc, vc, bt = _random_paged(gpu, ctx_lens, Hkv, BS, g)
     S = len(ctx_lens)
     q = torch.randn(S, Hq, 128, device=gpu, generator=g).bfloat16()
     ctx = torch.tensor(ctx_lens, device=gpu, dtype=torch.int32)
-    max_parts = (bt.shape[1] * BS + 255) // 256
+    max_parts = (bt.shape[1] * BS + ops.ATTN_DECODE_PART - 1) // ops.ATTN_DECODE_PART
     tmp_o = torch.empty(S, Hq, max_parts, 128, device=gpu)
     tmp_ml = torch.empty(S, Hq, max_parts, 2, device=gpu)
     out = torch.empty(S, Hq, 128, device=gpu, dtype=torch.bfloat16)
