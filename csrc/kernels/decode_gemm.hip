@@ -210,8 +210,13 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __rest
       const int ko = (b + u) * 64;
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
-        wa[u][rt][0].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko * wmul);
-        wa[u][rt][1].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko * wmul + wsec);
+        if (e.wnt) {
+          wa[u][rt][0].w = ld_nt16(wrow[rt] + ko * wmul);
+          wa[u][rt][1].w = ld_nt16(wrow[rt] + ko * wmul + wsec);
+        } else {
+          wa[u][rt][0].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko * wmul);
+          wa[u][rt][1].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko * wmul + wsec);
+        }
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
@@ -328,9 +333,12 @@ __global__ __launch_bounds__(256) void prep_kernel(LinOut delta, const int* __re
 //   6  4 waves, 2 row tiles
 //   7  4 waves, 4 row tiles (1 column tile only; else as 6)
 int g_variant = -1;
+int g_wnt = 0;
 
 template <int MT, int NW, int U, int RT, int EPI>
-void go(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, hipStream_t s) {
+void go(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e0, hipStream_t s) {
+  DecodeEpi e = e0;
+  e.wnt = g_wnt;
   decode_gemm_kernel<MT, NW, U, RT, EPI><<<N / (16 * RT), NW * 64, 0, s>>>(x, W, M, N, K, e);
 }
 
@@ -403,7 +411,11 @@ void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int
   }
 }
 
-void set_decode_gemm_variant(int v) { g_variant = v; }
+void set_decode_gemm_variant(int v) {
+  // v >= 100: variant v - 100 with non-temporal weight loads (A/B knob of bench_decode_gemm.py)
+  g_wnt = v >= 100;
+  g_variant = v >= 100 ? v - 100 : v;
+}
 
 void launch_embed_prep(const int* ids, const int* src, const int* prev, const bf16* table, float* resid, const bf16* w,
                        bf16* xw, float* ss, int T, int d, hipStream_t s) {

@@ -15,6 +15,7 @@ struct DecodeEpi {
   // 16-row x 32-k block is 1 KB contiguous in lane order, so one load instruction reads 1 KB and a
   // wave's k-slice of a row tile is one contiguous stream
   int wshuf = 0;
+  int wnt = 0;  // weight loads non-temporal (experiment knob, bench only)
   // prologue: RMSNorm row scale rsqrt(sum(ss_in[m][0..ss_tiles)) * inv_d + eps); ss_in == nullptr -> 1
   const float* ss_in = nullptr;
   int ss_tiles = 0;
