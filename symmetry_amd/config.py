@@ -38,6 +38,12 @@ REQUIRED_FIELDS = (
 
 DEFAULT_CONFIG_PATH = os.path.join(os.path.expanduser("~"), ".config", "symmetry", "provider.yaml")
 ENV_PREFIX = "SYMMETRY_"
+# optional fields (REF schema + native engine / provider options) an env override may name in any case
+OPTIONAL_FIELDS = ("apiKey", "dataCollectionEnabled", "maxConnections", "name", "weights", "tokenizer",
+                   "tensorParallelSize", "expertParallelSize", "maxBatchTokens", "maxModelLen", "kvCacheFraction",
+                   "blockSize", "maxTokens", "seed", "device", "useGraphs", "numKvBlocks", "maxBacklog",
+                   "decodeWeights", "prefillChunk", "strictServerAuth", "shareApiKey", "completionParser",
+                   "metricsInterval", "metricsFile", "bootstrap", "listenHost", "listenPort", "serveHttp")
 
 
 class ConfigError(Exception):
@@ -61,7 +67,7 @@ class ConfigManager:
             if not k.startswith(ENV_PREFIX):
                 continue
             field = k[len(ENV_PREFIX):]
-            for existing in list(self.config) + list(REQUIRED_FIELDS):
+            for existing in list(self.config) + list(REQUIRED_FIELDS) + list(OPTIONAL_FIELDS):
                 if existing.lower() == field.lower():
                     field = existing
                     break

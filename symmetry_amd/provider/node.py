@@ -124,6 +124,15 @@ class SymmetryProvider:
             logger.info(f"🔑 Server key: {cfg.get('serverKey')}")
             logger.info("🔗 Joining server, please wait.")
             await self.join_server()
+        self.http = None
+        if cfg.get("serveHttp") and getattr(self.backend, "name", "") == "native":
+            from ..serve.http import LocalAPIServer
+
+            self.http = LocalAPIServer(self.backend, str(cfg.get("modelName")), host=str(cfg.get("apiHostname")),
+                                       port=int(cfg.get("apiPort") or 0), path=str(cfg.get("apiPath")),
+                                       api_key=cfg.get("apiKey"), stats=self.stats)
+            port = await self.http.start()
+            logger.info(f"🌐 OpenAI-compatible API on http://{self.http.host}:{port}{self.http.path}")
         self.metrics_reporter = MetricsReporter(
             self.stats, interval_s=float(cfg.get("metricsInterval", 60) or 0),
             path=cfg.get("metricsFile"), log=lambda line: logger.info(f"📊 {line}"))
@@ -277,6 +286,8 @@ class SymmetryProvider:
     async def destroy(self) -> None:
         if getattr(self, "metrics_reporter", None) is not None:
             self.metrics_reporter.stop()
+        if getattr(self, "http", None) is not None:
+            await self.http.stop()
         for t in list(self._tasks):
             t.cancel()
         if self._provider_swarm is not None:
