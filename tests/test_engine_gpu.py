@@ -153,3 +153,27 @@ def test_top_k_one_in_graph_equals_greedy(gpu):
     b = eng.generate(prompt, SamplingParams(max_tokens=10, temperature=0.9, top_p=0.8, seed=3, ignore_eos=True))
     assert a == b
     assert any(k[2] for k in eng.runner.graphs)  # the filtered graph variant was captured and used
+
+
+def test_staggered_arrivals_mixed_steps_and_pipelining_match_oracle(gpu):
+    """GPU engine with graphs + pipelined decode: a long prompt arrives while others decode (mixed
+    prefill/decode steps), a short one arrives later; every sequence agrees with the fp32 oracle."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+
+    eng = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", max_num_seqs=6, max_model_len=1024,
+                                 num_kv_blocks=64, use_graphs=True, mixed_prefill_tokens=96))
+    prompts = {0: list(range(100, 140)), 1: list(range(500, 530)), 2: list(range(1000, 1300)), 3: [7, 8, 9]}
+    arrive = {0: 0, 1: 0, 2: 4, 3: 9}
+    seqs, step = {}, 0
+    while step < 500:
+        for i, t in arrive.items():
+            if t == step:
+                seqs[i] = eng.add_request(f"s{i}", prompts[i], SamplingParams(max_tokens=14, ignore_eos=True))
+        if len(seqs) == len(prompts) and not eng.has_unfinished():
+            break
+        eng.step()
+        step += 1
+    for i, s in seqs.items():
+        assert len(s.output_ids) == 14
+        _agree(eng.weights, prompts[i], s.output_ids, tol=0.08)
