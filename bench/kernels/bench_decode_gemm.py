@@ -24,6 +24,8 @@ SHAPES = {
     "down": ("resid", 4096, 14336), "lm_head": ("argmax", 128256, 4096),
     "qkv_tp8": ("qkv", 768, 4096), "o_tp8": ("f32", 4096, 512), "gate_up_tp8": ("swiglu", 3584, 4096),
     "down_tp8": ("f32", 4096, 1792), "lm_head_tp8": ("argmax", 16032, 4096),
+    # plain fp32-output twins: the difference to the fused shapes is the epilogue's cost
+    "qkv_f32": ("f32", 6144, 4096), "o_f32": ("f32", 4096, 4096), "gate_up_f32": ("f32", 28672, 4096),
 }
 
 
