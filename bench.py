@@ -47,6 +47,7 @@ def main() -> int:
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--persistent-mlp", action="store_true", help="O/gate_up/down as one persistent launch (A/B)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra decode steps after timing (for rocprof)")
     args = ap.parse_args()
 
@@ -75,7 +76,8 @@ def main() -> int:
     blocks = C * ((args.max_model_len + block - 1) // block) + 16
     cfg = EngineConfig(model=args.model, device="auto", seed=1234 + rank, max_num_seqs=C,
                        max_model_len=args.max_model_len, block_size=block, num_kv_blocks=blocks,
-                       use_graphs=not args.no_graphs, max_num_batched_tokens=max(8192, C * P))
+                       use_graphs=not args.no_graphs, max_num_batched_tokens=max(8192, C * P),
+                       persistent_mlp=args.persistent_mlp)
     t0 = time.perf_counter()
     eng = LLMEngine(cfg)
     t_load = time.perf_counter() - t0

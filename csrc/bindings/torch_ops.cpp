@@ -581,6 +581,50 @@ void sample_filtered(const Tensor& logits, const Tensor& temps, const Tensor& to
                          reinterpret_cast<const long long*>(step.data_ptr()), ptr<int>(out_ids), cur_stream(logits));
 }
 
+void decode_mlp(const Tensor& attn, const Tensor& Wo, const Tensor& Wgu, const Tensor& Wd, Tensor& resid,
+                const Tensor& ln2, const Tensor& w_next, Tensor& xw, Tensor& ss, Tensor& act, Tensor& ctl, double eps,
+                bool wshuf) {
+  for (const Tensor* t : {&attn, &Wo, &Wgu, &Wd, &ln2, &w_next, static_cast<const Tensor*>(&xw),
+                          static_cast<const Tensor*>(&act)}) {
+    check_gpu(*t, "decode_mlp tensor");
+    check_dtype(*t, at::kBFloat16, "decode_mlp tensor");
+  }
+  check_gpu(resid, "resid");
+  check_dtype(resid, at::kFloat, "resid");
+  check_gpu(ss, "ss");
+  check_dtype(ss, at::kFloat, "ss");
+  check_gpu(ctl, "ctl");
+  check_dtype(ctl, at::kInt, "ctl");
+  const int64_t M = attn.size(0), dq = attn.size(1), d = Wo.size(0), F = Wd.size(1);
+  TORCH_CHECK(M >= 1 && M <= 16, "decode_mlp: M must be in [1, 16]");
+  TORCH_CHECK(Wo.size(1) == dq && Wgu.size(0) == 2 * F && Wgu.size(1) == d && Wd.size(0) == d,
+              "decode_mlp: weight shapes");
+  TORCH_CHECK(dq % 512 == 0 && d % 512 == 0 && F % 512 == 0, "decode_mlp: every K must be a multiple of 512");
+  TORCH_CHECK(resid.numel() == M * d && xw.numel() == M * d && act.numel() == M * F, "decode_mlp: activations");
+  TORCH_CHECK(ss.dim() == 2 && ss.size(0) >= M && ss.size(1) == d / 16, "decode_mlp: ss [M, d/16]");
+  TORCH_CHECK(ln2.numel() == d && w_next.numel() == d && ctl.numel() >= DECODE_MLP_CTL_INTS, "decode_mlp: norms / ctl");
+  DecodeMlpArgs a;
+  a.attn = ptr<bf16>(attn);
+  a.Wo = ptr<bf16>(Wo);
+  a.Wgu = ptr<bf16>(Wgu);
+  a.Wd = ptr<bf16>(Wd);
+  a.resid = ptr<float>(resid);
+  a.ln2 = ptr<bf16>(ln2);
+  a.w_next = ptr<bf16>(w_next);
+  a.xw = ptr<bf16>(xw);
+  a.ss = ptr<float>(ss);
+  a.act = ptr<bf16>(act);
+  a.ctl = ptr<int>(ctl);
+  a.M = (int)M;
+  a.d = (int)d;
+  a.dq = (int)dq;
+  a.F = (int)F;
+  a.wshuf = wshuf ? 1 : 0;
+  a.eps = (float)eps;
+  const at::OptionalDeviceGuard g(attn.device());
+  launch_decode_mlp(a, cur_stream(attn));
+}
+
 void rownorm(const Tensor& xw, const Tensor& ss, double eps, Tensor& out) {
   check_gpu(xw, "xw");
   check_dtype(xw, at::kBFloat16, "xw");
@@ -641,6 +685,10 @@ TORCH_LIBRARY(symmetry_amd, m) {
         &embed_prep);
   m.def("add_prep(Tensor delta, Tensor(a!) resid, Tensor w, Tensor(b!) xw, Tensor(c!) ss) -> ()", &add_prep);
   m.def("rownorm(Tensor xw, Tensor ss, float eps, Tensor(a!) out) -> ()", &rownorm);
+  m.def(
+      "decode_mlp(Tensor attn, Tensor Wo, Tensor Wgu, Tensor Wd, Tensor(a!) resid, Tensor ln2, Tensor w_next, "
+      "Tensor(b!) xw, Tensor(c!) ss, Tensor(d!) act, Tensor(e!) ctl, float eps, bool wshuf=False) -> ()",
+      &decode_mlp);
   m.def(
       "sample_filtered(Tensor logits, Tensor temps, Tensor top_k, Tensor top_p, Tensor seeds, Tensor step, "
       "Tensor(a!) out_ids) -> ()",

@@ -54,6 +54,18 @@ SYM_DEV void store4bf(bf16* p, float a, float b, float c, float d) {
 
 // Epilogue of one finished 16x16 accumulator tile (rows n0.., columns = token rows 16*mt..).
 // Lane (r16, h) holds rows n0 + 4h .. n0 + 4h + 3 of token row m = 16 * mt + r16.
+// 4 bf16 as one 8-byte write-through (sc1) store: visible to a consumer on another XCD once the
+// storing wave's vmcnt has drained (MI355X_MICROARCH.md hand-off table)
+SYM_DEV void store4bf_sc1(bf16* p, float a, float b, float c, float d) {
+  Pack8 pk;
+  pk.h[0] = (bf16)a;
+  pk.h[1] = (bf16)b;
+  pk.h[2] = (bf16)c;
+  pk.h[3] = (bf16)d;
+  const unsigned long long v = ((unsigned long long)pk.u.y << 32) | pk.u.x;
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int EPI>
 SYM_DEV void epilogue(const DecodeEpi& e, f32x4 v, int tile, int m, bool mok, int h, int N) {
   const int n0 = tile * 16;
@@ -97,9 +109,16 @@ SYM_DEV void epilogue(const DecodeEpi& e, f32x4 v, int tile, int m, bool mok, in
     float sq = 0.f;
     if (mok) {
       float* rp = e.resid + (long long)m * N + n0 + 4 * h;
-      const float4 r = *reinterpret_cast<const float4*>(rp);
+      float4 r;
+      if (e.resid_sc1) {  // rewritten earlier in this launch (persistent MLP): bypass this CU's L1
+        r.x = __hip_atomic_load(rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r.y = __hip_atomic_load(rp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r.z = __hip_atomic_load(rp + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r.w = __hip_atomic_load(rp + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        r = *reinterpret_cast<const float4*>(rp);
+      }
       const float rr[4] = {r.x + v[0], r.y + v[1], r.z + v[2], r.w + v[3]};
-      *reinterpret_cast<float4*>(rp) = make_float4(rr[0], rr[1], rr[2], rr[3]);
       float wn[4];
       Pack8 wp;  // 4 bf16 of the next norm weight
       const uint2 raw = *reinterpret_cast<const uint2*>(e.w_next + n0 + 4 * h);
@@ -109,19 +128,36 @@ SYM_DEV void epilogue(const DecodeEpi& e, f32x4 v, int tile, int m, bool mok, in
         wn[i] = (float)wp.h[i];
         sq += rr[i] * rr[i];
       }
-      store4bf(e.xw_out + (long long)m * N + n0 + 4 * h, rr[0] * wn[0], rr[1] * wn[1], rr[2] * wn[2], rr[3] * wn[3]);
+      bf16* xo = e.xw_out + (long long)m * N + n0 + 4 * h;
+      if (e.sc1) {  // consumed inside the same persistent launch: write-through (sc1) stores
+#pragma unroll
+        for (int i = 0; i < 4; ++i) __hip_atomic_store(rp + i, rr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        store4bf_sc1(xo, rr[0] * wn[0], rr[1] * wn[1], rr[2] * wn[2], rr[3] * wn[3]);
+      } else {
+        *reinterpret_cast<float4*>(rp) = make_float4(rr[0], rr[1], rr[2], rr[3]);
+        store4bf(xo, rr[0] * wn[0], rr[1] * wn[1], rr[2] * wn[2], rr[3] * wn[3]);
+      }
     }
     sq += __shfl_xor(sq, 16, 64);
     sq += __shfl_xor(sq, 32, 64);
-    if (mok && h == 0) e.ss_out[(long long)m * (N / 16) + tile] = sq;
+    if (mok && h == 0) {
+      float* sp = e.ss_out + (long long)m * (N / 16) + tile;
+      if (e.sc1)
+        __hip_atomic_store(sp, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        *sp = sq;
+    }
   } else if constexpr (EPI == DECODE_EPI_SWIGLU) {
     float u[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) u[i] = __shfl_xor(v[i], 32, 64);
     if (mok && h < 2) {
       const int f = 8 * tile + 4 * h;
-      store4bf(e.act + (long long)m * (N / 2) + f, silu(v[0]) * u[0], silu(v[1]) * u[1], silu(v[2]) * u[2],
-               silu(v[3]) * u[3]);
+      bf16* ap = e.act + (long long)m * (N / 2) + f;
+      if (e.sc1)
+        store4bf_sc1(ap, silu(v[0]) * u[0], silu(v[1]) * u[1], silu(v[2]) * u[2], silu(v[3]) * u[3]);
+      else
+        store4bf(ap, silu(v[0]) * u[0], silu(v[1]) * u[1], silu(v[2]) * u[2], silu(v[3]) * u[3]);
     }
   } else {  // DECODE_EPI_ARGMAX
     const int mm = mok ? m : 0;
@@ -150,11 +186,18 @@ SYM_DEV void epilogue(const DecodeEpi& e, f32x4 v, int tile, int m, bool mok, in
   }
 }
 
-template <int MT, int NW, int U, int RT, int EPI>
-__global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __restrict__ x,
-                                                              const bf16* __restrict__ W, int M, int N, int K,
-                                                              DecodeEpi e) {
-  const int tile0 = blockIdx.x * RT;
+struct NoWait {
+  SYM_DEV void operator()() const {}
+};
+
+// One workgroup-tile of the decode GEMM (RT consecutive 16-row weight tiles starting at 16 * RT * blk).
+// `wait` runs after the first batch of weight loads has been issued and before any activation is read:
+// in the persistent MLP kernel it blocks until the producing phase has published the activations, so
+// the weight stream of this tile overlaps the dependency wait.
+template <int MT, int NW, int U, int RT, int EPI, typename WaitFn>
+SYM_DEV void gemm_tile(const bf16* __restrict__ x, const bf16* __restrict__ W, int M, int N, int K,
+                       const DecodeEpi& e, int blk, WaitFn wait) {
+  const int tile0 = blk * RT;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r16 = lane & 15, h = lane >> 4;
   const int wk = K / NW;
@@ -202,7 +245,7 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __rest
   };
 
   int b = 0;
-  bool rn_done = false;
+  bool rn_done = false, waited = false;
   for (; b + U <= nblk; b += U) {
     Pack8 wa[U][RT][2], xa[U][MT][2];
 #pragma unroll
@@ -218,6 +261,14 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __rest
           wa[u][rt][1].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko * wmul + wsec);
         }
       }
+    }
+    if (!waited) {
+      waited = true;
+      wait();
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ko = (b + u) * 64;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         xa[u][mt][0].u = ldx(mt, ko);
@@ -238,6 +289,7 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __rest
           acc[rt][mt] = mfma16(wa[u][rt][1].v, xa[u][mt][1].v, acc[rt][mt]);
         }
   }
+  if (!waited) wait();
   for (; b < nblk; ++b) {
     const int ko = b * 64;
     Pack8 w0[RT], w1[RT];
@@ -277,6 +329,13 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __rest
     for (int i = 0; i < 4; ++i) v[i] *= sc;
     epilogue<EPI>(e, v, tile0 + rt, m, mok, h, N);
   }
+}
+
+template <int MT, int NW, int U, int RT, int EPI>
+__global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __restrict__ x,
+                                                              const bf16* __restrict__ W, int M, int N, int K,
+                                                              DecodeEpi e) {
+  gemm_tile<MT, NW, U, RT, EPI>(x, W, M, N, K, e, blockIdx.x, NoWait{});
 }
 
 // ---- residual producers without a GEMM ----------------------------------------------------------
@@ -321,6 +380,107 @@ __global__ __launch_bounds__(256) void prep_kernel(LinOut delta, const int* __re
   }
   acc = block_sum<256>(acc, scratch);
   if (threadIdx.x == 0) ss[row] = acc;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Persistent decode MLP block: O-proj -> gate_up -> down of one layer in ONE launch (M <= 16 rows).
+//
+// Tiles of the three GEMMs are numbered in phase order (d/16 O tiles, 2F/16 gate_up tiles, d/16 down
+// tiles); resident workgroup b takes tiles b, b + grid, b + 2 grid, ...  A gate_up / down
+// tile first issues its weight loads, THEN waits for the previous phase's completion counter, then
+// reads the activations: the weight stream of the next phase overlaps the phase boundary that used
+// to be a kernel launch (launch gap + first-load latency + tail).  Deadlock-free by construction:
+// a workgroup runs its tiles in increasing order and the grid never exceeds the resident capacity, so
+// every awaited tile belongs to a running workgroup that reaches it before waiting on anything later.
+// Hand-off (MI355X_MICROARCH.md table): producers store resid / xw / ss / act write-through (sc1),
+// drain vmcnt, then bump an agent-scope counter; consumers first touch those lines after the counter
+// (caches were invalidated at kernel start, so plain loads see the written bytes).  Spins are bounded
+// (error flag instead of a hang); the last workgroup re-arms the control words for the next launch.
+// ---------------------------------------------------------------------------------------------------
+// Completion counters are spread over 64 cache lines per phase (tile i of a phase bumps line i % 64):
+// agent-scope atomics cross the XCDs to memory, so ~2k increments and ~1k pollers on ONE address
+// serialise; 64 lines cut the per-address traffic 64x, and a waiting wave polls all 64 with one load
+// per lane.  Layout (ints): [O lines | gate_up lines | done | err], 32-int (128 B) line stride.
+constexpr int MLP_LINES = 64, MLP_STRIDE = 32;
+constexpr int MLP_CNT_O = 0, MLP_CNT_GU = MLP_LINES * MLP_STRIDE, MLP_DONE = 2 * MLP_LINES * MLP_STRIDE,
+              MLP_ERR = MLP_DONE + MLP_STRIDE;
+static_assert(MLP_ERR + 1 <= DECODE_MLP_CTL_INTS, "ctl block too small");
+
+struct WaitFor {
+  const int* cnt;  // first line of the awaited phase
+  int n;           // tiles in that phase
+  int* err;
+  SYM_DEV void operator()() const {
+    if (threadIdx.x < 64) {
+      const int l = threadIdx.x;
+      const int target = n / MLP_LINES + (l < n % MLP_LINES ? 1 : 0);
+      const int* c = cnt + l * MLP_STRIDE;
+      int it = 0;
+      while (!__all(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target)) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++it > (1 << 22)) {  // ~0.2 s: never hang the GPU on a bug, flag it
+          if (l == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no activation load is hoisted above the wait
+  }
+};
+
+SYM_DEV void publish(int* cnt, int tile) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(cnt + (tile % MLP_LINES) * MLP_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NW, int U, int WPE>
+__global__ __launch_bounds__(NW * 64, WPE) void decode_mlp_kernel(DecodeMlpArgs a) {
+  const int nO = a.d / 16, nG = 2 * a.F / 16, nD = a.d / 16;
+  const int total = nO + nG + nD;
+  int* ctl = a.ctl;
+  DecodeEpi eo, eg, ed;
+  eo.wshuf = eg.wshuf = ed.wshuf = a.wshuf;
+  eo.resid = ed.resid = a.resid;
+  eo.w_next = a.ln2;
+  eo.xw_out = ed.xw_out = a.xw;
+  eo.ss_out = ed.ss_out = a.ss;
+  eo.sc1 = 1;
+  eg.ss_in = a.ss;
+  eg.ss_tiles = a.d / 16;
+  eg.inv_d = 1.f / (float)a.d;
+  eg.eps = a.eps;
+  eg.act = a.act;
+  eg.sc1 = 1;
+  ed.w_next = a.w_next;
+  ed.resid_sc1 = 1;
+  // static striding (no queue atomics on the critical path): round r of workgroup b is tile b + r * grid,
+  // so every O tile is in round 0 and phases are still dequeued in order
+  for (int t = blockIdx.x; t < total; t += gridDim.x) {
+    if (t < nO) {
+      gemm_tile<1, NW, U, 1, DECODE_EPI_RESID>(a.attn, a.Wo, a.M, a.d, a.dq, eo, t, NoWait{});
+      publish(ctl + MLP_CNT_O, t);
+    } else if (t < nO + nG) {
+      gemm_tile<1, NW, U, 1, DECODE_EPI_SWIGLU>(a.xw, a.Wgu, a.M, 2 * a.F, a.d, eg, t - nO,
+                                                WaitFor{ctl + MLP_CNT_O, nO, ctl + MLP_ERR});
+      publish(ctl + MLP_CNT_GU, t - nO);
+    } else {
+      gemm_tile<1, NW, U, 1, DECODE_EPI_RESID>(a.act, a.Wd, a.M, a.d, a.F, ed, t - nO - nG,
+                                               WaitFor{ctl + MLP_CNT_GU, nG, ctl + MLP_ERR});
+    }
+    __syncthreads();  // LDS reduction buffers are reused by the next tile
+  }
+  __shared__ int s_last;
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(ctl + MLP_DONE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (s_last) {  // last workgroup out (every other one is past its waits): re-arm for the next launch
+    for (int i = threadIdx.x; i < 2 * MLP_LINES; i += blockDim.x)
+      __hip_atomic_store(ctl + i * MLP_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(ctl + MLP_DONE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Decomposition variants (A/B: bench/kernels/bench_decode_gemm.py; chosen by decode_gemm_variant()):
@@ -411,7 +571,41 @@ void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int
   }
 }
 
+int g_mlp_cfg = -1;
+
+template <int NW, int U, int WPE>
+void go_mlp(const DecodeMlpArgs& a, hipStream_t s) {
+  static int resident = 0;
+  if (!resident) {  // one persistent workgroup per resident slot
+    int dev = 0, cus = 0, per_cu = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_mlp_kernel<NW, U, WPE>, NW * 64, 0);
+    resident = std::max(1, cus) * std::max(1, per_cu);
+  }
+  const int total = a.d / 16 + 2 * a.F / 16 + a.d / 16;
+  decode_mlp_kernel<NW, U, WPE><<<std::min(total, resident), NW * 64, 0, s>>>(a);
+}
+
+void launch_decode_mlp(const DecodeMlpArgs& a, hipStream_t s) {
+  // (waves per tile, k-blocks in flight per wave, waves per SIMD): A/B by bench/kernels/bench_decode_mlp.py
+  switch (g_mlp_cfg < 0 ? 0 : g_mlp_cfg) {
+    case 1: go_mlp<8, 4, 2>(a, s); break;   // 1 WG / CU, deeper
+    case 2: go_mlp<4, 2, 4>(a, s); break;   // 4 WGs / CU
+    case 3: go_mlp<4, 4, 3>(a, s); break;
+    case 4: go_mlp<16, 1, 4>(a, s); break;  // 1 WG / CU, 16 waves
+    case 5: go_mlp<8, 1, 4>(a, s); break;
+    case 6: go_mlp<4, 1, 6>(a, s); break;   // 6 WGs / CU
+    default: go_mlp<8, 2, 4>(a, s); break;  // 2 WGs / CU
+  }
+}
+
 void set_decode_gemm_variant(int v) {
+  // v >= 1000: persistent decode MLP configuration v - 1000 (launch_decode_mlp)
+  if (v >= 1000 || v == -1) {
+    g_mlp_cfg = v >= 1000 ? v - 1000 : -1;
+    if (v >= 1000) return;
+  }
   // v >= 100: variant v - 100 with non-temporal weight loads (A/B knob of bench_decode_gemm.py)
   g_wnt = v >= 100;
   g_variant = v >= 100 ? v - 100 : v;

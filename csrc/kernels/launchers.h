@@ -16,6 +16,8 @@ struct DecodeEpi {
   // wave's k-slice of a row tile is one contiguous stream
   int wshuf = 0;
   int wnt = 0;  // weight loads non-temporal (experiment knob, bench only)
+  int sc1 = 0;  // RESID / SWIGLU outputs as write-through stores (consumed within a persistent launch)
+  int resid_sc1 = 0;  // RESID reads the residual with L1-bypassing loads (written earlier in the launch)
   // prologue: RMSNorm row scale rsqrt(sum(ss_in[m][0..ss_tiles)) * inv_d + eps); ss_in == nullptr -> 1
   const float* ss_in = nullptr;
   int ss_tiles = 0;
@@ -43,6 +45,25 @@ struct DecodeEpi {
   unsigned long long* keys = nullptr;
   int n_offset = 0;
 };
+// Persistent decode MLP block (O-proj + residual + ln2 prep -> gate_up + SwiGLU -> down + residual + next
+// norm prep), M <= 16, every K % 512 == 0.  ctl: DECODE_MLP_CTL_INTS ints, zero-initialised once, re-armed by the kernel.
+constexpr int DECODE_MLP_CTL_INTS = 4224;
+struct DecodeMlpArgs {
+  const bf16* attn = nullptr;  // [M, dq] attention output
+  const bf16* Wo = nullptr;    // [d, dq]
+  const bf16* Wgu = nullptr;   // [2F, d] gate/up interleaved per 16 rows
+  const bf16* Wd = nullptr;    // [d, F]
+  float* resid = nullptr;      // [M, d] fp32 residual stream
+  const bf16* ln2 = nullptr;   // post-attention norm weight
+  const bf16* w_next = nullptr;  // next layer's input norm (or the final norm)
+  bf16* xw = nullptr;          // [M, d]
+  float* ss = nullptr;         // [M, d / 16]
+  bf16* act = nullptr;         // [M, F]
+  int* ctl = nullptr;
+  int M = 0, d = 0, dq = 0, F = 0, wshuf = 0;
+  float eps = 0.f;
+};
+void launch_decode_mlp(const DecodeMlpArgs& a, hipStream_t s);
 void set_decode_gemm_variant(int v);  // -1: default heuristic
 void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e,
                         hipStream_t s);

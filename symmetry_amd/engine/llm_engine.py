@@ -55,6 +55,7 @@ class EngineConfig:
     pipeline: bool = True                # enqueue decode step N+1 before step N's tokens reach the host
     mixed_prefill_tokens: int = 512      # prompt-chunk budget of steps that also carry decodes
     decode_weights: str = "auto"         # "preshuffled" | "shared" | "auto": extra MFMA-ordered decode copies
+    persistent_mlp: bool = False         # O -> gate_up -> down as one persistent launch (measured slower: profiles/)
     model_config: ModelConfig | None = None
 
     @classmethod
@@ -69,7 +70,8 @@ class EngineConfig:
              "maxTokens": "default_max_tokens", "tensorParallelSize": "tp_size", "expertParallelSize": "ep_size",
              "device": "device",
              "useGraphs": "use_graphs", "numKvBlocks": "num_kv_blocks", "decodeWeights": "decode_weights",
-             "prefillChunk": "mixed_prefill_tokens"}
+             "prefillChunk": "mixed_prefill_tokens",
+             "persistentMlp": "persistent_mlp"}
         for k, attr in m.items():
             if cfg.get(k) is not None:
                 setattr(ec, attr, type(getattr(ec, attr))(cfg[k]) if getattr(ec, attr) is not None else cfg[k])
@@ -118,7 +120,8 @@ class LLMEngine:
         self.weights: ModelWeights = weights
         self.load_time = time.perf_counter() - t0
         self.model = TransformerLM(weights, self.device, tp_comm=tp_comm, ep_comm=ep_comm,
-                                   max_decode_ctx=max_model_len, decode_weights=cfg.decode_weights)
+                                   max_decode_ctx=max_model_len, decode_weights=cfg.decode_weights,
+                                   persistent_mlp=cfg.persistent_mlp)
         self.tokenizer = load_tokenizer(mcfg, cfg.tokenizer or (cfg.weights if cfg.weights != "random" else None))
         nb = cfg.num_kv_blocks or self._auto_blocks(max_model_len)
         self.kv = KVCache(mcfg.num_layers, nb, mcfg.num_kv_heads // cfg.tp_size, mcfg.head_dim, cfg.block_size,

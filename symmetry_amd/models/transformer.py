@@ -119,7 +119,7 @@ class Workspace:
 
 class TransformerLM:
     def __init__(self, weights: ModelWeights, device, tp_comm=None, ep_comm=None, max_decode_ctx: int | None = None,
-                 decode_weights: str = "auto"):
+                 decode_weights: str = "auto", persistent_mlp: bool = False):
         self.cfg: ModelConfig = weights.cfg
         self.w = weights
         self.device = torch.device(device)
@@ -149,6 +149,7 @@ class TransformerLM:
         # so the host can enqueue step N+1 before it has seen step N's tokens (pipelined decode).
         self.last_ids = torch.zeros(MAX_STEP_SEQS, dtype=torch.int32, device=self.device)
         self.dgw = self._decode_copies(decode_weights)
+        self.persistent_mlp = persistent_mlp
 
     def _decode_copies(self, mode: str) -> dict:
         """MFMA-preshuffled copies of the decode-GEMM weights (1 KB contiguous per wave load:
@@ -170,6 +171,17 @@ class TransformerLM:
             for n in names:
                 out[(i, n)] = preshuffle(self.w.layer(i, n))
         return out
+
+    def _persistent_mlp_ok(self, T: int) -> bool:
+        """decode_mlp preconditions: single GPU dense model, <= 16 rows, K dims % 512, one weight layout."""
+        if not self.persistent_mlp or self.cfg.is_moe or self._tp_active() or T > 16:
+            return False
+        d, dq = self.cfg.hidden_size, self.hq * self.D
+        F = self.w.layer(0, "w_gu").shape[0] // 2
+        if d % 512 or dq % 512 or F % 512:
+            return False
+        shs = {self._dgw(0, n)[1] for n in ("wo", "w_gu", "w_down")}
+        return len(shs) == 1
 
     def _dgw(self, i: int, name: str):
         """(weight, wshuf) for decode GEMM `name` of layer i."""
@@ -250,14 +262,25 @@ class TransformerLM:
         attn = self._buf("attn", (T, self.hq, self.D), torch.bfloat16)
         ops.embed_prep(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), xw, ss_1, b.src, self.last_ids)
         ss = ss_1
+        persistent = self._persistent_mlp_ok(T)
+        ctl = self.ws.get("mlp_ctl", (ops.DECODE_MLP_CTL,), torch.int32, self.device, zeros=True) if persistent else None
         for i in range(cfg.num_layers):
             wq, shq = self._dgw(i, "wqkv")
             ops.dg_qkv(xw, wq, ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq,
                        self.hkv, wshuf=shq)
             self._attention(b, kv, i, q, attn)
-            ss = self._resid_proj("o", attn.view(T, self.hq * self.D), self._dgw(i, "wo"), resid, w.layer(i, "ln2"),
-                                  xw, ss_t, ss_1)
+            attn2d = attn.view(T, self.hq * self.D)
             nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
+            if persistent:
+                # O -> gate_up/SwiGLU -> down in one persistent launch: each phase's weight stream starts
+                # while the previous phase finishes (csrc/kernels/decode_gemm.hip, decode_mlp_kernel)
+                (wo, sh), (w_gu, _), (w_dn, _) = self._dgw(i, "wo"), self._dgw(i, "w_gu"), self._dgw(i, "w_down")
+                act = self._buf("act", (T, w_gu.shape[0] // 2), torch.bfloat16)
+                ops.decode_mlp(attn2d, wo, w_gu, w_dn, resid, w.layer(i, "ln2"), nxt, xw, ss_t, act, ctl, eps,
+                               wshuf=sh)
+                ss = ss_t
+                continue
+            ss = self._resid_proj("o", attn2d, self._dgw(i, "wo"), resid, w.layer(i, "ln2"), xw, ss_t, ss_1)
             if cfg.is_moe:
                 # router + experts are not decode GEMMs: materialise RMSNorm(resid) (one bf16 rounding)
                 xn = self._buf("x", (T, d), torch.bfloat16)

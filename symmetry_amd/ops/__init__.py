@@ -47,6 +47,7 @@ __all__ = [
     "add_prep",
     "rownorm",
     "sample_filtered",
+    "decode_mlp",
     "linear",
     "choose_splits",
 ]
@@ -196,6 +197,20 @@ def moe_combine(y, dst, ids, e_lo, e_hi, w, k, out, accumulate=False):
     if _gpu(out):
         return _native.ops().moe_combine(y, dst, ids, int(e_lo), int(e_hi), w, int(k), out, bool(accumulate))
     return reference.moe_combine(y, dst, ids, e_lo, e_hi, w, k, out, accumulate)
+
+
+DECODE_MLP_CTL = 4224  # csrc/kernels/launchers.h DECODE_MLP_CTL_INTS
+
+
+def decode_mlp(attn, Wo, Wgu, Wd, resid, ln2, w_next, xw, ss, act, ctl, eps, wshuf=False):
+    """Persistent O-proj -> gate_up/SwiGLU -> down block (one launch, M <= 16): the same result as
+    dg_resid(O) + dg_swiglu + dg_resid(down).  ``ctl``: int32[DECODE_MLP_CTL] zero-initialised once
+    (re-armed by the kernel; a non-zero word after a launch flags a dependency wait that gave up)."""
+    if _gpu(attn):
+        return _native.ops().decode_mlp(attn, Wo, Wgu, Wd, resid, ln2, w_next, xw, ss, act, ctl, float(eps),
+                                        bool(wshuf))
+    return reference.decode_mlp(attn, reference.unshuffled(Wo, wshuf), reference.unshuffled(Wgu, wshuf),
+                                reference.unshuffled(Wd, wshuf), resid, ln2, w_next, xw, ss, act, eps)
 
 
 def sample_filtered(logits, temps, top_k, top_p, seeds, step, out_ids):

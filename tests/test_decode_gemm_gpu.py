@@ -192,3 +192,61 @@ def test_preshuffled_weight_stream(gpu, M):
                 assert torch.equal(y0, y1), (v, N, K)
     finally:
         lib.decode_gemm_variant(-1)
+
+
+@pytest.mark.parametrize("M", [1, 4, 10, 16])
+@pytest.mark.parametrize("shuf", [False, True])
+def test_decode_mlp_persistent(gpu, M, shuf):
+    """Persistent O -> gate_up/SwiGLU -> down launch == the three separate fused GEMMs (and the fp32 ref);
+    the control block re-arms itself (ctl all zero after every launch, including graph replays)."""
+    from symmetry_amd.models.layout import preshuffle
+
+    d, dq, F = 4096, 4096, 14336
+    g = torch.Generator(device=gpu).manual_seed(21 + M)
+    attn = torch.randn(M, dq, device=gpu, generator=g).bfloat16()
+    Wo = (torch.randn(d, dq, device=gpu, generator=g) / dq ** 0.5).bfloat16()
+    Wgu = (torch.randn(2 * F, d, device=gpu, generator=g) / d ** 0.5).bfloat16()[gu_perm(F).to(gpu)].contiguous()
+    Wd = (torch.randn(d, F, device=gpu, generator=g) / F ** 0.5).bfloat16()
+    resid0 = torch.randn(M, d, device=gpu, generator=g)
+    ln2 = (torch.randn(d, device=gpu, generator=g) * 0.1 + 1).bfloat16()
+    wn = (torch.randn(d, device=gpu, generator=g) * 0.1 + 1).bfloat16()
+    W3 = [preshuffle(w) for w in (Wo, Wgu, Wd)] if shuf else [Wo, Wgu, Wd]
+
+    def buffers():
+        return (resid0.clone(), torch.empty(M, d, device=gpu, dtype=torch.bfloat16),
+                torch.empty(M, d // 16, device=gpu), torch.empty(M, F, device=gpu, dtype=torch.bfloat16))
+
+    # sequential fused path
+    r_s, xw_s, ss_s, act_s = buffers()
+    ops.dg_resid(attn, W3[0], r_s, ln2, xw_s, ss_s, wshuf=shuf)
+    ops.dg_swiglu(xw_s, W3[1], ss_s, 1e-5, act_s, wshuf=shuf)
+    ops.dg_resid(act_s, W3[2], r_s, wn, xw_s, ss_s, wshuf=shuf)
+    # persistent
+    ctl = torch.zeros(ops.DECODE_MLP_CTL, device=gpu, dtype=torch.int32)
+    r_p, xw_p, ss_p, act_p = buffers()
+    ops.decode_mlp(attn, *W3, r_p, ln2, wn, xw_p, ss_p, act_p, ctl, 1e-5, wshuf=shuf)
+    torch.cuda.synchronize()
+    assert not ctl.any(), ctl.tolist()
+    _close(act_p, act_s, atol=3e-2, rtol=2e-2)
+    _close(r_p, r_s, atol=3e-3, rtol=1e-3)
+    _close(xw_p, xw_s, atol=3e-2, rtol=2e-2)
+    _close(ss_p, ss_s, atol=1e-2, rtol=2e-3)
+    # fp32 reference
+    r_r, xw_r, ss_r = resid0.cpu().clone(), torch.empty(M, d, dtype=torch.bfloat16), torch.empty(M, d // 16)
+    act_r = torch.empty(M, F, dtype=torch.bfloat16)
+    ref.decode_mlp(attn.cpu(), Wo.cpu(), Wgu.cpu(), Wd.cpu(), r_r, ln2.cpu(), wn.cpu(), xw_r, ss_r, act_r, 1e-5)
+    _close(r_p, r_r, atol=5e-3, rtol=2e-3)
+    # graph replays: same inputs -> same outputs, counters re-armed each time
+    r_g, xw_g, ss_g, act_g = buffers()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            ops.decode_mlp(attn, *W3, r_g, ln2, wn, xw_g, ss_g, act_g, ctl, 1e-5, wshuf=shuf)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        r_g.copy_(resid0)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert not ctl.any(), ctl.tolist()
+        assert torch.equal(r_g, r_p) and torch.equal(act_g, act_p) and torch.equal(ss_g, ss_p)

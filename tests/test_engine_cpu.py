@@ -241,3 +241,19 @@ def test_decodes_keep_streaming_while_a_long_prompt_prefills():
         for j, t in enumerate(seq.output_ids):
             row = lg[len(prompt) - 1 + j]
             assert float(row.max() - row[t]) <= 0.05
+
+
+def test_persistent_mlp_path_matches_three_launch_path():
+    """persistentMlp: decode steps of a dense model run O -> gate_up -> down through ops.decode_mlp;
+    greedy outputs equal the default fused path (small-llama: every K % 512 == 0)."""
+    prompts = _prompts(3, seed=5, lo=4, hi=20)
+    outs = []
+    for persistent in (False, True):
+        eng = _engine("small-llama", max_num_seqs=4, use_graphs=False, persistent_mlp=persistent)
+        assert eng.runner.model._persistent_mlp_ok(3) == persistent
+        seqs = [eng.add_request(f"r{i}", p, SamplingParams(max_tokens=6, ignore_eos=True))
+                for i, p in enumerate(prompts)]
+        while eng.has_unfinished():
+            eng.step()
+        outs.append([s.output_ids for s in seqs])
+    assert outs[0] == outs[1]
