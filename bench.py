@@ -48,6 +48,8 @@ def main() -> int:
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--persistent-mlp", action="store_true", help="O/gate_up/down as one persistent launch (A/B)")
+    ap.add_argument("--attn-block", type=int, default=None, help="A/B: QKV -> attention -> O as one launch (0/1)")
+    ap.add_argument("--nt-weights", type=int, default=None, help="A/B: non-temporal decode weight loads (0/1)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra decode steps after timing (for rocprof)")
     args = ap.parse_args()
 
@@ -71,6 +73,10 @@ def main() -> int:
     if torch.cuda.is_available() and not ops.native_available():
         raise SystemExit("native kernels missing: run `python -m symmetry_amd._build` first")
 
+    if args.nt_weights is not None and ops.native_available():
+        from symmetry_amd.ops import _native
+        _native.ops().decode_gemm_nt(int(args.nt_weights))
+
     C, P, W, K = args.clients, args.prompt_len, args.warmup, args.steps
     block = 64
     blocks = C * ((args.max_model_len + block - 1) // block) + 16
@@ -78,6 +84,8 @@ def main() -> int:
                        max_model_len=args.max_model_len, block_size=block, num_kv_blocks=blocks,
                        use_graphs=not args.no_graphs, max_num_batched_tokens=max(8192, C * P),
                        persistent_mlp=args.persistent_mlp)
+    if args.attn_block is not None:
+        cfg.fused_attn_block = bool(args.attn_block)
     t0 = time.perf_counter()
     eng = LLMEngine(cfg)
     t_load = time.perf_counter() - t0

@@ -625,6 +625,98 @@ void decode_mlp(const Tensor& attn, const Tensor& Wo, const Tensor& Wgu, const T
   launch_decode_mlp(a, cur_stream(attn));
 }
 
+void decode_block(const Tensor& xw, const Tensor& Wqkv, const c10::optional<Tensor>& ss_in, double eps,
+                  const Tensor& positions, const Tensor& slots, const Tensor& cos_sin, Tensor& q, Tensor& k_cache,
+                  Tensor& v_cache, const Tensor& block_tables, const Tensor& ctx_lens, Tensor& attn, Tensor& tmp_o,
+                  Tensor& tmp_ml, Tensor& counters, double scale, const Tensor& Wo, Tensor& resid, const Tensor& ln2,
+                  Tensor& xw_out, Tensor& ss_out, Tensor& ctl, bool wshuf, const c10::optional<Tensor>& stamps, int64_t cfg) {
+  auto sh = dg_check(xw, Wqkv);
+  const int64_t M = sh.M, d = sh.K, Hkv = k_cache.size(1), Hq = sh.N / 128 - 2 * Hkv;
+  TORCH_CHECK(M <= 16, "decode_block: M must be in [1, 16]");
+  TORCH_CHECK(sh.N % 128 == 0 && Hq > 0 && Hq % Hkv == 0 && Hq / Hkv <= 8, "decode_block: heads (G <= 8)");
+  TORCH_CHECK(d % 512 == 0 && (Hq * 128) % 512 == 0, "decode_block: d and Hq * 128 must be multiples of 512");
+  for (auto* t : {&positions, &slots, &block_tables, &ctx_lens}) {
+    check_gpu(*t, "index tensor");
+    check_dtype(*t, at::kInt, "index tensor");
+  }
+  check_gpu(cos_sin, "cos_sin");
+  check_dtype(cos_sin, at::kFloat, "cos_sin");
+  check_cache(k_cache, v_cache);
+  for (const Tensor* t : {static_cast<const Tensor*>(&q), static_cast<const Tensor*>(&attn), &Wo, &ln2,
+                          static_cast<const Tensor*>(&xw_out)}) {
+    check_gpu(*t, "decode_block tensor");
+    check_dtype(*t, at::kBFloat16, "decode_block tensor");
+  }
+  for (const Tensor* t : {static_cast<const Tensor*>(&resid), static_cast<const Tensor*>(&ss_out),
+                          static_cast<const Tensor*>(&tmp_o), static_cast<const Tensor*>(&tmp_ml)}) {
+    check_gpu(*t, "decode_block tensor");
+    check_dtype(*t, at::kFloat, "decode_block tensor");
+  }
+  check_gpu(counters, "counters");
+  check_dtype(counters, at::kInt, "counters");
+  check_gpu(ctl, "ctl");
+  check_dtype(ctl, at::kInt, "ctl");
+  TORCH_CHECK(positions.numel() >= M && slots.numel() >= M && ctx_lens.numel() >= M, "decode_block: index tensors");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == 128, "decode_block: cos_sin [max_pos, 128]");
+  TORCH_CHECK(q.numel() >= M * Hq * 128 && attn.numel() == M * Hq * 128, "decode_block: q / attn");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= M, "decode_block: block_tables [>=M, max_blocks]");
+  const int64_t BS = k_cache.size(2), max_blocks = block_tables.size(1);
+  TORCH_CHECK(tmp_o.dim() == 4 && tmp_o.size(0) >= M && tmp_o.size(1) == Hq && tmp_o.size(3) == 128,
+              "decode_block: tmp_o [>=M, Hq, max_parts, 128]");
+  const int64_t max_parts = tmp_o.size(2);
+  TORCH_CHECK(max_parts * 256 >= max_blocks * BS, "decode_block: tmp_o has too few 256-token partitions");
+  TORCH_CHECK(tmp_ml.numel() >= M * Hq * max_parts * 2 && counters.numel() >= M * Hkv, "decode_block: tmp_ml / counters");
+  TORCH_CHECK(Wo.dim() == 2 && Wo.size(0) == d && Wo.size(1) == Hq * 128, "decode_block: Wo [d, Hq * 128]");
+  TORCH_CHECK(resid.numel() == M * d && xw_out.numel() == M * d && ln2.numel() == d, "decode_block: residual");
+  TORCH_CHECK(ss_out.dim() == 2 && ss_out.size(0) >= M && ss_out.size(1) == d / 16, "decode_block: ss_out [M, d/16]");
+  TORCH_CHECK(ctl.numel() >= DECODE_BLOCK_CTL_INTS && (Hkv + 10) * 32 <= DECODE_BLOCK_CTL_INTS, "decode_block: ctl");
+  DecodeBlockArgs a;
+  DecodeEpi e;
+  dg_norm_in(e, ss_in, M, d, eps);
+  a.xw = ptr<bf16>(xw);
+  a.Wqkv = ptr<bf16>(Wqkv);
+  a.ss_in = e.ss_in;
+  a.ss_tiles = e.ss_tiles;
+  a.inv_d = e.inv_d;
+  a.eps = e.eps;
+  a.positions = ptr<int>(positions);
+  a.slots = ptr<int>(slots);
+  a.cos_sin = ptr<float>(cos_sin);
+  a.q = ptr<bf16>(q);
+  a.k_cache = ptr<bf16>(k_cache);
+  a.v_cache = ptr<bf16>(v_cache);
+  a.block_tables = ptr<int>(block_tables);
+  a.ctx_lens = ptr<int>(ctx_lens);
+  a.attn = ptr<bf16>(attn);
+  a.tmp_o = ptr<float>(tmp_o);
+  a.tmp_ml = ptr<float>(tmp_ml);
+  a.part_counters = ptr<int>(counters);
+  a.max_blocks = (int)max_blocks;
+  a.max_parts = (int)max_parts;
+  a.scale_log2 = (float)scale * 1.4426950408889634f;
+  a.Wo = ptr<bf16>(Wo);
+  a.resid = ptr<float>(resid);
+  a.ln2 = ptr<bf16>(ln2);
+  a.xw_out = ptr<bf16>(xw_out);
+  a.ss_out = ptr<float>(ss_out);
+  a.ctl = ptr<int>(ctl);
+  a.M = (int)M;
+  a.d = (int)d;
+  a.Hq = (int)Hq;
+  a.Hkv = (int)Hkv;
+  a.BS = (int)BS;
+  a.wshuf = wshuf ? 1 : 0;
+  a.cfg = (int)cfg;
+  if (stamps.has_value()) {
+    check_gpu(*stamps, "stamps");
+    TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->numel() >= 4 * ((Hq + 2 * Hkv) * 8 + M * Hkv * max_parts + d / 16),
+                "decode_block: stamps int64 [grid, 4]");
+    a.stamps = reinterpret_cast<long long*>(stamps->data_ptr<int64_t>());
+  }
+  const at::OptionalDeviceGuard g(xw.device());
+  launch_decode_block(a, cur_stream(xw));
+}
+
 void rownorm(const Tensor& xw, const Tensor& ss, double eps, Tensor& out) {
   check_gpu(xw, "xw");
   check_dtype(xw, at::kBFloat16, "xw");
@@ -693,7 +785,14 @@ TORCH_LIBRARY(symmetry_amd, m) {
       "sample_filtered(Tensor logits, Tensor temps, Tensor top_k, Tensor top_p, Tensor seeds, Tensor step, "
       "Tensor(a!) out_ids) -> ()",
       &sample_filtered);
+  m.def(
+      "decode_block(Tensor xw, Tensor Wqkv, Tensor? ss_in, float eps, Tensor positions, Tensor slots, Tensor cos_sin, "
+      "Tensor(a!) q, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor ctx_lens, Tensor(d!) attn, "
+      "Tensor(e!) tmp_o, Tensor(f!) tmp_ml, Tensor(g!) counters, float scale, Tensor Wo, Tensor(h!) resid, Tensor ln2, "
+      "Tensor(i!) xw_out, Tensor(j!) ss_out, Tensor(k!) ctl, bool wshuf=False, Tensor(l!)? stamps=None, int cfg=0) -> ()",
+      &decode_block);
   m.def("decode_gemm_variant(int v) -> ()", [](int64_t v) { set_decode_gemm_variant((int)v); });
+  m.def("decode_gemm_nt(int on) -> ()", [](int64_t on) { set_decode_gemm_nt((int)on); });
   m.def("grouped_skinny(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y) -> ()", &grouped_skinny);
   m.def(
       "moe_combine(Tensor y, Tensor dst, Tensor ids, int e_lo, int e_hi, Tensor w, int k, Tensor(a!) out, "

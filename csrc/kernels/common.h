@@ -21,6 +21,11 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWave = 64;
 
+// v_mfma_f32_16x16x32_bf16: C[16x16] += A[16x32] . B[32x16] (fragment layout: cdna_hip_programming.md §3)
+SYM_DEV f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
 SYM_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -25,14 +25,12 @@
 // workgroups, so every epilogue sees final values), U 64-deep k blocks in flight per wave, partial
 // accumulators summed through LDS.  MFMA v_mfma_f32_16x16x32_bf16, natural k order (each load
 // instruction reads 16 rows x 64 contiguous bytes).
+#include "attn_decode.h"
 #include "common.h"
 #include "launchers.h"
 
 namespace {
 
-SYM_DEV f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
 
 SYM_DEV uint32_t ordered_bits(float f) {
   const uint32_t u = __float_as_uint(f);
@@ -91,11 +89,18 @@ SYM_DEV void epilogue(const DecodeEpi& e, f32x4 v, int tile, int m, bool mok, in
         o[i] = lo ? (v[i] * c - p[i] * s) : (v[i] * c + p[i] * s);
       }
       const int d = (lo ? 0 : 64) + dh;
+      bf16* dst = nullptr;
       if (head < e.Hq) {
-        store4bf(e.q_out + ((long long)m * e.Hq + head) * D + d, o[0], o[1], o[2], o[3]);
+        dst = e.q_out + ((long long)m * e.Hq + head) * D + d;
       } else if (slot >= 0) {
         const long long blk = slot / e.BS, off = slot % e.BS;
-        store4bf(e.k_cache + ((blk * e.Hkv + (head - e.Hq)) * e.BS + off) * D + d, o[0], o[1], o[2], o[3]);
+        dst = e.k_cache + ((blk * e.Hkv + (head - e.Hq)) * e.BS + off) * D + d;
+      }
+      if (dst) {
+        if (e.sc1)  // read by the attention role of the same (fused) launch
+          store4bf_sc1(dst, o[0], o[1], o[2], o[3]);
+        else
+          store4bf(dst, o[0], o[1], o[2], o[3]);
       }
     } else if (slot >= 0) {
       const int vh = head - e.Hq - e.Hkv;
@@ -103,7 +108,15 @@ SYM_DEV void epilogue(const DecodeEpi& e, f32x4 v, int tile, int m, bool mok, in
       const long long blk = slot / e.BS, off = slot % e.BS;
       bf16* vp = e.v_cache + ((blk * e.Hkv + vh) * D + d) * e.BS + off;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) vp[(long long)i * e.BS] = (bf16)v[i];
+      for (int i = 0; i < 4; ++i) {
+        if (e.sc1) {
+          const bf16 bv = (bf16)v[i];
+          __hip_atomic_store(reinterpret_cast<unsigned short*>(vp + (long long)i * e.BS),
+                             __builtin_bit_cast(unsigned short, bv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          vp[(long long)i * e.BS] = (bf16)v[i];
+        }
+      }
     }
   } else if constexpr (EPI == DECODE_EPI_RESID) {
     float sq = 0.f;
@@ -483,6 +496,219 @@ __global__ __launch_bounds__(NW * 64, WPE) void decode_mlp_kernel(DecodeMlpArgs 
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Fused decode attention block: QKV projection (+ RoPE, paged K/V write) -> split-KV attention ->
+// O-projection (+ residual, ln2 prep) of one layer in ONE launch (M <= 16 rows, TP = 1).
+//
+// Grid = [QKV tiles | attention units (seq, kv head, partition) | O tiles], 512 threads each.
+//   * QKV tile: the decode GEMM tile of the 5-launch path with write-through (sc1) q / K / V stores,
+//     then one add to its kv group's counter (8 (G + 2) tiles per group).
+//   * attention unit: loads its context length and block-table entries, polls its group's counter,
+//     acquires, then runs the standalone kernel's arithmetic (attn_decode.h) and stores its output rows
+//     write-through; the workgroup that produced final rows adds to a done line.
+//   * O tile: issues its whole weight slice (8 k-blocks per wave) FIRST, then polls the done lines,
+//     acquires and reads the attention output: the O weight stream overlaps the attention phase,
+//     which moves few bytes, and the two launch boundaries of the 5-launch path disappear.
+// Hand-offs follow MI355X_MICROARCH.md's valid forms: sc1 payload stores, every storing wave drains
+// vmcnt, a barrier, ONE lane adds to the counter; the consumer polls relaxed, ONE agent acquire, vmcnt,
+// barrier, then plain loads.  Deadlock freedom: consumers sit after every producer in the grid, and
+// workgroups are dispatched in grid order, so a waiting workgroup only waits for workgroups that are
+// already running; every spin is bounded (error word instead of a hang).  The last workgroup out
+// re-arms the control words for the next launch (graph-replay safe, no memset node).
+// Results are bitwise equal to dg_qkv + attn_decode + dg_resid with decode_gemm variant 0.
+// ---------------------------------------------------------------------------------------------------
+constexpr int DB_STRIDE = 32, DB_DONE_LINES = 8;
+
+SYM_DEV void db_publish(int* word) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores have landed
+  __syncthreads();                                   // ... and every other wave's
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave 0 polls `nlines` counter lines (line l must reach base + (l < rem)), then acquires for the CU.
+struct BlockWait {
+  const int* cnt;
+  int nlines, base, rem;
+  int* err;
+  long long* stamp;  // diagnostics: s_memrealtime when the wait completed (nullptr: off)
+  int no_acquire;    // A/B timing knob only
+  SYM_DEV void operator()() const {
+    if (threadIdx.x < 64) {
+      const int l = threadIdx.x;
+      const bool mine = l < nlines;
+      const int target = base + (l < rem ? 1 : 0);
+      const int* c = cnt + (mine ? l : 0) * DB_STRIDE;
+      int it = 0;
+      while (!__all(!mine || __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target)) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++it > (1 << 22)) {  // ~0.2 s: never hang the GPU on a bug, flag it
+          if (l == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      if (!no_acquire) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // drop this CU's stale L1 lines
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (stamp && threadIdx.x == 0) *stamp = (long long)__builtin_amdgcn_s_memrealtime();
+  }
+};
+
+// O-projection tile of the fused block (16 output columns n0.., M <= 16 rows, 8 waves splitting K = Hq * 128).
+// Before `wait` (the poll for the attention output): the first OPF k-blocks of every wave's weight slice
+// (all of them at Llama-3-8B sizes), and, on the epilogue wave, the residual and next-norm weight it will
+// read; after it: the attention rows (x) four k-blocks at a time, the LDS reduction and the residual
+// epilogue.  Same arithmetic as gemm_tile<1, 8, *, 1, RESID>.
+template <int OPF, typename WaitFn>
+SYM_DEV void o_tile_fused(const DecodeBlockArgs& a, int tile, WaitFn wait) {
+  const int K = a.Hq * 128, M = a.M, N = a.d;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, h = lane >> 4;
+  const int wk = K / 8, kbeg = wid * wk, nblk = wk / 64;
+  const int wmul = a.wshuf ? 16 : 1, wsec = a.wshuf ? 512 : 32;
+  const bf16* wrow = a.wshuf ? a.Wo + ((long long)tile * (K / 32) + kbeg / 32) * 512 + lane * 8
+                             : a.Wo + (long long)(16 * tile + r16) * K + kbeg + 8 * h;
+  const bool xok = r16 < M;
+  const bf16* xrow = a.attn + (long long)min(r16, M - 1) * K + kbeg + 8 * h;
+  Pack8 w[OPF][2];
+#pragma unroll
+  for (int u = 0; u < OPF; ++u) {
+    if (u < nblk) {
+      w[u][0].u = *reinterpret_cast<const uint4*>(wrow + u * 64 * wmul);
+      w[u][1].u = *reinterpret_cast<const uint4*>(wrow + u * 64 * wmul + wsec);
+    }
+  }
+  const int n0 = tile * 16;
+  const int m = r16;
+  float4 rpre = make_float4(0.f, 0.f, 0.f, 0.f);
+  uint2 wnpre = make_uint2(0, 0);
+  if (wid == 0 && xok) {  // bytes nobody writes in this launch: safe to read before the hand-off
+    rpre = *reinterpret_cast<const float4*>(a.resid + (long long)m * N + n0 + 4 * h);
+    wnpre = *reinterpret_cast<const uint2*>(a.ln2 + n0 + 4 * h);
+  }
+  wait();
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  auto ldx = [&](int ko) -> uint4 {
+    return xok ? *reinterpret_cast<const uint4*>(xrow + ko) : make_uint4(0, 0, 0, 0);
+  };
+#pragma unroll
+  for (int u = 0; u < OPF; u += 4) {  // x of 4 k-blocks per round trip (32 VGPRs next to the 64 of W)
+    Pack8 xa[4][2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (u + j < nblk) {
+        xa[j][0].u = ldx((u + j) * 64);
+        xa[j][1].u = ldx((u + j) * 64 + 32);
+      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (u + j < nblk) {
+        acc = mfma16(w[u + j][0].v, xa[j][0].v, acc);
+        acc = mfma16(w[u + j][1].v, xa[j][1].v, acc);
+      }
+  }
+  for (int b = OPF; b < nblk; ++b) {  // K > 8 * 64 * OPF (e.g. 70B at TP = 1): streamed after the wait
+    Pack8 w0, w1, x0, x1;
+    w0.u = *reinterpret_cast<const uint4*>(wrow + b * 64 * wmul);
+    w1.u = *reinterpret_cast<const uint4*>(wrow + b * 64 * wmul + wsec);
+    x0.u = ldx(b * 64);
+    x1.u = ldx(b * 64 + 32);
+    acc = mfma16(w0.v, x0.v, acc);
+    acc = mfma16(w1.v, x1.v, acc);
+  }
+  __shared__ f32x4 ored[8][64];
+  ored[wid][lane] = acc;
+  __syncthreads();
+  if (wid != 0) return;
+  f32x4 v = ored[0][lane];
+#pragma unroll
+  for (int ww = 1; ww < 8; ++ww) v += ored[ww][lane];
+  // residual epilogue (epilogue<DECODE_EPI_RESID> with the operands loaded before the wait)
+  float sq = 0.f;
+  if (xok) {
+    const float rr[4] = {rpre.x + v[0], rpre.y + v[1], rpre.z + v[2], rpre.w + v[3]};
+    Pack8 wp;
+    wp.u = make_uint4(wnpre.x, wnpre.y, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sq += rr[i] * rr[i];
+    *reinterpret_cast<float4*>(a.resid + (long long)m * N + n0 + 4 * h) = make_float4(rr[0], rr[1], rr[2], rr[3]);
+    store4bf(a.xw_out + (long long)m * N + n0 + 4 * h, rr[0] * (float)wp.h[0], rr[1] * (float)wp.h[1],
+             rr[2] * (float)wp.h[2], rr[3] * (float)wp.h[3]);
+  }
+  sq += __shfl_xor(sq, 16, 64);
+  sq += __shfl_xor(sq, 32, 64);
+  if (xok && h == 0) a.ss_out[(long long)m * (N / 16) + tile] = sq;
+}
+
+__global__ __launch_bounds__(512, 4) void decode_block_kernel(DecodeBlockArgs a) {
+  const int Hq = a.Hq, Hkv = a.Hkv, G = Hq / Hkv;
+  const int nQ = (Hq + 2 * Hkv) * 8, nA = a.M * Hkv * a.max_parts, nO = a.d / 16;
+  int* ctl = a.ctl;
+  int* done = ctl + Hkv * DB_STRIDE;
+  int* exit_word = done + DB_DONE_LINES * DB_STRIDE;
+  int* err = exit_word + DB_STRIDE;
+  const int b = blockIdx.x;
+  long long* st = a.stamps ? a.stamps + 4 * b : nullptr;
+  if (st && threadIdx.x == 0) {
+    st[0] = (long long)__builtin_amdgcn_s_memrealtime();
+    st[3] = b < nQ ? 0 : (b < nQ + nA ? 1 : 2);
+  }
+  if (b < nQ) {
+    DecodeEpi e;
+    e.wshuf = a.wshuf;
+    e.sc1 = 1;
+    e.ss_in = a.ss_in;
+    e.ss_tiles = a.ss_tiles;
+    e.inv_d = a.inv_d;
+    e.eps = a.eps;
+    e.positions = a.positions;
+    e.slots = a.slots;
+    e.cos_sin = a.cos_sin;
+    e.q_out = a.q;
+    e.k_cache = a.k_cache;
+    e.v_cache = a.v_cache;
+    e.Hq = Hq;
+    e.Hkv = Hkv;
+    e.BS = a.BS;
+    gemm_tile<1, 8, 4, 1, DECODE_EPI_QKV>(a.xw, a.Wqkv, a.M, nQ * 16, a.d, e, b, NoWait{});
+    const int head = b / 8;
+    const int grp = head < Hq ? head / G : (head < Hq + Hkv ? head - Hq : head - Hq - Hkv);
+    db_publish(ctl + grp * DB_STRIDE);
+  } else if (b < nQ + nA) {
+    const int u = b - nQ, per_part = a.M * Hkv;
+    const int part = u / per_part, seq = (u % per_part) / Hkv, kvh = u % Hkv;
+    const bool fin = attn_fused_unit<8>(a.q, a.k_cache, a.v_cache, a.block_tables, a.ctx_lens, a.attn, a.tmp_o,
+                                        a.tmp_ml, a.part_counters, Hq, Hkv, a.BS, a.max_blocks, a.max_parts,
+                                        a.scale_log2, seq, kvh, part,
+                                        BlockWait{ctl + kvh * DB_STRIDE, 1, 8 * (G + 2), 0, err,
+                                                  st ? st + 1 : nullptr, a.cfg & 2});
+    if (fin) db_publish(done + ((seq * Hkv + kvh) % DB_DONE_LINES) * DB_STRIDE);
+  } else {
+    const int units = a.M * Hkv;
+    o_tile_fused<8>(a, b - nQ - nA,
+                 BlockWait{done, DB_DONE_LINES, units / DB_DONE_LINES, units % DB_DONE_LINES, err,
+                           st ? st + 1 : nullptr, a.cfg & 2});
+  }
+  if (st && threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st[2] = (long long)__builtin_amdgcn_s_memrealtime();
+  }
+  // last workgroup out (every other one is past its waits): re-arm the counters for the next launch
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(exit_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (s_last) {
+    for (int i = threadIdx.x; i < Hkv + DB_DONE_LINES; i += blockDim.x)
+      __hip_atomic_store(ctl + i * DB_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(exit_word, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Decomposition variants (A/B: bench/kernels/bench_decode_gemm.py; chosen by decode_gemm_variant()):
 //   0  8 waves split K, 1 row tile, U = 4 / 2 / 1 k-blocks in flight for 1 / 2 / 3-4 column tiles
 //   1  8 waves, 1 row tile, deeper: U = 8 / 4 / 2
@@ -611,6 +837,8 @@ void set_decode_gemm_variant(int v) {
   g_variant = v >= 100 ? v - 100 : v;
 }
 
+void set_decode_gemm_nt(int on) { g_wnt = on ? 1 : 0; }
+
 void launch_embed_prep(const int* ids, const int* src, const int* prev, const bf16* table, float* resid, const bf16* w,
                        bf16* xw, float* ss, int T, int d, hipStream_t s) {
   if (T == 0) return;
@@ -621,4 +849,10 @@ void launch_embed_prep(const int* ids, const int* src, const int* prev, const bf
 void launch_add_prep(LinOut delta, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d, hipStream_t s) {
   if (T == 0) return;
   prep_kernel<1><<<T, 256, 0, s>>>(delta, nullptr, nullptr, nullptr, nullptr, resid, w, xw, ss, d);
+}
+
+void launch_decode_block(const DecodeBlockArgs& a, hipStream_t s) {
+  if (a.M == 0) return;
+  const int grid = (a.Hq + 2 * a.Hkv) * 8 + a.M * a.Hkv * a.max_parts + a.d / 16;  // max_parts: 256-token
+  decode_block_kernel<<<grid, 512, 0, s>>>(a);
 }

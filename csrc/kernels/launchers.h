@@ -64,7 +64,47 @@ struct DecodeMlpArgs {
   float eps = 0.f;
 };
 void launch_decode_mlp(const DecodeMlpArgs& a, hipStream_t s);
+// Fused decode attention block (QKV + RoPE + K/V write -> split-KV attention -> O + residual + ln2 prep),
+// M <= 16, D = 128, G = Hq / Hkv <= 8, d % 512 == 0.  ctl: DECODE_BLOCK_CTL_INTS ints, zero-initialised
+// once, re-armed by the kernel (word ctl[(Hkv + 9) * 32] != 0 after a launch: a dependency wait gave up).
+constexpr int DECODE_BLOCK_CTL_INTS = 1024;
+struct DecodeBlockArgs {
+  // QKV
+  const bf16* xw = nullptr;      // [M, d] normalised-input prep (deferred RMSNorm)
+  const bf16* Wqkv = nullptr;    // [(Hq + 2 Hkv) * 128, d]
+  const float* ss_in = nullptr;  // row sum-of-squares partials [M, ss_tiles]
+  int ss_tiles = 0;
+  float inv_d = 0.f, eps = 0.f;
+  const int* positions = nullptr;
+  const int* slots = nullptr;
+  const float* cos_sin = nullptr;
+  bf16* q = nullptr;             // [M, Hq, 128]
+  bf16* k_cache = nullptr;
+  bf16* v_cache = nullptr;
+  // attention
+  const int* block_tables = nullptr;
+  const int* ctx_lens = nullptr;
+  bf16* attn = nullptr;          // [M, Hq * 128]
+  float* tmp_o = nullptr;
+  float* tmp_ml = nullptr;
+  int* part_counters = nullptr;  // split-KV arrival counters [M * Hkv], self re-arming
+  int max_blocks = 0, max_parts = 0;
+  float scale_log2 = 0.f;
+  // O projection + residual
+  const bf16* Wo = nullptr;      // [d, Hq * 128]
+  float* resid = nullptr;
+  const bf16* ln2 = nullptr;
+  bf16* xw_out = nullptr;        // may alias xw: written only after every QKV tile has read it
+  float* ss_out = nullptr;       // [M, d / 16]; may alias ss_in (same argument)
+  int* ctl = nullptr;
+  long long* stamps = nullptr;   // optional [grid][4] s_memrealtime stamps (start, wait done, end, role)
+  int cfg = 0;                   // A/B knobs (bench_decode_block.py): 1 = O waits before its weight loads,
+                                 // 2 = no acquire after the polls (timing only: NOT a valid hand-off)
+  int M = 0, d = 0, Hq = 0, Hkv = 0, BS = 0, wshuf = 0;
+};
+void launch_decode_block(const DecodeBlockArgs& a, hipStream_t s);
 void set_decode_gemm_variant(int v);  // -1: default heuristic
+void set_decode_gemm_nt(int on);      // non-temporal weight-stream loads (keeps the variant choice)
 void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e,
                         hipStream_t s);
 void launch_embed_prep(const int* ids, const int* src, const int* prev, const bf16* table, float* resid, const bf16* w,

@@ -15,9 +15,6 @@
 
 namespace {
 
-SYM_DEV f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
 
 // One wave per token.  E <= 64 experts (lane e holds logit e), k <= 8.
 __global__ __launch_bounds__(256) void moe_route_kernel(LinOut logits, int ld, int T, int E, int k,

@@ -56,6 +56,7 @@ class EngineConfig:
     mixed_prefill_tokens: int = 512      # prompt-chunk budget of steps that also carry decodes
     decode_weights: str = "auto"         # "preshuffled" | "shared" | "auto": extra MFMA-ordered decode copies
     persistent_mlp: bool = False         # O -> gate_up -> down as one persistent launch (measured slower: profiles/)
+    fused_attn_block: bool = False       # QKV -> attention -> O as one launch per layer (decode_block)
     model_config: ModelConfig | None = None
 
     @classmethod
@@ -71,7 +72,7 @@ class EngineConfig:
              "device": "device",
              "useGraphs": "use_graphs", "numKvBlocks": "num_kv_blocks", "decodeWeights": "decode_weights",
              "prefillChunk": "mixed_prefill_tokens",
-             "persistentMlp": "persistent_mlp"}
+             "persistentMlp": "persistent_mlp", "fusedAttnBlock": "fused_attn_block"}
         for k, attr in m.items():
             if cfg.get(k) is not None:
                 setattr(ec, attr, type(getattr(ec, attr))(cfg[k]) if getattr(ec, attr) is not None else cfg[k])
@@ -121,7 +122,7 @@ class LLMEngine:
         self.load_time = time.perf_counter() - t0
         self.model = TransformerLM(weights, self.device, tp_comm=tp_comm, ep_comm=ep_comm,
                                    max_decode_ctx=max_model_len, decode_weights=cfg.decode_weights,
-                                   persistent_mlp=cfg.persistent_mlp)
+                                   persistent_mlp=cfg.persistent_mlp, fused_attn_block=cfg.fused_attn_block)
         self.tokenizer = load_tokenizer(mcfg, cfg.tokenizer or (cfg.weights if cfg.weights != "random" else None))
         nb = cfg.num_kv_blocks or self._auto_blocks(max_model_len)
         self.kv = KVCache(mcfg.num_layers, nb, mcfg.num_kv_heads // cfg.tp_size, mcfg.head_dim, cfg.block_size,

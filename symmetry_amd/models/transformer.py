@@ -119,7 +119,7 @@ class Workspace:
 
 class TransformerLM:
     def __init__(self, weights: ModelWeights, device, tp_comm=None, ep_comm=None, max_decode_ctx: int | None = None,
-                 decode_weights: str = "auto", persistent_mlp: bool = False):
+                 decode_weights: str = "auto", persistent_mlp: bool = False, fused_attn_block: bool = False):
         self.cfg: ModelConfig = weights.cfg
         self.w = weights
         self.device = torch.device(device)
@@ -150,6 +150,7 @@ class TransformerLM:
         self.last_ids = torch.zeros(MAX_STEP_SEQS, dtype=torch.int32, device=self.device)
         self.dgw = self._decode_copies(decode_weights)
         self.persistent_mlp = persistent_mlp
+        self.fused_attn_block = fused_attn_block
 
     def _decode_copies(self, mode: str) -> dict:
         """MFMA-preshuffled copies of the decode-GEMM weights (1 KB contiguous per wave load:
@@ -182,6 +183,16 @@ class TransformerLM:
             return False
         shs = {self._dgw(0, n)[1] for n in ("wo", "w_gu", "w_down")}
         return len(shs) == 1
+
+    def _attn_block_ok(self, b: ForwardBatch) -> bool:
+        """decode_block preconditions: a pure decode step on one GPU, <= 16 rows, GQA group <= 8, K dims
+        % 512, QKV and O in one weight layout."""
+        if not self.fused_attn_block or b.kind != "decode" or self._tp_active() or b.num_tokens > 16:
+            return False
+        d, dq = self.cfg.hidden_size, self.hq * self.D
+        if d % 512 or dq % 512 or self.hq // self.hkv > 8:
+            return False
+        return self._dgw(0, "wqkv")[1] == self._dgw(0, "wo")[1]
 
     def _dgw(self, i: int, name: str):
         """(weight, wshuf) for decode GEMM `name` of layer i."""
@@ -264,14 +275,31 @@ class TransformerLM:
         ss = ss_1
         persistent = self._persistent_mlp_ok(T)
         ctl = self.ws.get("mlp_ctl", (ops.DECODE_MLP_CTL,), torch.int32, self.device, zeros=True) if persistent else None
+        block = self._attn_block_ok(b)
+        if block:
+            span = b.block_tables.shape[1] * kv.block_size
+            max_parts = (span + ops.ATTN_BLOCK_PART - 1) // ops.ATTN_BLOCK_PART
+            tmp_o = self._buf("tmp_o_blk", (b.num_seqs, self.hq, max_parts, self.D), torch.float32)
+            tmp_ml = self._buf("tmp_ml_blk", (b.num_seqs, self.hq, max_parts, 2), torch.float32)
+            cnt = self.ws.get("attn_counters", (b.num_seqs * self.hkv,), torch.int32, self.device, zeros=True)
+            bctl = self.ws.get("block_ctl", (ops.DECODE_BLOCK_CTL,), torch.int32, self.device, zeros=True)
         for i in range(cfg.num_layers):
             wq, shq = self._dgw(i, "wqkv")
-            ops.dg_qkv(xw, wq, ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq,
-                       self.hkv, wshuf=shq)
-            self._attention(b, kv, i, q, attn)
             attn2d = attn.view(T, self.hq * self.D)
             nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
-            if persistent:
+            if block:
+                # QKV -> attention -> O + residual in one launch (csrc/kernels/decode_gemm.hip,
+                # decode_block_kernel): the O weight stream overlaps the attention phase
+                wo, _ = self._dgw(i, "wo")
+                ops.decode_block(xw, wq, ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i],
+                                 b.block_tables, b.ctx_lens, attn, tmp_o, tmp_ml, cnt, self.scale, wo, resid,
+                                 w.layer(i, "ln2"), xw, ss_t, bctl, wshuf=shq)
+                ss = ss_t
+            else:
+                ops.dg_qkv(xw, wq, ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq,
+                           self.hkv, wshuf=shq)
+                self._attention(b, kv, i, q, attn)
+            if persistent and not block:
                 # O -> gate_up/SwiGLU -> down in one persistent launch: each phase's weight stream starts
                 # while the previous phase finishes (csrc/kernels/decode_gemm.hip, decode_mlp_kernel)
                 (wo, sh), (w_gu, _), (w_dn, _) = self._dgw(i, "wo"), self._dgw(i, "w_gu"), self._dgw(i, "w_down")
@@ -280,7 +308,8 @@ class TransformerLM:
                                wshuf=sh)
                 ss = ss_t
                 continue
-            ss = self._resid_proj("o", attn2d, self._dgw(i, "wo"), resid, w.layer(i, "ln2"), xw, ss_t, ss_1)
+            if not block:
+                ss = self._resid_proj("o", attn2d, self._dgw(i, "wo"), resid, w.layer(i, "ln2"), xw, ss_t, ss_1)
             if cfg.is_moe:
                 # router + experts are not decode GEMMs: materialise RMSNorm(resid) (one bf16 rounding)
                 xn = self._buf("x", (T, d), torch.bfloat16)

@@ -200,6 +200,8 @@ def moe_combine(y, dst, ids, e_lo, e_hi, w, k, out, accumulate=False):
 
 
 DECODE_MLP_CTL = 4224  # csrc/kernels/launchers.h DECODE_MLP_CTL_INTS
+DECODE_BLOCK_CTL = 1024  # csrc/kernels/launchers.h DECODE_BLOCK_CTL_INTS
+ATTN_BLOCK_PART = 256  # tokens per split-KV partition inside decode_block (csrc/kernels/attn_decode.h PART_F)
 
 
 def decode_mlp(attn, Wo, Wgu, Wd, resid, ln2, w_next, xw, ss, act, ctl, eps, wshuf=False):
@@ -211,6 +213,23 @@ def decode_mlp(attn, Wo, Wgu, Wd, resid, ln2, w_next, xw, ss, act, ctl, eps, wsh
                                         bool(wshuf))
     return reference.decode_mlp(attn, reference.unshuffled(Wo, wshuf), reference.unshuffled(Wgu, wshuf),
                                 reference.unshuffled(Wd, wshuf), resid, ln2, w_next, xw, ss, act, eps)
+
+
+def decode_block(xw, Wqkv, ss_in, eps, positions, slots, cos_sin, q, k_cache, v_cache, block_tables, ctx_lens,
+                 attn, tmp_o, tmp_ml, counters, scale, Wo, resid, ln2, xw_out, ss_out, ctl, wshuf=False):
+    """Fused decode attention block (one launch, M <= 16): the same result as dg_qkv + attn_decode +
+    dg_resid(O).  ``ctl``: int32[DECODE_BLOCK_CTL] zero-initialised once (re-armed by the kernel; word
+    ``(Hkv + 9) * 32`` non-zero after a launch flags a dependency wait that gave up)."""
+    if _gpu(xw):
+        return _native.ops().decode_block(xw, Wqkv, ss_in, float(eps), positions, slots, cos_sin, q, k_cache, v_cache,
+                                          block_tables, ctx_lens, attn, tmp_o, tmp_ml, counters, float(scale), Wo,
+                                          resid, ln2, xw_out, ss_out, ctl, bool(wshuf))
+    Hkv = k_cache.shape[1]
+    Hq = Wqkv.shape[0] // 128 - 2 * Hkv
+    reference.dg_qkv(xw, reference.unshuffled(Wqkv, wshuf), ss_in, eps, positions, slots, cos_sin, q, k_cache,
+                     v_cache, Hq, Hkv)
+    reference.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, attn, tmp_o, tmp_ml, scale)
+    reference.dg_resid(attn.view(attn.shape[0], -1), reference.unshuffled(Wo, wshuf), resid, ln2, xw_out, ss_out)
 
 
 def sample_filtered(logits, temps, top_k, top_p, seeds, step, out_ids):

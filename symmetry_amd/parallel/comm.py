@@ -8,6 +8,10 @@ Two interchangeable implementations of one small interface
   into the decode hipGraph; rides xGMI on an MI355X node.
 * :class:`TorchComm` -- ``torch.distributed`` on a process group (gloo on the
   CPU for the multi-process tests; RCCL through c10d on GPUs).
+* :class:`HostStagedComm` -- GPU tensors reduced through a gloo group on the
+  host.  Not a fast path: it lets several ranks share ONE GPU (RCCL refuses
+  duplicate devices), so the sharded HIP kernels of a TP/EP launch can be
+  checked on a one-GPU box (``SYMMETRY_TP_COMM=gloo``; eager steps only).
 
 xGMI is point-to-point (7 links x ~153 GB/s per GPU), so the per-layer
 decode all-reduce (16 KiB x batch for 70B) is latency-bound: the model
@@ -61,6 +65,30 @@ class TorchComm(Comm):
 
     def broadcast(self, t, src=0):
         dist.broadcast(t, src=src, group=self.group)
+
+
+class HostStagedComm(Comm):
+    """Collectives on device tensors via host copies and a gloo group (see module docstring)."""
+
+    def __init__(self, group=None):
+        self.inner = TorchComm(group)
+        self.rank, self.world = self.inner.rank, self.inner.world
+
+    def all_reduce(self, t, op="sum"):
+        h = t.detach().cpu()
+        self.inner.all_reduce(h, op)
+        t.copy_(h)
+
+    def all_gather(self, t):
+        return self.inner.all_gather(t.detach().cpu()).to(t.device)
+
+    def all_to_all_rows(self, send, send_counts, recv_counts):
+        return self.inner.all_to_all_rows(send.detach().cpu(), send_counts, recv_counts).to(send.device)
+
+    def broadcast(self, t, src=0):
+        h = t.detach().cpu()
+        self.inner.broadcast(h, src)
+        t.copy_(h)
 
 
 class RcclComm(Comm):

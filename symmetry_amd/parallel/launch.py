@@ -15,7 +15,7 @@ import os
 import torch
 import torch.distributed as dist
 
-from .comm import RcclComm, TorchComm
+from .comm import HostStagedComm, RcclComm, TorchComm
 
 
 def init_distributed(backend: str | None = None) -> tuple[int, int, int]:
@@ -25,16 +25,22 @@ def init_distributed(backend: str | None = None) -> tuple[int, int, int]:
     if world > 1 and not dist.is_initialized():
         if torch.cuda.is_available():
             torch.cuda.set_device(local)
-        backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
+        staged = os.environ.get("SYMMETRY_TP_COMM", "rccl").lower() == "gloo"
+        backend = backend or ("nccl" if torch.cuda.is_available() and not staged else "gloo")
         kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
         dist.init_process_group(backend, **kw)
     return rank, world, local
 
 
 def make_comms(on_gpu: bool):
+    """TP/EP communicator + the gloo metadata group.  ``SYMMETRY_TP_COMM=gloo`` on GPUs selects the
+    host-staged communicator (ranks sharing one GPU for kernel checks; no hipGraphs)."""
     cpu_group = dist.new_group(backend="gloo")
-    comm = RcclComm(bootstrap_group=cpu_group) if on_gpu else TorchComm(cpu_group)
-    return comm, cpu_group
+    if not on_gpu:
+        return TorchComm(cpu_group), cpu_group
+    if os.environ.get("SYMMETRY_TP_COMM", "rccl").lower() == "gloo":
+        return HostStagedComm(cpu_group), cpu_group
+    return RcclComm(bootstrap_group=cpu_group), cpu_group
 
 
 def init_tp_engine(ecfg):

@@ -250,3 +250,107 @@ def test_decode_mlp_persistent(gpu, M, shuf):
         torch.cuda.synchronize()
         assert not ctl.any(), ctl.tolist()
         assert torch.equal(r_g, r_p) and torch.equal(act_g, act_p) and torch.equal(ss_g, ss_p)
+
+
+@pytest.mark.parametrize("M", [1, 4, 10, 16])
+@pytest.mark.parametrize("Hq,Hkv,d,shuf", [(32, 8, 4096, True), (32, 8, 4096, False), (16, 2, 2048, True)])
+def test_decode_block_fused_equals_three_launches(gpu, M, Hq, Hkv, d, shuf):
+    """QKV -> attention -> O in one launch (decode_block) vs dg_qkv + attn_decode + dg_resid with decode_gemm
+    variant 0: the QKV tiles (q, K/V cache) are bitwise equal; attention uses 256-token partitions (one
+    32-token group per wave) instead of 512, so its output and what follows match to bf16 rounding,
+    including multi-partition contexts (split-KV combine inside the launch).  The O tile given the SAME
+    attention rows is bitwise equal; the control block re-arms itself, also under graph replay."""
+    import math
+
+    from symmetry_amd.models.layout import preshuffle
+    from symmetry_amd.ops import _native
+
+    D, BS = 128, 64
+    g = torch.Generator(device=gpu).manual_seed(100 + M)
+    ctx_lens = [(37 * i * i + 100 * i + 1) % 2100 + 1 for i in range(M)]
+    max_blocks = max((c + BS - 1) // BS for c in ctx_lens) + 1
+    NB = sum((c + BS - 1) // BS for c in ctx_lens) + 3
+    kc0 = torch.randn(NB, Hkv, BS, D, device=gpu, generator=g).bfloat16()
+    vc0 = torch.randn(NB, Hkv, D, BS, device=gpu, generator=g).bfloat16()
+    perm = torch.randperm(NB, generator=torch.Generator().manual_seed(5)).tolist()
+    bt = torch.zeros(M, max_blocks, dtype=torch.int32)
+    i = 0
+    for s, c in enumerate(ctx_lens):
+        for blk in range((c + BS - 1) // BS):
+            bt[s, blk] = perm[i]
+            i += 1
+    pos = torch.tensor([c - 1 for c in ctx_lens], dtype=torch.int32)
+    slots = torch.tensor([int(bt[s, p // BS]) * BS + p % BS for s, p in enumerate(pos.tolist())], dtype=torch.int32)
+    bt, pos, slots = bt.to(gpu), pos.to(gpu), slots.to(gpu)
+    ctx = torch.tensor(ctx_lens, device=gpu, dtype=torch.int32)
+    N = (Hq + 2 * Hkv) * D
+    xw = torch.randn(M, d, device=gpu, generator=g).bfloat16()
+    ss_in = torch.rand(M, d // 16, device=gpu, generator=g) * 16 + 1
+    Wqkv = (torch.randn(N, d, device=gpu, generator=g) / d ** 0.5).bfloat16()[qkv_perm(Hq, Hkv, D).to(gpu)].contiguous()
+    Wo = (torch.randn(d, Hq * D, device=gpu, generator=g) / (Hq * D) ** 0.5).bfloat16()
+    if shuf:
+        Wqkv, Wo = preshuffle(Wqkv), preshuffle(Wo)
+    resid0 = torch.randn(M, d, device=gpu, generator=g)
+    ln2 = (torch.randn(d, device=gpu, generator=g) * 0.1 + 1).bfloat16()
+    cs = ref.rope_table(4096, D, 500000.0, device=gpu)
+    scale = 1 / math.sqrt(D)
+    max_parts = (max_blocks * BS + ops.ATTN_BLOCK_PART - 1) // ops.ATTN_BLOCK_PART
+
+    def state():
+        return dict(kc=kc0.clone(), vc=vc0.clone(), q=torch.empty(M, Hq, D, device=gpu, dtype=torch.bfloat16),
+                    attn=torch.empty(M, Hq, D, device=gpu, dtype=torch.bfloat16), resid=resid0.clone(),
+                    xw=xw.clone(), ss=ss_in.clone(), tmp_o=torch.empty(M, Hq, max_parts, D, device=gpu),
+                    tmp_ml=torch.empty(M, Hq, max_parts, 2, device=gpu),
+                    cnt=torch.zeros(M * Hkv, device=gpu, dtype=torch.int32))
+
+    nat = _native.ops()
+    nat.decode_gemm_variant(0)
+    try:
+        a = state()
+        ss_t = torch.empty(M, d // 16, device=gpu)
+        ops.dg_qkv(a["xw"], Wqkv, a["ss"], 1e-5, pos, slots, cs, a["q"], a["kc"], a["vc"], Hq, Hkv, wshuf=shuf)
+        ops.attn_decode(a["q"], a["kc"], a["vc"], bt, ctx, a["attn"], a["tmp_o"], a["tmp_ml"], a["cnt"], scale)
+        ops.dg_resid(a["attn"].view(M, -1), Wo, a["resid"], ln2, a["xw"], ss_t, wshuf=shuf)
+        a["ss"] = ss_t
+        bf = state()
+        ctl = torch.zeros(ops.DECODE_BLOCK_CTL, device=gpu, dtype=torch.int32)
+        # ss_in and ss_out alias, xw and xw_out alias: the engine's buffers
+        ops.decode_block(bf["xw"], Wqkv, bf["ss"], 1e-5, pos, slots, cs, bf["q"], bf["kc"], bf["vc"], bt, ctx,
+                         bf["attn"], bf["tmp_o"], bf["tmp_ml"], bf["cnt"], scale, Wo, bf["resid"], ln2, bf["xw"],
+                         bf["ss"], ctl, wshuf=shuf)
+        torch.cuda.synchronize()
+        assert not ctl.any(), ctl.nonzero().flatten().tolist()
+        assert not bf["cnt"].any()
+        for k in ("q", "kc", "vc"):
+            assert torch.equal(bf[k], a[k]), k
+        _close(bf["attn"], a["attn"], atol=2e-2, rtol=2e-2)
+        _close(bf["resid"], a["resid"], atol=2e-2, rtol=1e-2)
+        # the O tile itself is bitwise the 3-launch one: feed the fused attention rows to dg_resid
+        r2, xw2, ss2 = resid0.clone(), torch.empty_like(xw), torch.empty(M, d // 16, device=gpu)
+        ops.dg_resid(bf["attn"].view(M, -1), Wo, r2, ln2, xw2, ss2, wshuf=shuf)
+        assert torch.equal(r2, bf["resid"]) and torch.equal(xw2, bf["xw"]) and torch.equal(ss2, bf["ss"])
+        # attention against the fp32 reference
+        at_r = torch.empty(M, Hq, D, dtype=torch.bfloat16)
+        ref.attn_decode(bf["q"].cpu(), bf["kc"].cpu(), bf["vc"].cpu(), bt.cpu(), ctx.cpu(), at_r, scale=scale)
+        _close(bf["attn"], at_r, atol=2e-2, rtol=2e-2)
+        # graph replays from the same inputs: identical outputs, counters re-armed every time
+        gr = state()
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=s):
+                ops.decode_block(gr["xw"], Wqkv, gr["ss"], 1e-5, pos, slots, cs, gr["q"], gr["kc"], gr["vc"], bt, ctx,
+                                 gr["attn"], gr["tmp_o"], gr["tmp_ml"], gr["cnt"], scale, Wo, gr["resid"], ln2,
+                                 gr["xw"], gr["ss"], ctl, wshuf=shuf)
+        torch.cuda.synchronize()
+        for _ in range(3):
+            gr["resid"].copy_(resid0)
+            gr["xw"].copy_(xw)
+            gr["ss"].copy_(ss_in)
+            graph.replay()
+            torch.cuda.synchronize()
+            assert not ctl.any()
+            for k in ("q", "attn", "resid", "xw", "ss"):
+                assert torch.equal(gr[k], bf[k]), k
+    finally:
+        nat.decode_gemm_variant(-1)

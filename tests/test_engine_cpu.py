@@ -257,3 +257,24 @@ def test_persistent_mlp_path_matches_three_launch_path():
             eng.step()
         outs.append([s.output_ids for s in seqs])
     assert outs[0] == outs[1]
+
+
+def test_fused_attn_block_path_matches_default_path(monkeypatch):
+    """fusedAttnBlock: decode steps run QKV -> attention -> O through ops.decode_block (one launch per layer
+    on the GPU); greedy outputs equal the default path, and prefill steps keep the general path."""
+    from symmetry_amd import ops
+
+    calls = []
+    orig = ops.decode_block
+    monkeypatch.setattr(ops, "decode_block", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    prompts = _prompts(3, seed=7, lo=4, hi=20)
+    outs = []
+    for block in (False, True):
+        eng = _engine("small-llama", max_num_seqs=4, use_graphs=False, fused_attn_block=block)
+        seqs = [eng.add_request(f"r{i}", p, SamplingParams(max_tokens=6, ignore_eos=True))
+                for i, p in enumerate(prompts)]
+        while eng.has_unfinished():
+            eng.step()
+        outs.append([s.output_ids for s in seqs])
+        assert bool(calls) == block
+    assert outs[0] == outs[1]

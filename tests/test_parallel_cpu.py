@@ -71,6 +71,18 @@ def _comm_worker(rank, world):
     sc = [1, 2] if rank == 0 else [2, 1]
     rc = [1, 2] if rank == 0 else [2, 1]
     r = c.all_to_all_rows(send, sc, rc)
+    # the host-staged communicator (GPU ranks sharing one device) must agree with the plain one
+    from symmetry_amd.parallel.comm import HostStagedComm
+
+    hs = HostStagedComm()
+    t2 = torch.full((4,), float(rank + 1))
+    hs.all_reduce(t2)
+    assert torch.equal(t2, t)
+    assert torch.equal(hs.all_gather(torch.tensor([[rank, rank]])), g)
+    assert torch.equal(hs.all_to_all_rows(send, sc, rc), r)
+    b = torch.tensor([rank + 5])
+    hs.broadcast(b, src=1)
+    assert int(b) == 6
     return t.tolist(), int(m), g.tolist(), r.tolist()
 
 
