@@ -344,8 +344,8 @@ SYM_DEV void gemm_tile(const bf16* __restrict__ x, const bf16* __restrict__ W, i
   }
 }
 
-template <int MT, int NW, int U, int RT, int EPI>
-__global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(const bf16* __restrict__ x,
+template <int MT, int NW, int U, int RT, int EPI, int WPE = 1>
+__global__ __launch_bounds__(NW * 64, WPE) void decode_gemm_kernel(const bf16* __restrict__ x,
                                                               const bf16* __restrict__ W, int M, int N, int K,
                                                               DecodeEpi e) {
   gemm_tile<MT, NW, U, RT, EPI>(x, W, M, N, K, e, blockIdx.x, NoWait{});
@@ -718,14 +718,130 @@ __global__ __launch_bounds__(512, 4) void decode_block_kernel(DecodeBlockArgs a)
 //   5  8 waves, 4 row tiles (1 column tile only; else as 3)
 //   6  4 waves, 2 row tiles
 //   7  4 waves, 4 row tiles (1 column tile only; else as 6)
+//   8  4 waves, 1 row tile, U <= 2 (70 VGPRs): 7 waves / SIMD resident
+//  11  x-resident persistent: 16 waves per CU, x loaded once per workgroup, tiles walked with the next
+//      tile's weights in flight (M <= 16, K in {1024, 2048, 4096}; else variant 0)
+// ---------------------------------------------------------------------------------------------------
+// x-resident persistent decode GEMM (M <= 16, K == 16 * 64 * U): one 16-wave workgroup per CU walks row tiles
+// t = b, b + grid, ...; each wave loads ITS k-slice of the activations x ONCE (U k-blocks, 8U VGPRs) and keeps
+// it for every tile, so the per-tile L1/TA traffic is the weight stream alone (with row-tile-per-workgroup
+// kernels the x fragments cost as many load instructions as the weights at M = 16, and gate_up ran 41 us at
+// M = 1 vs 53 us at M = 16).  The next tile's weights are issued right after this tile's MFMAs and are in
+// flight while it is reduced (LDS, double-buffered) and finished by wave 0 (16 waves x 8 KB per CU in
+// flight is above the ~50 KB Little's-law need); the grid gives every CU the same tile count.
+// ---------------------------------------------------------------------------------------------------
+template <int U, int EPI>
+__global__ __launch_bounds__(1024) void decode_gemm_xres_kernel(const bf16* __restrict__ x, const bf16* __restrict__ W,
+                                                                int M, int N, int K, DecodeEpi e) {
+  constexpr int NW = 16;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, h = lane >> 4;
+  const int kbeg = wid * (K / NW);
+  const int ntiles = N / 16;
+  const int wmul = e.wshuf ? 16 : 1, wsec = e.wshuf ? 512 : 32;
+  auto wptr = [&](int t) -> const bf16* {
+    return e.wshuf ? W + ((long long)t * (K / 32) + kbeg / 32) * 512 + lane * 8
+                   : W + (long long)(16 * t + r16) * K + kbeg + 8 * h;
+  };
+  int t = blockIdx.x;
+  Pack8 wa[U][2];
+  {
+    const bf16* wp = wptr(t);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      wa[u][0].u = *reinterpret_cast<const uint4*>(wp + u * 64 * wmul);
+      wa[u][1].u = *reinterpret_cast<const uint4*>(wp + u * 64 * wmul + wsec);
+    }
+  }
+  const bool xok = r16 < M;
+  const bf16* xrow = x + (long long)min(r16, M - 1) * K + kbeg + 8 * h;
+  Pack8 xa[U][2];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    xa[u][0].u = xok ? *reinterpret_cast<const uint4*>(xrow + u * 64) : make_uint4(0, 0, 0, 0);
+    xa[u][1].u = xok ? *reinterpret_cast<const uint4*>(xrow + u * 64 + 32) : make_uint4(0, 0, 0, 0);
+  }
+  __shared__ float rn_s[16];
+  if (e.ss_in) {  // deferred-RMSNorm row scales, once per workgroup
+    for (int m = wid; m < M; m += NW) {
+      float sacc = 0.f;
+      for (int i = lane; i < e.ss_tiles; i += 64) sacc += e.ss_in[(long long)m * e.ss_tiles + i];
+      sacc = wave_sum(sacc);
+      if (lane == 0) rn_s[m] = rsqrtf(sacc * e.inv_d + e.eps);
+    }
+  }
+  __shared__ f32x4 red[2][NW][64];
+  int buf = 0;
+  for (;;) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc = mfma16(wa[u][0].v, xa[u][0].v, acc);
+      acc = mfma16(wa[u][1].v, xa[u][1].v, acc);
+    }
+    // keep the next loads behind this tile's MFMAs: they reuse wa's registers (no renamed second copy)
+    __builtin_amdgcn_sched_barrier(0);
+    const int tn = t + gridDim.x;
+    if (tn < ntiles) {  // next tile's weight stream in flight during this tile's reduction and epilogue
+      const bf16* wp = wptr(tn);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        wa[u][0].u = *reinterpret_cast<const uint4*>(wp + u * 64 * wmul);
+        wa[u][1].u = *reinterpret_cast<const uint4*>(wp + u * 64 * wmul + wsec);
+      }
+    }
+    red[buf][wid][lane] = acc;
+    __syncthreads();
+    if (wid == 0) {
+      f32x4 v = red[buf][0][lane];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) {
+        v += red[buf][w][lane];
+        if ((w & 3) == 3) asm volatile("" : "+v"(v)::"memory");  // <= 4 partials in registers at a time
+      }
+      const int m = r16;
+      const bool mok = m < M;
+      const float sc = (e.ss_in && mok) ? rn_s[m] : 1.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] *= sc;
+      epilogue<EPI>(e, v, t, m, mok, h, N);
+    }
+    buf ^= 1;
+    if (tn >= ntiles) break;
+    t = tn;
+  }
+}
+
+int g_num_cus = 0;
+
+template <int EPI>
+bool go_xres(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, hipStream_t s) {
+  if (M > 16 || K % 1024 || K > 4096) return false;
+  if (!g_num_cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    g_num_cus = std::max(1, g_num_cus);
+  }
+  const int ntiles = N / 16;
+  const int per = (ntiles + g_num_cus - 1) / g_num_cus;  // equal tile count per workgroup
+  const int grid = (ntiles + per - 1) / per;
+  switch (K / 1024) {
+    case 1: decode_gemm_xres_kernel<1, EPI><<<grid, 1024, 0, s>>>(x, W, M, N, K, e); return true;
+    case 2: decode_gemm_xres_kernel<2, EPI><<<grid, 1024, 0, s>>>(x, W, M, N, K, e); return true;
+    case 4: decode_gemm_xres_kernel<4, EPI><<<grid, 1024, 0, s>>>(x, W, M, N, K, e); return true;
+    default: return false;
+  }
+}
+
 int g_variant = -1;
 int g_wnt = 0;
 
-template <int MT, int NW, int U, int RT, int EPI>
+template <int MT, int NW, int U, int RT, int EPI, int WPE = 1>
 void go(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e0, hipStream_t s) {
   DecodeEpi e = e0;
   e.wnt = g_wnt;
-  decode_gemm_kernel<MT, NW, U, RT, EPI><<<N / (16 * RT), NW * 64, 0, s>>>(x, W, M, N, K, e);
+  decode_gemm_kernel<MT, NW, U, RT, EPI, WPE><<<N / (16 * RT), NW * 64, 0, s>>>(x, W, M, N, K, e);
 }
 
 template <int MT, int EPI>
@@ -741,7 +857,13 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
     if (e.wshuf) {
       // preshuffled stream (profiles/decode_gemm_preshuffle_r1.jsonl): 1 KB loads make the x-fragment
       // sharing of multi-tile workgroups unnecessary; wide N prefers 4 waves per tile
-      if (N >= 12288) v = M > 16 ? 3 : (M <= 4 ? 0 : 4);
+      // x-resident persistent tiles (profiles/decode_gemm_xres_r1.jsonl, M = 10: gate_up 49.1 -> 40.9 us,
+      // qkv 15.6 -> 13.4, lm_head 205.9 -> 190.5; = variant 2 on the one-tile-per-CU O projection), except
+      // the vocabulary projection at <= 4 rows where the 8-wave split stays ahead
+      if (M <= 16 && K % 1024 == 0 && K <= 4096 && !(N >= 65536 && M <= 4)) v = 11;
+      // wide N at 5..16 rows otherwise: 7 resident 4-wave workgroups per CU (gate_up's 1792 tiles in one
+      // round): 45.3 vs 46.9 us (profiles/decode_gemm_occupancy_r1.jsonl)
+      else if (N >= 12288) v = M > 16 ? 3 : (M <= 4 ? 0 : 8);
       else if (N <= 4096 && K % 1024 == 0) v = 2;  // few row tiles: split K over 16 waves
       else v = 0;
     } else if (M <= 4) {
@@ -762,6 +884,14 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
   if (K % 512) v = (v == 6 || v == 7) ? 6 : 4;  // e.g. Llama-3-8B down_proj under TP=8: K = 1792
   if (v == 6 && N % 32) v = 4;
   constexpr int UH = U0 > 1 ? U0 / 2 : 1;
+  if (v == 11) {
+    if constexpr (MT == 1) {
+      DecodeEpi ex = e;
+      ex.wnt = g_wnt;
+      if (go_xres<EPI>(x, W, M, N, K, ex, s)) return;
+    }
+    v = 0;
+  }
   switch (v) {
     case 1: go<MT, 8, U1, 1, EPI>(x, W, M, N, K, e, s); break;
     case 2: go<MT, 16, U0, 1, EPI>(x, W, M, N, K, e, s); break;
@@ -770,6 +900,10 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
     case 5: if constexpr (MT == 1) go<1, 8, 1, 4, EPI>(x, W, M, N, K, e, s); break;
     case 6: go<MT, 4, UH, 2, EPI>(x, W, M, N, K, e, s); break;
     case 7: if constexpr (MT == 1) go<1, 4, 2, 4, EPI>(x, W, M, N, K, e, s); break;
+    // occupancy-bounded: 7 waves / SIMD = 7 four-wave workgroups per CU, so Llama-3-8B gate_up's 1792
+    // row tiles are all resident at once (one round, no second-round tail)
+    case 8: go<MT, 4, (U0 > 2 ? 2 : U0), 1, EPI, 7>(x, W, M, N, K, e, s); break;
+
     default: go<MT, 8, U0, 1, EPI>(x, W, M, N, K, e, s); break;
   }
 }
