@@ -302,27 +302,49 @@ SYM_DEV void gemm_tile(const bf16* __restrict__ x, const bf16* __restrict__ W, i
           acc[rt][mt] = mfma16(wa[u][rt][1].v, xa[u][mt][1].v, acc[rt][mt]);
         }
   }
-  if (!waited) wait();
-  for (; b < nblk; ++b) {
-    const int ko = b * 64;
-    Pack8 w0[RT], w1[RT];
+  // the remaining nblk % U k-blocks as ONE predicated batch (a per-block loop would pay one memory round
+  // trip per block: Llama-3-8B down_proj at 16 waves has 14 = 3 x 4 + 2 blocks per wave)
+  if (b < nblk) {
+    const int rem = nblk - b;
+    Pack8 wa[U][RT][2], xa[U][MT][2];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      w0[rt].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko * wmul);
-      w1[rt].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko * wmul + wsec);
-    }
+    for (int u = 0; u < U; ++u) {
+      if (u < rem) {
+        const int ko = (b + u) * 64;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      Pack8 x0, x1;
-      x0.u = ldx(mt, ko);
-      x1.u = ldx(mt, ko + 32);
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        acc[rt][mt] = mfma16(w0[rt].v, x0.v, acc[rt][mt]);
-        acc[rt][mt] = mfma16(w1[rt].v, x1.v, acc[rt][mt]);
+        for (int rt = 0; rt < RT; ++rt) {
+          wa[u][rt][0].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko * wmul);
+          wa[u][rt][1].u = *reinterpret_cast<const uint4*>(wrow[rt] + ko * wmul + wsec);
+        }
       }
     }
+    if (!waited) {
+      waited = true;
+      wait();
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < rem) {
+        const int ko = (b + u) * 64;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          xa[u][mt][0].u = ldx(mt, ko);
+          xa[u][mt][1].u = ldx(mt, ko + 32);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (u < rem)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            acc[rt][mt] = mfma16(wa[u][rt][0].v, xa[u][mt][0].v, acc[rt][mt]);
+            acc[rt][mt] = mfma16(wa[u][rt][1].v, xa[u][mt][1].v, acc[rt][mt]);
+          }
   }
+  if (!waited) wait();
   if (!rn_done) row_scales();
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
@@ -864,7 +886,8 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
       // wide N at 5..16 rows otherwise: 7 resident 4-wave workgroups per CU (gate_up's 1792 tiles in one
       // round): 45.3 vs 46.9 us (profiles/decode_gemm_occupancy_r1.jsonl)
       else if (N >= 12288) v = M > 16 ? 3 : (M <= 4 ? 0 : 8);
-      else if (N <= 4096 && K % 1024 == 0) v = 2;  // few row tiles: split K over 16 waves
+      else if (N <= 4096 && K % 1024 == 0) v = K > 4096 ? 4 : 2;  // few row tiles: split K (down_proj: 4 waves,
+                                                                  // 24.2 vs 25.7 us at M = 10)
       else v = 0;
     } else if (M <= 4) {
       v = 0;
@@ -902,7 +925,10 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
     case 7: if constexpr (MT == 1) go<1, 4, 2, 4, EPI>(x, W, M, N, K, e, s); break;
     // occupancy-bounded: 7 waves / SIMD = 7 four-wave workgroups per CU, so Llama-3-8B gate_up's 1792
     // row tiles are all resident at once (one round, no second-round tail)
-    case 8: go<MT, 4, (U0 > 2 ? 2 : U0), 1, EPI, 7>(x, W, M, N, K, e, s); break;
+    case 8:  // one column tile only (the 7-waves-per-SIMD register budget)
+      if constexpr (MT == 1) go<1, 4, 2, 1, EPI, 7>(x, W, M, N, K, e, s);
+      else go<MT, 4, U0, 1, EPI>(x, W, M, N, K, e, s);
+      break;
 
     default: go<MT, 8, U0, 1, EPI>(x, W, M, N, K, e, s); break;
   }
