@@ -28,6 +28,9 @@
 // Prefill (K4): grid (q tile, kv_head * G); each wave owns 16 query rows of
 // one head, causal + varlen + chunked prefill (queries are the LAST qlen
 // positions of a context of length ctx), reading K/V from the paged cache.
+#include <stdlib.h>
+#include <string.h>
+
 #include "attn_decode.h"
 #include "common.h"
 #include "launchers.h"
@@ -274,6 +277,256 @@ __global__ __launch_bounds__(128 * HPW) void attn_prefill_lds_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Prefill, 32x32x16 MFMA (K4, default for GQA groups of 4k heads): same workgroup shape as the
+// LDS-staged kernel above (4 query heads of one kv head x 64 query rows, 8 waves, every K/V tile read
+// from the paged cache once per workgroup and double-buffered through LDS), with the per-wave math
+// re-tiled for v_mfma_f32_32x32x16_bf16 (cdna_hip_programming.md §3, T12-T14):
+//   * a wave owns 32 query rows of one head; per 64-key tile it issues 16 S^T MFMAs and 16 P.V MFMAs
+//     (32 cycles each) and runs ONE online-softmax update over 32 scores per lane (the 16x16 kernel
+//     pays two updates, four cross-lane shuffles and two O rescales per 64 keys);
+//   * S^T = K . Q^T with the K rows permuted (row r loads key r with bits 2 and 3 swapped) so that
+//     accumulator registers 8s..8s+7 of a lane hold 8 CONSECUTIVE keys: the bf16-packed accumulator
+//     is directly the B operand of O^T += V^T . P^T, and the matching V^T fragment is one contiguous
+//     16-byte LDS read (no transpose, no permute);
+//   * the contraction over D is permuted the same way for Q/K: lane half hh covers dims 64hh..64hh+63,
+//     so a lane's K fragment reads are 128 contiguous bytes of one key row;
+//   * the row max crosses lane halves with one v_permlane32_swap; exp2 is the raw v_exp_f32 with the
+//     1/sqrt(D)*log2(e) scale folded into one fma; masks are evaluated only on tiles that touch the
+//     causal diagonal or the context end;
+//   * deferred rescale (T13): the running max moves only when a tile's max exceeds it by > 8 (log2
+//     units), so O and l are rescaled on a few tiles instead of every tile (P <= 2^8 before the bf16
+//     cast: relative precision unchanged);
+//   * the block-table reads of a tile are issued one tile ahead of its K/V loads (a dependent
+//     table -> K/V load pair per tile exposed ~2 memory latencies per iteration: 2.5x slower);
+//   * heavier tiles first: workgroup x takes tile (num_tiles - 1 - x), so the long causal rows of a
+//     sequence start in the first wave of workgroups instead of forming the tail.
+// ---------------------------------------------------------------------------------------------
+SYM_DEV f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+SYM_DEV float xhalf_max(float v) {  // max with the lane 32 apart (same query column, other key half)
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+SYM_DEV float xhalf_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+constexpr float kRescaleThr = 8.f;  // T13 threshold, log2 units
+
+template <bool kMask>
+SYM_DEV void prefill_tile32(const bf16* __restrict__ sk, const bf16* __restrict__ sv, const bf16x8 (&qf)[8],
+                            float scale_log2, int t0, int mypos, f32x16 (&o)[4], float& m, float& lsum) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31, hh = lane >> 5;
+  const int pr = (r & 3) | ((r & 4) << 1) | ((r & 8) >> 1) | (r & 16);  // bits 2 <-> 3
+  f32x16 s[2];
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    const bf16* kr = sk + (32 * st + pr) * KST + 64 * hh;
+    bf16x8 kf[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) kf[kk] = *reinterpret_cast<const bf16x8*>(kr + 8 * kk);
+    f32x16 acc = {};
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) acc = mfma32(kf[kk], qf[kk], acc);
+    s[st] = acc;
+  }
+  // register i of subtile st holds key t0 + 32 st + 16 (i >> 3) + 8 hh + (i & 7)
+  if constexpr (kMask) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int t = t0 + 32 * st + 16 * (i >> 3) + 8 * hh + (i & 7);
+        if (t > mypos) s[st][i] = -INFINITY;
+      }
+  }
+  float tmax = s[0][0];
+#pragma unroll
+  for (int i = 1; i < 16; ++i) tmax = fmaxf(tmax, s[0][i]);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, s[1][i]);
+  tmax = xhalf_max(tmax) * scale_log2;
+  if (__builtin_expect(!__all(tmax <= m + kRescaleThr), 0)) {
+    const float mn = fmaxf(m, tmax);
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);  // m = -inf on the first tile: alpha = 0
+    m = mn;
+    lsum *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+  }
+  float psum = 0.f;
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    Pack8 pf[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = __builtin_amdgcn_exp2f(fmaf(s[st][i], scale_log2, -m));
+      psum += p;
+      pf[i >> 3].h[i & 7] = (bf16)p;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(sv + (32 * dt + r) * VST + 32 * st + 16 * ks + 8 * hh);
+        o[dt] = mfma32(vf, pf[ks].v, o[dt]);
+      }
+    }
+  }
+  lsum += psum;
+}
+
+// NW = 8: the workgroup covers 64 query rows (two row halves) of 4 heads; NW = 4: 32 rows (the
+// half is blockIdx.z & 1), so two workgroups share a CU and their barriers interleave.
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 2) void attn_prefill_m32_kernel(
+    const bf16* __restrict__ q, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    const int* __restrict__ block_tables, const int* __restrict__ ctx_lens, const int* __restrict__ cu_q,
+    const int* __restrict__ tiles, bf16* __restrict__ out, int Hq, int Hkv, int BS, int max_blocks,
+    float scale_log2, int prio) {
+  constexpr int HPW = 4, NT = NW * 64, CH = 1024 / NT;  // 16-B chunks per thread per K (and V) tile
+  static_assert(CH == 2 || CH == 4, "2 or 4 staging chunks");
+  constexpr int KROWS = NT / 16, VROWS = NT / 8;          // tile rows one pass of the workgroup covers
+  __shared__ bf16 sK[2][64 * KST];
+  __shared__ bf16 sV[2][D * VST];
+  const int tile = gridDim.x - 1 - blockIdx.x, kvh = blockIdx.y;
+  const int G = Hq / Hkv;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = lane & 31, hh = lane >> 5;
+  const int slice = NW == 8 ? blockIdx.z : blockIdx.z >> 1;
+  const int head = kvh * G + slice * HPW + wid % HPW;
+  const int half = NW == 8 ? wid / HPW : (blockIdx.z & 1);
+  if (prio && __builtin_amdgcn_readfirstlane(wid) >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  const int seq = tiles[2 * tile], qrow0 = tiles[2 * tile + 1];
+  const int qstart = cu_q[seq], qlen = cu_q[seq + 1] - qstart;
+  const int ctx = ctx_lens[seq];
+  const int pos0 = ctx - qlen;
+  const int* bt = block_tables + (long long)seq * max_blocks;
+  const int row0 = qrow0 + 32 * half;
+  const int kend_wg = NW == 8 ? min(ctx, pos0 + min(qrow0 + 64, qlen)) : min(ctx, pos0 + min(row0 + 32, qlen));
+  if (NW == 4 && row0 >= qlen) return;  // whole workgroup past the prompt (uniform)
+  const bool wave_live = row0 < qlen;
+  const int kend_w = min(ctx, pos0 + min(row0 + 32, qlen));  // keys [0, kend_w) visible to some row
+  const int minpos_w = pos0 + row0;                           // the wave's first query position
+  const int myrow = row0 + c;
+  const bool row_ok = myrow < qlen;
+  const int mypos = row_ok ? pos0 + myrow : ctx - 1;  // rows past the prompt attend like the last one
+
+  bf16x8 qf[8];
+  if (row_ok) {
+    const bf16* qp = q + ((long long)(qstart + myrow) * Hq + head) * D + 64 * hh;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) qf[kk] = ld16(qp + 8 * kk);
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) qf[kk] = zero8();
+  }
+  f32x16 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
+  float m = -INFINITY, lsum = 0.f;
+
+  // Cooperative tile staging: CH x 16 B of K and of V per thread.  The paged-cache block ids of a tile
+  // are fetched one tile AHEAD of its K/V loads, so issuing those loads never waits on a block-table
+  // read.  Keys past the context read the block of the last key (finite: the cache is zero-initialised
+  // and only ever written with finite K/V; masked anyway).
+  uint4 rk0, rk1, rk2, rk3, rv0, rv1, rv2, rv3;  // named registers (an array here lands in scratch)
+  int ik0, ik1, ik2, ik3, iv;
+  const int ck = threadIdx.x >> 4, pk = (threadIdx.x & 15) * 8;  // K: token ck + KROWS j, piece pk
+  const int dv = threadIdx.x >> 3, tv8 = 8 * (threadIdx.x & 7);   // V: dim dv + VROWS j, tokens tv8..+7
+  const long long kvoff = (long long)kvh * BS * D, bstride = (long long)Hkv * BS * D;
+  const int last = ctx - 1;
+  const int ntiles = (kend_wg + 63) / 64;
+  auto kid = [&](int t0, int j) { return bt[min(t0 + ck + KROWS * j, last) / BS]; };
+  auto kld = [&](int t0, int j, int ib) {
+    const int kt = min(t0 + ck + KROWS * j, last);
+    return *reinterpret_cast<const uint4*>(k_cache + ib * bstride + kvoff + (long long)(kt % BS) * D + pk);
+  };
+  auto vld = [&](int t0, int j) {
+    const int vt = min(t0 + tv8, last & ~7);
+    return *reinterpret_cast<const uint4*>(v_cache + iv * bstride + kvoff + (long long)(dv + VROWS * j) * BS +
+                                           vt % BS);
+  };
+#define FETCH_IDS(t0)                            \
+  do {                                           \
+    ik0 = kid(t0, 0);                            \
+    ik1 = kid(t0, 1);                            \
+    if constexpr (CH > 2) ik2 = kid(t0, 2);      \
+    if constexpr (CH > 2) ik3 = kid(t0, 3);      \
+    iv = bt[min((t0) + tv8, last) / BS];         \
+  } while (0)
+#define ISSUE(t0)                                               \
+  do {                                                          \
+    rk0 = kld(t0, 0, ik0);                                      \
+    rk1 = kld(t0, 1, ik1);                                      \
+    if constexpr (CH > 2) rk2 = kld(t0, 2, ik2);                \
+    if constexpr (CH > 2) rk3 = kld(t0, 3, ik3);                \
+    rv0 = vld(t0, 0);                                           \
+    rv1 = vld(t0, 1);                                           \
+    if constexpr (CH > 2) rv2 = vld(t0, 2);                     \
+    if constexpr (CH > 2) rv3 = vld(t0, 3);                     \
+  } while (0)
+#define ST1(buf, j, rkj, rvj)                                                        \
+  do {                                                                               \
+    *reinterpret_cast<uint4*>(&sK[buf][(ck + KROWS * (j)) * KST + pk]) = rkj;        \
+    *reinterpret_cast<uint4*>(&sV[buf][(dv + VROWS * (j)) * VST + tv8]) = rvj;       \
+  } while (0)
+#define STORE_TILE(buf)                              \
+  do {                                               \
+    ST1(buf, 0, rk0, rv0);                           \
+    ST1(buf, 1, rk1, rv1);                           \
+    if constexpr (CH > 2) ST1(buf, 2, rk2, rv2);     \
+    if constexpr (CH > 2) ST1(buf, 3, rk3, rv3);     \
+  } while (0)
+
+  if (ntiles > 0) {
+    FETCH_IDS(0);
+    ISSUE(0);
+    if (ntiles > 1) FETCH_IDS(64);
+    STORE_TILE(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < ntiles; ++it) {
+    const int t0 = it * 64;
+    if (it + 1 < ntiles) {
+      ISSUE(t0 + 64);
+      if (it + 2 < ntiles) FETCH_IDS(t0 + 128);
+    }
+    if (wave_live && t0 < kend_w) {
+      if (t0 + 63 > minpos_w)
+        prefill_tile32<true>(sK[it & 1], sV[it & 1], qf, scale_log2, t0, mypos, o, m, lsum);
+      else
+        prefill_tile32<false>(sK[it & 1], sV[it & 1], qf, scale_log2, t0, mypos, o, m, lsum);
+    }
+    if (it + 1 < ntiles) STORE_TILE((it + 1) & 1);
+    __syncthreads();
+  }
+#undef FETCH_IDS
+#undef ISSUE
+#undef ST1
+#undef STORE_TILE
+  const float l = xhalf_sum(lsum);
+  if (!row_ok) return;
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  // O^T[dt] register i of lane (c, hh): dim 32 dt + 8 (i >> 2) + 4 hh + (i & 3), query row c
+  bf16* op = out + ((long long)(qstart + myrow) * Hq + head) * D + 4 * hh;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (bf16)(o[dt][4 * g + e] * inv);
+      *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * g) = v;
+    }
+}
+
 }  // namespace
 
 void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,
@@ -292,6 +545,20 @@ void launch_attn_prefill(const bf16* q, const bf16* k_cache, const bf16* v_cache
   if (num_tiles == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
   const int G = Hq / Hkv;
+  // A/B knob SYMMETRY_ATTN_PREFILL: "lds" = the 16x16x32 LDS kernel, "w4" = 4-wave 32-row workgroups,
+  // "prio" = static s_setprio(1) for the second half of the waves (cdna_hip_programming.md T5)
+  static const char* knob = getenv("SYMMETRY_ATTN_PREFILL");
+  static const bool use_lds = knob && strstr(knob, "lds"), w4 = knob && strstr(knob, "w4");
+  static const int prio = (knob && strstr(knob, "prio")) ? 1 : 0;
+  if (!use_lds && BS % 8 == 0 && G % 4 == 0) {
+    if (w4)
+      attn_prefill_m32_kernel<4><<<dim3(num_tiles, Hkv, G / 2), 256, 0, s>>>(
+          q, k_cache, v_cache, block_tables, ctx_lens, cu_q, tiles, out, Hq, Hkv, BS, max_blocks, scale_log2, prio);
+    else
+      attn_prefill_m32_kernel<8><<<dim3(num_tiles, Hkv, G / 4), 512, 0, s>>>(
+          q, k_cache, v_cache, block_tables, ctx_lens, cu_q, tiles, out, Hq, Hkv, BS, max_blocks, scale_log2, prio);
+    return;
+  }
   if (BS % 8 == 0 && (G == 1 || G == 2 || G % 4 == 0)) {
     // LDS-staged kernel: the kv head's query heads share every K/V tile (slices of <= 4 heads)
     const int hpw = G >= 4 ? 4 : G;
