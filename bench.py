@@ -50,6 +50,8 @@ def main() -> int:
     ap.add_argument("--persistent-mlp", action="store_true", help="O/gate_up/down as one persistent launch (A/B)")
     ap.add_argument("--attn-block", type=int, default=None, help="A/B: QKV -> attention -> O as one launch (0/1)")
     ap.add_argument("--nt-weights", type=int, default=None, help="A/B: non-temporal decode weight loads (0/1)")
+    ap.add_argument("--max-batched-tokens", type=int, default=None, help="A/B: token budget of a pure-prefill step")
+    ap.add_argument("--mixed-prefill-tokens", type=int, default=None, help="A/B: prompt budget of mixed steps")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra decode steps after timing (for rocprof)")
     args = ap.parse_args()
 
@@ -84,6 +86,10 @@ def main() -> int:
                        max_model_len=args.max_model_len, block_size=block, num_kv_blocks=blocks,
                        use_graphs=not args.no_graphs, max_num_batched_tokens=max(8192, C * P),
                        persistent_mlp=args.persistent_mlp)
+    if args.max_batched_tokens is not None:
+        cfg.max_num_batched_tokens = args.max_batched_tokens
+    if args.mixed_prefill_tokens is not None:
+        cfg.mixed_prefill_tokens = args.mixed_prefill_tokens
     if args.attn_block is not None:
         cfg.fused_attn_block = bool(args.attn_block)
     t0 = time.perf_counter()
