@@ -527,6 +527,222 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_prefill_m32_kernel(
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Prefill, 32x32x16 MFMA, software-pipelined per 32-key subtile (K4 default).
+// Same workgroup / wave decomposition and operand tricks as attn_prefill_m32_kernel, restructured so
+// that a wave's VALU work hides under its own MFMAs: the online-softmax update is per 32-key subtile
+// and the loop body for subtile j is
+//     [rescale decision for j]  ->  S(j+1) = K . Q^T MFMAs  ||  exp2 / bf16 pack / row-sum of S(j)
+//                               ->  P(j) . V MFMAs         ||  row max of S(j+1)
+// (an MFMA holds the wave's issue for 8 of its 32 cycles, so independent VALU placed between MFMAs
+// runs in the remaining slots; cdna_hip_programming.md T15, MI355X_MICROARCH.md cycle constants).
+// Masks apply only to the <= 2 subtiles of a wave that touch the causal diagonal / context end (a
+// uniform branch).  K/V tiles are TRIPLE-buffered in LDS (107.5 KB, one workgroup per CU at this
+// register budget anyway): tile t+1 is resident while tile t is consumed, so S(j+1) can cross a tile
+// boundary, and tile t+2's global loads are in flight for a whole iteration.
+// ---------------------------------------------------------------------------------------------
+SYM_DEV void s_subtile(const bf16* __restrict__ sk, const bf16x8 (&qf)[8], f32x16& acc) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31, hh = lane >> 5;
+  const int pr = (r & 3) | ((r & 4) << 1) | ((r & 8) >> 1) | (r & 16);  // bits 2 <-> 3
+  const bf16* kr = sk + pr * KST + 64 * hh;
+  bf16x8 kf[8];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) kf[kk] = *reinterpret_cast<const bf16x8*>(kr + 8 * kk);
+  acc = f32x16{};
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) acc = mfma32(kf[kk], qf[kk], acc);
+}
+
+SYM_DEV void mask_subtile(f32x16& s, int kbase, int mypos) {
+  const int hh = (threadIdx.x & 63) >> 5;
+  const int lim = mypos - kbase - 8 * hh;  // register i holds key kbase + 16 (i >> 3) + 8 hh + (i & 7)
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (16 * (i >> 3) + (i & 7) > lim) s[i] = -INFINITY;
+}
+
+SYM_DEV float subtile_max(const f32x16& s, float scale_log2) {
+  float t = fmaxf(fmaxf(s[0], s[1]), s[2]);
+#pragma unroll
+  for (int i = 3; i < 15; i += 2) t = fmaxf(fmaxf(t, s[i]), s[i + 1]);
+  t = fmaxf(t, s[15]);
+  return xhalf_max(t) * scale_log2;
+}
+
+__global__ __launch_bounds__(512, 2) void attn_prefill_m32p_kernel(
+    const bf16* __restrict__ q, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    const int* __restrict__ block_tables, const int* __restrict__ ctx_lens, const int* __restrict__ cu_q,
+    const int* __restrict__ tiles, bf16* __restrict__ out, int Hq, int Hkv, int bs_shift, int max_blocks,
+    float scale_log2) {
+  const int BS = 1 << bs_shift, bs_mask = BS - 1;  // power-of-two blocks: no integer division per tile
+  constexpr int HPW = 4, KROWS = 32, VROWS = 64;
+  constexpr int TILE_ELEMS = 64 * KST + D * VST;  // one K tile + one V^T tile
+  __shared__ bf16 smem[3 * TILE_ELEMS];
+  const int tile = blockIdx.y, kvh = blockIdx.x;  // tiles arrive heaviest first (engine order)
+  const int G = Hq / Hkv;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform to the compiler
+  const int c = lane & 31, hh = lane >> 5;
+  const int head = kvh * G + blockIdx.z * HPW + wid % HPW;
+  const int half = wid / HPW;
+  const int seq = tiles[2 * tile], qrow0 = tiles[2 * tile + 1];
+  const int qstart = cu_q[seq], qlen = cu_q[seq + 1] - qstart;
+  const int ctx = ctx_lens[seq];
+  const int pos0 = ctx - qlen;
+  const int* bt = block_tables + (long long)seq * max_blocks;
+  const int row0 = qrow0 + 32 * half;
+  const int kend_wg = min(ctx, pos0 + min(qrow0 + 64, qlen));
+  const bool wave_live = row0 < qlen;
+  const int kend_w = min(ctx, pos0 + min(row0 + 32, qlen));  // keys [0, kend_w) visible to some row
+  const int minpos_w = pos0 + row0;                           // the wave's first query position
+  const int nsub = wave_live ? (kend_w + 31) >> 5 : 0;        // 32-key subtiles this wave processes
+  const int myrow = row0 + c;
+  const bool row_ok = myrow < qlen;
+  const int mypos = row_ok ? pos0 + myrow : ctx - 1;  // rows past the prompt attend like the last one
+
+  bf16x8 qf[8];
+  if (row_ok) {
+    const bf16* qp = q + ((long long)(qstart + myrow) * Hq + head) * D + 64 * hh;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) qf[kk] = ld16(qp + 8 * kk);
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) qf[kk] = zero8();
+  }
+  f32x16 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
+  float m = -INFINITY, lsum = 0.f;
+
+  // tile staging (see attn_prefill_m32_kernel): 2 x 16 B of K and of V per thread, block ids one tile ahead
+  const int ck = threadIdx.x >> 4, pk = (threadIdx.x & 15) * 8;
+  const int dv = threadIdx.x >> 3, tv8 = 8 * (threadIdx.x & 7);
+  const long long kvoff = (long long)kvh * BS * D;
+  const size_t bstride = (size_t)Hkv * BS * D;
+  const int last = ctx - 1;
+  const int ntiles = (kend_wg + 63) / 64;
+  struct Ids { int k0, k1, v; };
+  struct Stage { uint4 k0, k1, v0, v1; };
+  auto fetch_ids = [&](int t0) {
+    return Ids{bt[min(t0 + ck, last) >> bs_shift], bt[min(t0 + ck + KROWS, last) >> bs_shift],
+               bt[min(t0 + tv8, last) >> bs_shift]};
+  };
+  // per-thread constant parts of the K / V addresses (elements)
+  const bf16* kbase = k_cache + kvoff + pk;
+  const bf16* vbase = v_cache + kvoff + (long long)dv * BS;
+  auto issue = [&](int t0, const Ids& id) {
+    const int k0 = min(t0 + ck, last), k1 = min(t0 + ck + KROWS, last), v0 = min(t0 + tv8, last & ~7);
+    Stage st;
+    st.k0 = *reinterpret_cast<const uint4*>(kbase + (size_t)(unsigned)id.k0 * bstride + ((k0 & bs_mask) << 7));
+    st.k1 = *reinterpret_cast<const uint4*>(kbase + (size_t)(unsigned)id.k1 * bstride + ((k1 & bs_mask) << 7));
+    const bf16* vb = vbase + (size_t)(unsigned)id.v * bstride + (v0 & bs_mask);
+    st.v0 = *reinterpret_cast<const uint4*>(vb);
+    st.v1 = *reinterpret_cast<const uint4*>(vb + VROWS * BS);
+    return st;
+  };
+  auto store = [&](int t, const Stage& st) {
+    bf16* sk = smem + (t % 3) * TILE_ELEMS;
+    bf16* sv = sk + 64 * KST;
+    *reinterpret_cast<uint4*>(sk + ck * KST + pk) = st.k0;
+    *reinterpret_cast<uint4*>(sk + (ck + KROWS) * KST + pk) = st.k1;
+    *reinterpret_cast<uint4*>(sv + dv * VST + tv8) = st.v0;
+    *reinterpret_cast<uint4*>(sv + (dv + VROWS) * VST + tv8) = st.v1;
+  };
+
+  // prologue: tiles 0 and 1 loaded together (one memory round trip), tile 2's loads in flight
+  Stage stg;
+  Ids ids;
+  if (ntiles > 0) {
+    const Ids i0 = fetch_ids(0), i1 = fetch_ids(ntiles > 1 ? 64 : 0);
+    stg = issue(0, i0);
+    Stage s1;
+    if (ntiles > 1) s1 = issue(64, i1);
+    if (ntiles > 2) ids = fetch_ids(128);
+    store(0, stg);
+    if (ntiles > 1) store(1, s1);
+  }
+  __syncthreads();
+  if (ntiles > 2) {
+    stg = issue(128, ids);
+    if (ntiles > 3) ids = fetch_ids(192);
+  }
+
+  f32x16 sa, sb;  // scores of the current / next subtile (named: static register allocation)
+  float tmax = -INFINITY;
+  if (nsub > 0) {
+    s_subtile(smem, qf, sa);
+    tmax = subtile_max(sa, scale_log2);
+  }
+
+  // one subtile step: j = 2 it + ST, current scores in SC, next into SN
+#define SUBTILE_STEP(ST, SC, SN)                                                                          \
+  do {                                                                                                    \
+    const int j = 2 * it + (ST);                                                                          \
+    if (j < nsub) {                                                                                       \
+      if (32 * j + 31 > minpos_w) { /* diagonal / context-end subtile: mask, then its true max */         \
+        mask_subtile(SC, 32 * j, mypos);                                                                  \
+        tmax = subtile_max(SC, scale_log2);                                                               \
+      }                                                                                                   \
+      if (!__all(tmax <= m + kRescaleThr)) {                                                              \
+        const float mn = fmaxf(m, tmax);                                                                  \
+        const float alpha = __builtin_amdgcn_exp2f(m - mn); /* first subtile: m = -inf, alpha = 0 */      \
+        m = mn;                                                                                           \
+        lsum *= alpha;                                                                                    \
+        _Pragma("unroll") for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;                                  \
+      }                                                                                                   \
+      /* branch-free from here: S(j+1) unconditionally (past the wave's last subtile it is an unused */   \
+      /* stale-LDS product) so the exps of S(j) interleave with its MFMAs, and S(j+1)'s row max with */   \
+      /* the P.V MFMAs (an upper bound until a masked subtile recomputes it above) */                    \
+      s_subtile((ST) == 0 ? cur_k + 32 * KST : nxt_k, qf, SN);                                            \
+      Pack8 pf[2];                                                                                        \
+      float psum = 0.f;                                                                                   \
+      _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                                    \
+        const float p = __builtin_amdgcn_exp2f(fmaf(SC[i], scale_log2, -m));                              \
+        psum += p;                                                                                        \
+        pf[i >> 3].h[i & 7] = (bf16)p;                                                                    \
+      }                                                                                                   \
+      lsum += psum;                                                                                       \
+      _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                                    \
+        _Pragma("unroll") for (int dt = 0; dt < 4; ++dt) {                                                \
+          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(cur_v + (32 * dt + c) * VST + 32 * (ST) +    \
+                                                             16 * ks + 8 * hh);                           \
+          o[dt] = mfma32(vf, pf[ks].v, o[dt]);                                                            \
+        }                                                                                                 \
+      tmax = subtile_max(SN, scale_log2);                                                                 \
+    }                                                                                                     \
+  } while (0)
+
+  for (int it = 0; it < ntiles; ++it) {
+    const bf16* cur_k = smem + (it % 3) * TILE_ELEMS;
+    const bf16* cur_v = cur_k + 64 * KST;
+    const bf16* nxt_k = smem + ((it + 1) % 3) * TILE_ELEMS;
+    SUBTILE_STEP(0, sa, sb);
+    SUBTILE_STEP(1, sb, sa);
+    if (it + 2 < ntiles) store(it + 2, stg);
+    __syncthreads();
+    if (it + 3 < ntiles) {
+      stg = issue(64 * (it + 3), ids);
+      if (it + 4 < ntiles) ids = fetch_ids(64 * (it + 4));
+    }
+  }
+#undef SUBTILE_STEP
+  const float l = xhalf_sum(lsum);
+  if (!row_ok) return;
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  bf16* op = out + ((long long)(qstart + myrow) * Hq + head) * D + 4 * hh;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (bf16)(o[dt][4 * g + e] * inv);
+      *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * g) = v;
+    }
+}
+
 }  // namespace
 
 void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,
@@ -545,11 +761,19 @@ void launch_attn_prefill(const bf16* q, const bf16* k_cache, const bf16* v_cache
   if (num_tiles == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
   const int G = Hq / Hkv;
-  // A/B knob SYMMETRY_ATTN_PREFILL: "lds" = the 16x16x32 LDS kernel, "w4" = 4-wave 32-row workgroups,
-  // "prio" = static s_setprio(1) for the second half of the waves (cdna_hip_programming.md T5)
+  // A/B knob SYMMETRY_ATTN_PREFILL: "lds" = the 16x16x32 LDS kernel, "m32np" = the 32x32 kernel without
+  // the subtile software pipeline, "w4" = its 4-wave 32-row workgroups, "prio" = its static s_setprio(1)
+  // for the second half of the waves (cdna_hip_programming.md T5)
   static const char* knob = getenv("SYMMETRY_ATTN_PREFILL");
   static const bool use_lds = knob && strstr(knob, "lds"), w4 = knob && strstr(knob, "w4");
   static const int prio = (knob && strstr(knob, "prio")) ? 1 : 0;
+  static const bool nopipe = knob && strstr(knob, "m32np");
+  if (!use_lds && !nopipe && !w4 && !prio && BS >= 8 && (BS & (BS - 1)) == 0 && G % 4 == 0) {
+    attn_prefill_m32p_kernel<<<dim3(Hkv, num_tiles, G / 4), 512, 0, s>>>(
+        q, k_cache, v_cache, block_tables, ctx_lens, cu_q, tiles, out, Hq, Hkv, __builtin_ctz(BS), max_blocks,
+        scale_log2);
+    return;
+  }
   if (!use_lds && BS % 8 == 0 && G % 4 == 0) {
     if (w4)
       attn_prefill_m32_kernel<4><<<dim3(num_tiles, Hkv, G / 2), 256, 0, s>>>(

@@ -179,6 +179,10 @@ class ModelRunner:
             tiles = []
             for i, n in enumerate(counts):
                 tiles.extend((i, r) for r in range(0, n, 64))
+            # heaviest first (keys visible to the tile's last row): the causal tail of a long prompt starts
+            # in the first wave of attention workgroups instead of finishing last
+            if len(tiles) > 1:
+                tiles.sort(key=lambda t: -(ctx[t[0]] - counts[t[0]] + min(t[1] + 64, counts[t[0]])))
             host[lay.tiles:lay.tiles + 2 * len(tiles)] = np.asarray(tiles, dtype=np.int32).reshape(-1)
             host[lay.last:lay.last + 2 * lay.nseq] = (cu[1:] - 1).astype(np.int64).view(np.int32)
 
