@@ -149,7 +149,8 @@ void check_cache(const Tensor& k_cache, const Tensor& v_cache) {
   check_dtype(k_cache, at::kBFloat16, "k_cache");
   check_dtype(v_cache, at::kBFloat16, "v_cache");
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(3) == 128, "attention kernels require head_dim == 128");
-  TORCH_CHECK(k_cache.size(2) % 32 == 0, "attention kernels require block_size % 32 == 0");
+  TORCH_CHECK(k_cache.size(2) % 32 == 0 && (k_cache.size(2) & (k_cache.size(2) - 1)) == 0,
+              "attention kernels require a power-of-two block_size >= 32");
   TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(2) == 128 && v_cache.size(3) == k_cache.size(2),
               "v_cache must be [NB, Hkv, D, BS]");
 }

@@ -70,12 +70,13 @@ SYM_DEV void compute_group(const KVFrag& f, const bf16x8 (&qf)[4], float scale_l
   gmax = fmaxf(gmax, __shfl_xor(gmax, 32, 64));
   const float m_new = fmaxf(m, gmax);
   // m_new == -inf only if this column saw no visible token yet (causal prefill rows); keep zeros.
-  const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m - m_new);
+  // raw v_exp_f32 (the ocml exp2f adds a denormal range reduction softmax does not need)
+  const float alpha = (m_new == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m - m_new);
   Pack8 pf;
   float psum = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float p = (m_new == -INFINITY) ? 0.f : exp2f(x[j] - m_new);
+    const float p = (m_new == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(x[j] - m_new);
     psum += p;
     pf.h[j] = (bf16)p;
   }
@@ -247,7 +248,8 @@ SYM_DEV void attn_decode_unit(const bf16* __restrict__ q, const bf16* __restrict
   // fetched (in-bounds: clamped to the row) but never dereferenced.
   const int* bt = block_tables + (long long)seq * max_blocks;
   const int tok0 = part * PART + wid * 64;
-  const int bi0 = min(tok0 / BS, max_blocks - 1), bi1 = min((tok0 + 32) / BS, max_blocks - 1);
+  const int bsh = __builtin_ctz(BS);  // block sizes are powers of two (launchers check)
+  const int bi0 = min(tok0 >> bsh, max_blocks - 1), bi1 = min((tok0 + 32) >> bsh, max_blocks - 1);
   const int blk_pre0 = bt[bi0], blk_pre1 = bt[bi1];
   bf16x8 qf[4];
   load_q(q, seq, Hq, kvh, G, qf);
@@ -266,7 +268,7 @@ SYM_DEV void attn_decode_unit(const bf16* __restrict__ q, const bf16* __restrict
     if (g < ngroups) {
       const int tbase = tok0 + 32 * g;
       const long long blk = g == 0 ? blk_pre0 : blk_pre1;
-      const int boff = tbase % BS;
+      const int boff = tbase & (BS - 1);
       load_group(k_cache + ((blk * Hkv + kvh) * BS + boff) * D, v_cache + (blk * Hkv + kvh) * (long long)D * BS + boff,
                  BS, f[g]);
     }
@@ -300,13 +302,13 @@ SYM_DEV bool attn_fused_unit(const bf16* __restrict__ q, const bf16* __restrict_
   const int h = lane >> 4;
   const int* bt = block_tables + (long long)seq * max_blocks;
   const int tok0 = part * PART_F + wid * 32;
-  const int blk = bt[min(tok0 / BS, max_blocks - 1)];
+  const int blk = bt[min(tok0 >> __builtin_ctz(BS), max_blocks - 1)];
   const int ctx = ctx_lens[seq];
   if (part * PART_F >= ctx) return false;
   const bool has = tok0 < ctx;
   const bool newest = has && ctx - 1 < tok0 + 32;  // this wave's group holds the token written this step
-  const bf16* kb = k_cache + (((long long)blk * Hkv + kvh) * BS + tok0 % BS) * D;
-  const bf16* vb = v_cache + ((long long)blk * Hkv + kvh) * (long long)D * BS + tok0 % BS;
+  const bf16* kb = k_cache + (((long long)blk * Hkv + kvh) * BS + (tok0 & (BS - 1))) * D;
+  const bf16* vb = v_cache + ((long long)blk * Hkv + kvh) * (long long)D * BS + (tok0 & (BS - 1));
   KVFrag f;
   if (has && !newest) load_group(kb, vb, BS, f);  // bytes no workgroup of this launch writes
   wait();
