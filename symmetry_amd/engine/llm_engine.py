@@ -57,6 +57,7 @@ class EngineConfig:
     decode_weights: str = "auto"         # "preshuffled" | "shared" | "auto": extra MFMA-ordered decode copies
     persistent_mlp: bool = False         # O -> gate_up -> down as one persistent launch (measured slower: profiles/)
     fused_attn_block: bool = False       # QKV -> attention -> O as one launch per layer (decode_block)
+    enable_prefix_caching: bool = True   # adopt cached KV blocks of a known prompt prefix (multi-turn chats)
     model_config: ModelConfig | None = None
 
     @classmethod
@@ -72,10 +73,14 @@ class EngineConfig:
              "device": "device",
              "useGraphs": "use_graphs", "numKvBlocks": "num_kv_blocks", "decodeWeights": "decode_weights",
              "prefillChunk": "mixed_prefill_tokens",
-             "persistentMlp": "persistent_mlp", "fusedAttnBlock": "fused_attn_block"}
+             "persistentMlp": "persistent_mlp", "fusedAttnBlock": "fused_attn_block",
+             "enablePrefixCaching": "enable_prefix_caching"}
         for k, attr in m.items():
             if cfg.get(k) is not None:
-                setattr(ec, attr, type(getattr(ec, attr))(cfg[k]) if getattr(ec, attr) is not None else cfg[k])
+                cur, val = getattr(ec, attr), cfg[k]
+                if isinstance(cur, bool) and isinstance(val, str):  # env overrides arrive as strings
+                    val = val.strip().lower() in ("1", "true", "yes", "on")
+                setattr(ec, attr, type(cur)(val) if cur is not None else val)
         for k, v in overrides.items():
             setattr(ec, k, v)
         return ec
@@ -127,7 +132,7 @@ class LLMEngine:
         nb = cfg.num_kv_blocks or self._auto_blocks(max_model_len)
         self.kv = KVCache(mcfg.num_layers, nb, mcfg.num_kv_heads // cfg.tp_size, mcfg.head_dim, cfg.block_size,
                           self.device)
-        self.blocks = BlockManager(nb, cfg.block_size)
+        self.blocks = BlockManager(nb, cfg.block_size, prefix_caching=cfg.enable_prefix_caching)
         self.scheduler = Scheduler(
             SchedulerConfig(max_num_seqs=min(cfg.max_num_seqs, 64 if self.device.type != "cpu" else cfg.max_num_seqs),
                             max_num_batched_tokens=cfg.max_num_batched_tokens, max_model_len=max_model_len,
@@ -291,6 +296,9 @@ class LLMEngine:
             for seq, n, keep in zip(batch.seqs, batch.num_new_tokens, batch.sample):
                 seq.num_computed += n
                 seq.num_pending += int(keep)
+                if batch.kind == "prefill" and n > 1:
+                    # prompt blocks completed by this (enqueued) step become adoptable by later arrivals
+                    self.blocks.register(seq)
         return {"batch": batch, "handle": handle, "t0": t0}
 
     def _complete(self, fl: dict, t_launch: float) -> list[RequestOutput]:

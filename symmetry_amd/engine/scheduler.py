@@ -19,16 +19,42 @@ from .sequence import Sequence, SeqStatus
 
 
 class BlockManager:
-    def __init__(self, num_blocks: int, block_size: int, reserved: int = 1):
+    """Paged KV block pool with optional automatic prefix caching.
+
+    Prefix caching (vLLM-style, block granular): a FULL block whose KV has been computed is registered
+    under the hash chain of the token ids it holds (``hash(parent_hash, tokens)``), so the identity of
+    a block covers its whole prefix.  A new sequence adopts the longest run of cached blocks matching
+    its prompt (reference counts: shared blocks are read-only, a sequence only ever writes positions
+    >= its ``num_computed``, i.e. past the adopted blocks), and skips their prefill.  A released block
+    that holds registered content goes to an LRU list instead of the free list: it stays adoptable
+    until the allocator runs out of never-used blocks and evicts it.  This is what makes a chat
+    provider fast on multi-turn conversations: the reference's clients resend the whole message list
+    every turn (``src/provider.ts:312-316``), so each turn's prompt starts with the previous turn's
+    prompt + answer.  KV writes and reads are ordered on the engine's stream, so a block released with
+    a write still in flight is reused only by later launches.
+    """
+
+    def __init__(self, num_blocks: int, block_size: int, reserved: int = 1, prefix_caching: bool = False):
         # block 0 is reserved as the scratch block of padded (graph) batch rows
         self.block_size = block_size
         self.num_blocks = num_blocks
         self.free = collections.deque(range(reserved, num_blocks))
         self.reserved = reserved
+        self.prefix_caching = prefix_caching
+        self.ref = [0] * num_blocks
+        self.block_hash: dict[int, int] = {}        # block -> content hash (registered blocks)
+        self.cached: dict[int, int] = {}            # content hash -> block
+        self.evictable: collections.OrderedDict[int, None] = collections.OrderedDict()  # ref 0, LRU order
+        self.hit_tokens = 0
+        self.query_tokens = 0
 
     @property
     def num_free(self) -> int:
-        return len(self.free)
+        return len(self.free) + len(self.evictable)
+
+    def utilization(self) -> float:
+        usable = self.num_blocks - self.reserved
+        return 1.0 - self.num_free / max(1, usable)
 
     def blocks_needed(self, seq: Sequence, num_tokens: int) -> int:
         need = (num_tokens + self.block_size - 1) // self.block_size
@@ -37,20 +63,79 @@ class BlockManager:
     def can_grow(self, seq: Sequence, num_tokens: int) -> bool:
         return self.blocks_needed(seq, num_tokens) <= self.num_free
 
+    def _alloc(self) -> int:
+        if self.free:
+            b = self.free.popleft()
+        else:  # evict the least recently released cached block
+            b, _ = self.evictable.popitem(last=False)
+            del self.cached[self.block_hash.pop(b)]
+        self.ref[b] = 1
+        return b
+
     def grow(self, seq: Sequence, num_tokens: int) -> None:
         n = self.blocks_needed(seq, num_tokens)
         if n > self.num_free:
             raise MemoryError("out of KV blocks")
         for _ in range(n):
-            seq.block_table.append(self.free.popleft())
+            seq.block_table.append(self._alloc())
+
+    # ---- prefix caching ------------------------------------------------------------------------
+    def _chain(self, tokens: list, nblocks: int):
+        bs, h = self.block_size, 0
+        for i in range(nblocks):
+            h = hash((h, tuple(tokens[i * bs:(i + 1) * bs])))
+            yield i, h
+
+    def match_prefix(self, seq: Sequence) -> int:
+        """Adopt the cached blocks of the longest matching full-block prefix of a sequence that has no
+        KV yet; returns the number of tokens whose prefill is skipped.  At least one prompt token is
+        always left to compute (its logits give the first output token)."""
+        if not self.prefix_caching or seq.block_table or seq.num_computed:
+            return 0
+        tokens = seq.token_ids
+        target = seq.prefill_target
+        nfull = max(0, target - 1) // self.block_size  # >= 1 token left to prefill
+        self.query_tokens += target
+        for _, h in self._chain(tokens, nfull):
+            b = self.cached.get(h)
+            if b is None:
+                break
+            if self.ref[b] == 0:
+                self.evictable.pop(b, None)
+            self.ref[b] += 1
+            seq.block_table.append(b)
+        n = len(seq.block_table) * self.block_size
+        seq.num_computed = n
+        self.hit_tokens += n
+        return n
+
+    def register(self, seq: Sequence) -> None:
+        """Register the sequence's full blocks whose KV is computed and whose token ids are known."""
+        if not self.prefix_caching:
+            return
+        tokens = seq.token_ids
+        nfull = min(seq.num_computed, len(tokens)) // self.block_size
+        nfull = min(nfull, len(seq.block_table))
+        for i, h in self._chain(tokens, nfull):
+            b = seq.block_table[i]
+            if b in self.block_hash:       # already registered (adopted, or registered earlier)
+                continue
+            if h in self.cached:           # same content computed elsewhere: keep the first copy
+                continue
+            self.block_hash[b] = h
+            self.cached[h] = b
 
     def release(self, seq: Sequence) -> None:
-        self.free.extend(seq.block_table)
+        self.register(seq)
+        for b in seq.block_table:
+            self.ref[b] -= 1
+            if self.ref[b] > 0:
+                continue
+            if b in self.block_hash:
+                self.evictable[b] = None
+            else:
+                self.free.append(b)
         seq.block_table = []
-
-    def utilization(self) -> float:
-        usable = self.num_blocks - self.reserved
-        return 1.0 - self.num_free / max(1, usable)
 
 
 @dataclass
@@ -145,6 +230,8 @@ class Scheduler:
 
         def take(seq: Sequence) -> bool:
             nonlocal budget
+            if not seq.block_table and not seq.num_computed:
+                self.blocks.match_prefix(seq)  # adopt cached KV of a known prefix (no-op when disabled)
             remaining = seq.prefill_target - seq.num_computed
             n = min(remaining, budget) if self.cfg.enable_chunked_prefill else remaining
             if n <= 0 or n > budget:
