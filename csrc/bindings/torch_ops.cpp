@@ -179,7 +179,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, 
   const int64_t max_parts = tmp_o.size(2);
   TORCH_CHECK(tmp_ml.numel() >= S * Hq * max_parts * 2, "tmp_ml too small");
   const int64_t BS = k_cache.size(2), max_blocks = block_tables.size(1);
-  TORCH_CHECK(max_parts * 512 >= max_blocks * BS, "tmp_o has too few partitions for the block table span");
+  TORCH_CHECK(max_parts * 256 >= max_blocks * BS, "tmp_o has too few partitions for the block table span");
   check_gpu(counters, "counters");
   check_dtype(counters, at::kInt, "counters");
   TORCH_CHECK(counters.numel() >= S * Hkv, "counters must hold num_seqs * Hkv zero-initialised ints");

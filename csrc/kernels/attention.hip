@@ -17,8 +17,8 @@
 // contiguous bytes.  Softmax is online (running max / sum per query column),
 // in base 2 with the 1/sqrt(D)*log2(e) scale folded into one multiply.
 //
-// Decode (K5): grid (seq, kv_head, partition); 8 waves x 64 tokens = 512
-// tokens per partition; the G = Hq/Hkv query heads of a kv head are the MFMA
+// Decode (K5): grid (seq, kv_head, partition); 8 waves x 32 tokens = 256
+// tokens per partition (two workgroups resident per CU); the G = Hq/Hkv query heads of a kv head are the MFMA
 // columns (K/V are read once per kv head).  Multi-partition sequences write
 // fp32 partials that the last-arriving partition combines (split-KV,
 // flash-decoding, one launch).
@@ -40,7 +40,7 @@ namespace {
 // ---------------------------------------------------------------------------------------------
 // Decode (body: attn_decode.h, shared with the fused decode block launch)
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(DWAVES * 64) void attn_decode_kernel(
+__global__ __launch_bounds__(DWAVES * 64, 4) void attn_decode_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
     const int* __restrict__ block_tables, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
     float* __restrict__ tmp_o, float* __restrict__ tmp_ml, int* __restrict__ counters, int Hq, int Hkv, int BS,

@@ -8,7 +8,9 @@ namespace {
 
 constexpr int D = 128;
 constexpr int DWAVES = 8;            // waves per decode workgroup
-constexpr int PART = DWAVES * 64;    // tokens per decode partition: contexts <= 512 need no combine
+constexpr int PART = DWAVES * 32;    // tokens per decode partition (one 32-token group per wave): contexts
+                                     // <= 256 need no combine; ~120 VGPRs -> two workgroups per CU, so one
+                                     // unit's loads overlap another's finish (bench_attn_decode.py)
 
 SYM_DEV bf16x8 ld16(const bf16* p) {
   Pack8 pk;
@@ -194,20 +196,39 @@ SYM_DEV bool attn_finish(const f32x4 (&o)[8], float m, float lsum, int ctx, int 
   __syncthreads();
   if (!s_last) return false;
   if (active) {
+    // partials read 4 partitions at a time (40 independent loads in flight per batch) with an online
+    // max: one memory round trip per 4 partitions instead of a dependent load chain per partition
     M = -INFINITY;
-    for (int p = 0; p < nparts; ++p)
-      M = fmaxf(M, __hip_atomic_load(tmp_ml + (base + p) * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     L = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    for (int p = 0; p < nparts; ++p) {
-      const float mp = __hip_atomic_load(tmp_ml + (base + p) * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const float lp = __hip_atomic_load(tmp_ml + (base + p) * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const float f = exp2f(mp - M);
-      L += lp * f;
-      const float* po = tmp_o + (base + p) * D + d0;
+    for (int p0 = 0; p0 < nparts; p0 += 4) {
+      float mp[4], lp[4], vp[4][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += __hip_atomic_load(po + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * f;
+      for (int i = 0; i < 4; ++i) {
+        const int p = min(p0 + i, nparts - 1);  // duplicates past the end are masked below
+        mp[i] = __hip_atomic_load(tmp_ml + (base + p) * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lp[i] = __hip_atomic_load(tmp_ml + (base + p) * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float* po = tmp_o + (base + p) * D + d0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vp[i][j] = __hip_atomic_load(po + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      float mb = M;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (p0 + i < nparts) mb = fmaxf(mb, mp[i]);
+      const float fo = __builtin_amdgcn_exp2f(M - mb);  // M = -inf on the first batch: 0
+      L *= fo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] *= fo;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float f = p0 + i < nparts ? __builtin_amdgcn_exp2f(mp[i] - mb) : 0.f;
+        L += lp[i] * f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += vp[i][j] * f;
+      }
+      M = mb;
     }
     const float inv = 1.f / L;
 #pragma unroll
@@ -247,10 +268,9 @@ SYM_DEV void attn_decode_unit(const bf16* __restrict__ q, const bf16* __restrict
   // the K/V stream instead of three (ctx -> block table -> K/V).  Entries past the context are
   // fetched (in-bounds: clamped to the row) but never dereferenced.
   const int* bt = block_tables + (long long)seq * max_blocks;
-  const int tok0 = part * PART + wid * 64;
+  const int tok0 = part * PART + wid * 32;
   const int bsh = __builtin_ctz(BS);  // block sizes are powers of two (launchers check)
-  const int bi0 = min(tok0 >> bsh, max_blocks - 1), bi1 = min((tok0 + 32) >> bsh, max_blocks - 1);
-  const int blk_pre0 = bt[bi0], blk_pre1 = bt[bi1];
+  const int blk = bt[min(tok0 >> bsh, max_blocks - 1)];
   bf16x8 qf[4];
   load_q(q, seq, Hq, kvh, G, qf);
   const int ctx = ctx_lens[seq];
@@ -259,26 +279,12 @@ SYM_DEV void attn_decode_unit(const bf16* __restrict__ q, const bf16* __restrict
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, lsum = 0.f;
-  // Both 32-token groups of this wave are loaded before either is computed: one memory round trip
-  // (block table -> K/V) instead of one per group.
-  const int ngroups = tok0 >= ctx ? 0 : (tok0 + 32 >= ctx ? 1 : 2);
-  KVFrag f[2];
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    if (g < ngroups) {
-      const int tbase = tok0 + 32 * g;
-      const long long blk = g == 0 ? blk_pre0 : blk_pre1;
-      const int boff = tbase & (BS - 1);
-      load_group(k_cache + ((blk * Hkv + kvh) * BS + boff) * D, v_cache + (blk * Hkv + kvh) * (long long)D * BS + boff,
-                 BS, f[g]);
-    }
-  }
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    if (g < ngroups) {
-      const int tbase = tok0 + 32 * g;
-      compute_group(f[g], qf, scale_log2, [&](int a, int r) { return tbase + 8 * h + 4 * a + r < ctx; }, o, m, lsum);
-    }
+  if (tok0 < ctx) {
+    KVFrag f;
+    const int boff = tok0 & (BS - 1);
+    load_group(k_cache + (((long long)blk * Hkv + kvh) * BS + boff) * D,
+               v_cache + ((long long)blk * Hkv + kvh) * (long long)D * BS + boff, BS, f);
+    compute_group(f, qf, scale_log2, [&](int a, int r) { return tok0 + 8 * h + 4 * a + r < ctx; }, o, m, lsum);
   }
   attn_finish<GMAX, false>(o, m, lsum, ctx, PART, seq, kvh, part, Hq, Hkv, max_parts, out, tmp_o, tmp_ml, counters);
 }

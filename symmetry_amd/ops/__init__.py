@@ -86,7 +86,7 @@ def rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv,
     return reference.rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, perm)
 
 
-ATTN_DECODE_PART = 512  # context tokens per split-KV partition of attn_decode (csrc/kernels/attention.hip)
+ATTN_DECODE_PART = 256  # context tokens per split-KV partition of attn_decode (csrc/kernels/attn_decode.h PART)
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters, scale):
