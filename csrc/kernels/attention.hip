@@ -40,12 +40,15 @@ namespace {
 // ---------------------------------------------------------------------------------------------
 // Decode (body: attn_decode.h, shared with the fused decode block launch)
 // ---------------------------------------------------------------------------------------------
+// GMAX >= G query heads per kv head: the cross-wave merge stages GMAX columns in LDS (GMAX = 4 for
+// Llama-3 GQA: 17 KB instead of 68 KB, so LDS no longer caps the resident workgroups per CU)
+template <int GMAX>
 __global__ __launch_bounds__(DWAVES * 64, 4) void attn_decode_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
     const int* __restrict__ block_tables, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
     float* __restrict__ tmp_o, float* __restrict__ tmp_ml, int* __restrict__ counters, int Hq, int Hkv, int BS,
     int max_blocks, int max_parts, float scale_log2) {
-  attn_decode_unit<16>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters, Hq, Hkv, BS,
+  attn_decode_unit<GMAX>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters, Hq, Hkv, BS,
                        max_blocks, max_parts, scale_log2, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
@@ -751,8 +754,16 @@ void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache,
   if (num_seqs == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(num_seqs, Hkv, max_parts);
-  attn_decode_kernel<<<grid, DWAVES * 64, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters,
-                                          Hq, Hkv, BS, max_blocks, max_parts, scale_log2);
+  const int G = Hq / Hkv;
+  if (G <= 4)
+    attn_decode_kernel<4><<<grid, DWAVES * 64, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml,
+                                                       counters, Hq, Hkv, BS, max_blocks, max_parts, scale_log2);
+  else if (G <= 8)
+    attn_decode_kernel<8><<<grid, DWAVES * 64, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml,
+                                                       counters, Hq, Hkv, BS, max_blocks, max_parts, scale_log2);
+  else
+    attn_decode_kernel<16><<<grid, DWAVES * 64, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml,
+                                                        counters, Hq, Hkv, BS, max_blocks, max_parts, scale_log2);
 }
 
 void launch_attn_prefill(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,
