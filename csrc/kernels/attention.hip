@@ -25,9 +25,10 @@
 // The grid is sized for the max context so the launch is hipGraph-capturable;
 // partitions past a sequence's context exit at once.
 //
-// Prefill (K4): grid (q tile, kv_head * G); each wave owns 16 query rows of
-// one head, causal + varlen + chunked prefill (queries are the LAST qlen
+// Prefill (K4): causal + varlen + chunked prefill (queries are the LAST qlen
 // positions of a context of length ctx), reading K/V from the paged cache.
+// Default: attn_prefill_m32p_kernel (32x32x16 MFMA, GQA heads share K/V tiles,
+// see its comment); the 16x16 kernels remain for GQA groups of 1/2 heads.
 #include <stdlib.h>
 #include <string.h>
 
@@ -286,8 +287,7 @@ __global__ __launch_bounds__(128 * HPW) void attn_prefill_lds_kernel(
 // from the paged cache once per workgroup and double-buffered through LDS), with the per-wave math
 // re-tiled for v_mfma_f32_32x32x16_bf16 (cdna_hip_programming.md §3, T12-T14):
 //   * a wave owns 32 query rows of one head; per 64-key tile it issues 16 S^T MFMAs and 16 P.V MFMAs
-//     (32 cycles each) and runs ONE online-softmax update over 32 scores per lane (the 16x16 kernel
-//     pays two updates, four cross-lane shuffles and two O rescales per 64 keys);
+//     (32 cycles each); the online softmax runs per 32-key subtile over 16 scores per lane;
 //   * S^T = K . Q^T with the K rows permuted (row r loads key r with bits 2 and 3 swapped) so that
 //     accumulator registers 8s..8s+7 of a lane hold 8 CONSECUTIVE keys: the bf16-packed accumulator
 //     is directly the B operand of O^T += V^T . P^T, and the matching V^T fragment is one contiguous
@@ -302,8 +302,9 @@ __global__ __launch_bounds__(128 * HPW) void attn_prefill_lds_kernel(
 //     cast: relative precision unchanged);
 //   * the block-table reads of a tile are issued one tile ahead of its K/V loads (a dependent
 //     table -> K/V load pair per tile exposed ~2 memory latencies per iteration: 2.5x slower);
-//   * heavier tiles first: workgroup x takes tile (num_tiles - 1 - x), so the long causal rows of a
-//     sequence start in the first wave of workgroups instead of forming the tail.
+//   * heavier tiles first: the engine orders the tiles by visible keys, descending, and the grid has the
+//     kv head fastest, so the long causal rows of a sequence start in the first wave of workgroups
+//     instead of forming the tail (1x4096: 241 -> 162 us).
 // ---------------------------------------------------------------------------------------------
 SYM_DEV f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -321,219 +322,10 @@ SYM_DEV float xhalf_sum(float v) {
 
 constexpr float kRescaleThr = 8.f;  // T13 threshold, log2 units
 
-template <bool kMask>
-SYM_DEV void prefill_tile32(const bf16* __restrict__ sk, const bf16* __restrict__ sv, const bf16x8 (&qf)[8],
-                            float scale_log2, int t0, int mypos, f32x16 (&o)[4], float& m, float& lsum) {
-  const int lane = threadIdx.x & 63;
-  const int r = lane & 31, hh = lane >> 5;
-  const int pr = (r & 3) | ((r & 4) << 1) | ((r & 8) >> 1) | (r & 16);  // bits 2 <-> 3
-  f32x16 s[2];
-#pragma unroll
-  for (int st = 0; st < 2; ++st) {
-    const bf16* kr = sk + (32 * st + pr) * KST + 64 * hh;
-    bf16x8 kf[8];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) kf[kk] = *reinterpret_cast<const bf16x8*>(kr + 8 * kk);
-    f32x16 acc = {};
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) acc = mfma32(kf[kk], qf[kk], acc);
-    s[st] = acc;
-  }
-  // register i of subtile st holds key t0 + 32 st + 16 (i >> 3) + 8 hh + (i & 7)
-  if constexpr (kMask) {
-#pragma unroll
-    for (int st = 0; st < 2; ++st)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int t = t0 + 32 * st + 16 * (i >> 3) + 8 * hh + (i & 7);
-        if (t > mypos) s[st][i] = -INFINITY;
-      }
-  }
-  float tmax = s[0][0];
-#pragma unroll
-  for (int i = 1; i < 16; ++i) tmax = fmaxf(tmax, s[0][i]);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, s[1][i]);
-  tmax = xhalf_max(tmax) * scale_log2;
-  if (__builtin_expect(!__all(tmax <= m + kRescaleThr), 0)) {
-    const float mn = fmaxf(m, tmax);
-    const float alpha = __builtin_amdgcn_exp2f(m - mn);  // m = -inf on the first tile: alpha = 0
-    m = mn;
-    lsum *= alpha;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
-  }
-  float psum = 0.f;
-#pragma unroll
-  for (int st = 0; st < 2; ++st) {
-    Pack8 pf[2];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float p = __builtin_amdgcn_exp2f(fmaf(s[st][i], scale_log2, -m));
-      psum += p;
-      pf[i >> 3].h[i & 7] = (bf16)p;
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(sv + (32 * dt + r) * VST + 32 * st + 16 * ks + 8 * hh);
-        o[dt] = mfma32(vf, pf[ks].v, o[dt]);
-      }
-    }
-  }
-  lsum += psum;
-}
-
-// NW = 8: the workgroup covers 64 query rows (two row halves) of 4 heads; NW = 4: 32 rows (the
-// half is blockIdx.z & 1), so two workgroups share a CU and their barriers interleave.
-template <int NW>
-__global__ __launch_bounds__(NW * 64, 2) void attn_prefill_m32_kernel(
-    const bf16* __restrict__ q, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
-    const int* __restrict__ block_tables, const int* __restrict__ ctx_lens, const int* __restrict__ cu_q,
-    const int* __restrict__ tiles, bf16* __restrict__ out, int Hq, int Hkv, int BS, int max_blocks,
-    float scale_log2, int prio) {
-  constexpr int HPW = 4, NT = NW * 64, CH = 1024 / NT;  // 16-B chunks per thread per K (and V) tile
-  static_assert(CH == 2 || CH == 4, "2 or 4 staging chunks");
-  constexpr int KROWS = NT / 16, VROWS = NT / 8;          // tile rows one pass of the workgroup covers
-  __shared__ bf16 sK[2][64 * KST];
-  __shared__ bf16 sV[2][D * VST];
-  const int tile = gridDim.x - 1 - blockIdx.x, kvh = blockIdx.y;
-  const int G = Hq / Hkv;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int c = lane & 31, hh = lane >> 5;
-  const int slice = NW == 8 ? blockIdx.z : blockIdx.z >> 1;
-  const int head = kvh * G + slice * HPW + wid % HPW;
-  const int half = NW == 8 ? wid / HPW : (blockIdx.z & 1);
-  if (prio && __builtin_amdgcn_readfirstlane(wid) >= NW / 2) __builtin_amdgcn_s_setprio(1);
-  const int seq = tiles[2 * tile], qrow0 = tiles[2 * tile + 1];
-  const int qstart = cu_q[seq], qlen = cu_q[seq + 1] - qstart;
-  const int ctx = ctx_lens[seq];
-  const int pos0 = ctx - qlen;
-  const int* bt = block_tables + (long long)seq * max_blocks;
-  const int row0 = qrow0 + 32 * half;
-  const int kend_wg = NW == 8 ? min(ctx, pos0 + min(qrow0 + 64, qlen)) : min(ctx, pos0 + min(row0 + 32, qlen));
-  if (NW == 4 && row0 >= qlen) return;  // whole workgroup past the prompt (uniform)
-  const bool wave_live = row0 < qlen;
-  const int kend_w = min(ctx, pos0 + min(row0 + 32, qlen));  // keys [0, kend_w) visible to some row
-  const int minpos_w = pos0 + row0;                           // the wave's first query position
-  const int myrow = row0 + c;
-  const bool row_ok = myrow < qlen;
-  const int mypos = row_ok ? pos0 + myrow : ctx - 1;  // rows past the prompt attend like the last one
-
-  bf16x8 qf[8];
-  if (row_ok) {
-    const bf16* qp = q + ((long long)(qstart + myrow) * Hq + head) * D + 64 * hh;
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) qf[kk] = ld16(qp + 8 * kk);
-  } else {
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) qf[kk] = zero8();
-  }
-  f32x16 o[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
-  float m = -INFINITY, lsum = 0.f;
-
-  // Cooperative tile staging: CH x 16 B of K and of V per thread.  The paged-cache block ids of a tile
-  // are fetched one tile AHEAD of its K/V loads, so issuing those loads never waits on a block-table
-  // read.  Keys past the context read the block of the last key (finite: the cache is zero-initialised
-  // and only ever written with finite K/V; masked anyway).
-  uint4 rk0, rk1, rk2, rk3, rv0, rv1, rv2, rv3;  // named registers (an array here lands in scratch)
-  int ik0, ik1, ik2, ik3, iv;
-  const int ck = threadIdx.x >> 4, pk = (threadIdx.x & 15) * 8;  // K: token ck + KROWS j, piece pk
-  const int dv = threadIdx.x >> 3, tv8 = 8 * (threadIdx.x & 7);   // V: dim dv + VROWS j, tokens tv8..+7
-  const long long kvoff = (long long)kvh * BS * D, bstride = (long long)Hkv * BS * D;
-  const int last = ctx - 1;
-  const int ntiles = (kend_wg + 63) / 64;
-  auto kid = [&](int t0, int j) { return bt[min(t0 + ck + KROWS * j, last) / BS]; };
-  auto kld = [&](int t0, int j, int ib) {
-    const int kt = min(t0 + ck + KROWS * j, last);
-    return *reinterpret_cast<const uint4*>(k_cache + ib * bstride + kvoff + (long long)(kt % BS) * D + pk);
-  };
-  auto vld = [&](int t0, int j) {
-    const int vt = min(t0 + tv8, last & ~7);
-    return *reinterpret_cast<const uint4*>(v_cache + iv * bstride + kvoff + (long long)(dv + VROWS * j) * BS +
-                                           vt % BS);
-  };
-#define FETCH_IDS(t0)                            \
-  do {                                           \
-    ik0 = kid(t0, 0);                            \
-    ik1 = kid(t0, 1);                            \
-    if constexpr (CH > 2) ik2 = kid(t0, 2);      \
-    if constexpr (CH > 2) ik3 = kid(t0, 3);      \
-    iv = bt[min((t0) + tv8, last) / BS];         \
-  } while (0)
-#define ISSUE(t0)                                               \
-  do {                                                          \
-    rk0 = kld(t0, 0, ik0);                                      \
-    rk1 = kld(t0, 1, ik1);                                      \
-    if constexpr (CH > 2) rk2 = kld(t0, 2, ik2);                \
-    if constexpr (CH > 2) rk3 = kld(t0, 3, ik3);                \
-    rv0 = vld(t0, 0);                                           \
-    rv1 = vld(t0, 1);                                           \
-    if constexpr (CH > 2) rv2 = vld(t0, 2);                     \
-    if constexpr (CH > 2) rv3 = vld(t0, 3);                     \
-  } while (0)
-#define ST1(buf, j, rkj, rvj)                                                        \
-  do {                                                                               \
-    *reinterpret_cast<uint4*>(&sK[buf][(ck + KROWS * (j)) * KST + pk]) = rkj;        \
-    *reinterpret_cast<uint4*>(&sV[buf][(dv + VROWS * (j)) * VST + tv8]) = rvj;       \
-  } while (0)
-#define STORE_TILE(buf)                              \
-  do {                                               \
-    ST1(buf, 0, rk0, rv0);                           \
-    ST1(buf, 1, rk1, rv1);                           \
-    if constexpr (CH > 2) ST1(buf, 2, rk2, rv2);     \
-    if constexpr (CH > 2) ST1(buf, 3, rk3, rv3);     \
-  } while (0)
-
-  if (ntiles > 0) {
-    FETCH_IDS(0);
-    ISSUE(0);
-    if (ntiles > 1) FETCH_IDS(64);
-    STORE_TILE(0);
-  }
-  __syncthreads();
-  for (int it = 0; it < ntiles; ++it) {
-    const int t0 = it * 64;
-    if (it + 1 < ntiles) {
-      ISSUE(t0 + 64);
-      if (it + 2 < ntiles) FETCH_IDS(t0 + 128);
-    }
-    if (wave_live && t0 < kend_w) {
-      if (t0 + 63 > minpos_w)
-        prefill_tile32<true>(sK[it & 1], sV[it & 1], qf, scale_log2, t0, mypos, o, m, lsum);
-      else
-        prefill_tile32<false>(sK[it & 1], sV[it & 1], qf, scale_log2, t0, mypos, o, m, lsum);
-    }
-    if (it + 1 < ntiles) STORE_TILE((it + 1) & 1);
-    __syncthreads();
-  }
-#undef FETCH_IDS
-#undef ISSUE
-#undef ST1
-#undef STORE_TILE
-  const float l = xhalf_sum(lsum);
-  if (!row_ok) return;
-  const float inv = l > 0.f ? 1.f / l : 0.f;
-  // O^T[dt] register i of lane (c, hh): dim 32 dt + 8 (i >> 2) + 4 hh + (i & 3), query row c
-  bf16* op = out + ((long long)(qstart + myrow) * Hq + head) * D + 4 * hh;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      bf16x4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (bf16)(o[dt][4 * g + e] * inv);
-      *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * g) = v;
-    }
-}
-
 
 // ---------------------------------------------------------------------------------------------
 // Prefill, 32x32x16 MFMA, software-pipelined per 32-key subtile (K4 default).
-// Same workgroup / wave decomposition and operand tricks as attn_prefill_m32_kernel, restructured so
+// Same workgroup / wave decomposition and operand tricks as described above, restructured so
 // that a wave's VALU work hides under its own MFMAs: the online-softmax update is per 32-key subtile
 // and the loop body for subtile j is
 //     [rescale decision for j]  ->  S(j+1) = K . Q^T MFMAs  ||  exp2 / bf16 pack / row-sum of S(j)
@@ -619,7 +411,10 @@ __global__ __launch_bounds__(512, 2) void attn_prefill_m32p_kernel(
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
   float m = -INFINITY, lsum = 0.f;
 
-  // tile staging (see attn_prefill_m32_kernel): 2 x 16 B of K and of V per thread, block ids one tile ahead
+  // Cooperative tile staging: 2 x 16 B of K and of V per thread.  The paged-cache block ids of a tile are
+  // fetched one tile AHEAD of its K/V loads, so issuing those loads never waits on a block-table read.
+  // Keys past the context read the block of the last key (finite: the cache is zero-initialised and only
+  // ever written with finite K/V; masked anyway).
   const int ck = threadIdx.x >> 4, pk = (threadIdx.x & 15) * 8;
   const int dv = threadIdx.x >> 3, tv8 = 8 * (threadIdx.x & 7);
   const long long kvoff = (long long)kvh * BS * D;
@@ -772,26 +567,13 @@ void launch_attn_prefill(const bf16* q, const bf16* k_cache, const bf16* v_cache
   if (num_tiles == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
   const int G = Hq / Hkv;
-  // A/B knob SYMMETRY_ATTN_PREFILL: "lds" = the 16x16x32 LDS kernel, "m32np" = the 32x32 kernel without
-  // the subtile software pipeline, "w4" = its 4-wave 32-row workgroups, "prio" = its static s_setprio(1)
-  // for the second half of the waves (cdna_hip_programming.md T5)
+  // A/B knob SYMMETRY_ATTN_PREFILL=lds: the previous 16x16x32 LDS kernel (profiles/attn_prefill_r1.jsonl)
   static const char* knob = getenv("SYMMETRY_ATTN_PREFILL");
-  static const bool use_lds = knob && strstr(knob, "lds"), w4 = knob && strstr(knob, "w4");
-  static const int prio = (knob && strstr(knob, "prio")) ? 1 : 0;
-  static const bool nopipe = knob && strstr(knob, "m32np");
-  if (!use_lds && !nopipe && !w4 && !prio && BS >= 8 && (BS & (BS - 1)) == 0 && G % 4 == 0) {
+  static const bool use_lds = knob && strstr(knob, "lds");
+  if (!use_lds && BS >= 8 && (BS & (BS - 1)) == 0 && G % 4 == 0) {
     attn_prefill_m32p_kernel<<<dim3(Hkv, num_tiles, G / 4), 512, 0, s>>>(
         q, k_cache, v_cache, block_tables, ctx_lens, cu_q, tiles, out, Hq, Hkv, __builtin_ctz(BS), max_blocks,
         scale_log2);
-    return;
-  }
-  if (!use_lds && BS % 8 == 0 && G % 4 == 0) {
-    if (w4)
-      attn_prefill_m32_kernel<4><<<dim3(num_tiles, Hkv, G / 2), 256, 0, s>>>(
-          q, k_cache, v_cache, block_tables, ctx_lens, cu_q, tiles, out, Hq, Hkv, BS, max_blocks, scale_log2, prio);
-    else
-      attn_prefill_m32_kernel<8><<<dim3(num_tiles, Hkv, G / 4), 512, 0, s>>>(
-          q, k_cache, v_cache, block_tables, ctx_lens, cu_q, tiles, out, Hq, Hkv, BS, max_blocks, scale_log2, prio);
     return;
   }
   if (BS % 8 == 0 && (G == 1 || G == 2 || G % 4 == 0)) {
