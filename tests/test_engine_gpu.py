@@ -177,3 +177,22 @@ def test_staggered_arrivals_mixed_steps_and_pipelining_match_oracle(gpu):
     for i, s in seqs.items():
         assert len(s.output_ids) == 14
         _agree(eng.weights, prompts[i], s.output_ids, tol=0.08)
+
+
+@pytest.mark.parametrize("model", ["small-llama", "tiny-mixtral"])
+def test_prefix_cache_multi_turn_on_gpu_matches_oracle(gpu, model):
+    """Multi-turn chat on the native path: turn 2 adopts turn 1's cached KV blocks (prompt + answer) and
+    prefills only the tail through the chunked-prefill attention kernel; outputs match the fp32 oracle."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+
+    eng = LLMEngine(EngineConfig(model=model, device="cuda:0", max_num_seqs=4, max_model_len=1024,
+                                 num_kv_blocks=64, block_size=32, use_graphs=True))
+    turn1 = eng.tokenizer.apply_chat_template([{"role": "user", "content": "tell me about the swarm " * 6}])
+    out1 = eng.generate(turn1, SamplingParams(max_tokens=24, ignore_eos=True))
+    turn2 = turn1 + out1 + eng.tokenizer.encode(" and now the provider")
+    hits0 = eng.blocks.hit_tokens
+    out2 = eng.generate(turn2, SamplingParams(max_tokens=12, ignore_eos=True))
+    assert eng.blocks.hit_tokens - hits0 >= (len(turn1) // 32) * 32
+    _agree(eng.weights, turn1, out1, tol=0.08)
+    _agree(eng.weights, turn2, out2, tol=0.08)
