@@ -349,3 +349,44 @@ def test_block_manager_prefix_match_leaves_one_token():
     assert bm.match_prefix(s3) == 8
     assert s3.block_table == [s1_b for s1_b in s2.block_table] + [s3.block_table[1]]
     assert bm.ref[s3.block_table[0]] == 2
+
+
+def test_randomized_soak_prefix_sharing_aborts_preemption():
+    """Random arrivals sharing prompt prefixes, random aborts, a KV pool small enough to force preemption
+    and LRU eviction of cached blocks: every finished sequence matches the fp32 oracle, every block and
+    reference count is returned at the end."""
+    import random
+
+    rnd = random.Random(7)
+    eng = _engine(num_kv_blocks=9, block_size=16, max_num_seqs=6)
+    bases = [_prompts(1, seed=30 + i, lo=40, hi=41)[0] for i in range(3)]
+    live, done, aborted, every = {}, [], set(), []
+    n = 0
+    for step in range(400):
+        if n < 16 and rnd.random() < 0.3:
+            p = list(rnd.choice(bases)) + [rnd.randrange(256) for _ in range(rnd.randrange(1, 20))]
+            s = eng.add_request(f"q{n}", p, SamplingParams(max_tokens=rnd.randrange(2, 12), ignore_eos=True))
+            live[f"q{n}"] = (p, s)
+            every.append(s)
+            n += 1
+        if live and rnd.random() < 0.05:
+            rid = rnd.choice(sorted(live))
+            eng.abort(rid)
+            aborted.add(rid)
+            live.pop(rid)
+        if eng.has_unfinished():
+            eng.step()
+        for rid, (p, s) in list(live.items()):
+            if s.status.finished:
+                done.append((p, s))
+                live.pop(rid)
+        if n >= 16 and not live and not eng.has_unfinished():
+            break
+    assert len(done) + len(aborted) == n and done
+    for p, s in done:
+        assert len(s.output_ids) == s.params.max_tokens
+        _agree(eng.weights, p, s.output_ids, tol=0.05)
+    assert all(r == 0 for r in eng.blocks.ref)
+    assert eng.blocks.num_free == eng.blocks.num_blocks - eng.blocks.reserved
+    assert eng.blocks.hit_tokens > 0
+    assert sum(s.num_preemptions for s in every) > 0
