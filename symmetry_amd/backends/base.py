@@ -30,7 +30,9 @@ class Backend:
     async def stop(self) -> None:
         pass
 
-    def stream(self, request: dict) -> AsyncIterator[Chunk]:  # pragma: no cover - interface
+    def stream(self, request: dict, scope: bytes = b"") -> AsyncIterator[Chunk]:  # pragma: no cover - interface
+        """Stream one chat request.  ``scope``: identity of the requesting client (the peer's public key);
+        backends that cache per-client state (the native engine's KV prefix cache) keep it per scope."""
         raise NotImplementedError
 
     def stats(self) -> dict:

@@ -56,7 +56,7 @@ class NativeBackend(Backend):
             await asyncio.to_thread(self.aengine.stop)
             self.aengine = None
 
-    async def stream(self, request: dict):
+    async def stream(self, request: dict, scope: bytes = b""):
         await self.start()
         messages = request.get("messages") or []
         if not isinstance(messages, list):
@@ -65,7 +65,7 @@ class NativeBackend(Backend):
         rid = f"chatcmpl-{next(_ids)}-{int(time.time() * 1000)}"
         created = int(time.time())
         first = True
-        async for out in self.aengine.generate(rid, messages=messages, params=params):
+        async for out in self.aengine.generate(rid, messages=messages, params=params, cache_scope=scope):
             if out.error:
                 raise BackendError(out.error)
             if out.text or first or out.finished:

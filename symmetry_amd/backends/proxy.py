@@ -51,7 +51,7 @@ class ProxyBackend(Backend):
             body.pop("messages")
         return url, headers, body
 
-    async def stream(self, request: dict):
+    async def stream(self, request: dict, scope: bytes = b""):
         await self.start()
         url, headers, body = self.build_stream_request(request.get("messages"))
         provider = str(self.cfg.get("apiProvider"))

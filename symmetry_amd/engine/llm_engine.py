@@ -191,9 +191,12 @@ class LLMEngine:
         return max(16, budget // per_block)
 
     def add_request(self, request_id: str, prompt_ids: list, params: SamplingParams | None = None,
-                    callback=None) -> Sequence:
+                    callback=None, cache_scope: bytes = b"") -> Sequence:
+        """``cache_scope``: prefix-cache namespace (the provider passes the client's public key, so one
+        client's conversation reuses only its own cached KV blocks)."""
         params = params or SamplingParams(max_tokens=self.cfg.default_max_tokens)
-        seq = Sequence(request_id, list(prompt_ids), params, eos_ids=tuple(self.model_cfg.eos_token_ids))
+        seq = Sequence(request_id, list(prompt_ids), params, eos_ids=tuple(self.model_cfg.eos_token_ids),
+                       cache_scope=bytes(cache_scope))
         if params.seed is not None:
             seq.sampling_seed = int(params.seed)
         else:
@@ -316,6 +319,7 @@ class LLMEngine:
         self._last_done = now
         self.metrics.on_step(batch.kind, len(batch.seqs), batch.num_tokens, dt, self.blocks.utilization(),
                              len(self.scheduler.waiting))
+        self.metrics.prefix_hits, self.metrics.prefix_queries = self.blocks.hit_tokens, self.blocks.query_tokens
         outs = []
         with self.lock:
             for seq, keep, tok in zip(batch.seqs, batch.sample, ids):
@@ -443,7 +447,7 @@ class AsyncEngine:
         self.engine.shutdown()
 
     async def generate(self, request_id: str, messages: list | None = None, prompt_ids: list | None = None,
-                       params: SamplingParams | None = None):
+                       params: SamplingParams | None = None, cache_scope: bytes = b""):
         """Async iterator of RequestOutput for one request; aborts the sequence if the consumer goes away.
 
         The engine thread never blocks on a consumer: outputs are buffered, and a consumer that falls
@@ -469,7 +473,7 @@ class AsyncEngine:
 
         if prompt_ids is None:
             prompt_ids = self.engine.tokenizer.apply_chat_template(messages or [])
-        self.engine.add_request(request_id, prompt_ids, params, cb)
+        self.engine.add_request(request_id, prompt_ids, params, cb, cache_scope=cache_scope)
         self.start()
         self._wake.set()
         finished = False

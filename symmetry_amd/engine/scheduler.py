@@ -12,7 +12,10 @@ preempted (recomputed later) when the cache runs out.
 """
 from __future__ import annotations
 
+import array
 import collections
+import hashlib
+import os
 from dataclasses import dataclass, field
 
 from .sequence import Sequence, SeqStatus
@@ -42,11 +45,12 @@ class BlockManager:
         self.reserved = reserved
         self.prefix_caching = prefix_caching
         self.ref = [0] * num_blocks
-        self.block_hash: dict[int, int] = {}        # block -> content hash (registered blocks)
-        self.cached: dict[int, int] = {}            # content hash -> block
+        self.block_hash: dict[int, bytes] = {}      # block -> content key (registered blocks)
+        self.cached: dict[bytes, int] = {}          # content key -> block
         self.evictable: collections.OrderedDict[int, None] = collections.OrderedDict()  # ref 0, LRU order
         self.hit_tokens = 0
         self.query_tokens = 0
+        self._key = os.urandom(32)
 
     @property
     def num_free(self) -> int:
@@ -80,10 +84,16 @@ class BlockManager:
             seq.block_table.append(self._alloc())
 
     # ---- prefix caching ------------------------------------------------------------------------
-    def _chain(self, tokens: list, nblocks: int):
-        bs, h = self.block_size, 0
+    def _chain(self, tokens: list, nblocks: int, scope: bytes = b""):
+        """Content keys of the first ``nblocks`` full blocks: a keyed BLAKE2b chain over the token ids.
+        Keyed with a per-process secret and collision resistant, so clients of a public provider cannot
+        craft a prompt whose blocks alias another client's cached prefix (Python's ``hash`` is neither);
+        rooted in the sequence's ``cache_scope`` (the client's public key), so clients never share blocks
+        (no cross-client TTFT side channel either)."""
+        bs, h = self.block_size, hashlib.blake2b(scope, digest_size=16, key=self._key).digest()
         for i in range(nblocks):
-            h = hash((h, tuple(tokens[i * bs:(i + 1) * bs])))
+            blk = tokens[i * bs:(i + 1) * bs]
+            h = hashlib.blake2b(h + array.array("q", blk).tobytes(), digest_size=16, key=self._key).digest()
             yield i, h
 
     def match_prefix(self, seq: Sequence) -> int:
@@ -96,7 +106,7 @@ class BlockManager:
         target = seq.prefill_target
         nfull = max(0, target - 1) // self.block_size  # >= 1 token left to prefill
         self.query_tokens += target
-        for _, h in self._chain(tokens, nfull):
+        for _, h in self._chain(tokens, nfull, seq.cache_scope):
             b = self.cached.get(h)
             if b is None:
                 break
@@ -116,7 +126,7 @@ class BlockManager:
         tokens = seq.token_ids
         nfull = min(seq.num_computed, len(tokens)) // self.block_size
         nfull = min(nfull, len(seq.block_table))
-        for i, h in self._chain(tokens, nfull):
+        for i, h in self._chain(tokens, nfull, seq.cache_scope):
             b = seq.block_table[i]
             if b in self.block_hash:       # already registered (adopted, or registered earlier)
                 continue

@@ -82,6 +82,7 @@ class Sequence:
     num_preemptions: int = 0
     sampling_seed: int = 0
     output_text: str = ""
+    cache_scope: bytes = b""       # prefix-cache namespace (client identity)
 
     @property
     def token_ids(self) -> list:

@@ -243,7 +243,10 @@ class SymmetryProvider:
         req = data.get("data") or {}
         emitter_key = req.get("key")
         completion = ""
-        gen = self.backend.stream(req)
+        # prefix-cache scope: a client's multi-turn prompts reuse its own cached KV only (no cross-client
+        # aliasing, no cross-client TTFT side channel on a public provider)
+        scope = bytes(getattr(peer, "remotePublicKey", b"") or b"")
+        gen = self.backend.stream(req, scope=scope)
         try:
             header_sent = False
             async for chunk in gen:

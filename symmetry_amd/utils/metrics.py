@@ -36,6 +36,8 @@ class EngineMetrics:
         self.itl = deque(maxlen=window)
         self.batch = deque(maxlen=window)
         self.kv_util = 0.0
+        self.prefix_hits = 0      # prompt tokens whose prefill was skipped (adopted cached KV blocks)
+        self.prefix_queries = 0   # prompt tokens looked up in the prefix cache
         self.queue_depth = 0
         self.active_peers = 0
         # engine step timer (seconds): host scheduling + enqueue, host blocked on the GPU, streaming out
@@ -99,6 +101,8 @@ class EngineMetrics:
                 "prefill_steps": self.steps["prefill"],
                 "decode_steps": self.steps["decode"],
                 "kv_utilization": round(self.kv_util, 4),
+                "prefix_cache_hit_tokens": self.prefix_hits,
+                "prefix_cache_hit_rate": round(self.prefix_hits / self.prefix_queries, 4) if self.prefix_queries else 0.0,
                 "queue_depth": self.queue_depth,
                 "active_peers": self.active_peers,
                 "aborted": self.aborted,

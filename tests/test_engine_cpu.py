@@ -390,3 +390,22 @@ def test_randomized_soak_prefix_sharing_aborts_preemption():
     assert eng.blocks.num_free == eng.blocks.num_blocks - eng.blocks.reserved
     assert eng.blocks.hit_tokens > 0
     assert sum(s.num_preemptions for s in every) > 0
+
+
+def test_prefix_cache_is_scoped_per_client():
+    """The provider passes the client's public key as the cache scope: the same prompt from another client
+    recomputes its prefill instead of adopting the first client's blocks."""
+    eng = _engine(block_size=16)
+    p = _prompts(1, seed=40, lo=70, hi=71)[0]
+    eng.add_request("a", p, SamplingParams(max_tokens=3, ignore_eos=True), cache_scope=b"peer-A")
+    while eng.has_unfinished():
+        eng.step()
+    h0 = eng.blocks.hit_tokens
+    eng.add_request("b", p, SamplingParams(max_tokens=3, ignore_eos=True), cache_scope=b"peer-B")
+    while eng.has_unfinished():
+        eng.step()
+    assert eng.blocks.hit_tokens == h0  # other client: no adoption
+    eng.add_request("a2", p, SamplingParams(max_tokens=3, ignore_eos=True), cache_scope=b"peer-A")
+    while eng.has_unfinished():
+        eng.step()
+    assert eng.blocks.hit_tokens - h0 == (len(p) - 1) // 16 * 16  # same client: adopted
