@@ -24,6 +24,9 @@ SHAPES = {
     "down": ("resid", 4096, 14336), "lm_head": ("argmax", 128256, 4096),
     "qkv_tp8": ("qkv", 768, 4096), "o_tp8": ("f32", 4096, 512), "gate_up_tp8": ("swiglu", 3584, 4096),
     "down_tp8": ("f32", 4096, 1792), "lm_head_tp8": ("argmax", 16032, 4096),
+    # Llama-3-70B at TP=1 (config 4 on one GPU)
+    "qkv_70b": ("qkv", 10240, 8192), "o_70b": ("resid", 8192, 8192), "gate_up_70b": ("swiglu", 57344, 8192),
+    "down_70b": ("resid", 8192, 28672),
     # plain fp32-output twins: the difference to the fused shapes is the epilogue's cost
     "qkv_f32": ("f32", 6144, 4096), "o_f32": ("f32", 4096, 4096), "gate_up_f32": ("f32", 28672, 4096),
 }
@@ -44,8 +47,9 @@ def make_call(epi, x, W, M, N, K, dev, sh=False):
         act = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
         return lambda w: ops.dg_swiglu(x, w, ss, 1e-5, act, wshuf=sh)
     if epi == "qkv":
-        hkv = N // 128 // 6
-        hq = 4 * hkv
+        g = 8 if N == 10240 else 4  # Llama-3-70B: 64 q / 8 kv heads; 8B (and shards): 32 / 8
+        hkv = N // 128 // (g + 2)
+        hq = g * hkv
         cs = torch.rand(4096, 128, device=dev)
         pos = torch.arange(M, device=dev, dtype=torch.int32)
         slots = torch.arange(M, device=dev, dtype=torch.int32)
