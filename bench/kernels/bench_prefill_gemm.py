@@ -33,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, nargs="+", default=[128, 256, 512, 1280, 4096])
     ap.add_argument("--tune-file", default=None)
+    ap.add_argument("--alt", action="store_true", help="also time the transposed orientation y^T = W x^T")
     args = ap.parse_args()
     dev = torch.device("cuda")
     ws = {k: torch.randn(n, kk, device=dev).bfloat16() * 0.02 for k, (n, kk) in SHAPES.items()}
@@ -55,6 +56,11 @@ def main():
             row = {"T": T, "gemm": k, "N": N, "K": K, "default_us": round(d, 1),
                    "default_tflops": round(2 * T * N * K / d / 1e6, 1),
                    "default_TBps": round(2 * N * K / d / 1e6, 2)}
+            if args.alt:
+                yt = torch.empty(N, T, device=dev, dtype=torch.bfloat16)
+                a = timeit(lambda: torch.matmul(ws[k], x.t(), out=yt))
+                a2 = timeit(lambda: y.copy_(torch.matmul(ws[k], x.t(), out=yt).t()))
+                row.update({"alt_us": round(a, 1), "alt_plus_transpose_us": round(a2, 1)})
             if args.tune_file:
                 torch.matmul(x, ws[k].t(), out=y)  # tunes this shape
                 torch.cuda.synchronize()
