@@ -885,7 +885,10 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
       if (M <= 16 && K % 1024 == 0 && K <= 4096 && !(N >= 65536 && M <= 4)) v = 11;
       // wide N at 5..16 rows otherwise: 7 resident 4-wave workgroups per CU (gate_up's 1792 tiles in one
       // round): 45.3 vs 46.9 us (profiles/decode_gemm_occupancy_r1.jsonl)
-      else if (N >= 12288) v = M > 16 ? 3 : (M <= 4 ? 0 : 8);
+      // above 16 rows (profiles/decode_gemm_bigm_r1.jsonl, M = 64): wide N shares each x fragment over
+      // four row tiles (gate_up 93.6 -> 76.7 us, lm_head 367 -> 307), qkv over two (43.7 -> 33.3)
+      else if (N >= 12288) v = M > 16 ? (M > 24 ? 12 : 3) : (M <= 4 ? 0 : 8);
+      else if (M > 16 && N > 4096) v = 3;
       else if (N <= 4096 && K % 1024 == 0) v = K > 4096 ? 4 : 2;  // few row tiles: split K (down_proj: 4 waves,
                                                                   // 24.2 vs 25.7 us at M = 10)
       else v = 0;
@@ -904,6 +907,7 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
   if (v == 2 && K % 1024) v = 0;
   if ((v == 5 || v == 7) && (MT > 1 || N % 64)) v = v == 5 ? 3 : 6;
   if ((v == 3 || v == 6) && N % 32) v = 0;
+  if ((v == 12 || v == 13) && N % 64) v = 0;
   if (K % 512) v = (v == 6 || v == 7) ? 6 : 4;  // e.g. Llama-3-8B down_proj under TP=8: K = 1792
   if (v == 6 && N % 32) v = 4;
   constexpr int UH = U0 > 1 ? U0 / 2 : 1;
@@ -929,6 +933,11 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
       if constexpr (MT == 1) go<1, 4, 2, 1, EPI, 7>(x, W, M, N, K, e, s);
       else go<MT, 4, U0, 1, EPI>(x, W, M, N, K, e, s);
       break;
+
+    // 17..64 rows: the x fragments every workgroup re-reads from L2 scale with MT, so four 16-row weight
+    // tiles share each fragment (x traffic = weight traffic at M = 64); one k-block in flight per wave
+    case 12: go<MT, 4, 1, 4, EPI>(x, W, M, N, K, e, s); break;
+    case 13: go<MT, 8, 1, 4, EPI>(x, W, M, N, K, e, s); break;
 
     default: go<MT, 8, U0, 1, EPI>(x, W, M, N, K, e, s); break;
   }

@@ -26,6 +26,7 @@ hipGraph-capturable.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -37,6 +38,13 @@ from .layout import apply_decode_layout
 from .weights import ModelWeights
 
 SKINNY_MAX_M = 64
+# Decode steps with at least this many rows run the O and down projections as k-split skinny GEMMs into
+# fp32 slabs (summed by add_prep) instead of one fused dg_resid launch: those projections have only
+# N / 16 = 256 row tiles, so every workgroup re-reads all M rows of x over the full K range and the x
+# traffic outgrows the weight stream as M grows (bench.py ms/step, fused vs split: 24 rows 4.38 vs 4.42,
+# 32 rows 4.75 vs 4.66, 64 rows 6.86 vs 6.12; profiles/decode_splitk_resid_r1.jsonl).
+# SYMMETRY_SPLITK_RESID_ROWS=0 disables it (A/B).
+SPLITK_RESID_ROWS = int(os.environ.get("SYMMETRY_SPLITK_RESID_ROWS", "32"))
 MAX_STEP_SEQS = 4096  # sequences per step (rows of last_ids)
 SIGN64 = -(1 << 63)
 
@@ -250,9 +258,16 @@ class TransformerLM:
     def _tp_active(self) -> bool:
         return self.tp is not None and self.tp_size > 1
 
-    def _resid_proj(self, name, x, Wsh, resid, w_next, xw, ss_t, ss_1) -> torch.Tensor:
+    def _resid_proj(self, name, x, Wsh, resid, w_next, xw, ss_t, ss_1, w_row=None) -> torch.Tensor:
         """Row-parallel projection + residual add + next-norm prep; returns the ss partials to use."""
         W, sh = Wsh
+        M = x.shape[0]
+        if w_row is not None and not self._tp_active() and 0 < SPLITK_RESID_ROWS <= M:
+            N, K = w_row.shape
+            y = self._buf(name + ".slab", (ops.choose_splits(N, K), M, N), torch.float32)
+            ops.skinny_gemm(x, w_row, y)
+            ops.add_prep(y, resid, w_next, xw, ss_1)
+            return ss_1
         if self._tp_active():
             y = self._buf(name + ".f32", (x.shape[0], W.shape[0]), torch.float32)
             ops.dg_f32(x, W, None, 0.0, y, wshuf=sh)
@@ -309,7 +324,8 @@ class TransformerLM:
                 ss = ss_t
                 continue
             if not block:
-                ss = self._resid_proj("o", attn2d, self._dgw(i, "wo"), resid, w.layer(i, "ln2"), xw, ss_t, ss_1)
+                ss = self._resid_proj("o", attn2d, self._dgw(i, "wo"), resid, w.layer(i, "ln2"), xw, ss_t, ss_1,
+                                     w.layer(i, "wo"))
             if cfg.is_moe:
                 # router + experts are not decode GEMMs: materialise RMSNorm(resid) (one bf16 rounding)
                 xn = self._buf("x", (T, d), torch.bfloat16)
@@ -320,7 +336,8 @@ class TransformerLM:
                 w_gu, shg = self._dgw(i, "w_gu")
                 act = self._buf("act", (T, w_gu.shape[0] // 2), torch.bfloat16)
                 ops.dg_swiglu(xw, w_gu, ss, eps, act, wshuf=shg)
-                ss = self._resid_proj("down", act, self._dgw(i, "w_down"), resid, nxt, xw, ss_t, ss_1)
+                ss = self._resid_proj("down", act, self._dgw(i, "w_down"), resid, nxt, xw, ss_t, ss_1,
+                                     w.layer(i, "w_down"))
         n = b.num_seqs
         if b.kind == "decode":
             xl, sl = xw, ss

@@ -280,6 +280,28 @@ def test_fused_attn_block_path_matches_default_path(monkeypatch):
     assert outs[0] == outs[1]
 
 
+def test_splitk_resid_path_for_wide_decode_batches(monkeypatch):
+    """Decode steps with >= SPLITK_RESID_ROWS rows run O / down as k-split skinny GEMMs + add_prep; the
+    outputs follow the naive fp32 forward (teacher forcing) like the fused dg_resid path."""
+    from symmetry_amd import ops
+    from symmetry_amd.models import transformer
+
+    calls = []
+    orig = ops.add_prep  # dense model, no TP: add_prep only runs on the split path
+    monkeypatch.setattr(ops, "add_prep", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    monkeypatch.setattr(transformer, "SPLITK_RESID_ROWS", 2)
+    eng = _engine("small-llama", max_num_seqs=4, use_graphs=False)
+    prompts = _prompts(3, seed=11, lo=4, hi=20)
+    seqs = [eng.add_request(f"r{i}", p, SamplingParams(max_tokens=6, ignore_eos=True))
+            for i, p in enumerate(prompts)]
+    while eng.has_unfinished():
+        eng.step()
+    assert calls
+    for p, s in zip(prompts, seqs):
+        assert len(s.output_ids) == 6
+        _agree(eng.weights, p, s.output_ids, tol=0.05)
+
+
 # ---- automatic prefix caching ------------------------------------------------------------------
 def test_prefix_cache_multi_turn_skips_shared_prefill_and_matches_reference():
     """Turn 2 of a chat resends turn 1's prompt + answer (REF src/provider.ts:312-316): the engine adopts
