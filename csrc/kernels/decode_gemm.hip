@@ -895,7 +895,9 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
     } else if (M <= 4) {
       v = 0;
     } else if (N >= 12288) {
-      v = 7;
+      // row-major wide N above 16 rows (the lm_head, whose weights are never preshuffled): 4 row tiles per
+      // workgroup, lm_head 268 -> 224 us at M = 24, 421 -> 335 at M = 64 (profiles/decode_gemm_bigm_row_r1.jsonl)
+      v = M > 16 ? 12 : 7;
     } else if (N >= 6144 && K >= 4096) {
       v = 3;
     } else if (N <= 4096 && K >= 4096) {

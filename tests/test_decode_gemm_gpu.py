@@ -62,7 +62,7 @@ def test_dg_resid(gpu, M, N, K):
 
 
 @pytest.mark.parametrize("M", MS)
-@pytest.mark.parametrize("F,K", [(1792, 4096), (512, 256)])
+@pytest.mark.parametrize("F,K", [(1792, 4096), (512, 256), (14336, 4096)])
 def test_dg_swiglu(gpu, M, F, K):
     x, W, s = _inputs(gpu, M, 2 * F, K, seed=3)
     W = W[gu_perm(F).to(gpu)].contiguous()
@@ -96,9 +96,10 @@ def test_dg_qkv(gpu, M, Hq, Hkv, K):
     _close(vc, vc_r, atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M", MS)
-def test_dg_argmax(gpu, M):
-    N, K = 16032, 4096  # Llama-3 vocab shard at TP=8
+# 16032: Llama-3 vocab shard at TP=8; 128256: the full vocabulary (4-row-tile variant above 16 rows)
+@pytest.mark.parametrize("M,N", [(m, 16032) for m in MS] + [(33, 128256), (64, 128256)])
+def test_dg_argmax(gpu, M, N):
+    K = 4096
     x, W, s = _inputs(gpu, M, N, K, seed=6)
     g = torch.Generator(device=gpu).manual_seed(7)
     temps = torch.where(torch.arange(M, device=gpu) % 2 == 0, 0.0, 0.8).float()
@@ -173,7 +174,7 @@ def test_rope_cache_perm_and_swiglu_interleaved(gpu):
     _close(a, a_r, atol=2e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("M", [1, 10, 33])
+@pytest.mark.parametrize("M", [1, 10, 33, 64])
 def test_preshuffled_weight_stream(gpu, M):
     """MFMA-preshuffled weights (1 KB contiguous per wave load) give the row-major result exactly."""
     from symmetry_amd.models.layout import preshuffle
@@ -181,7 +182,7 @@ def test_preshuffled_weight_stream(gpu, M):
 
     lib = _native.ops()
     try:
-        for v in (0, 3, 4, 7):  # same decomposition on both layouts -> same summation order -> bitwise equal
+        for v in (0, 3, 4, 7, 12, 13):  # same decomposition on both layouts -> same summation order -> bitwise equal
             lib.decode_gemm_variant(v)
             for N, K in ((4096, 4096), (28672, 4096), (4096, 1792)):
                 x, W, s = _inputs(gpu, M, N, K, seed=12)
