@@ -887,7 +887,8 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
       // round): 45.3 vs 46.9 us (profiles/decode_gemm_occupancy_r1.jsonl)
       // above 16 rows (profiles/decode_gemm_bigm_r1.jsonl, M = 64): wide N shares each x fragment over
       // four row tiles (gate_up 93.6 -> 76.7 us, lm_head 367 -> 307), qkv over two (43.7 -> 33.3)
-      else if (N >= 12288) v = M > 16 ? (M > 24 ? 12 : 3) : (M <= 4 ? 0 : 8);
+      // (eight row tiles from 25 rows: gate_up 77.0 -> 69.1 us at M = 64, profiles/decode_gemm_rt8_r1.jsonl)
+      else if (N >= 12288) v = M > 16 ? (M > 24 ? 14 : 3) : (M <= 4 ? 0 : 8);
       else if (M > 16 && N > 4096) v = 3;
       else if (N <= 4096 && K % 1024 == 0) v = K > 4096 ? 4 : 2;  // few row tiles: split K (down_proj: 4 waves,
                                                                   // 24.2 vs 25.7 us at M = 10)
@@ -897,7 +898,7 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
     } else if (N >= 12288) {
       // row-major wide N above 16 rows (the lm_head, whose weights are never preshuffled): 4 row tiles per
       // workgroup, lm_head 268 -> 224 us at M = 24, 421 -> 335 at M = 64 (profiles/decode_gemm_bigm_row_r1.jsonl)
-      v = M > 16 ? 12 : 7;
+      v = M > 16 ? (M > 24 ? 14 : 12) : 7;  // eight row tiles from 25 rows: 335 -> 311 us at M = 64
     } else if (N >= 6144 && K >= 4096) {
       v = 3;
     } else if (N <= 4096 && K >= 4096) {
@@ -909,7 +910,8 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
   if (v == 2 && K % 1024) v = 0;
   if ((v == 5 || v == 7) && (MT > 1 || N % 64)) v = v == 5 ? 3 : 6;
   if ((v == 3 || v == 6) && N % 32) v = 0;
-  if ((v == 12 || v == 13) && N % 64) v = 0;
+  if ((v == 12 || v == 13 || v == 16) && N % 64) v = 0;
+  if ((v == 14 || v == 15) && (N % 128 || MT == 1)) v = 0;
   if (K % 512) v = (v == 6 || v == 7) ? 6 : 4;  // e.g. Llama-3-8B down_proj under TP=8: K = 1792
   if (v == 6 && N % 32) v = 4;
   constexpr int UH = U0 > 1 ? U0 / 2 : 1;
@@ -940,6 +942,9 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
     // tiles share each fragment (x traffic = weight traffic at M = 64); one k-block in flight per wave
     case 12: go<MT, 4, 1, 4, EPI>(x, W, M, N, K, e, s); break;
     case 13: go<MT, 8, 1, 4, EPI>(x, W, M, N, K, e, s); break;
+    case 14: go<MT, 4, 1, 8, EPI>(x, W, M, N, K, e, s); break;
+    case 15: go<MT, 2, 1, 8, EPI>(x, W, M, N, K, e, s); break;
+    case 16: go<MT, 2, 1, 4, EPI>(x, W, M, N, K, e, s); break;
 
     default: go<MT, 8, U0, 1, EPI>(x, W, M, N, K, e, s); break;
   }

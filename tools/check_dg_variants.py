@@ -11,7 +11,7 @@ for (N, K) in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]:
     for M in [17, 33, 64]:
         x = torch.randn(M, K, device=dev).bfloat16()
         ref = x.float() @ W.float().t()
-        for v in [12, 13]:
+        for v in [12, 13, 14, 15, 16]:
             lib.decode_gemm_variant(v)
             y = torch.full((M, N), float("nan"), device=dev)
             ops.dg_f32(x, W, None, 0.0, y)
