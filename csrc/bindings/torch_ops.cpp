@@ -553,10 +553,13 @@ void add_prep(const Tensor& delta, Tensor& resid, const Tensor& w, Tensor& xw, T
   check_dtype(xw, at::kBFloat16, "xw");
   check_gpu(ss, "ss");
   check_dtype(ss, at::kFloat, "ss");
-  TORCH_CHECK(xw.numel() == T * d && w.numel() == d && ss.numel() >= T && d % 8 == 0, "add_prep: shape mismatch");
+  // ss [>=T] / [>=T, 1]: one sum per row; [>=T, P]: P per-row partials over column slices
+  const int64_t P = ss.dim() == 2 ? ss.size(1) : 1;
+  TORCH_CHECK(ss.is_contiguous() && P >= 1 && P <= 16 && d % (8 * P) == 0, "add_prep: ss parts must divide d / 8");
+  TORCH_CHECK(xw.numel() == T * d && w.numel() == d && ss.numel() >= T * P && d % 8 == 0, "add_prep: shape mismatch");
   const at::OptionalDeviceGuard g(resid.device());
   launch_add_prep(linout(delta, T, d, "delta"), ptr<float>(resid), ptr<bf16>(w), ptr<bf16>(xw), ptr<float>(ss), (int)T,
-                  (int)d, cur_stream(resid));
+                  (int)d, (int)P, cur_stream(resid));
 }
 
 void sample_filtered(const Tensor& logits, const Tensor& temps, const Tensor& top_k, const Tensor& top_p,

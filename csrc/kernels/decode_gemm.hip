@@ -384,19 +384,22 @@ __global__ __launch_bounds__(256) void prep_kernel(LinOut delta, const int* __re
                                                    const bf16* __restrict__ table, float* __restrict__ resid,
                                                    const bf16* __restrict__ w, bf16* __restrict__ xw,
                                                    float* __restrict__ ss, int d) {
+  // gridDim.y column parts per row (wide decode batches: 64 rows x 1 workgroup is latency-bound); part p
+  // covers columns [p d / P, (p + 1) d / P) and writes its own partial ss[row][p]
   __shared__ float scratch[4];
-  const int row = blockIdx.x;
-  const long long rb = (long long)row * d;
+  const int row = blockIdx.x, P = gridDim.y, dp = d / P;
+  const long long rb = (long long)row * d + (long long)blockIdx.y * dp;
   float acc = 0.f;
   long long tok = 0;
   if constexpr (MODE == 0) {
     const int sr = src ? src[row] : -1;
     tok = sr >= 0 ? prev[sr] : ids[row];
   }
-  for (int vi = threadIdx.x; vi < d / 8; vi += 256) {
+  const bf16* wp = w + (long long)blockIdx.y * dp;
+  for (int vi = threadIdx.x; vi < dp / 8; vi += 256) {
     float r[8], g[8];
     if constexpr (MODE == 0) {
-      load8(table + tok * d + vi * 8, r);
+      load8(table + tok * d + (long long)blockIdx.y * dp + vi * 8, r);
     } else {
       float dd[8];
       load8f(resid + rb + vi * 8, r);
@@ -405,7 +408,7 @@ __global__ __launch_bounds__(256) void prep_kernel(LinOut delta, const int* __re
       for (int i = 0; i < 8; ++i) r[i] += dd[i];
     }
     store8f(resid + rb + vi * 8, r);
-    load8(w + vi * 8, g);
+    load8(wp + vi * 8, g);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       acc += r[i] * r[i];
@@ -414,7 +417,7 @@ __global__ __launch_bounds__(256) void prep_kernel(LinOut delta, const int* __re
     store8(xw + rb + vi * 8, g);
   }
   acc = block_sum<256>(acc, scratch);
-  if (threadIdx.x == 0) ss[row] = acc;
+  if (threadIdx.x == 0) ss[row * P + blockIdx.y] = acc;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -1019,12 +1022,13 @@ void launch_embed_prep(const int* ids, const int* src, const int* prev, const bf
                        bf16* xw, float* ss, int T, int d, hipStream_t s) {
   if (T == 0) return;
   LinOut none{nullptr, 0, 1, 0};
-  prep_kernel<0><<<T, 256, 0, s>>>(none, ids, src, prev, table, resid, w, xw, ss, d);
+  prep_kernel<0><<<dim3(T, 1), 256, 0, s>>>(none, ids, src, prev, table, resid, w, xw, ss, d);
 }
 
-void launch_add_prep(LinOut delta, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d, hipStream_t s) {
+void launch_add_prep(LinOut delta, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d, int parts,
+                     hipStream_t s) {
   if (T == 0) return;
-  prep_kernel<1><<<T, 256, 0, s>>>(delta, nullptr, nullptr, nullptr, nullptr, resid, w, xw, ss, d);
+  prep_kernel<1><<<dim3(T, parts), 256, 0, s>>>(delta, nullptr, nullptr, nullptr, nullptr, resid, w, xw, ss, d);
 }
 
 void launch_decode_block(const DecodeBlockArgs& a, hipStream_t s) {

@@ -109,7 +109,9 @@ void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int
                         hipStream_t s);
 void launch_embed_prep(const int* ids, const int* src, const int* prev, const bf16* table, float* resid, const bf16* w,
                        bf16* xw, float* ss, int T, int d, hipStream_t s);
-void launch_add_prep(LinOut delta, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d, hipStream_t s);
+// ss: [T][parts] partial sums of squares (parts column slices of each row, one workgroup each)
+void launch_add_prep(LinOut delta, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d, int parts,
+                     hipStream_t s);
 void launch_rownorm(const bf16* xw, const float* ss, int ss_tiles, float eps, bf16* out, int T, int d, hipStream_t s);
 
 // norm.hip

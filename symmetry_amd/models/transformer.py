@@ -266,8 +266,11 @@ class TransformerLM:
             N, K = w_row.shape
             y = self._buf(name + ".slab", (ops.choose_splits(N, K), M, N), torch.float32)
             ops.skinny_gemm(x, w_row, y)
-            ops.add_prep(y, resid, w_next, xw, ss_1)
-            return ss_1
+            # four workgroups per row (64 rows x 1 workgroup is latency-bound), four ss partials per row
+            parts = 4 if N % 32 == 0 else 1
+            ss_p = self._buf("ss_p", (M, parts), torch.float32)
+            ops.add_prep(y, resid, w_next, xw, ss_p)
+            return ss_p
         if self._tp_active():
             y = self._buf(name + ".f32", (x.shape[0], W.shape[0]), torch.float32)
             ops.dg_f32(x, W, None, 0.0, y, wshuf=sh)

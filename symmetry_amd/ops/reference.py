@@ -303,7 +303,10 @@ def embed_prep(ids, table, resid, w, xw, ss, src=None, prev=None) -> None:
     r = table[resolve_ids(ids, src, prev)].float()
     resid[:T].copy_(r)
     xw[:T].copy_((r * w.float()).to(xw.dtype))
-    ss.view(-1)[:T].copy_(r.pow(2).sum(-1))  # ss: [>=T] or [>=T, 1] (one tile per row)
+    if ss.dim() == 2 and ss.shape[1] > 1:  # [>=T, P]: partial sums over P column slices of each row
+        ss[:T].copy_(r.pow(2).view(T, ss.shape[1], -1).sum(-1))
+    else:
+        ss.view(-1)[:T].copy_(r.pow(2).sum(-1))  # ss: [>=T] or [>=T, 1] (one tile per row)
 
 
 def add_prep(delta, resid, w, xw, ss) -> None:
@@ -312,7 +315,10 @@ def add_prep(delta, resid, w, xw, ss) -> None:
     r = resid[:T]
     r.add_(d)
     xw[:T].copy_((r * w.float()).to(xw.dtype))
-    ss.view(-1)[:T].copy_(r.pow(2).sum(-1))  # ss: [>=T] or [>=T, 1] (one tile per row)
+    if ss.dim() == 2 and ss.shape[1] > 1:  # [>=T, P]: partial sums over P column slices of each row
+        ss[:T].copy_(r.pow(2).view(T, ss.shape[1], -1).sum(-1))
+    else:
+        ss.view(-1)[:T].copy_(r.pow(2).sum(-1))  # ss: [>=T] or [>=T, 1] (one tile per row)
 
 
 def rownorm(xw, ss, eps, out) -> None:

@@ -120,6 +120,25 @@ def test_dg_argmax(gpu, M, N):
     assert torch.equal(keys.cpu()[greedy], k_ref[greedy])
 
 
+@pytest.mark.parametrize("T,P", [(33, 4), (64, 4), (3, 2)])
+def test_add_prep_partial_sums_from_slabs(gpu, T, P):
+    """add_prep over fp32 k-split slabs with P workgroups per row: ss holds P column-slice partials."""
+    d = 4096
+    g = torch.Generator(device=gpu).manual_seed(9)
+    w = (torch.randn(d, device=gpu, generator=g) * 0.1 + 1).bfloat16()
+    resid = torch.randn(T, d, device=gpu, generator=g)
+    slabs = torch.randn(4, T, d, device=gpu, generator=g)
+    xw = torch.empty(T, d, device=gpu, dtype=torch.bfloat16)
+    ss = torch.empty(T, P, device=gpu)
+    r_ref, xw_ref, ss_ref = resid.cpu(), torch.empty(T, d, dtype=torch.bfloat16), torch.empty(T, P)
+    ops.add_prep(slabs, resid, w, xw, ss)
+    ref.add_prep(slabs.cpu(), r_ref, w.cpu(), xw_ref, ss_ref)
+    _close(resid, r_ref, atol=1e-5)
+    _close(xw, xw_ref, atol=1e-2, rtol=1e-2)
+    _close(ss, ss_ref, atol=1e-2, rtol=1e-4)
+    assert torch.allclose(ss.sum(1).cpu(), r_ref.pow(2).sum(1), rtol=1e-4)
+
+
 @pytest.mark.parametrize("T,d", [(1, 4096), (13, 4096), (5, 256)])
 def test_prep_and_rownorm(gpu, T, d):
     g = torch.Generator(device=gpu).manual_seed(8)
