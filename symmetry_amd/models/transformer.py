@@ -42,9 +42,11 @@ SKINNY_MAX_M = 64
 # fp32 slabs (summed by add_prep) instead of one fused dg_resid launch: those projections have only
 # N / 16 = 256 row tiles, so every workgroup re-reads all M rows of x over the full K range and the x
 # traffic outgrows the weight stream as M grows (bench.py ms/step, fused vs split: 24 rows 4.38 vs 4.42,
-# 32 rows 4.75 vs 4.66, 64 rows 6.86 vs 6.12; profiles/decode_splitk_resid_r1.jsonl).
+# 32 rows 4.75 vs 4.66, 64 rows 6.86 vs 6.12; profiles/decode_splitk_resid_r1.jsonl).  With the
+# column-sliced add_prep the crossover moved to 21..24 rows (fused vs split: 20 rows 4.15 vs 4.19,
+# 24 rows 4.34 vs 4.32, 28 rows 4.45 vs 4.44; 1/10/16 rows stay fused; profiles/decode_splitk_small_m_r1.jsonl).
 # SYMMETRY_SPLITK_RESID_ROWS=0 disables it (A/B).
-SPLITK_RESID_ROWS = int(os.environ.get("SYMMETRY_SPLITK_RESID_ROWS", "32"))
+SPLITK_RESID_ROWS = int(os.environ.get("SYMMETRY_SPLITK_RESID_ROWS", "24"))
 MAX_STEP_SEQS = 4096  # sequences per step (rows of last_ids)
 SIGN64 = -(1 << 63)
 
