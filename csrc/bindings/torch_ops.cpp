@@ -525,7 +525,10 @@ void embed_prep(const Tensor& ids, const Tensor& table, Tensor& resid, const Ten
   check_dtype(xw, at::kBFloat16, "xw");
   check_gpu(ss, "ss");
   check_dtype(ss, at::kFloat, "ss");
-  TORCH_CHECK(resid.numel() == T * d && xw.numel() == T * d && w.numel() == d && ss.numel() >= T && d % 8 == 0,
+  // ss [>=T] / [>=T, 1]: one sum per row; [>=T, P]: P per-row partials over column slices (as add_prep)
+  const int64_t P = ss.dim() == 2 ? ss.size(1) : 1;
+  TORCH_CHECK(ss.is_contiguous() && P >= 1 && P <= 16 && d % (8 * P) == 0, "embed_prep: ss parts must divide d / 8");
+  TORCH_CHECK(resid.numel() == T * d && xw.numel() == T * d && w.numel() == d && ss.numel() >= T * P && d % 8 == 0,
               "embed_prep: shape mismatch");
   const int* sp = nullptr;
   const int* pp = nullptr;
@@ -541,7 +544,7 @@ void embed_prep(const Tensor& ids, const Tensor& table, Tensor& resid, const Ten
   }
   const at::OptionalDeviceGuard g(ids.device());
   launch_embed_prep(ptr<int>(ids), sp, pp, ptr<bf16>(table), ptr<float>(resid), ptr<bf16>(w), ptr<bf16>(xw),
-                    ptr<float>(ss), (int)T, (int)d, cur_stream(ids));
+                    ptr<float>(ss), (int)T, (int)d, (int)P, cur_stream(ids));
 }
 
 void add_prep(const Tensor& delta, Tensor& resid, const Tensor& w, Tensor& xw, Tensor& ss) {

@@ -1019,10 +1019,10 @@ void set_decode_gemm_variant(int v) {
 void set_decode_gemm_nt(int on) { g_wnt = on ? 1 : 0; }
 
 void launch_embed_prep(const int* ids, const int* src, const int* prev, const bf16* table, float* resid, const bf16* w,
-                       bf16* xw, float* ss, int T, int d, hipStream_t s) {
+                       bf16* xw, float* ss, int T, int d, int parts, hipStream_t s) {
   if (T == 0) return;
   LinOut none{nullptr, 0, 1, 0};
-  prep_kernel<0><<<dim3(T, 1), 256, 0, s>>>(none, ids, src, prev, table, resid, w, xw, ss, d);
+  prep_kernel<0><<<dim3(T, parts), 256, 0, s>>>(none, ids, src, prev, table, resid, w, xw, ss, d);
 }
 
 void launch_add_prep(LinOut delta, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d, int parts,

@@ -107,8 +107,9 @@ void set_decode_gemm_variant(int v);  // -1: default heuristic
 void set_decode_gemm_nt(int on);      // non-temporal weight-stream loads (keeps the variant choice)
 void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e,
                         hipStream_t s);
+// ss: [T][parts] partial sums of squares, as launch_add_prep
 void launch_embed_prep(const int* ids, const int* src, const int* prev, const bf16* table, float* resid, const bf16* w,
-                       bf16* xw, float* ss, int T, int d, hipStream_t s);
+                       bf16* xw, float* ss, int T, int d, int parts, hipStream_t s);
 // ss: [T][parts] partial sums of squares (parts column slices of each row, one workgroup each)
 void launch_add_prep(LinOut delta, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d, int parts,
                      hipStream_t s);

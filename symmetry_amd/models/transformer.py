@@ -45,6 +45,10 @@ SKINNY_MAX_M = 64
 # 32 rows 4.75 vs 4.66, 64 rows 6.86 vs 6.12; profiles/decode_splitk_resid_r1.jsonl).  With the
 # column-sliced add_prep the crossover moved to 21..24 rows (fused vs split: 20 rows 4.15 vs 4.19,
 # 24 rows 4.34 vs 4.32, 28 rows 4.45 vs 4.44; 1/10/16 rows stay fused; profiles/decode_splitk_small_m_r1.jsonl).
+# Re-checked with 3 alternating runs per arm (profiles/decode_splitk_threshold_ab_r2.jsonl, mean [min, max]):
+# 24 rows fused 4.323 [4.317, 4.330] vs split 4.288 [4.285, 4.289] ms/step, p50 TTFT 40.43 vs 40.49 ms;
+# 28 rows 4.443 [4.433, 4.453] vs 4.427 [4.417, 4.435], TTFT 47.07 vs 46.89: the split path wins by more than
+# the run-to-run spread at 24 rows and TTFT does not move, so the threshold stays at 24.
 # SYMMETRY_SPLITK_RESID_ROWS=0 disables it (A/B).
 SPLITK_RESID_ROWS = int(os.environ.get("SYMMETRY_SPLITK_RESID_ROWS", "24"))
 MAX_STEP_SEQS = 4096  # sequences per step (rows of last_ids)

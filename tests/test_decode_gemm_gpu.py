@@ -139,6 +139,25 @@ def test_add_prep_partial_sums_from_slabs(gpu, T, P):
     assert torch.allclose(ss.sum(1).cpu(), r_ref.pow(2).sum(1), rtol=1e-4)
 
 
+@pytest.mark.parametrize("T,P", [(33, 4), (3, 2)])
+def test_embed_prep_partial_sums(gpu, T, P):
+    """embed_prep with ss [T, P]: P column-slice partials per row, the same layout as add_prep."""
+    d = 4096
+    g = torch.Generator(device=gpu).manual_seed(10)
+    table = torch.randn(300, d, device=gpu, generator=g).bfloat16()
+    ids = torch.randint(0, 300, (T,), device=gpu, generator=g, dtype=torch.int32)
+    w = (torch.randn(d, device=gpu, generator=g) * 0.1 + 1).bfloat16()
+    resid = torch.empty(T, d, device=gpu)
+    xw = torch.empty(T, d, device=gpu, dtype=torch.bfloat16)
+    ss = torch.full((T, P), float("nan"), device=gpu)
+    ops.embed_prep(ids, table, resid, w, xw, ss)
+    r_ref, xw_ref, ss_ref = torch.empty(T, d), torch.empty(T, d, dtype=torch.bfloat16), torch.empty(T, P)
+    ref.embed_prep(ids.cpu(), table.cpu(), r_ref, w.cpu(), xw_ref, ss_ref)
+    _close(resid, r_ref, atol=0)
+    _close(xw, xw_ref, atol=1e-2, rtol=1e-2)
+    _close(ss, ss_ref, atol=1e-2, rtol=1e-4)
+
+
 @pytest.mark.parametrize("T,d", [(1, 4096), (13, 4096), (5, 256)])
 def test_prep_and_rownorm(gpu, T, d):
     g = torch.Generator(device=gpu).manual_seed(8)

@@ -39,6 +39,32 @@ def test_engine_gpu_matches_oracle(gpu, model):
         _agree(eng.weights, p, s.output_ids, tol=0.08)
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_splitk_resid_path_native(gpu, monkeypatch, graphs):
+    """The k-split O/down chain on the GPU (skinny_gemm into fp32 slabs -> add_prep with P = 4 column
+    partials -> dg_swiglu / dg_qkv / dg_argmax reading the 4-column ss) against the fp32 oracle; the
+    threshold is lowered so a small batch takes the path the engine uses from SPLITK_RESID_ROWS rows."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+    from symmetry_amd.models import transformer
+
+    calls = []
+    orig = ops.add_prep  # dense model, no TP: add_prep only runs on the split path
+    monkeypatch.setattr(ops, "add_prep", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    monkeypatch.setattr(transformer, "SPLITK_RESID_ROWS", 2)
+    eng = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", max_num_seqs=6, max_model_len=1024,
+                                 num_kv_blocks=64, use_graphs=graphs))
+    prompts = [list(range(300 + 11 * i, 330 + 13 * i)) for i in range(5)]
+    seqs = [eng.add_request(f"k{i}", p, SamplingParams(max_tokens=10, ignore_eos=True))
+            for i, p in enumerate(prompts)]
+    while eng.has_unfinished():
+        eng.step()
+    assert calls
+    for p, s in zip(prompts, seqs):
+        assert len(s.output_ids) == 10
+        _agree(eng.weights, p, s.output_ids, tol=0.08)
+
+
 def test_graph_replay_equals_eager(gpu):
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
     from symmetry_amd.engine.sequence import SamplingParams
