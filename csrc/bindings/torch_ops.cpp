@@ -232,6 +232,29 @@ void skinny_gemm(const Tensor& x, const Tensor& w, Tensor& y, int64_t variant) {
                      (int)variant);
 }
 
+// Medium-M projection (65..256 rows) into fp32 split-K slabs; w is the MFMA-preshuffled weight copy.
+void mgemm(const Tensor& x, const Tensor& w, Tensor& y, int64_t rw) {
+  check_gpu(x, "x");
+  check_gpu(w, "w");
+  check_gpu(y, "y");
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(w, at::kBFloat16, "w");
+  check_dtype(y, at::kFloat, "y");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 3, "mgemm: x [M,K], w [N,K], y [S,M,N]");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0), S = y.size(0);
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && y.is_contiguous(), "mgemm: contiguous operands");
+  TORCH_CHECK(w.size(1) == K, "mgemm: K mismatch");
+  TORCH_CHECK(M >= 1 && M <= 256, "mgemm: M must be in [1, 256]");
+  TORCH_CHECK(rw >= 1 && rw <= 4 && (M <= 128 || rw <= 2), "mgemm: rw in 1..4 (<= 2 above 128 rows)");
+  TORCH_CHECK(N % (64 * rw) == 0, "mgemm: N must be a multiple of 64 * rw");
+  TORCH_CHECK(S >= 1 && K % (S * 64) == 0, "mgemm: K must be a multiple of 64 * nsplit");
+  // 32-bit buffer offsets (x rows are addressed up to 16 * ceil(M / 16) * K * 2 bytes)
+  TORCH_CHECK((M + 255) * K * 2 < (1LL << 31) && N * K * 2 < (1LL << 31), "mgemm: operands exceed 2 GB");
+  TORCH_CHECK(y.size(1) == M && y.size(2) == N, "mgemm: y shape mismatch");
+  const at::OptionalDeviceGuard g(x.device());
+  launch_mgemm(ptr<bf16>(x), ptr<bf16>(w), ptr<float>(y), (int)M, (int)N, (int)K, (int)S, (int)rw, cur_stream(x));
+}
+
 void lm_head_sample(const Tensor& x, const Tensor& w, const Tensor& temps, const Tensor& seeds, const Tensor& step,
                     Tensor& tile_keys, Tensor& out_keys, Tensor& out_ids, int64_t n_offset,
                     const c10::optional<Tensor>& logits) {
@@ -758,6 +781,8 @@ TORCH_LIBRARY(symmetry_amd, m) {
       "Tensor tiles, Tensor(a!) out, float scale) -> ()",
       &attn_prefill);
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) y, int variant=0) -> ()", &skinny_gemm);
+  m.def("mgemm(Tensor x, Tensor w, Tensor(a!) y, int rw) -> ()", &mgemm);
+  m.def("mgemm_nt(int on) -> ()", [](int64_t on) { set_mgemm_nt((int)on); });
   m.def(
       "lm_head_sample(Tensor x, Tensor w, Tensor temps, Tensor seeds, Tensor step, Tensor(a!) tile_keys, "
       "Tensor(b!) out_keys, Tensor(c!) out_ids, int n_offset, Tensor(d!)? logits) -> ()",

@@ -115,6 +115,11 @@ void launch_add_prep(LinOut delta, float* resid, const bf16* w, bf16* xw, float*
                      hipStream_t s);
 void launch_rownorm(const bf16* xw, const float* ss, int ss_tiles, float eps, bf16* out, int T, int d, hipStream_t s);
 
+// mgemm.hip -- medium-M (65..256 tokens) projection into fp32 split-K slabs y[S][M][N]; W is the
+// MFMA-preshuffled weight copy, 64 * rw | N, 64 * S | K
+void launch_mgemm(const bf16* x, const bf16* Wshuf, float* y, int M, int N, int K, int S, int rw, hipStream_t s);
+void set_mgemm_nt(int on);  // non-temporal weight DMA (A/B knob)
+
 // norm.hip
 void launch_rms_norm(LinOut x, const bf16* w, bf16* out, int T, int d, float eps, hipStream_t s);
 void launch_add_rms_norm(LinOut delta, float* residual, const bf16* w, bf16* out, int T, int d, float eps,

@@ -1,0 +1,201 @@
+// Medium-M projection GEMM (prefill chunks of 65..256 tokens): fp32 split-K slabs
+//   y[s][m][n] = sum_{k in slice s} x[m][k] * W[n][k],   x [M][K], W [N][K] bf16, M <= 256.
+//
+// Why a separate kernel: at these M a projection is still weight-streaming (Llama-3-8B: 128 tokens x
+// 436 MB of weights per layer), but the library GEMM picks tiles that leave most CUs idle or stream the
+// weights at 1.3-2.7 TB/s (profiles/prefill_gemm_hipblaslt_r1.jsonl), and the decode kernels re-read
+// x once per 16-row weight tile (built for M <= 64).  Here every CU streams its own weight rows once,
+// while the activation slice it needs is shared by its 4 waves through LDS:
+//
+//   * orientation Y^T = W . x^T on v_mfma_f32_16x16x32_bf16: the weight tile is the A operand and comes
+//     from the MFMA-preshuffled weight copy (models/layout.py::preshuffle, the decode layout), so every
+//     weight DMA instruction reads 1 KB contiguous; x fragments are the B operand;
+//   * workgroup = 4 waves x RW 16-row weight tiles (64 RW output features) x all M tokens x one k slice;
+//     the k split S is chosen on the host so the grid fills the 256 CUs; partial sums go to fp32 slabs
+//     that the consumer (rope_cache / add_rms_norm / swiglu, LinOut) sums in its prologue, as the skinny
+//     decode GEMM's do;
+//   * x AND the weight blocks stream through an LDS ring of 64-deep chunks by LDS-DMA (buffer loads: x
+//     rows past M read as zeros), up to 4 chunks ahead (as many as 160 KB of LDS holds), so one counted
+//     vmcnt per chunk covers both operands (an ordinary weight load beside LDS-DMA makes hipcc drain
+//     vmcnt to 0 at its first use: cdna_hip_programming.md §5 item 4(b)); a preshuffled weight block is
+//     1 KB in fragment order, so its DMA and its ds_read_b128 are both lane-linear; the 16-B chunk index
+//     of each 128-B x row is XOR-swizzled with (row >> 1) & 7 on the DMA source and on the read, which
+//     makes the x fragment reads bank-conflict free;
+//   * the 16x16 accumulator of (weight tile, token tile) holds 4 consecutive features of one token per
+//     lane: one float4 store per accumulator into the slab.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+constexpr int MG_THR = 256;
+constexpr int MG_LDS = 160 * 1024;
+
+typedef __attribute__((address_space(3))) void lds_t;
+
+SYM_DEV __amdgpu_buffer_rsrc_t mg_rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL), 0x00020000);
+}
+
+SYM_DEV void mg_dma(__amdgpu_buffer_rsrc_t r, int voff, int soff, char* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_t*)lds, 16, voff, soff, 0, 0);
+}
+
+// non-temporal (aux = 2) LDS-DMA for the once-read weight stream (MI355X_MICROARCH.md row nt-weights)
+SYM_DEV void mg_dma_nt(__amdgpu_buffer_rsrc_t r, int voff, int soff, char* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_t*)lds, 16, voff, soff, 0, 2);
+}
+
+template <int MT, int RW>
+struct MgCfg {
+  static constexpr int XB = 16 * MT * 128;                   // x bytes of one 64-deep chunk
+  static constexpr int WB = 4 * RW * 2 * 1024;               // weight bytes of one chunk (2 blocks per tile)
+  static constexpr int SLOT = XB + WB;
+  static constexpr int SLOTS = MG_LDS / SLOT > 5 ? 5 : MG_LDS / SLOT;
+  static constexpr int D = SLOTS - 1;                        // chunks in flight ahead of the computed one
+  static constexpr int NX = 16 * MT / 32;                    // x DMA instructions per wave per chunk
+  static constexpr int NDMA = NX + 2 * RW;                   // DMA instructions per wave per chunk
+  static constexpr int VM_KEEP = (D - 1) * NDMA;             // younger DMAs left in flight at the wait
+  static_assert(D >= 1 && VM_KEEP <= 63, "mgemm config");
+};
+
+// MT: 16-token tiles (M <= 16 MT); RW: 16-row weight tiles per wave.  Weights MFMA-preshuffled
+// (models/layout.py::preshuffle): block (t, kb) = 16 rows x 32 k, 1 KB in fragment order.
+template <int MT, int RW, bool WNT>
+__global__ __launch_bounds__(MG_THR, 1) void mgemm_kernel(const bf16* __restrict__ x, const bf16* __restrict__ W,
+                                                           float* __restrict__ y, int M, int N, int K, int kslice) {
+  using C = MgCfg<MT, RW>;
+  __shared__ __attribute__((aligned(1024))) char smem[C::SLOTS * C::SLOT];
+  asm volatile("" ::: "a0");  // accumulators may live in AGPRs
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int split = blockIdx.y;
+  const int k0 = split * kslice;
+  const int nch = kslice / 64;
+  const int tile0 = (blockIdx.x * 4 + wid) * RW;  // first 16-row weight tile of this wave
+
+  // ---- x DMA: wave w fills rows (NX w + i) * 8 .. + 8 of each chunk; lane -> (row lane >> 3, 16-B chunk
+  // lane & 7), source chunk swizzled by (row >> 1) & 7.  Rows >= M read as zeros (buffer range).
+  const __amdgpu_buffer_rsrc_t rx = mg_rsrc(x, (long long)M * K * 2);
+  int vx[C::NX];
+#pragma unroll
+  for (int i = 0; i < C::NX; ++i) {
+    const int row = (C::NX * wid + i) * 8 + (lane >> 3);
+    vx[i] = row * K * 2 + 16 * ((lane & 7) ^ ((row >> 1) & 7)) + k0 * 2;
+  }
+  // ---- weight DMA: the wave's own tiles, block (tile, 2c + s) -> its 1 KB LDS block, lane-linear
+  const __amdgpu_buffer_rsrc_t rw = mg_rsrc(W, (long long)N * K * 2);
+  const int vw = (tile0 * (K / 32) + k0 / 32) * 1024 + lane * 16;
+  const int wstride = (K / 32) * 1024;  // bytes between consecutive weight tiles
+  char* const dx = smem + (C::NX * wid) * 1024;
+  char* const dw = smem + C::XB + wid * RW * 2 * 1024;
+
+  auto issue = [&](int c, int slot) {
+    const int xo = c * 128, wo = c * 2048;
+#pragma unroll
+    for (int i = 0; i < C::NX; ++i) mg_dma(rx, vx[i], xo, dx + slot * C::SLOT + i * 1024);
+#pragma unroll
+    for (int rt = 0; rt < RW; ++rt) {
+      if constexpr (WNT) {
+        mg_dma_nt(rw, vw + rt * wstride, wo, dw + slot * C::SLOT + (2 * rt) * 1024);
+        mg_dma_nt(rw, vw + rt * wstride, wo + 1024, dw + slot * C::SLOT + (2 * rt + 1) * 1024);
+      } else {
+        mg_dma(rw, vw + rt * wstride, wo, dw + slot * C::SLOT + (2 * rt) * 1024);
+        mg_dma(rw, vw + rt * wstride, wo + 1024, dw + slot * C::SLOT + (2 * rt + 1) * 1024);
+      }
+    }
+  };
+
+  // ---- fragment reads: x lane holds token (16 mt + (lane & 15)), k 8 (lane >> 4) .. + 8 of step s
+  // (swizzled chunk 4 s + (lane >> 4)); weight block reads are lane-linear (fragment order)
+  const int fr = lane & 15;
+  const int xo0 = fr * 128 + 16 * ((lane >> 4) ^ ((fr >> 1) & 7));
+  const int xo1 = fr * 128 + 16 * ((4 + (lane >> 4)) ^ ((fr >> 1) & 7));
+  const int wo_l = C::XB + wid * RW * 2 * 1024 + lane * 16;
+
+  f32x4 acc[RW][MT];
+#pragma unroll
+  for (int rt = 0; rt < RW; ++rt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int slot) {
+    const char* const sb = smem + slot * C::SLOT;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 wf[RW], xf[MT];
+#pragma unroll
+      for (int rt = 0; rt < RW; ++rt) wf[rt] = *(const bf16x8*)(sb + wo_l + (2 * rt + s) * 1024);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) xf[mt] = *(const bf16x8*)(sb + (s ? xo1 : xo0) + mt * 2048);
+#pragma unroll
+      for (int rt = 0; rt < RW; ++rt)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = mfma16(wf[rt], xf[mt], acc[rt][mt]);
+    }
+  };
+
+  // prologue: chunks 0 .. D-1 in flight
+#pragma unroll
+  for (int c = 0; c < C::D; ++c)
+    if (c < nch) issue(c, c);
+
+  // chunk c lives in ring slot c % SLOTS.  Before computing it: wait until this wave's DMAs of chunk c
+  // have landed (the D - 1 younger chunks stay in flight), barrier (every wave's x rows of the chunk are
+  // visible), then refill the slot of chunk c - 1 (all its reads happened before this barrier) with c + D.
+  int slot = 0;
+  for (int c = 0; c < nch; ++c) {
+    if (c + C::D - 1 < nch) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::VM_KEEP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (c + C::D < nch) issue(c + C::D, slot == 0 ? C::SLOTS - 1 : slot - 1);
+    compute(slot);
+    slot = slot == C::SLOTS - 1 ? 0 : slot + 1;
+  }
+
+  // ---- epilogue: lane holds features 16 t + 4 (lane >> 4) .. + 3 of token 16 mt + (lane & 15)
+  float* ys = y + (long long)split * M * N;
+#pragma unroll
+  for (int rt = 0; rt < RW; ++rt) {
+    const int n = 16 * (tile0 + rt) + 4 * (lane >> 4);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = 16 * mt + (lane & 15);
+      if (m < M)
+        *reinterpret_cast<float4*>(ys + (long long)m * N + n) =
+            make_float4(acc[rt][mt][0], acc[rt][mt][1], acc[rt][mt][2], acc[rt][mt][3]);
+    }
+  }
+}
+
+int g_mgemm_nt = 0;
+
+template <int MT, int RW>
+void launch_mt_rw(const bf16* x, const bf16* W, float* y, int M, int N, int K, int S, hipStream_t s) {
+  if (g_mgemm_nt)
+    mgemm_kernel<MT, RW, true><<<dim3(N / (64 * RW), S), dim3(MG_THR), 0, s>>>(x, W, y, M, N, K, K / S);
+  else
+    mgemm_kernel<MT, RW, false><<<dim3(N / (64 * RW), S), dim3(MG_THR), 0, s>>>(x, W, y, M, N, K, K / S);
+}
+
+template <int MT>
+void launch_mt(const bf16* x, const bf16* W, float* y, int M, int N, int K, int S, int rw, hipStream_t s) {
+  switch (rw) {
+    case 1: launch_mt_rw<MT, 1>(x, W, y, M, N, K, S, s); break;
+    case 3: launch_mt_rw<MT, 3>(x, W, y, M, N, K, S, s); break;
+    case 4: launch_mt_rw<MT, 4>(x, W, y, M, N, K, S, s); break;
+    default: launch_mt_rw<MT, 2>(x, W, y, M, N, K, S, s); break;
+  }
+}
+
+}  // namespace
+
+void set_mgemm_nt(int on) { g_mgemm_nt = on; }
+
+void launch_mgemm(const bf16* x, const bf16* Wshuf, float* y, int M, int N, int K, int S, int rw, hipStream_t s) {
+  if (M <= 128)
+    launch_mt<8>(x, Wshuf, y, M, N, K, S, rw, s);
+  else
+    launch_mt<16>(x, Wshuf, y, M, N, K, S, rw, s);
+}

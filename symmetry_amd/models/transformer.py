@@ -17,8 +17,9 @@ Two paths over the same weights (stored in the decode layout, models/layout.py):
   with RMSNorm deferred into the consuming GEMM (csrc/kernels/decode_gemm.hip) and the final
   norm + lm_head + sampling in dg_argmax.  Under TP the row-parallel projections write fp32,
   are all-reduced, and add_prep does the residual + norm prep.
-* general (long prefills): library GEMM (hipBLASLt through torch.matmul) + fused elementwise
-  kernels, with the layout flags on rope_cache / swiglu.
+* general (prefills): projections of 65..256 rows on the medium-M split-K kernel (mgemm, where it beats
+  the library: ops.choose_mgemm), longer ones on the library GEMM (hipBLASLt through torch.matmul), +
+  fused elementwise kernels that also sum the split-K slabs, with the layout flags on rope_cache / swiglu.
 
 All intermediates live in a preallocated :class:`Workspace`, so the decode forward is
 hipGraph-capturable.
@@ -213,6 +214,10 @@ class TransformerLM:
         t = self.dgw.get((i, name))
         return (t, True) if t is not None else (self.w.layer(i, name), False)
 
+    def _shuf(self, i: int, name: str):
+        """The MFMA-preshuffled copy of weight `name` of layer i, or None (medium-M prefill GEMMs)."""
+        return self.dgw.get((i, name))
+
     def _fused_supported(self) -> bool:
         """Shape contract of the fused decode GEMMs: D == 128, every K % 256 == 0, every N % 16 == 0."""
         cfg = self.cfg
@@ -226,14 +231,21 @@ class TransformerLM:
     def _buf(self, name, shape, dtype):
         return self.ws.get(name, shape, dtype, self.device)
 
-    def _linear(self, name: str, x: torch.Tensor, w: torch.Tensor, reduce: bool = False) -> torch.Tensor:
-        """x [T, K] bf16 -> LinOut: fp32 slabs [S, T, N] (skinny) or bf16 [T, N] (library GEMM)."""
+    def _linear(self, name: str, x: torch.Tensor, w: torch.Tensor, reduce: bool = False,
+                wshuf: torch.Tensor | None = None) -> torch.Tensor:
+        """x [T, K] bf16 -> LinOut: fp32 slabs [S, T, N] (skinny / medium-M) or bf16 [T, N] (library GEMM).
+        ``wshuf``: the MFMA-preshuffled copy of ``w`` if one exists (enables the medium-M kernel)."""
         T, K = x.shape
         N = w.shape[0]
+        pick = ops.choose_mgemm(T, N, K) if wshuf is not None and T > SKINNY_MAX_M else None
         if T <= SKINNY_MAX_M:
             S = ops.choose_splits(N, K)
             y = self._buf(name + ".slab", (S, T, N), torch.float32)
             ops.skinny_gemm(x, w, y)
+        elif pick is not None:
+            rw, S = pick
+            y = self._buf(name + ".slab", (S, T, N), torch.float32)
+            ops.mgemm(x, wshuf, y, rw)
         else:
             y = self._buf(name + ".bf16", (T, N), torch.bfloat16)
             ops.linear(x, w, out=y)
@@ -375,20 +387,21 @@ class TransformerLM:
             tok = reference.resolve_ids(b.input_ids, b.src, self.last_ids).to(torch.int32)
         ops.embed_rms_norm(tok, w["embed"], resid, w.layer(0, "ln1"), eps, x)
         for i in range(cfg.num_layers):
-            qkv = self._linear("qkv", x, w.layer(i, "wqkv"))
+            qkv = self._linear("qkv", x, w.layer(i, "wqkv"), wshuf=self._shuf(i, "wqkv"))
             ops.rope_cache(qkv, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq, self.hkv,
                            perm=True)
             self._attention(b, kv, i, q, attn)
-            o = self._linear("o", attn.view(T, self.hq * self.D), w.layer(i, "wo"), reduce=True)
+            o = self._linear("o", attn.view(T, self.hq * self.D), w.layer(i, "wo"), reduce=True,
+                             wshuf=self._shuf(i, "wo"))
             ops.add_rms_norm(o, resid, w.layer(i, "ln2"), eps, x)
             if cfg.is_moe:
                 mlp = self.moe.forward(i, x)
             else:
-                gu = self._linear("gu", x, w.layer(i, "w_gu"))
+                gu = self._linear("gu", x, w.layer(i, "w_gu"), wshuf=self._shuf(i, "w_gu"))
                 F = gu.shape[-1] // 2
                 act = self._buf("act", (T, F), torch.bfloat16)
                 ops.swiglu(gu, act, interleaved=True)
-                mlp = self._linear("down", act, w.layer(i, "w_down"), reduce=True)
+                mlp = self._linear("down", act, w.layer(i, "w_down"), reduce=True, wshuf=self._shuf(i, "w_down"))
             nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
             ops.add_rms_norm(mlp, resid, nxt, eps, x)
         return self.sample(b, x)

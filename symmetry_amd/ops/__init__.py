@@ -33,6 +33,8 @@ __all__ = [
     "attn_decode",
     "attn_prefill",
     "skinny_gemm",
+    "mgemm",
+    "choose_mgemm",
     "lm_head_sample",
     "swiglu",
     "moe_route_permute",
@@ -109,6 +111,45 @@ def skinny_gemm(x, w, y, variant: int = 0):
     if _gpu(x):
         return _native.ops().skinny_gemm(x, w, y, int(variant))
     return reference.skinny_gemm(x, w, y)
+
+
+MGEMM_MAX_M = 256
+_MGEMM_ON = os.environ.get("SYMMETRY_MGEMM", "1") != "0"  # A/B switch: 0 keeps every prefill on the library
+
+
+def mgemm(x, w_shuf, y, rw: int):
+    """Medium-M (65..256 rows) projection into fp32 split-K slabs y [S, M, N] (the skinny_gemm contract,
+    summed by the LinOut consumers); ``w_shuf`` is the MFMA-preshuffled weight (models/layout.py)."""
+    if _gpu(x):
+        return _native.ops().mgemm(x, w_shuf, y, int(rw))
+    return reference.skinny_gemm(x, reference.unshuffled(w_shuf, True), y)
+
+
+def choose_mgemm(M: int, N: int, K: int, cus: int = 256):
+    """(rw, S) of mgemm for an [M, K] x [N, K]^T projection, or None where the library GEMM is the better
+    choice.  Measured on MI355X (profiles/mgemm_r2.jsonl, each arm followed by its real consumer kernel):
+    mgemm wins for the narrow projections (N <= 8192: Llama-3-8B qkv / o / down) up to 192 rows, and for
+    long-K or wider ones (down, qkv) up to 256 rows; the wide gate_up (N = 28672) stays on hipBLASLt, which
+    already streams it at ~5.5 TB/s.  Among the grids of 128..256 workgroups (a second wave of workgroups
+    always lost), pick the smallest modelled time: per-CU intake of weight rows + activation rows over the
+    k slice at ~60 GB/s, plus the S fp32 slabs written here and summed by the consumer (~1.5 TB/s)."""
+    if not _MGEMM_ON or M > MGEMM_MAX_M or K % 64 or N > 8192 or (M > 192 and K < 8192 and N < 6144):
+        return None
+    mpad = 128 if M <= 128 else 256
+    best = None
+    for rw in (1, 2, 3, 4):
+        if N % (64 * rw) or (M > 128 and rw > 2):
+            continue
+        for S in range(1, K // 64 + 1):
+            if (K // 64) % S:
+                continue
+            wgs = N // (64 * rw) * S
+            if wgs < cus // 2 or wgs > cus:
+                continue
+            t = (64 * rw + mpad) * (K // S) * 2 / 60e3 + S * M * N * 4 / 1.5e6  # us
+            if best is None or t < best[0]:
+                best = (t, rw, S)
+    return None if best is None else (best[1], best[2])
 
 
 def lm_head_sample(x, w, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset=0, logits=None):

@@ -65,6 +65,28 @@ def test_splitk_resid_path_native(gpu, monkeypatch, graphs):
         _agree(eng.weights, p, s.output_ids, tol=0.08)
 
 
+@pytest.mark.parametrize("lens", [(40, 45), (70, 60, 50), (256,)])
+def test_medium_m_prefill_native(gpu, monkeypatch, lens):
+    """Prefill steps of 65..256 tokens run their projections on mgemm (split-K slabs summed by rope_cache /
+    add_rms_norm / swiglu) and still generate the oracle's tokens."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+
+    calls = []
+    orig = ops.mgemm
+    monkeypatch.setattr(ops, "mgemm", lambda *a, **k: calls.append(a[0].shape[0]) or orig(*a, **k))
+    eng = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", max_num_seqs=4, max_model_len=1024,
+                                 num_kv_blocks=64, use_graphs=True))
+    prompts = [list(range(400 + 17 * i, 400 + 17 * i + n)) for i, n in enumerate(lens)]
+    seqs = [eng.add_request(f"m{i}", p, SamplingParams(max_tokens=6, ignore_eos=True)) for i, p in enumerate(prompts)]
+    while eng.has_unfinished():
+        eng.step()
+    assert calls and all(64 < m <= 256 for m in calls), calls
+    for p, s in zip(prompts, seqs):
+        assert len(s.output_ids) == 6
+        _agree(eng.weights, p, s.output_ids, tol=0.08)
+
+
 def test_graph_replay_equals_eager(gpu):
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
     from symmetry_amd.engine.sequence import SamplingParams

@@ -173,6 +173,26 @@ def test_skinny_gemm(gpu, M, N, K):
     _close(y.sum(0), ref_y, atol=2e-3 * math.sqrt(K) * 0.1 + 1e-3, rtol=1e-3)
 
 
+@pytest.mark.parametrize("M", [65, 100, 128, 129, 200, 256])
+@pytest.mark.parametrize("N,K,rw,S", [(512, 1024, 1, 4), (768, 2048, 3, 8), (1024, 3584, 2, 7), (512, 512, 4, 1)])
+def test_mgemm(gpu, M, N, K, rw, S):
+    """Medium-M split-K GEMM on the preshuffled weight: every slab is the partial product over its k slice
+    (fp32 reference), rows past M untouched; ragged M (not a multiple of 16) exercises the zero-filled rows."""
+    from symmetry_amd.models.layout import preshuffle
+
+    if M > 128 and rw > 2:
+        pytest.skip("rw <= 2 above 128 rows")
+    g = torch.Generator(device=gpu).manual_seed(M * 7 + N)
+    x = torch.randn(M, K, device=gpu, generator=g).bfloat16()
+    w = (torch.randn(N, K, device=gpu, generator=g) * 0.02).bfloat16()
+    y = torch.full((S, M, N), float("nan"), device=gpu)
+    ops.mgemm(x, preshuffle(w), y, rw)
+    kc = K // S
+    for s in range(S):
+        ref_s = x[:, s * kc:(s + 1) * kc].float() @ w[:, s * kc:(s + 1) * kc].float().t()
+        _close(y[s], ref_s, atol=2e-3 * math.sqrt(kc) * 0.1 + 1e-3, rtol=1e-3)
+
+
 def test_lm_head_sample(gpu):
     M, N, K = 10, 128256 // 16 * 16, 4096
     g = torch.Generator(device=gpu).manual_seed(7)

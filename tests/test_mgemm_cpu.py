@@ -1,0 +1,66 @@
+"""Medium-M projection path (ops.mgemm / ops.choose_mgemm) on the CPU: the tile chooser only returns
+configurations the kernel accepts, the CPU op matches the split-K slab contract, and the general forward
+gives the same logits with its projections routed through mgemm slabs."""
+import pytest
+import torch
+
+from symmetry_amd import ops
+from symmetry_amd.models.layout import preshuffle
+from symmetry_amd.ops import reference
+
+
+@pytest.mark.parametrize("M", [65, 80, 128, 129, 192, 256])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 4096), (4096, 14336), (28672, 4096), (1536, 1024),
+                                 (1024, 3584), (7168, 1024), (10240, 8192), (8192, 28672)])
+def test_chooser_respects_kernel_contract(M, N, K):
+    pick = ops.choose_mgemm(M, N, K)
+    if pick is None:
+        return
+    rw, S = pick
+    assert 1 <= rw <= 4 and (M <= 128 or rw <= 2)
+    assert N % (64 * rw) == 0 and K % (64 * S) == 0
+    assert 128 <= N // (64 * rw) * S <= 256
+
+
+def test_chooser_keeps_wide_and_long_prefills_on_the_library():
+    assert ops.choose_mgemm(128, 28672, 4096) is None  # gate_up: hipBLASLt streams it at ~5.5 TB/s
+    assert ops.choose_mgemm(300, 4096, 4096) is None   # beyond the medium range
+    assert ops.choose_mgemm(256, 4096, 4096) is None   # o at 256 rows: library measured faster
+    assert ops.choose_mgemm(128, 4096, 14336) == (2, 8)
+
+
+def test_cpu_op_matches_slab_contract():
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(100, 512, generator=g).bfloat16()
+    w = (torch.randn(256, 512, generator=g) * 0.05).bfloat16()
+    y = torch.empty(4, 100, 256)
+    ops.mgemm(x, preshuffle(w), y, 1)
+    ref = torch.empty_like(y)
+    reference.skinny_gemm(x, w, ref)
+    assert torch.allclose(y, ref)
+
+
+def test_general_forward_through_mgemm_slabs(monkeypatch):
+    """An 80-token prefill on the general path with the projections routed through mgemm slabs (CPU op on
+    preshuffled copies) generates the fp32 oracle's greedy tokens."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+    from symmetry_amd.models import reference_model as rm
+
+    calls = []
+    real = ops.mgemm
+    monkeypatch.setattr(ops, "choose_mgemm", lambda M, N, K, cus=256: (1, 2) if N % 64 == 0 and M > 64 else None)
+    monkeypatch.setattr(ops, "mgemm", lambda *a: calls.append(a[0].shape[0]) or real(*a))
+    eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=2, max_model_len=256,
+                                 num_kv_blocks=32, block_size=16, use_graphs=False, seed=0))
+    m = eng.model
+    m.fused = False
+    m.dgw = {(i, n): preshuffle(m.w.layer(i, n)) for i in range(m.cfg.num_layers)
+             for n in ("wqkv", "wo", "w_gu", "w_down")}
+    prompt = [3 + (7 * i) % 400 for i in range(80)]
+    out = eng.generate(prompt, SamplingParams(max_tokens=5, temperature=0.0))
+    assert calls and set(calls) == {80}
+    lg = rm.forward_logits(eng.weights.to("cpu"), prompt + out[:-1])
+    for j, t in enumerate(out):
+        row = lg[len(prompt) - 1 + j]
+        assert float(row.max() - row[t]) <= 0.05, (j, t, int(row.argmax()))
