@@ -79,15 +79,23 @@ def main():
             t_lib_c = timed(lambda: (torch.matmul(x, w.t(), out=yb), consume(yb)))
             print(json.dumps({"T": T, "gemm": name, "arm": "hipblaslt", "gemm_us": round(t_lib, 2),
                               "with_consumer_us": round(t_lib_c, 2)}), flush=True)
+            if T <= 64:  # the general path's kernel below 65 rows: split-K skinny GEMM into slabs
+                Ss = ops.choose_splits(N, K)
+                ysk = torch.empty(Ss, T, N, device=dev, dtype=torch.float32)
+                t_sk = timed(lambda: ops.skinny_gemm(x, w, ysk))
+                t_sk_c = timed(lambda: (ops.skinny_gemm(x, w, ysk), consume(ysk)))
+                print(json.dumps({"T": T, "gemm": name, "arm": f"skinny S{Ss}", "gemm_us": round(t_sk, 2),
+                                  "with_consumer_us": round(t_sk_c, 2)}), flush=True)
+                t_lib_c = min(t_lib_c, t_sk_c)
             pick = ops.choose_mgemm(T, N, K)
             for rw in (1, 2, 3, 4):
                 if N % (64 * rw) or (T > 128 and rw > 2):
                     continue
-                for S in (1, 2, 4, 7, 8, 14, 16, 28, 32):
+                for S in (1, 2, 4, 7, 8, 14, 16, 28, 32, 56, 64):
                     if (K // 64) % S:
                         continue
                     wgs = N // (64 * rw) * S
-                    if wgs < 128 or wgs > 1024:
+                    if wgs < 128 or wgs > (512 if T <= 64 else 1024):
                         continue
                     y = torch.empty(S, T, N, device=dev, dtype=torch.float32)
                     ops.mgemm(x, ws, y, rw)

@@ -1,4 +1,4 @@
-// Medium-M projection GEMM (prefill chunks of 65..256 tokens): fp32 split-K slabs
+// Medium-M projection GEMM (17..256 rows: prefill chunks, wide decode batches): fp32 split-K slabs
 //   y[s][m][n] = sum_{k in slice s} x[m][k] * W[n][k],   x [M][K], W [N][K] bf16, M <= 256.
 //
 // Why a separate kernel: at these M a projection is still weight-streaming (Llama-3-8B: 128 tokens x
@@ -15,7 +15,7 @@
 //     that the consumer (rope_cache / add_rms_norm / swiglu, LinOut) sums in its prologue, as the skinny
 //     decode GEMM's do;
 //   * x AND the weight blocks stream through an LDS ring of 64-deep chunks by LDS-DMA (buffer loads: x
-//     rows past M read as zeros), up to 4 chunks ahead (as many as 160 KB of LDS holds), so one counted
+//     rows past M read as zeros), up to 7 chunks ahead (as many as 160 KB of LDS holds), so one counted
 //     vmcnt per chunk covers both operands (an ordinary weight load beside LDS-DMA makes hipcc drain
 //     vmcnt to 0 at its first use: cdna_hip_programming.md §5 item 4(b)); a preshuffled weight block is
 //     1 KB in fragment order, so its DMA and its ds_read_b128 are both lane-linear; the 16-B chunk index
@@ -52,9 +52,9 @@ struct MgCfg {
   static constexpr int XB = 16 * MT * 128;                   // x bytes of one 64-deep chunk
   static constexpr int WB = 4 * RW * 2 * 1024;               // weight bytes of one chunk (2 blocks per tile)
   static constexpr int SLOT = XB + WB;
-  static constexpr int SLOTS = MG_LDS / SLOT > 5 ? 5 : MG_LDS / SLOT;
+  static constexpr int SLOTS = MG_LDS / SLOT > 8 ? 8 : MG_LDS / SLOT;
   static constexpr int D = SLOTS - 1;                        // chunks in flight ahead of the computed one
-  static constexpr int NX = 16 * MT / 32;                    // x DMA instructions per wave per chunk
+  static constexpr int NX = 16 * MT / 32;                    // x DMA instructions per wave per chunk (MT >= 2)
   static constexpr int NDMA = NX + 2 * RW;                   // DMA instructions per wave per chunk
   static constexpr int VM_KEEP = (D - 1) * NDMA;             // younger DMAs left in flight at the wait
   static_assert(D >= 1 && VM_KEEP <= 63, "mgemm config");
@@ -181,6 +181,11 @@ void launch_mt_rw(const bf16* x, const bf16* W, float* y, int M, int N, int K, i
 
 template <int MT>
 void launch_mt(const bf16* x, const bf16* W, float* y, int M, int N, int K, int S, int rw, hipStream_t s) {
+  if constexpr (MT > 8) {  // 256 rows: at most 2 weight tiles per wave (accumulators + LDS ring)
+    if (rw == 1) launch_mt_rw<MT, 1>(x, W, y, M, N, K, S, s);
+    else launch_mt_rw<MT, 2>(x, W, y, M, N, K, S, s);
+    return;
+  }
   switch (rw) {
     case 1: launch_mt_rw<MT, 1>(x, W, y, M, N, K, S, s); break;
     case 3: launch_mt_rw<MT, 3>(x, W, y, M, N, K, S, s); break;
@@ -194,7 +199,11 @@ void launch_mt(const bf16* x, const bf16* W, float* y, int M, int N, int K, int 
 void set_mgemm_nt(int on) { g_mgemm_nt = on; }
 
 void launch_mgemm(const bf16* x, const bf16* Wshuf, float* y, int M, int N, int K, int S, int rw, hipStream_t s) {
-  if (M <= 128)
+  if (M <= 32)
+    launch_mt<2>(x, Wshuf, y, M, N, K, S, rw, s);
+  else if (M <= 64)
+    launch_mt<4>(x, Wshuf, y, M, N, K, S, rw, s);
+  else if (M <= 128)
     launch_mt<8>(x, Wshuf, y, M, N, K, S, rw, s);
   else
     launch_mt<16>(x, Wshuf, y, M, N, K, S, rw, s);

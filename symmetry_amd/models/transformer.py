@@ -52,6 +52,12 @@ SKINNY_MAX_M = 64
 # the run-to-run spread at 24 rows and TTFT does not move, so the threshold stays at 24.
 # SYMMETRY_SPLITK_RESID_ROWS=0 disables it (A/B).
 SPLITK_RESID_ROWS = int(os.environ.get("SYMMETRY_SPLITK_RESID_ROWS", "24"))
+# Steps with at least this many rows (and <= 64) run the general path -- medium-M projections (mgemm) +
+# consumer kernels -- instead of the fused decode GEMMs, whose per-row-tile x re-reads grow with M.
+# bench.py ms/step, fused vs general, 2 alternating runs each (profiles/general_rows_ab_r2.jsonl):
+# 10 rows 3.22 vs 3.90, 16 3.42 vs 3.94, 24 4.30 vs 3.98, 32 4.52 vs 4.07, 48 5.11 vs 4.37, 64 5.78 vs 4.63.
+# Decode batches are padded to buckets (.., 16, 24, ..), so 17..24-row steps run as 24.  0 disables.
+GENERAL_ROWS = int(os.environ.get("SYMMETRY_GENERAL_ROWS", "24"))
 MAX_STEP_SEQS = 4096  # sequences per step (rows of last_ids)
 SIGN64 = -(1 << 63)
 
@@ -237,15 +243,15 @@ class TransformerLM:
         ``wshuf``: the MFMA-preshuffled copy of ``w`` if one exists (enables the medium-M kernel)."""
         T, K = x.shape
         N = w.shape[0]
-        pick = ops.choose_mgemm(T, N, K) if wshuf is not None and T > SKINNY_MAX_M else None
-        if T <= SKINNY_MAX_M:
-            S = ops.choose_splits(N, K)
-            y = self._buf(name + ".slab", (S, T, N), torch.float32)
-            ops.skinny_gemm(x, w, y)
-        elif pick is not None:
+        pick = ops.choose_mgemm(T, N, K) if wshuf is not None else None
+        if pick is not None:
             rw, S = pick
             y = self._buf(name + ".slab", (S, T, N), torch.float32)
             ops.mgemm(x, wshuf, y, rw)
+        elif T <= SKINNY_MAX_M:
+            S = ops.choose_splits(N, K)
+            y = self._buf(name + ".slab", (S, T, N), torch.float32)
+            ops.skinny_gemm(x, w, y)
         else:
             y = self._buf(name + ".bf16", (T, N), torch.bfloat16)
             ops.linear(x, w, out=y)
@@ -268,9 +274,14 @@ class TransformerLM:
     @torch.no_grad()
     def forward(self, b: ForwardBatch, kv: KVCache) -> torch.Tensor:
         """Run one step; returns sampled token ids [num_seqs] int32 (device)."""
-        if self.fused and b.num_tokens <= SKINNY_MAX_M:
+        if self.fused and b.num_tokens <= SKINNY_MAX_M and not self._general_rows(b.num_tokens):
             return self._forward_fused(b, kv)
         return self._forward_general(b, kv)
+
+    def _general_rows(self, T: int) -> bool:
+        """Steps of GENERAL_ROWS..64 rows take the general path (medium-M projections + consumer kernels)
+        instead of the fused decode GEMMs: dense model on one GPU with the preshuffled weight copies."""
+        return (0 < GENERAL_ROWS <= T and bool(self.dgw) and not self.cfg.is_moe and not self._tp_active())
 
     # ------------------------------------------------------------------------------------------
     def _tp_active(self) -> bool:
@@ -414,6 +425,12 @@ class TransformerLM:
         keys = self._buf("keys", (n,), torch.int64)
         ntiles = self.vocab_shard // 16
         logits = self._buf("logits", (n, self.vocab_shard), torch.float32) if b.need_logits or b.filtered else None
+        if self.fused and n <= SKINNY_MAX_M:
+            # the decode lm_head kernel (row-tile variants for wide batches), on already-normalised rows
+            tk = self._buf("tile_keys", (n * ntiles,), torch.int64)
+            ops.dg_argmax(xl, self.w["lm_head"], None, self.cfg.rms_eps, b.temps, b.seeds, b.step, tk, keys, ids,
+                          self.tp_rank * self.vocab_shard, logits)
+            return self._finish_sampling(b, ids, keys, logits)
         for m0 in range(0, n, SKINNY_MAX_M):
             m1 = min(n, m0 + SKINNY_MAX_M)
             tk = self._buf("tile_keys", ((m1 - m0) * ntiles,), torch.int64)

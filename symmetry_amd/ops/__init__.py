@@ -126,19 +126,25 @@ def mgemm(x, w_shuf, y, rw: int):
 
 
 def choose_mgemm(M: int, N: int, K: int, cus: int = 256):
-    """(rw, S) of mgemm for an [M, K] x [N, K]^T projection, or None where the library GEMM is the better
-    choice.  Measured on MI355X (profiles/mgemm_r2.jsonl, each arm followed by its real consumer kernel):
-    mgemm wins for the narrow projections (N <= 8192: Llama-3-8B qkv / o / down) up to 192 rows, and for
-    long-K or wider ones (down, qkv) up to 256 rows; the wide gate_up (N = 28672) stays on hipBLASLt, which
-    already streams it at ~5.5 TB/s.  Among the grids of 128..256 workgroups (a second wave of workgroups
-    always lost), pick the smallest modelled time: per-CU intake of weight rows + activation rows over the
-    k slice at ~60 GB/s, plus the S fp32 slabs written here and summed by the consumer (~1.5 TB/s)."""
-    if not _MGEMM_ON or M > MGEMM_MAX_M or K % 64 or N > 8192 or (M > 192 and K < 8192 and N < 6144):
+    """(rw, S) of mgemm for an [M, K] x [N, K]^T projection, or None where another kernel is the better
+    choice.  Measured on MI355X (profiles/mgemm_r2.jsonl, mgemm_small_r2.jsonl; each arm followed by its
+    real consumer kernel): up to 64 rows mgemm beats both the split-K skinny GEMM and hipBLASLt on every
+    Llama-3-8B projection; above 64 rows it wins for the narrow ones (N <= 8192: qkv / o / down) up to 192
+    rows and for long-K or wider ones (down, qkv) up to 256, while the wide gate_up (N = 28672) stays on
+    hipBLASLt.  A second wave of workgroups always lost, so only grids of 128..256 workgroups are
+    considered, ranked by a linear model fitted to those sweeps: per-workgroup intake (64 rw weight rows +
+    M activation rows over the k slice) at a per-CU rate that drops with the LDS ring depth (fewer slots
+    at more rows), plus the S fp32 slabs written here and summed by the consumer, plus a fixed cost per
+    workgroup spread over the grid."""
+    if not _MGEMM_ON or M > MGEMM_MAX_M or K % 64:
         return None
-    mpad = 128 if M <= 128 else 256
+    if M > 64 and (N > 8192 or (M > 192 and K < 8192 and N < 6144)):
+        return None
+    mt = 2 if M <= 32 else 4 if M <= 64 else 8 if M <= 128 else 16
+    a_us_mb, b_us_mb = {2: (11.5, 2.2), 4: (11.5, 2.2), 8: (20.0, 1.0), 16: (30.0, 1.0)}[mt]
     best = None
     for rw in (1, 2, 3, 4):
-        if N % (64 * rw) or (M > 128 and rw > 2):
+        if N % (64 * rw) or (mt == 16 and rw > 2):
             continue
         for S in range(1, K // 64 + 1):
             if (K // 64) % S:
@@ -146,7 +152,8 @@ def choose_mgemm(M: int, N: int, K: int, cus: int = 256):
             wgs = N // (64 * rw) * S
             if wgs < cus // 2 or wgs > cus:
                 continue
-            t = (64 * rw + mpad) * (K // S) * 2 / 60e3 + S * M * N * 4 / 1.5e6  # us
+            t = (a_us_mb * (64 * rw + M) * (K // S) * 2 / 1e6 + b_us_mb * S * M * N * 4 / 1e6
+                 + 1000.0 / wgs)  # per-workgroup fixed cost (prologue, epilogue), spread over the grid
             if best is None or t < best[0]:
                 best = (t, rw, S)
     return None if best is None else (best[1], best[2])

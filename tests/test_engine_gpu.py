@@ -65,6 +65,32 @@ def test_splitk_resid_path_native(gpu, monkeypatch, graphs):
         _agree(eng.weights, p, s.output_ids, tol=0.08)
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_general_rows_decode_native(gpu, monkeypatch, graphs):
+    """Decode steps on the general path (mgemm projections -> rope_cache / add_rms_norm / swiglu summing
+    the slabs -> decode lm_head on normalised rows), as wide batches run it, against the fp32 oracle; the
+    threshold is lowered so a small batch takes it."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+    from symmetry_amd.models import transformer
+
+    calls = []
+    orig = ops.mgemm
+    monkeypatch.setattr(ops, "mgemm", lambda *a, **k: calls.append(a[0].shape[0]) or orig(*a, **k))
+    monkeypatch.setattr(transformer, "GENERAL_ROWS", 1)
+    eng = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", max_num_seqs=6, max_model_len=1024,
+                                 num_kv_blocks=64, use_graphs=graphs))
+    prompts = [list(range(700 + 9 * i, 720 + 11 * i)) for i in range(5)]
+    seqs = [eng.add_request(f"gr{i}", p, SamplingParams(max_tokens=8, ignore_eos=True))
+            for i, p in enumerate(prompts)]
+    while eng.has_unfinished():
+        eng.step()
+    assert calls and min(calls) <= 8  # decode steps went through mgemm
+    for p, s in zip(prompts, seqs):
+        assert len(s.output_ids) == 8
+        _agree(eng.weights, p, s.output_ids, tol=0.08)
+
+
 @pytest.mark.parametrize("lens", [(40, 45), (70, 60, 50), (256,)])
 def test_medium_m_prefill_native(gpu, monkeypatch, lens):
     """Prefill steps of 65..256 tokens run their projections on mgemm (split-K slabs summed by rope_cache /

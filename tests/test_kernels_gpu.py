@@ -173,7 +173,7 @@ def test_skinny_gemm(gpu, M, N, K):
     _close(y.sum(0), ref_y, atol=2e-3 * math.sqrt(K) * 0.1 + 1e-3, rtol=1e-3)
 
 
-@pytest.mark.parametrize("M", [65, 100, 128, 129, 200, 256])
+@pytest.mark.parametrize("M", [1, 17, 40, 64, 65, 100, 128, 129, 200, 256])
 @pytest.mark.parametrize("N,K,rw,S", [(512, 1024, 1, 4), (768, 2048, 3, 8), (1024, 3584, 2, 7), (512, 512, 4, 1)])
 def test_mgemm(gpu, M, N, K, rw, S):
     """Medium-M split-K GEMM on the preshuffled weight: every slab is the partial product over its k slice
