@@ -62,10 +62,13 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if torch.cuda.is_available():
-        torch.cuda.set_device(local)
+        torch.cuda.set_device(local % torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo",
-                                device_id=torch.device("cuda", local) if torch.cuda.is_available() else None)
+        # SYMMETRY_DIST_BACKEND=gloo rehearses the multi-rank flow with several ranks on one GPU (RCCL
+        # refuses two ranks on one device); the driver's multi-GPU runs use RCCL
+        backend = os.environ.get("SYMMETRY_DIST_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(backend, device_id=torch.device("cuda", local)
+                                if torch.cuda.is_available() and backend == "nccl" else None)
 
     from symmetry_amd import ops
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
