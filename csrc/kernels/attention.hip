@@ -54,6 +54,218 @@ __global__ __launch_bounds__(DWAVES * 64, 4) void attn_decode_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
+// Decode, long contexts: one wave per (seq, kv head, 384-token partition) streaming its K/V groups
+// through a private LDS ring by LDS-DMA
+// ---------------------------------------------------------------------------------------------
+// The grid kernel above gives every wave ONE 32-token group: at 2K+ contexts each unit is one load round
+// trip followed by a cross-wave merge and a split-KV publish, so HBM idles through the finish phases
+// (2.9 TB/s at 2K in a real decode step).  Here a single-wave workgroup walks SG groups of its partition
+// with up to 3 groups' K/V in flight by LDS-DMA (16 KB per group, a 64 KB ring, two workgroups per CU:
+// ~96 KB in flight per CU without spending registers), reuses the group math of attn_decode.h
+// (compute_group) on fragments read from the ring, and publishes one partial per 384 tokens into the same
+// split-KV combine.  LDS images are XOR-swizzled so every fragment read is bank-conflict free:
+//   K: 32 token rows x 256 B, 16-B chunk ^ ((t & 3) | ((t >> 4) & 1) << 3);
+//   V: 128 dim rows x 64 B (32 tokens), chunk ^ {0, 2, 3, 1}[(d >> 2) & 3].
+// SG: 32-token groups per streamed partition; SNS: ring slots (16 KB each: K 8 KB + V 8 KB)
+
+SYM_DEV int kswz(int t) { return (t & 3) | (((t >> 4) & 1) << 3); }
+SYM_DEV int vswz(int d) { return (0x1320 >> (4 * ((d >> 2) & 3))) & 3; }
+
+SYM_DEV unsigned sm_addr(const char* p) {
+  return (unsigned)(unsigned long long)(const __attribute__((address_space(3))) char*)p;
+}
+
+SYM_DEV void glds16(const bf16* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+template <int N>
+SYM_DEV void wait_vm_groups() {  // all but the N youngest groups' 16 DMAs each
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+}
+
+template <int GMAX, int SG, int SNS>
+__global__ __launch_bounds__(64) void attn_decode_stream_kernel(
+    const bf16* __restrict__ q, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    const int* __restrict__ block_tables, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
+    float* __restrict__ tmp_o, float* __restrict__ tmp_ml, int* __restrict__ counters, int Hq, int Hkv, int BS,
+    int max_blocks, int max_parts, float scale_log2) {
+  static_assert((SNS & (SNS - 1)) == 0 && SNS >= 2 && SNS <= 4 + 1, "ring slots");
+  constexpr int SPART = SG * 32;
+  __shared__ __attribute__((aligned(1024))) char smem[SNS * 16384];
+  const int seq = blockIdx.x, kvh = blockIdx.y, part = blockIdx.z;
+  const int lane = threadIdx.x;
+  const int r16 = lane & 15, h = lane >> 4;
+  const int G = Hq / Hkv;
+  const int bsh = __builtin_ctz(BS);
+  const int* bt = block_tables + (long long)seq * max_blocks;
+  const int t0 = part * SPART;
+  // context, this lane's block-table entry (lane g: group g of the partition) and the query are
+  // independent loads: one round trip before the stream starts
+  const int myblk = bt[min((t0 + 32 * min(lane, SG - 1)) >> bsh, max_blocks - 1)];
+  bf16x8 qf[4];
+  load_q(q, seq, Hq, kvh, G, qf);
+  const int ctx = ctx_lens[seq];
+  if (t0 >= ctx) return;
+  const int ng = min(SG, (ctx - t0 + 31) >> 5);
+
+  // DMA of group g into ring slot so: K rows token-major (8 x 1 KB: 4 rows of 256 B each), V rows
+  // dim-major (8 x 1 KB: 16 dims x 64 B each); the swizzle permutes the SOURCE chunks, the LDS image
+  // is written lane-linear
+  const int kt = lane >> 4, kc = lane & 15;   // K: row within a 4-row piece, chunk
+  const int vd = lane >> 2, vc = lane & 3;    // V: dim within a 16-dim piece, chunk
+  auto issue = [&](int g, int so) {
+    const int blk = __shfl(myblk, g, 64);
+    const int boff = (t0 + 32 * g) & (BS - 1);
+    const bf16* kb = k_cache + (((long long)blk * Hkv + kvh) * BS + boff) * D;
+    const bf16* vb = v_cache + ((long long)blk * Hkv + kvh) * (long long)D * BS + boff;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = 4 * j + kt;
+      glds16(kb + t * D + 8 * (kc ^ kswz(t)), smem + so + j * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = 16 * j + vd;
+      glds16(vb + (long long)d * BS + 8 * (vc ^ vswz(d)), smem + so + 8192 + j * 1024);
+    }
+  };
+
+  f32x4 o[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;
+
+  // fragment read offsets (load_group's layouts): K row trow(a), dims 32 h + 8 i = chunk 4 h + i;
+  // V row 16 dt + r16, chunk h
+  const unsigned base = sm_addr(smem);
+  int koff[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int trow = (r16 >> 2) * 8 + 4 * a + (r16 & 3);
+    koff[a] = trow * 256;
+  }
+#pragma unroll
+  for (int g = 0; g < SNS - 1; ++g)
+    if (g < ng) issue(g, g * 16384);
+  for (int g = 0; g < ng; ++g) {
+    // this group's 16 DMAs landed; the (up to SNS - 2) younger groups stay in flight
+    const int younger = min(ng - 1 - g, SNS - 2);
+    if (younger >= 3) wait_vm_groups<3>();
+    else if (younger == 2) wait_vm_groups<2>();
+    else if (younger == 1) wait_vm_groups<1>();
+    else wait_vm_groups<0>();
+    const int so = (g & (SNS - 1)) * 16384;
+    if (g + SNS - 1 < ng) issue(g + SNS - 1, ((g + SNS - 1) & (SNS - 1)) * 16384);  // slot of g - 1, read before
+    KVFrag f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int trow = (r16 >> 2) * 8 + 4 * a + (r16 & 3);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        f.k[a][i] = *(const bf16x8*)(smem + so + koff[a] + 16 * ((4 * h + i) ^ kswz(trow)));
+    }
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      const int d = 16 * dt + r16;
+      f.v[dt] = *(const bf16x8*)(smem + so + 8192 + d * 64 + 16 * (h ^ vswz(d)));
+    }
+    const int tg = t0 + 32 * g;
+    compute_group(f, qf, scale_log2, [&](int a, int r) { return tg + 8 * h + 4 * a + r < ctx; }, o, m, lsum);
+  }
+  (void)base;
+
+  // ---- finish: one wave holds the whole partition state.  Lane (c = r16, h) owns query column c,
+  // dims 16 dt + 4 h + r.
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  const int nparts = (ctx + SPART - 1) / SPART;
+  const bool col = r16 < G;
+  const int head = kvh * G + r16;
+  if (nparts == 1) {
+    if (col) {
+      const float inv = 1.f / lsum;
+      bf16* op = out + ((long long)seq * Hq + head) * D + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[dt][r] * inv);
+        *reinterpret_cast<bf16x4*>(op + 16 * dt) = v;
+      }
+    }
+    return;
+  }
+  // split-KV publish (write-through partials, drained, then the arrival counter; the last partition
+  // combines: the hand-off protocol of attn_finish in attn_decode.h)
+  if (col) {
+    const long long pb = (((long long)seq * Hq + head) * max_parts + part);
+    float* po = tmp_o + pb * D + 4 * h;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        __hip_atomic_store(po + 16 * dt + r, o[dt][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (h == 0) {
+      __hip_atomic_store(tmp_ml + pb * 2, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(tmp_ml + pb * 2 + 1, lsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int* cnt = counters + (long long)seq * Hkv + kvh;
+  int old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0, 64);
+  if (old != nparts - 1) return;
+  // combine: lane (qq = lane >> 4 within a batch of 4 query columns, 8 dims d0 = (lane & 15) * 8)
+  const int d0 = (lane & 15) * 8;
+  for (int c0 = 0; c0 < G; c0 += 4) {
+    const int qq = c0 + (lane >> 4);
+    if (qq < G) {
+      const long long bb = ((long long)seq * Hq + kvh * G + qq) * max_parts;
+      float M = -INFINITY, L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int p0 = 0; p0 < nparts; p0 += 4) {
+        float mp[4], lp[4], vp[4][8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int p = min(p0 + i, nparts - 1);
+          mp[i] = __hip_atomic_load(tmp_ml + (bb + p) * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          lp[i] = __hip_atomic_load(tmp_ml + (bb + p) * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const float* po = tmp_o + (bb + p) * D + d0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) vp[i][j] = __hip_atomic_load(po + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        float mb = M;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (p0 + i < nparts) mb = fmaxf(mb, mp[i]);
+        const float fo = __builtin_amdgcn_exp2f(M - mb);
+        L *= fo;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] *= fo;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float f = p0 + i < nparts ? __builtin_amdgcn_exp2f(mp[i] - mb) : 0.f;
+          L += lp[i] * f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += vp[i][j] * f;
+        }
+        M = mb;
+      }
+      const float inv = 1.f / L;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] *= inv;
+      store8(out + ((long long)seq * Hq + kvh * G + qq) * D + d0, acc);
+    }
+  }
+  if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Prefill (varlen, causal, paged, chunked)
 // ---------------------------------------------------------------------------------------------
 // tiles[i] = {seq, first query row within the seq's new tokens}; a tile is 64 query rows
@@ -543,13 +755,46 @@ __global__ __launch_bounds__(512, 2) void attn_prefill_m32p_kernel(
 
 }  // namespace
 
+static int g_attn_stream_min = [] {
+  const char* knob = getenv("SYMMETRY_ATTN_STREAM_MIN");
+  return knob ? atoi(knob) : 1024;
+}();
+
+void set_attn_stream_min(int tokens) { g_attn_stream_min = tokens; }
+
+// A/B knob (partition length x ring depth of the streaming kernel): SYMMETRY_ATTN_STREAM_CFG
+static int g_attn_stream_cfg = [] {
+  const char* knob = getenv("SYMMETRY_ATTN_STREAM_CFG");
+  return knob ? atoi(knob) : 0;
+}();
+
 void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,
                         const int* ctx_lens, bf16* out, float* tmp_o, float* tmp_ml, int* counters, int num_seqs,
                         int Hq, int Hkv, int BS, int max_blocks, int max_parts, float scale, hipStream_t s) {
   if (num_seqs == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(num_seqs, Hkv, max_parts);
   const int G = Hq / Hkv;
+  // block tables spanning >= g_attn_stream_min tokens (the graph's context bucket): the streaming
+  // one-wave kernel
+  const int span = max_blocks * BS;
+  if (g_attn_stream_min > 0 && span >= g_attn_stream_min && BS >= 32 && G <= 16) {
+    // partitions of SG 32-token groups (>= 256 tokens: sparts <= max_parts, sized for 256-token ones)
+    auto run = [&](auto kern, int sg) {
+      const dim3 g(num_seqs, Hkv, (span + 32 * sg - 1) / (32 * sg));
+      kern<<<g, 64, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters, Hq, Hkv, BS,
+                            max_blocks, max_parts, scale_log2);
+    };
+    switch (g_attn_stream_cfg) {
+      case 1: run(attn_decode_stream_kernel<16, 8, 4>, 8); break;
+      case 2: run(attn_decode_stream_kernel<16, 12, 2>, 12); break;
+      case 3: run(attn_decode_stream_kernel<16, 24, 4>, 24); break;
+      case 4: run(attn_decode_stream_kernel<16, 16, 4>, 16); break;
+      case 5: run(attn_decode_stream_kernel<16, 8, 2>, 8); break;
+      default: run(attn_decode_stream_kernel<16, 12, 4>, 12); break;
+    }
+    return;
+  }
+  dim3 grid(num_seqs, Hkv, max_parts);
   if (G <= 4)
     attn_decode_kernel<4><<<grid, DWAVES * 64, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml,
                                                        counters, Hq, Hkv, BS, max_blocks, max_parts, scale_log2);

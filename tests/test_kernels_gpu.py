@@ -105,9 +105,17 @@ def _random_paged(gpu, ctx_lens, Hkv, BS, g, extra_blocks=3):
     return kc, vc, bt.to(gpu)
 
 
+@pytest.fixture(params=["grid", "stream"])
+def attn_decode_kernel(request):
+    """The grid split-KV kernel and the streaming long-context kernel (chosen by block-table span)."""
+    torch.ops.symmetry_amd.attn_stream_min(0 if request.param == "grid" else 1)
+    yield request.param
+    torch.ops.symmetry_amd.attn_stream_min(1024)
+
+
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 1), (16, 16)])
 @pytest.mark.parametrize("BS", [32, 64])
-def test_attn_decode(gpu, Hq, Hkv, BS):
+def test_attn_decode(gpu, attn_decode_kernel, Hq, Hkv, BS):
     g = torch.Generator(device=gpu).manual_seed(3)
     ctx_lens = [1, 17, 64, 255, 256, 257, 511, 512, 513, 1000, 2049, 4100]
     kc, vc, bt = _random_paged(gpu, ctx_lens, Hkv, BS, g)
