@@ -252,6 +252,11 @@ class TransformerLM:
             S = ops.choose_splits(N, K)
             y = self._buf(name + ".slab", (S, T, N), torch.float32)
             ops.skinny_gemm(x, w, y)
+        elif not self.cfg.is_moe and (S := ops.lib_splits(T, N, K)) > 1 and K % S == 0:
+            # (dense models only: fp32 slabs instead of bf16 GEMM outputs shift MoE router logits enough to
+            # flip near-tied top-2 choices against the fp32 oracle of the tiny random test model)
+            y = self._buf(name + ".slab", (S, T, N), torch.float32)
+            ops.linear_splitk(x, w, y)
         else:
             y = self._buf(name + ".bf16", (T, N), torch.bfloat16)
             ops.linear(x, w, out=y)

@@ -51,6 +51,8 @@ __all__ = [
     "sample_filtered",
     "decode_mlp",
     "linear",
+    "lib_splits",
+    "linear_splitk",
     "choose_splits",
 ]
 
@@ -290,6 +292,32 @@ def sample_filtered(logits, temps, top_k, top_p, seeds, step, out_ids):
 def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """Plain library GEMM ``x @ w.T`` (hipBLASLt via torch on the GPU) for prefill-sized M."""
     return torch.matmul(x, w.t(), out=out)
+
+
+def lib_splits(M: int, N: int, K: int) -> int:
+    """k split of a library prefill GEMM run as one strided-batched GEMM into fp32 slabs (linear_splitk).
+    The narrow projections (N <= 8192) of 257..768-token prefills (and long-K ones up to 1536) leave most CUs
+    idle as one GEMM; measured (profiles/prefill_splitk_lib_r2.jsonl, each with its consumer): 512 tokens
+    down 81 -> 65 us (S = 4), o 34 -> 32, qkv 32 -> 28 (S = 2); 1280 tokens down 141 -> 132 (S = 2); beyond,
+    the single GEMM wins."""
+    if N > 8192 or N < 256 or not _MGEMM_ON:  # (N < 256: MoE routers keep their single GEMM)
+        return 1
+    if M <= 768:
+        return 4 if K >= 8192 else 2
+    if M <= 1536 and K >= 8192:
+        return 2
+    return 1
+
+
+def linear_splitk(x: torch.Tensor, w: torch.Tensor, y: torch.Tensor) -> None:
+    """y [S, M, N] fp32 = the S k-slice partial products of x @ w.T (the skinny_gemm slab contract) as one
+    strided-batched library GEMM with fp32 output (hipBLASLt), summed by the LinOut consumer."""
+    S, M, N = y.shape
+    K = x.shape[1]
+    if x.device.type == "cpu":
+        return reference.skinny_gemm(x, w, y)
+    kc = K // S
+    torch.bmm(x.view(M, S, kc).permute(1, 0, 2), w.view(N, S, kc).permute(1, 2, 0), out_dtype=torch.float32, out=y)
 
 
 def choose_splits(N: int, K: int, target_wgs: int = 1024, min_k_per_wave: int = 128) -> int:

@@ -113,6 +113,28 @@ def test_medium_m_prefill_native(gpu, monkeypatch, lens):
         _agree(eng.weights, p, s.output_ids, tol=0.08)
 
 
+@pytest.mark.parametrize("lens", [(300,), (200, 400)])
+def test_splitk_library_prefill_native(gpu, monkeypatch, lens):
+    """257..768-token prefills: narrow projections as k-split strided-batched hipBLASLt GEMMs with fp32
+    slabs (ops.linear_splitk) summed by the consumer kernels, against the fp32 oracle."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+
+    calls = []
+    orig = ops.linear_splitk
+    monkeypatch.setattr(ops, "linear_splitk", lambda x, w, y: calls.append(tuple(y.shape)) or orig(x, w, y))
+    eng = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", max_num_seqs=4, max_model_len=1024,
+                                 num_kv_blocks=64, use_graphs=True))
+    prompts = [list(range(900 + 13 * i, 900 + 13 * i + n)) for i, n in enumerate(lens)]
+    seqs = [eng.add_request(f"s{i}", p, SamplingParams(max_tokens=5, ignore_eos=True)) for i, p in enumerate(prompts)]
+    while eng.has_unfinished():
+        eng.step()
+    assert calls
+    for p, s in zip(prompts, seqs):
+        assert len(s.output_ids) == 5
+        _agree(eng.weights, p, s.output_ids, tol=0.08)
+
+
 def test_graph_replay_equals_eager(gpu):
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
     from symmetry_amd.engine.sequence import SamplingParams

@@ -97,3 +97,25 @@ def test_general_rows_decode_matches_fused(monkeypatch):
                 row = lg[len(p) - 1 + j]
                 assert float(row.max() - row[t]) <= 0.08, (general, j, t, int(row.argmax()))
     assert [o[0] for o in outs[0]] == [o[0] for o in outs[1]]
+
+
+def test_splitk_library_prefill_matches_oracle(monkeypatch):
+    """A 300-token prefill runs its narrow projections as k-split batched library GEMMs into fp32 slabs
+    (ops.linear_splitk, summed by the consumers) and still generates the fp32 oracle's tokens."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+    from symmetry_amd.models import reference_model as rm
+
+    calls = []
+    real = ops.linear_splitk
+    monkeypatch.setattr(ops, "linear_splitk", lambda x, w, y: calls.append(tuple(y.shape)) or real(x, w, y))
+    eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=2, max_model_len=512,
+                                 num_kv_blocks=32, block_size=16, use_graphs=False, seed=0))
+    eng.model.fused = False
+    prompt = [3 + (11 * i) % 450 for i in range(300)]
+    out = eng.generate(prompt, SamplingParams(max_tokens=3, temperature=0.0))
+    assert calls and all(c[0] == 2 and c[1] == 300 for c in calls), calls
+    lg = rm.forward_logits(eng.weights.to("cpu"), prompt + out[:-1])
+    for j, t in enumerate(out):
+        row = lg[len(prompt) - 1 + j]
+        assert float(row.max() - row[t]) <= 0.05, (j, t, int(row.argmax()))
