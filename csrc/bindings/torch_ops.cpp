@@ -611,6 +611,31 @@ void sample_filtered(const Tensor& logits, const Tensor& temps, const Tensor& to
                          reinterpret_cast<const long long*>(step.data_ptr()), ptr<int>(out_ids), cur_stream(logits));
 }
 
+void logits_argmax(const Tensor& logits, const Tensor& temps, const Tensor& seeds, const Tensor& step, int64_t n_offset,
+                   Tensor& out_keys, Tensor& out_ids) {
+  check_gpu(logits, "logits");
+  check_dtype(logits, at::kFloat, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "logits_argmax: logits [B, V] contiguous");
+  const int64_t B = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(n_offset >= 0 && n_offset + V < (1LL << 31), "logits_argmax: vocab index range");
+  for (const Tensor* t : {&temps, &seeds, &step, static_cast<const Tensor*>(&out_keys),
+                          static_cast<const Tensor*>(&out_ids)})
+    check_gpu(*t, "sampling tensor");
+  check_dtype(temps, at::kFloat, "temps");
+  check_dtype(seeds, at::kLong, "seeds");
+  check_dtype(step, at::kLong, "step");
+  check_dtype(out_keys, at::kLong, "out_keys");
+  check_dtype(out_ids, at::kInt, "out_ids");
+  TORCH_CHECK(temps.numel() >= B && seeds.numel() >= B && out_keys.numel() >= B && out_ids.numel() >= B &&
+                  step.numel() >= 1,
+              "logits_argmax: per-row tensors too short");
+  const at::OptionalDeviceGuard g(logits.device());
+  launch_logits_argmax(ptr<float>(logits), (int)B, (int)V, ptr<float>(temps),
+                       reinterpret_cast<const long long*>(seeds.data_ptr()),
+                       reinterpret_cast<const long long*>(step.data_ptr()), (int)n_offset,
+                       reinterpret_cast<unsigned long long*>(out_keys.data_ptr()), ptr<int>(out_ids), cur_stream(logits));
+}
+
 void decode_mlp(const Tensor& attn, const Tensor& Wo, const Tensor& Wgu, const Tensor& Wd, Tensor& resid,
                 const Tensor& ln2, const Tensor& w_next, Tensor& xw, Tensor& ss, Tensor& act, Tensor& ctl, double eps,
                 bool wshuf) {
@@ -818,6 +843,10 @@ TORCH_LIBRARY(symmetry_amd, m) {
       "sample_filtered(Tensor logits, Tensor temps, Tensor top_k, Tensor top_p, Tensor seeds, Tensor step, "
       "Tensor(a!) out_ids) -> ()",
       &sample_filtered);
+  m.def(
+      "logits_argmax(Tensor logits, Tensor temps, Tensor seeds, Tensor step, int n_offset, Tensor(a!) out_keys, "
+      "Tensor(b!) out_ids) -> ()",
+      &logits_argmax);
   m.def(
       "decode_block(Tensor xw, Tensor Wqkv, Tensor? ss_in, float eps, Tensor positions, Tensor slots, Tensor cos_sin, "
       "Tensor(a!) q, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor ctx_lens, Tensor(d!) attn, "

@@ -155,6 +155,11 @@ void launch_argmax_reduce(const unsigned long long* tile_keys, int M, int ntiles
 // filter (or greedy) keep out_ids untouched
 void launch_sample_filtered(const float* logits, int B, int V, const float* temps, const int* top_k, const float* top_p,
                             const long long* seeds, const long long* step, int* out_ids, hipStream_t s);
+// greedy / temperature (Gumbel-max) sampling over fp32 logits [B, V]: the fused lm_head
+// epilogue's keys and RNG, for decode batches wider than the fused kernels
+void launch_logits_argmax(const float* logits, int B, int V, const float* temps, const long long* seeds,
+                          const long long* step, int n_offset, unsigned long long* out_keys, int* out_ids,
+                          hipStream_t s);
 
 // activation.hip
 void launch_swiglu(LinOut gu, bf16* out, int T, int F, hipStream_t s, int interleaved = 0);

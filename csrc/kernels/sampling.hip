@@ -154,7 +154,53 @@ __global__ __launch_bounds__(NT) void sample_filtered_kernel(const float* __rest
   }
 }
 
+// Greedy / plain-temperature sampling over materialised fp32 logits [B, V], for decode batches wider
+// than the fused lm_head kernels take (> 64 rows; the logits come from one library GEMM).  Same packed
+// key (order-preserving value bits, ~global vocab index: the smallest index wins a tie) and the same
+// counter-based Gumbel noise, v / t - log(-log(u)), as the fused epilogue (skinny_gemm.hip), so a row
+// samples the same token whichever path its batch took.  One workgroup per row, the row read once.
+__global__ __launch_bounds__(NT) void logits_argmax_kernel(const float* __restrict__ logits, int V,
+                                                           const float* __restrict__ temps,
+                                                           const long long* __restrict__ seeds,
+                                                           const long long* __restrict__ step, int n_offset,
+                                                           unsigned long long* __restrict__ out_keys,
+                                                           int* __restrict__ out_ids) {
+  __shared__ unsigned long long s_best[NT / 64];
+  const int r = blockIdx.x;
+  const float t = temps[r];
+  const float* row = logits + (long long)r * V;
+  const unsigned long long seed = (unsigned long long)seeds[r] ^ ((unsigned long long)step[0] << 20);
+  unsigned long long best = 0;
+  for (int i = threadIdx.x; i < V; i += NT) {
+    const uint32_t g = (uint32_t)(n_offset + i);
+    float v = row[i];
+    if (t > 0.f) v = v / t - __logf(-__logf(uniform01(seed, (unsigned long long)g)));
+    const unsigned long long key = ((unsigned long long)okey(v) << 32) | (unsigned long long)(0xFFFFFFFFu - g);
+    best = key > best ? key : best;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long b = __shfl_xor(best, o, 64);
+    best = b > best ? b : best;
+  }
+  if ((threadIdx.x & 63) == 0) s_best[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = s_best[0];
+    for (int i = 1; i < NT / 64; ++i) b = s_best[i] > b ? s_best[i] : b;
+    out_keys[r] = b;
+    out_ids[r] = (int)(0xFFFFFFFFu - (uint32_t)(b & 0xFFFFFFFFull));
+  }
+}
+
 }  // namespace
+
+void launch_logits_argmax(const float* logits, int B, int V, const float* temps, const long long* seeds,
+                          const long long* step, int n_offset, unsigned long long* out_keys, int* out_ids,
+                          hipStream_t s) {
+  if (B == 0) return;
+  logits_argmax_kernel<<<B, NT, 0, s>>>(logits, V, temps, seeds, step, n_offset, out_keys, out_ids);
+}
 
 void launch_sample_filtered(const float* logits, int B, int V, const float* temps, const int* top_k, const float* top_p,
                             const long long* seeds, const long long* step, int* out_ids, hipStream_t s) {

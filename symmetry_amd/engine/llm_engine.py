@@ -27,7 +27,7 @@ from ..models.config import ModelConfig, resolve
 from ..models.transformer import KVCache, TransformerLM
 from ..models.weights import ModelWeights, ShardSpec, load_hf_weights, random_weights
 from ..utils.metrics import EngineMetrics
-from .model_runner import ModelRunner
+from .model_runner import FUSED_DECODE_ROWS, MAX_DECODE_ROWS, ModelRunner
 from .scheduler import BlockManager, Scheduler, SchedulerConfig
 from .sequence import SamplingParams, Sequence, SeqStatus
 from .tokenizer import IncrementalDetokenizer, load_tokenizer
@@ -135,7 +135,7 @@ class LLMEngine:
                           self.device)
         self.blocks = BlockManager(nb, cfg.block_size, prefix_caching=cfg.enable_prefix_caching)
         self.scheduler = Scheduler(
-            SchedulerConfig(max_num_seqs=min(cfg.max_num_seqs, 64 if self.device.type != "cpu" else cfg.max_num_seqs),
+            SchedulerConfig(max_num_seqs=min(cfg.max_num_seqs, self._max_decode_rows(mcfg)),
                             max_num_batched_tokens=cfg.max_num_batched_tokens, max_model_len=max_model_len,
                             mixed_prefill_tokens=cfg.mixed_prefill_tokens),
             self.blocks)
@@ -165,6 +165,14 @@ class LLMEngine:
                 with open(path) as f:
                     return from_hf_config(json.load(f), name=cfg.model)
         return resolve(cfg.model)
+
+    def _max_decode_rows(self, mcfg: ModelConfig) -> int:
+        """Concurrent sequences per decode step on the GPU: up to MAX_DECODE_ROWS for a dense model on one
+        GPU (rows past the fused decode kernels run the general path on the medium-M GEMM, one graph per
+        bucket), FUSED_DECODE_ROWS under TP / for MoE (the CPU reference path: MAX_DECODE_ROWS)."""
+        if self.device.type == "cpu":
+            return MAX_DECODE_ROWS
+        return MAX_DECODE_ROWS if (not mcfg.is_moe and self.cfg.tp_size == 1) else FUSED_DECODE_ROWS
 
     def _graph_safe(self, tp_comm, ep_comm) -> bool:
         """Decode hipGraphs need every collective to be capturable (our RCCL communicator) and no

@@ -25,7 +25,9 @@ import torch
 from ..models.transformer import ForwardBatch, KVCache, TransformerLM
 from .scheduler import ScheduledBatch
 
-DECODE_BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64)
+DECODE_BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256)
+MAX_DECODE_ROWS = 256  # dense single-GPU models (general path on the medium-M GEMM); others: FUSED_DECODE_ROWS
+FUSED_DECODE_ROWS = 64
 CTX_BUCKETS = (512, 2048, 8192, 32768, 131072)  # tokens (multiples of the 512-token attention partition)
 CMD_STOP, CMD_CAPTURE = -1, 2  # control headers of the rank-0 -> worker metadata plane
 HEADER_LEN = 7  # kind, T, rows, max_blocks, prefill tiles, real seqs, filtered-sampling flag
@@ -104,7 +106,7 @@ class ModelRunner:
         self.max_blocks = math.ceil(max_model_len / kv.block_size)
         self.max_num_seqs = max_num_seqs
         self.buckets = [b for b in DECODE_BUCKETS if b < max_num_seqs] + [max_num_seqs]
-        self.buckets = sorted(set(b for b in self.buckets if b <= 64))
+        self.buckets = sorted(set(b for b in self.buckets if b <= MAX_DECODE_ROWS))
         bs = kv.block_size
         self.ctx_blocks = sorted({math.ceil(min(c, max_model_len) / bs) for c in CTX_BUCKETS} | {self.max_blocks})
         self.ctx_blocks = [b for b in self.ctx_blocks if b <= self.max_blocks]

@@ -9,7 +9,7 @@ Per layer (SURVEY.md §3.6)::
 
 Two paths over the same weights (stored in the decode layout, models/layout.py):
 
-* fused (<= 64 rows: every decode step, short prefills) -- five launches per dense layer::
+* fused (decode steps and short prefills below GENERAL_ROWS rows) -- five launches per dense layer::
 
       dg_qkv (norm scale + RoPE + KV write) -> attention -> dg_resid (O, residual add, ln2 prep)
       -> dg_swiglu (norm scale + SwiGLU) -> dg_resid (down, residual add, next-ln1 prep)
@@ -17,9 +17,11 @@ Two paths over the same weights (stored in the decode layout, models/layout.py):
   with RMSNorm deferred into the consuming GEMM (csrc/kernels/decode_gemm.hip) and the final
   norm + lm_head + sampling in dg_argmax.  Under TP the row-parallel projections write fp32,
   are all-reduced, and add_prep does the residual + norm prep.
-* general (prefills): projections of 65..256 rows on the medium-M split-K kernel (mgemm, where it beats
-  the library: ops.choose_mgemm), longer ones on the library GEMM (hipBLASLt through torch.matmul), +
-  fused elementwise kernels that also sum the split-K slabs, with the layout flags on rope_cache / swiglu.
+* general (prefills, and decode steps of GENERAL_ROWS..256 rows): projections of up to 256 rows on the
+  medium-M split-K kernel (mgemm, where it beats the library: ops.choose_mgemm), longer ones on the
+  library GEMM (hipBLASLt through torch.matmul), + fused elementwise kernels that also sum the split-K
+  slabs, with the layout flags on rope_cache / swiglu; batches wider than 64 rows sample from one fp32
+  logits GEMM (logits_argmax: the fused sampler's keys and RNG).
 
 All intermediates live in a preallocated :class:`Workspace`, so the decode forward is
 hipGraph-capturable.
@@ -52,7 +54,7 @@ SKINNY_MAX_M = 64
 # the run-to-run spread at 24 rows and TTFT does not move, so the threshold stays at 24.
 # SYMMETRY_SPLITK_RESID_ROWS=0 disables it (A/B).
 SPLITK_RESID_ROWS = int(os.environ.get("SYMMETRY_SPLITK_RESID_ROWS", "24"))
-# Steps with at least this many rows (and <= 64) run the general path -- medium-M projections (mgemm) +
+# Steps with at least this many rows run the general path -- medium-M projections (mgemm) +
 # consumer kernels -- instead of the fused decode GEMMs, whose per-row-tile x re-reads grow with M.
 # bench.py ms/step, fused vs general, 2 alternating runs each (profiles/general_rows_ab_r2.jsonl):
 # 10 rows 3.22 vs 3.90, 16 3.42 vs 3.94, 24 4.30 vs 3.98, 32 4.52 vs 4.07, 48 5.11 vs 4.37, 64 5.78 vs 4.63.
@@ -436,12 +438,16 @@ class TransformerLM:
             ops.dg_argmax(xl, self.w["lm_head"], None, self.cfg.rms_eps, b.temps, b.seeds, b.step, tk, keys, ids,
                           self.tp_rank * self.vocab_shard, logits)
             return self._finish_sampling(b, ids, keys, logits)
-        for m0 in range(0, n, SKINNY_MAX_M):
-            m1 = min(n, m0 + SKINNY_MAX_M)
-            tk = self._buf("tile_keys", ((m1 - m0) * ntiles,), torch.int64)
-            ops.lm_head_sample(xl[m0:m1].contiguous() if m0 or m1 < n else xl, self.w["lm_head"],
-                               b.temps[m0:m1], b.seeds[m0:m1], b.step, tk, keys[m0:m1], ids[m0:m1],
-                               self.tp_rank * self.vocab_shard, logits[m0:m1] if logits is not None else None)
+        if n <= SKINNY_MAX_M:
+            tk = self._buf("tile_keys", (n * ntiles,), torch.int64)
+            ops.lm_head_sample(xl, self.w["lm_head"], b.temps, b.seeds, b.step, tk, keys, ids,
+                               self.tp_rank * self.vocab_shard, logits)
+            return self._finish_sampling(b, ids, keys, logits)
+        # wide batches (> 64 rows): the lm_head becomes compute-shaped -- one library GEMM into fp32
+        # logits, then the fused epilogue's greedy / Gumbel-max keys over each row
+        logits = self._buf("logits", (n, self.vocab_shard), torch.float32)
+        ops.linear_splitk(xl.contiguous(), self.w["lm_head"], logits.view(1, n, self.vocab_shard))
+        ops.logits_argmax(logits, b.temps, b.seeds, b.step, keys, ids, self.tp_rank * self.vocab_shard)
         return self._finish_sampling(b, ids, keys, logits)
 
     def _finish_sampling(self, b: ForwardBatch, ids, keys, logits) -> torch.Tensor:

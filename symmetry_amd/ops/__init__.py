@@ -289,6 +289,14 @@ def sample_filtered(logits, temps, top_k, top_p, seeds, step, out_ids):
     return reference.sample_filtered(logits, temps, top_k, top_p, seeds, step, out_ids)
 
 
+def logits_argmax(logits, temps, seeds, step, out_keys, out_ids, n_offset=0):
+    """Greedy / temperature (Gumbel-max) sampling over fp32 logits [B, V]: the keys and RNG of the fused
+    lm_head epilogue, for decode batches wider than the fused kernels (> 64 rows)."""
+    if _gpu(logits):
+        return _native.ops().logits_argmax(logits, temps, seeds, step, int(n_offset), out_keys, out_ids)
+    return reference.logits_argmax(logits, temps, seeds, step, out_keys, out_ids, n_offset)
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """Plain library GEMM ``x @ w.T`` (hipBLASLt via torch on the GPU) for prefill-sized M."""
     return torch.matmul(x, w.t(), out=out)

@@ -227,6 +227,13 @@ def lm_head_sample(x, w, temps, seeds, step, tile_keys, out_keys, out_ids, n_off
     out_ids[:M].copy_(ids.to(out_ids.dtype))
 
 
+def logits_argmax(logits, temps, seeds, step, out_keys, out_ids, n_offset: int = 0) -> None:
+    keys, ids = sample_keys(logits, temps, seeds, int(step.reshape(-1)[0]), n_offset)
+    M = logits.shape[0]
+    out_keys[:M].copy_(keys)
+    out_ids[:M].copy_(ids.to(out_ids.dtype))
+
+
 def swiglu(gu, out, interleaved: bool = False) -> None:
     g = linout_sum(gu)
     F = out.shape[1]

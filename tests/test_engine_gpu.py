@@ -91,6 +91,31 @@ def test_general_rows_decode_native(gpu, monkeypatch, graphs):
         _agree(eng.weights, p, s.output_ids, tol=0.08)
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_wide_decode_batches_native(gpu, monkeypatch, graphs):
+    """More than 64 concurrent sequences: decode steps of 65..256 rows run the general path (mgemm
+    projections, one graph per bucket) and sample from one fp32 logits GEMM + logits_argmax; spot-check
+    sequences against the fp32 oracle."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+
+    rows = []
+    orig = ops.logits_argmax
+    monkeypatch.setattr(ops, "logits_argmax", lambda lg, *a, **k: rows.append(lg.shape[0]) or orig(lg, *a, **k))
+    n = 90
+    eng = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", max_num_seqs=n, max_model_len=256,
+                                 num_kv_blocks=4 * n, use_graphs=graphs))
+    assert eng.scheduler.cfg.max_num_seqs == n
+    prompts = [list(range(300 + 7 * i, 300 + 7 * i + 10 + i % 5)) for i in range(n)]
+    seqs = [eng.add_request(f"w{i}", p, SamplingParams(max_tokens=6, ignore_eos=True)) for i, p in enumerate(prompts)]
+    while eng.has_unfinished():
+        eng.step()
+    assert rows and max(rows) >= 90  # prefill of all 90 and the 96-row decode bucket sampled wide
+    for i in (0, 41, 89):
+        assert len(seqs[i].output_ids) == 6
+        _agree(eng.weights, prompts[i], seqs[i].output_ids, tol=0.08)
+
+
 @pytest.mark.parametrize("lens", [(40, 45), (70, 60, 50), (256,)])
 def test_medium_m_prefill_native(gpu, monkeypatch, lens):
     """Prefill steps of 65..256 tokens run their projections on mgemm (split-K slabs summed by rope_cache /

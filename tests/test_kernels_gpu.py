@@ -226,6 +226,29 @@ def test_lm_head_sample(gpu):
     assert (ids[5:] == ids_ref[5:]).float().mean() >= 0.8
 
 
+def test_logits_argmax(gpu):
+    """Wide-batch sampler over materialised fp32 logits: the fused epilogue's keys and RNG (greedy rows
+    and Gumbel-max rows, with a vocab-shard offset) against the torch port: the same tokens, keys equal
+    up to a few ulps of the noised value (device __logf)."""
+    M, N = 70, 32000
+    g = torch.Generator(device=gpu).manual_seed(17)
+    logits = torch.randn(M, N, device=gpu, generator=g) * 3
+    logits[3, 100] = logits[3, 200] = 1e3  # tie: the smaller vocab index wins
+    temps = torch.zeros(M, device=gpu)
+    temps[40:] = 0.7
+    seeds = torch.arange(M, device=gpu, dtype=torch.int64) * 104729 - 5
+    step = torch.tensor([23], device=gpu, dtype=torch.int64)
+    out_keys = torch.empty(M, device=gpu, dtype=torch.int64)
+    out_ids = torch.empty(M, device=gpu, dtype=torch.int32)
+    ops.logits_argmax(logits, temps, seeds, step, out_keys, out_ids, n_offset=64000)
+    keys_ref, ids_ref = ref.sample_keys(logits.cpu(), temps.cpu(), seeds.cpu(), 23, 64000)
+    assert int(out_ids[3]) == 64100
+    assert torch.equal(out_ids.cpu().long(), ids_ref)
+    kk = out_keys.cpu()
+    assert torch.equal(kk & 0xFFFFFFFF, keys_ref & 0xFFFFFFFF)  # same winning index
+    assert int(((kk >> 32) - (keys_ref >> 32)).abs().max()) <= 4  # value bits: __logf vs torch.log ulps
+
+
 def test_swiglu(gpu):
     T, F = 7, 14336
     g = torch.Generator(device=gpu).manual_seed(8)

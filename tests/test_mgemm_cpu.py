@@ -119,3 +119,46 @@ def test_splitk_library_prefill_matches_oracle(monkeypatch):
     for j, t in enumerate(out):
         row = lg[len(prompt) - 1 + j]
         assert float(row.max() - row[t]) <= 0.05, (j, t, int(row.argmax()))
+
+
+def test_wide_decode_batches_sample_from_logits(monkeypatch):
+    """Decode steps with more than 64 sequences (the GPU scheduler admits up to MAX_DECODE_ROWS for dense
+    models) sample from one fp32 logits GEMM + logits_argmax and still follow the fp32 oracle; temperature
+    rows draw the same token as the fused sampler's key on the same logits."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.model_runner import MAX_DECODE_ROWS
+    from symmetry_amd.engine.sequence import SamplingParams
+    from symmetry_amd.models import reference_model as rm
+
+    rows = []
+    real = ops.logits_argmax
+    monkeypatch.setattr(ops, "logits_argmax", lambda lg, *a, **k: rows.append(lg.shape[0]) or real(lg, *a, **k))
+    n = 70
+    eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=n, max_model_len=64,
+                                 num_kv_blocks=2 * n + 8, block_size=16, use_graphs=False, seed=0))
+    assert eng.scheduler.cfg.max_num_seqs == n <= MAX_DECODE_ROWS
+    prompts = [[3 + (5 * i + 7 * k) % 400 for k in range(4 + i % 3)] for i in range(n)]
+    seqs = [eng.add_request(f"w{i}", p, SamplingParams(max_tokens=3, temperature=0.0)) for i, p in enumerate(prompts)]
+    while eng.has_unfinished():
+        eng.step()
+    assert rows and min(rows) == n  # the prefill and every decode step sampled all rows at once
+    lw = eng.weights.to("cpu")
+    for i in (0, 33, 69):
+        p, s = prompts[i], seqs[i]
+        lg = rm.forward_logits(lw, p + s.output_ids[:-1])
+        for j, t in enumerate(s.output_ids):
+            row = lg[len(p) - 1 + j]
+            assert float(row.max() - row[t]) <= 0.05, (i, j, t, int(row.argmax()))
+    # sampled rows: logits_argmax's key == the fused lm_head sampler's key on the same logits
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(3, 64, generator=g).bfloat16()
+    w = (torch.randn(96, 64, generator=g) * 0.2).bfloat16()
+    temps = torch.tensor([0.0, 0.9, 1.3])
+    seeds = torch.tensor([11, -4, 77], dtype=torch.int64)
+    step = torch.tensor([5], dtype=torch.int64)
+    k1, i1 = torch.empty(3, dtype=torch.int64), torch.empty(3, dtype=torch.int32)
+    k2, i2 = torch.empty(3, dtype=torch.int64), torch.empty(3, dtype=torch.int32)
+    lg = torch.empty(3, 96)
+    ops.lm_head_sample(x, w, temps, seeds, step, torch.empty(3 * 6, dtype=torch.int64), k1, i1, 32, lg)
+    ops.logits_argmax(lg, temps, seeds, step, k2, i2, 32)
+    assert torch.equal(k1, k2) and torch.equal(i1, i2)
