@@ -41,8 +41,13 @@ def main():
     ap.add_argument("--seqs", type=int, default=10)
     ap.add_argument("--ctx", type=int, nargs="+", default=[64, 160, 512, 2048, 8192])
     ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--span", type=int, default=0, help="block-table width in tokens (the graph's context "
+                    "bucket; 0: just the context)")
+    ap.add_argument("--wave", type=int, nargs="+", default=[-1],
+                    help="attn_wave min-units settings to compare (-1: leave the default; 0: never; 1: always)")
     args = ap.parse_args()
     dev = torch.device("cuda")
+    ops._native.ops()  # load the extension (registers torch.ops.symmetry_amd)
     Hq, Hkv, D, BS = 32, 8, 128, 64
     S, L = args.seqs, args.layers
     tiny = torch.zeros(64, device=dev)
@@ -53,6 +58,10 @@ def main():
         kc = [torch.randn(NB, Hkv, BS, D, device=dev).bfloat16() for _ in range(L)]
         vc = [torch.randn(NB, Hkv, D, BS, device=dev).bfloat16() for _ in range(L)]
         bt = (torch.arange(S * nb, dtype=torch.int32, device=dev) + 1).view(S, nb)
+        width = max(nb, args.span // BS)
+        if width > nb:
+            bt = torch.cat([bt, torch.zeros(S, width - nb, dtype=torch.int32, device=dev)], 1).contiguous()
+            nb = width
         ctxs = torch.full((S,), ctx, dtype=torch.int32, device=dev)
         q = torch.randn(S, Hq, D, device=dev).bfloat16()
         out = torch.empty_like(q)
@@ -60,11 +69,15 @@ def main():
         tmp_o = torch.empty(S, Hq, parts, D, device=dev)
         tmp_ml = torch.empty(S, Hq, parts, 2, device=dev)
         cnt = torch.zeros(S * Hkv, dtype=torch.int32, device=dev)
-        us = timed(lambda i: ops.attn_decode(q, kc[i % L], vc[i % L], bt, ctxs, out, tmp_o, tmp_ml, cnt,
-                                             1 / math.sqrt(D)), L)
-        kv_bytes = 2 * S * ctx * Hkv * D * 2
-        print(json.dumps({"kernel": "attn_decode", "seqs": S, "ctx": ctx, "us": round(us, 2),
-                          "TBps": round(kv_bytes / us / 1e6, 3)}), flush=True)
+        for wv in args.wave:
+            if wv >= 0:
+                torch.ops.symmetry_amd.attn_wave(wv, 0)
+            us = timed(lambda i: ops.attn_decode(q, kc[i % L], vc[i % L], bt, ctxs, out, tmp_o, tmp_ml, cnt,
+                                                 1 / math.sqrt(D)), L)
+            kv_bytes = 2 * S * ctx * Hkv * D * 2
+            print(json.dumps({"kernel": "attn_decode", "seqs": S, "ctx": ctx, "span": nb * BS, "wave": wv,
+                              "us": round(us, 2), "TBps": round(kv_bytes / us / 1e6, 3)}), flush=True)
+        torch.ops.symmetry_amd.attn_wave(1024, 513)
         del kc, vc
 
 

@@ -809,6 +809,8 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("mgemm(Tensor x, Tensor w, Tensor(a!) y, int rw) -> ()", &mgemm);
   m.def("mgemm_nt(int on) -> ()", [](int64_t on) { set_mgemm_nt((int)on); });
   m.def("attn_stream_min(int tokens) -> ()", [](int64_t t) { set_attn_stream_min((int)t); });
+  m.def("attn_wave(int min_units, int min_span) -> ()",
+        [](int64_t u, int64_t span) { set_attn_wave((int)u, (int)span); });
   m.def(
       "lm_head_sample(Tensor x, Tensor w, Tensor temps, Tensor seeds, Tensor step, Tensor(a!) tile_keys, "
       "Tensor(b!) out_keys, Tensor(c!) out_ids, int n_offset, Tensor(d!)? logits) -> ()",

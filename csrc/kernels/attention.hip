@@ -54,6 +54,88 @@ __global__ __launch_bounds__(DWAVES * 64, 4) void attn_decode_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
+// Decode, wide batches: one wave per (seq, kv head) walking its whole context
+// ---------------------------------------------------------------------------------------------
+// The grid kernel spends an 8-wave workgroup per (seq, kv head, 256-token partition): built for a few
+// sequences, where spreading one context over 8 waves shortens the step.  At wide decode batches (128-256
+// sequences of 0.5-4K tokens) the units outnumber the resident workgroups several times over and each
+// unit's latency chain (metadata, K/V, cross-wave LDS merge, split-KV publish) is paid per round: K/V
+// streams at 4.3-5.0 TB/s (grid / streaming kernels).  Here a unit is ONE wave that walks the 32-token
+// groups of its context with the next group's K/V loads in flight (two register sets), keeps the online
+// softmax in registers (compute_group, attn_decode.h) and writes its output rows itself: no LDS, no
+// barrier, no partials.  The 2048 units of a 256-sequence Llama-3-8B step are resident at once (two
+// waves per SIMD).  The block-table row (<= 64 entries) is read once, one entry per lane, and each
+// group's block number is a lane read (v_readlane) instead of a dependent load: no load in the loop
+// besides the K/V stream, so the compiler's counted waits keep the next group's loads in flight.
+constexpr int WAVE_UNITS = 4;  // units (waves) per workgroup
+
+__global__ __launch_bounds__(WAVE_UNITS * 64, 2) void attn_decode_wave_kernel(
+    const bf16* __restrict__ q, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    const int* __restrict__ block_tables, const int* __restrict__ ctx_lens, bf16* __restrict__ out, int num_units,
+    int Hq, int Hkv, int BS, int max_blocks, float scale_log2) {
+  const int lane = threadIdx.x & 63;
+  const int unit = blockIdx.x * WAVE_UNITS + (threadIdx.x >> 6);
+  if (unit >= num_units) return;  // uniform over the wave
+  const int seq = unit / Hkv, kvh = unit - seq * Hkv;
+  const int G = Hq / Hkv;
+  const int c = lane & 15, h = lane >> 4;
+  const int bsh = __builtin_ctz(BS);
+  const int* bt = block_tables + (long long)seq * max_blocks;
+  const int btv = bt[min(lane, max_blocks - 1)];  // max_blocks <= 64 (launcher)
+  bf16x8 qf[4];
+  load_q(q, seq, Hq, kvh, G, qf);
+  const int ctx = ctx_lens[seq];
+  const int ngroups = (ctx + 31) >> 5;
+
+  auto issue = [&](int g, KVFrag& f) {
+    const int tok0 = g << 5;
+    const int blk = __builtin_amdgcn_readlane(btv, tok0 >> bsh);
+    const int boff = tok0 & (BS - 1);
+    load_group(k_cache + (((long long)blk * Hkv + kvh) * BS + boff) * D,
+               v_cache + ((long long)blk * Hkv + kvh) * (long long)D * BS + boff, BS, f);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the compute (no load sinking)
+  };
+  f32x4 o[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;
+  auto compute = [&](const KVFrag& f, int g) {
+    const int tok0 = g << 5;
+    compute_group(f, qf, scale_log2, [&](int a, int r) { return tok0 + 8 * h + 4 * a + r < ctx; }, o, m, lsum);
+  };
+  // two register sets: group g computes while g + 1 loads.  The prefetch is unconditional (the last
+  // group is re-read past the end): a conditional one makes the compiler's wait before the compute drain
+  // the prefetched loads too (vmcnt(0) at the merge point), serialising the stream.
+  const int last = max(ngroups - 1, 0);
+  KVFrag f0, f1;
+  issue(0, f0);
+  for (int g = 0; g < ngroups; g += 2) {
+    issue(min(g + 1, last), f1);
+    compute(f0, g);
+    if (g + 1 >= ngroups) break;
+    issue(min(g + 2, last), f0);
+    compute(f1, g + 1);
+  }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (c < G) {
+    // lane (c, h) holds dims 16 dt + 4 h .. + 3 of query column c
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16* op = out + ((long long)seq * Hq + kvh * G + c) * D + 4 * h;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      union {
+        uint2 u;
+        bf16 h[4];
+      } pk;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pk.h[r] = (bf16)(o[dt][r] * inv);
+      *reinterpret_cast<uint2*>(op + 16 * dt) = pk.u;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Decode, long contexts: one wave per (seq, kv head, 384-token partition) streaming its K/V groups
 // through a private LDS ring by LDS-DMA
 // ---------------------------------------------------------------------------------------------
@@ -762,6 +844,25 @@ static int g_attn_stream_min = [] {
 
 void set_attn_stream_min(int tokens) { g_attn_stream_min = tokens; }
 
+// wide batches: the one-wave-per-(seq, kv head) kernel from this many units (seqs x kv heads) for block
+// tables spanning at least this many tokens (and <= 64 blocks).  bench_attn_decode.py --wave 0 1
+// (profiles/attn_decode_wave_r2.jsonl): at >= 128 sequences x 700-3000 tokens it streams K/V at 5.1-5.9 TB/s
+// vs 4.3-5.0 for the grid / streaming kernels (-8..-20 %); at 64 sequences, or ~170-token contexts in the
+// 512-token bucket, those stay ahead.  SYMMETRY_ATTN_WAVE_UNITS (0: never) / SYMMETRY_ATTN_WAVE_SPAN.
+static int g_attn_wave_units = [] {
+  const char* knob = getenv("SYMMETRY_ATTN_WAVE_UNITS");
+  return knob ? atoi(knob) : 1024;
+}();
+static int g_attn_wave_span = [] {
+  const char* knob = getenv("SYMMETRY_ATTN_WAVE_SPAN");
+  return knob ? atoi(knob) : 513;
+}();
+
+void set_attn_wave(int min_units, int min_span) {
+  g_attn_wave_units = min_units;
+  g_attn_wave_span = min_span;
+}
+
 // A/B knob (partition length x ring depth of the streaming kernel): SYMMETRY_ATTN_STREAM_CFG
 static int g_attn_stream_cfg = [] {
   const char* knob = getenv("SYMMETRY_ATTN_STREAM_CFG");
@@ -777,6 +878,13 @@ void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache,
   // block tables spanning >= g_attn_stream_min tokens (the graph's context bucket): the streaming
   // one-wave kernel
   const int span = max_blocks * BS;
+  if (g_attn_wave_units > 0 && num_seqs * Hkv >= g_attn_wave_units && span >= g_attn_wave_span && G <= 16 &&
+      max_blocks <= 64) {
+    const int units = num_seqs * Hkv;
+    attn_decode_wave_kernel<<<(units + WAVE_UNITS - 1) / WAVE_UNITS, WAVE_UNITS * 64, 0, s>>>(
+        q, k_cache, v_cache, block_tables, ctx_lens, out, units, Hq, Hkv, BS, max_blocks, scale_log2);
+    return;
+  }
   if (g_attn_stream_min > 0 && span >= g_attn_stream_min && BS >= 32 && G <= 16) {
     // partitions of SG 32-token groups (>= 256 tokens: sparts <= max_parts, sized for 256-token ones)
     auto run = [&](auto kern, int sg) {

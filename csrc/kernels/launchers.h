@@ -138,6 +138,8 @@ void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache,
                         int Hq, int Hkv, int BS, int max_blocks, int max_parts, float scale, hipStream_t s);
 // decode attention switches to the streaming long-context kernel from this block-table span (0: never)
 void set_attn_stream_min(int tokens);
+// wide batches: one wave per (seq, kv head) from min_units units for spans of >= min_span tokens
+void set_attn_wave(int min_units, int min_span);
 void launch_attn_prefill(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,
                          const int* ctx_lens, const int* cu_q, const int* tiles, int num_tiles, bf16* out, int Hq,
                          int Hkv, int BS, int max_blocks, float scale, hipStream_t s);

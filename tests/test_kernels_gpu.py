@@ -108,9 +108,11 @@ def _random_paged(gpu, ctx_lens, Hkv, BS, g, extra_blocks=3):
 @pytest.fixture(params=["grid", "stream"])
 def attn_decode_kernel(request):
     """The grid split-KV kernel and the streaming long-context kernel (chosen by block-table span)."""
+    torch.ops.symmetry_amd.attn_wave(0, 0)
     torch.ops.symmetry_amd.attn_stream_min(0 if request.param == "grid" else 1)
     yield request.param
     torch.ops.symmetry_amd.attn_stream_min(1024)
+    torch.ops.symmetry_amd.attn_wave(1024, 513)
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 1), (16, 16)])
@@ -137,6 +139,35 @@ def test_attn_decode(gpu, attn_decode_kernel, Hq, Hkv, BS):
     out2 = torch.empty_like(out)
     ops.attn_decode(q, kc, vc, bt, ctx, out2, tmp_o, tmp_ml, cnt, scale)
     assert torch.equal(out, out2)
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 1), (16, 16)])
+@pytest.mark.parametrize("BS", [32, 64])
+def test_attn_decode_wave(gpu, Hq, Hkv, BS):
+    """One wave per (seq, kv head) walking the whole context (wide decode batches, block tables of <= 64
+    entries): forced on for a small batch, against the fp32 reference."""
+    g = torch.Generator(device=gpu).manual_seed(4)
+    ctx_lens = [c for c in (1, 17, 31, 32, 33, 64, 200, 255, 256, 257, 511, 700, 1000, 2000, 4000)
+                if c <= 63 * BS]
+    kc, vc, bt = _random_paged(gpu, ctx_lens, Hkv, BS, g)
+    assert bt.shape[1] <= 64
+    S = len(ctx_lens)
+    q = torch.randn(S, Hq, 128, device=gpu, generator=g).bfloat16()
+    ctx = torch.tensor(ctx_lens, device=gpu, dtype=torch.int32)
+    max_parts = (bt.shape[1] * BS + ops.ATTN_DECODE_PART - 1) // ops.ATTN_DECODE_PART
+    tmp_o = torch.empty(S, Hq, max_parts, 128, device=gpu)
+    tmp_ml = torch.empty(S, Hq, max_parts, 2, device=gpu)
+    out = torch.full((S, Hq, 128), float("nan"), device=gpu, dtype=torch.bfloat16)
+    cnt = torch.zeros(S * Hkv, device=gpu, dtype=torch.int32)
+    scale = 1 / math.sqrt(128)
+    torch.ops.symmetry_amd.attn_wave(1, 0)
+    try:
+        ops.attn_decode(q, kc, vc, bt, ctx, out, tmp_o, tmp_ml, cnt, scale)
+    finally:
+        torch.ops.symmetry_amd.attn_wave(1024, 513)
+    out_r = torch.empty(S, Hq, 128, dtype=torch.bfloat16)
+    ref.attn_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), ctx.cpu(), out_r, scale=scale)
+    _close(out, out_r, atol=2e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 8), (64, 8), (16, 8)])
