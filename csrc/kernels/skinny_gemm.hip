@@ -196,23 +196,37 @@ __global__ __launch_bounds__(NT) void skinny_gemm_kernel(const bf16* __restrict_
   }
 }
 
-__global__ __launch_bounds__(256) void argmax_reduce_kernel(const unsigned long long* __restrict__ keys, int ntiles,
-                                                            unsigned long long* __restrict__ out_keys,
-                                                            int* __restrict__ out_ids) {
+// One 1024-thread workgroup per row; each thread issues its (up to) 8 key loads of a 8K-key chunk before
+// reducing them, so a Llama-3 vocabulary (8016 tile keys per row) costs one memory round trip instead of a
+// chain of dependent ones (12.8 -> a few us per decode step at 10 rows).
+constexpr int AR_NT = 1024, AR_U = 8;
+
+__global__ __launch_bounds__(AR_NT) void argmax_reduce_kernel(const unsigned long long* __restrict__ keys, int ntiles,
+                                                              unsigned long long* __restrict__ out_keys,
+                                                              int* __restrict__ out_ids) {
   const int m = blockIdx.x;
   const unsigned long long* k = keys + (long long)m * ntiles;
   unsigned long long best = 0;
-  for (int i = threadIdx.x; i < ntiles; i += 256) best = k[i] > best ? k[i] : best;
+  for (int base = 0; base < ntiles; base += AR_NT * AR_U) {
+    unsigned long long v[AR_U];
+#pragma unroll
+    for (int u = 0; u < AR_U; ++u) {
+      const int i = base + u * AR_NT + threadIdx.x;
+      v[u] = i < ntiles ? k[i] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < AR_U; ++u) best = v[u] > best ? v[u] : best;
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     unsigned long long v = __shfl_xor(best, o, 64);
     best = v > best ? v : best;
   }
-  __shared__ unsigned long long sm[4];
+  __shared__ unsigned long long sm[AR_NT / 64];
   if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = best;
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int i = 1; i < 4; ++i) best = sm[i] > best ? sm[i] : best;
+    for (int i = 1; i < AR_NT / 64; ++i) best = sm[i] > best ? sm[i] : best;
     if (out_keys) out_keys[m] = best;
     if (out_ids) out_ids[m] = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
   }
@@ -267,5 +281,5 @@ void launch_skinny_gemm_argmax(const bf16* x, const bf16* W, float* logits_or_nu
 
 void launch_argmax_reduce(const unsigned long long* tile_keys, int M, int ntiles, unsigned long long* out_keys,
                           int* out_ids, hipStream_t s) {
-  argmax_reduce_kernel<<<M, 256, 0, s>>>(tile_keys, ntiles, out_keys, out_ids);
+  argmax_reduce_kernel<<<M, AR_NT, 0, s>>>(tile_keys, ntiles, out_keys, out_ids);
 }
