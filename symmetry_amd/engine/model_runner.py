@@ -16,6 +16,7 @@
 """
 from __future__ import annotations
 
+import itertools
 import math
 import time
 
@@ -129,16 +130,70 @@ class ModelRunner:
             self._pinned[key] = t
         return t[:n]
 
+    def _fill_decode(self, lay: _Layout, host: np.ndarray, seqs, prev_rows: dict | None) -> None:
+        """_fill for a decode step (one token per sequence), vectorised: at 128-256 concurrent sequences the
+        per-sequence Python of the generic packer cost more host time than the GPU step (wide batches)."""
+        BS, n, T = self.block_size, len(seqs), lay.T
+        host[:] = 0
+        ids = np.empty(n, dtype=np.int64)
+        src = np.full(T, -1, dtype=np.int64)
+        pos = np.empty(n, dtype=np.int64)
+        for i, s in enumerate(seqs):
+            p = s.num_computed
+            pos[i] = p
+            npr = len(s.prompt_ids)
+            if p < npr:
+                ids[i] = s.prompt_ids[p]
+            elif p - npr < len(s.output_ids):
+                ids[i] = s.output_ids[p - npr]
+            else:  # pending token (pipelined decode): resolved on the device
+                ids[i] = 0
+                src[i] = prev_rows[s.seq_id]
+        # block tables: one flat conversion, scattered into the [rows, max_blocks] view
+        lens = np.fromiter((len(s.block_table) for s in seqs), dtype=np.int64, count=n)
+        flat = np.fromiter(itertools.chain.from_iterable(s.block_table for s in seqs), dtype=np.int64,
+                           count=int(lens.sum()))
+        btv = host[lay.bt:lay.bt + lay.nseq * lay.max_blocks].reshape(lay.nseq, lay.max_blocks)
+        rows = np.repeat(np.arange(n), lens)
+        cols = np.arange(flat.size) - np.repeat(np.cumsum(lens) - lens, lens)
+        btv[rows, cols] = flat
+        blk = btv[np.arange(n), pos // BS].astype(np.int64)
+        host[lay.ids:lay.ids + n] = ids
+        host[lay.src:lay.src + T] = src
+        host[lay.pos:lay.pos + n] = pos
+        host[lay.slots:lay.slots + n] = blk * BS + pos % BS
+        host[lay.slots + n:lay.slots + T] = -1
+        host[lay.ctx:lay.ctx + n] = pos + 1
+        host[lay.ctx + n:lay.ctx + lay.nseq] = 1
+        prm = [s.params for s in seqs]
+        host[lay.temps:lay.temps + n] = np.fromiter((q.temperature for q in prm), np.float32, n).view(np.int32)
+        host[lay.topk:lay.topk + n] = np.fromiter((q.top_k for q in prm), np.int64, n)
+        host[lay.topp:lay.topp + lay.nseq] = np.ones(lay.nseq, dtype=np.float32).view(np.int32)
+        host[lay.topp:lay.topp + n] = np.fromiter((q.top_p for q in prm), np.float32, n).view(np.int32)
+        # _seq_seed, vectorised (uint64 arithmetic wraps mod 2^64 like the Python masks)
+        seed = np.fromiter((s.sampling_seed & 0xFFFFFFFFFFFFFFFF for s in seqs), np.uint64, n)
+        nout = np.fromiter((len(s.output_ids) for s in seqs), np.uint64, n)
+        with np.errstate(over="ignore"):
+            x = seed * np.uint64(0x100000001B3) + nout * np.uint64(_SEED_MIX)
+        x ^= x >> np.uint64(29)
+        host[lay.seeds:lay.seeds + 2 * n] = x.view(np.int32)
+
     def _fill(self, lay: _Layout, host: np.ndarray, seqs, counts, prev_rows: dict | None = None) -> None:
         """Pack one step's metadata.  A decode row whose input token is still in flight (sampled by the
         previous, not yet completed step: pipelined decode) gets id 0 and src = that step's output row;
         the embedding kernel then reads the token from device memory."""
+        if not lay.prefill and seqs:
+            self._fill_decode(lay, host, seqs, prev_rows)
+        else:
+            self._fill_generic(lay, host, seqs, counts, prev_rows)
+
+    def _fill_generic(self, lay: _Layout, host: np.ndarray, seqs, counts, prev_rows: dict | None = None) -> None:
         BS = self.block_size
         ids, pos, slots, src = [], [], [], []
         ctx, temps, seeds, topk, topp = [], [], [], [], []
         for seq, n in zip(seqs, counts):
             start = seq.num_computed
-            toks = seq.token_ids[start:start + n]
+            toks = seq.token_slice(start, n)
             if len(toks) < n:  # pending token (pipelined decode): resolved on the device
                 toks = toks + [0] * (n - len(toks))
                 src.extend([-1] * (n - 1) + [prev_rows[seq.seq_id]])

@@ -278,6 +278,12 @@ class Scheduler:
         ready = [s for s in self.running if not s.in_prefill and len(s.output_ids) + s.num_pending < s.params.max_tokens]
         # ensure a cache slot for each decoding sequence; preempt the newest on exhaustion
         ready.sort(key=lambda s: s.arrival_time)
+        bs = self.blocks.block_size
+        growing = [s for s in ready if s.num_computed + 1 > len(s.block_table) * bs]
+        if len(growing) <= self.blocks.num_free:  # common case: every sequence gets its slot, no preemption
+            for s in growing:
+                self.blocks.grow(s, s.num_computed + 1)
+            return ScheduledBatch("decode", ready, [1] * len(ready), [True] * len(ready), []) if ready else None
         out = []
         while ready:
             seq = ready.pop(0)

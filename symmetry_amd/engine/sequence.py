@@ -88,6 +88,15 @@ class Sequence:
     def token_ids(self) -> list:
         return self.prompt_ids + self.output_ids
 
+    def token_slice(self, start: int, n: int) -> list:
+        """token_ids[start:start + n] without concatenating the whole prompt + output list."""
+        npr = len(self.prompt_ids)
+        if start + n <= npr:
+            return self.prompt_ids[start:start + n]
+        if start >= npr:
+            return self.output_ids[start - npr:start - npr + n]
+        return self.prompt_ids[start:] + self.output_ids[:start + n - npr]
+
     @property
     def num_tokens(self) -> int:
         return len(self.prompt_ids) + len(self.output_ids)

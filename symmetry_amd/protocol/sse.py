@@ -94,8 +94,18 @@ def _dump(obj) -> str:
     return json.dumps(obj, separators=(",", ":"), ensure_ascii=False)
 
 
+_esc = json.encoder.encode_basestring  # the C string encoder json.dumps(..., ensure_ascii=False) uses
+
+
 def chunk_event(completion_id: str, model: str, content: str | None = None, *, role: str | None = None,
                 finish_reason: str | None = None, created: int | None = None, usage: dict | None = None) -> str:
+    if role is None and usage is None and content is not None:
+        # per-token fast path (one event per token per client on the serving hot path): the same bytes as
+        # the generic encoding below, assembled from C-escaped strings instead of a json.dumps of a dict
+        return ('data: {"id":' + _esc(completion_id) + ',"object":"chat.completion.chunk","created":'
+                + str(int(created if created is not None else time.time())) + ',"model":' + _esc(model)
+                + ',"system_fingerprint":"symmetry_amd","choices":[{"index":0,"delta":{"content":' + _esc(content)
+                + '},"finish_reason":' + ("null" if finish_reason is None else _esc(finish_reason)) + "}]}\n\n")
     delta: dict = {}
     if role is not None:
         delta["role"] = role

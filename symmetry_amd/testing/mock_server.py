@@ -53,7 +53,8 @@ class SymmetryServer:
         return identity.server_topic(self.server_key)
 
     async def start(self) -> None:
-        self.swarm = Swarm(self.kp, bootstrap=self.bootstrap)
+        # the server is every client's and provider's first hop: no small peer cap (Swarm's default is 64)
+        self.swarm = Swarm(self.kp, bootstrap=self.bootstrap, max_peers=4096)
         self.swarm.on("connection", self._on_connection)
         await self.swarm.join(self.topic, server=True, client=False).flushed()
         self._ping_task = asyncio.ensure_future(self._pinger())
