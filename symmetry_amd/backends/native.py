@@ -76,5 +76,56 @@ class NativeBackend(Backend):
             if out.finished:
                 yield Chunk(sse.done_event().encode("utf-8"), "")
 
+    async def stream_direct(self, request: dict, write, scope: bytes = b"", backlog: int | None = None) -> None:
+        """The stream of :meth:`stream`, written by the engine's per-step output callback itself: each
+        output becomes its SSE event and ``write(raw, delta)`` runs right there on the event loop -- no task
+        wake-up and no async-generator hops per token (at 100+ concurrent clients those cost more event-loop
+        time than the encoding and the encrypted send).  ``write`` returns True (accepted), False (accepted,
+        but the peer is congested) or None (the peer is gone: the request is aborted).  A peer that stays
+        congested for ``backlog`` outputs is a stalled reader: its request is aborted and BackendError
+        raised, as the queue-based path does.  Returns when the request has finished."""
+        await self.start()
+        messages = request.get("messages") or []
+        if not isinstance(messages, list):
+            raise BackendError("messages must be a list")
+        params = SamplingParams.from_request(request, default_max_tokens=self.engine.cfg.default_max_tokens)
+        rid = f"chatcmpl-{next(_ids)}-{int(time.time() * 1000)}"
+        created = int(time.time())
+        limit = int(backlog or self.aengine.queue_limit)
+        done = asyncio.get_running_loop().create_future()
+        st = {"first": True, "congested": 0}
+
+        def finish(exc: BaseException | None = None) -> None:
+            if not done.done():
+                done.set_exception(exc) if exc is not None else done.set_result(None)
+
+        def on_output(out) -> None:
+            if done.done():
+                return
+            if out.error:
+                return finish(BackendError(out.error))
+            if out.text or st["first"] or out.finished:
+                ev = sse.chunk_event(rid, self.model_name, out.text, role="assistant" if st["first"] else None,
+                                     finish_reason=out.finish_reason if out.finished else None, created=created)
+                st["first"] = False
+                ok = write(ev.encode("utf-8"), out.text)
+                if ok is None:  # peer gone
+                    self.aengine.abort(rid)
+                    return finish()
+                st["congested"] = 0 if ok else st["congested"] + 1
+                if st["congested"] > limit and not out.finished:
+                    self.aengine.abort(rid)
+                    return finish(BackendError(f"client too slow: more than {limit} outputs behind"))
+            if out.finished:
+                write(sse.done_event().encode("utf-8"), "")
+                finish()
+
+        self.aengine.submit(rid, on_output, messages=messages, params=params, cache_scope=scope)
+        try:
+            await done
+        finally:
+            if not done.done() or done.cancelled():
+                self.aengine.abort(rid)
+
     def stats(self) -> dict:
         return self.engine.metrics.summary() if self.aengine is not None else {}

@@ -486,6 +486,28 @@ class AsyncEngine:
             self._thread.join(timeout=10)
         self.engine.shutdown()
 
+    def submit(self, request_id: str, on_output, messages: list | None = None, prompt_ids: list | None = None,
+               params: SamplingParams | None = None, cache_scope: bytes = b"") -> None:
+        """Callback form of :meth:`generate` for the serving hot path: ``on_output(out)`` runs on the calling
+        event loop for every output (a step's outputs arrive as one batch, see the class note), with no
+        per-token task switch or async-generator hop.  The caller aborts through :meth:`abort`."""
+        loop = asyncio.get_running_loop()
+
+        def cb(out: RequestOutput) -> None:
+            if self._batch and threading.current_thread() is self._thread:
+                self._pending.append((loop, on_output, out))
+            else:
+                loop.call_soon_threadsafe(on_output, out)
+
+        if prompt_ids is None:
+            prompt_ids = self.engine.tokenizer.apply_chat_template(messages or [])
+        self.engine.add_request(request_id, prompt_ids, params, cb, cache_scope=cache_scope)
+        self.start()
+        self._wake.set()
+
+    def abort(self, request_id: str) -> None:
+        self.engine.abort(request_id)
+
     async def generate(self, request_id: str, messages: list | None = None, prompt_ids: list | None = None,
                        params: SamplingParams | None = None, cache_scope: bytes = b""):
         """Async iterator of RequestOutput for one request; aborts the sequence if the consumer goes away.

@@ -246,18 +246,39 @@ class SymmetryProvider:
         # prefix-cache scope: a client's multi-turn prompts reuse its own cached KV only (no cross-client
         # aliasing, no cross-client TTFT side channel on a public provider)
         scope = bytes(getattr(peer, "remotePublicKey", b"") or b"")
-        gen = self.backend.stream(req, scope=scope)
+        direct = getattr(self.backend, "stream_direct", None)
+        gen = None if direct is not None else self.backend.stream(req, scope=scope)
         try:
             header_sent = False
-            async for chunk in gen:
-                if not header_sent:
-                    peer.write(emitter_header(emitter_key))
-                    header_sent = True
-                if not peer.writable:
-                    break
-                completion += chunk.delta
-                if not peer.write(chunk.raw):
-                    await peer.drain()
+            if direct is not None:
+                # native engine: each token's event is written by the engine's per-step output callback on
+                # this loop (no per-token task switch); a congested peer is bounded by maxBacklog outputs
+                parts: list = []
+
+                def write(raw: bytes, delta: str):
+                    nonlocal header_sent
+                    if not header_sent:
+                        peer.write(emitter_header(emitter_key))
+                        header_sent = True
+                    if not peer.writable:
+                        return None
+                    parts.append(delta)
+                    return bool(peer.write(raw))
+
+                try:
+                    await direct(req, write, scope=scope)
+                finally:
+                    completion = "".join(parts)
+            else:
+                async for chunk in gen:
+                    if not header_sent:
+                        peer.write(emitter_header(emitter_key))
+                        header_sent = True
+                    if not peer.writable:
+                        break
+                    completion += chunk.delta
+                    if not peer.write(chunk.raw):
+                        await peer.drain()
             if not peer.writable:
                 return
             if not header_sent:
@@ -276,7 +297,8 @@ class SymmetryProvider:
                 peer.write(sse.error_event(message))
                 peer.write(create_message(Keys.INFERENCE_ENDED, emitter_key))
         finally:
-            await gen.aclose()
+            if gen is not None:
+                await gen.aclose()
 
     # ------------------------------------------------------------------------------------------
     def stats(self) -> dict:

@@ -90,3 +90,43 @@ def test_backend_fault_mid_stream_sends_error_and_keeps_serving(tmp_path):
             assert r2.ended
 
     run(main())
+
+
+def test_direct_stream_congested_and_vanished_peers():
+    """The callback streaming path (NativeBackend.stream_direct, used by the provider node): a peer that
+    stays congested for maxBacklog outputs has its request aborted with BackendError; a peer that is gone
+    aborts its request at once; a healthy one gets role, one event per token, finish_reason and [DONE]."""
+    import json
+
+    from symmetry_amd.backends.base import BackendError
+    from symmetry_amd.backends.native import NativeBackend
+
+    async def main():
+        eng = _tiny_engine()
+        be = NativeBackend({"modelName": "tiny-llama", "maxBacklog": 3}, engine=eng)
+        await be.start()
+        try:
+            req = {"messages": [{"role": "user", "content": "hi"}], "max_tokens": 40, "ignore_eos": True}
+            congested = []
+            try:
+                await be.stream_direct(req, lambda raw, d: congested.append(raw) or False)
+                raise AssertionError("expected a slow-consumer abort")
+            except BackendError as exc:
+                assert "too slow" in str(exc)
+            assert 3 < len(congested) < 40
+            gone = []
+            await be.stream_direct(req, lambda raw, d: gone.append(raw) and None)
+            assert len(gone) == 1
+            ok = []
+            await be.stream_direct(req, lambda raw, d: ok.append(raw) or True)
+            events = [r.decode() for r in ok]
+            assert events[-1] == "data: [DONE]\n\n"
+            objs = [json.loads(e[len("data: "):]) for e in events[:-1]]
+            assert objs[0]["choices"][0]["delta"].get("role") == "assistant"
+            assert objs[-1]["choices"][0]["finish_reason"] == "length"
+            assert 2 <= len(objs) <= 40  # tokens that complete no UTF-8 text carry no event
+            assert await _wait(lambda: not eng.has_unfinished())
+        finally:
+            await be.stop()
+
+    run(main())
