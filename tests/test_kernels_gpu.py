@@ -89,6 +89,32 @@ def test_rope_cache(gpu, kind):
     _close(vc, vc_r, atol=1e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("kind", ["bf16", "slabs"])
+def test_rope_cache_prefill_groups(gpu, kind):
+    """Prefill-sized rope_cache (8-row groups): 16-byte V token runs for aligned consecutive slots, the
+    per-token fallback for unaligned runs, scattered slots, padding rows and a ragged last group."""
+    Hq, Hkv, D, BS, NB = 32, 8, 128, 64, 12
+    slots_l = list(range(3 * BS + 5, 3 * BS + 5 + 37)) + list(range(5 * BS, 5 * BS + 56))
+    slots_l += [9 * BS + 1, -1, 7 * BS + 63, 10 * BS + 8, -1, 11 * BS, 2 * BS + 9]
+    T = len(slots_l)  # 100: twelve full groups and a ragged one
+    g = torch.Generator(device=gpu).manual_seed(12)
+    N = (Hq + 2 * Hkv) * D
+    qkv = torch.randn(T, N, device=gpu, generator=g).bfloat16() if kind == "bf16" else torch.randn(
+        2, T, N, device=gpu, generator=g)
+    pos = torch.randint(0, 4000, (T,), device=gpu, generator=g, dtype=torch.int32)
+    slots = torch.tensor(slots_l, device=gpu, dtype=torch.int32)
+    cs = ref.rope_table(8192, D, 500000.0).to(gpu)
+    q = torch.empty(T, Hq, D, device=gpu, dtype=torch.bfloat16)
+    kc, vc = _make_cache(gpu, NB, Hkv, BS)
+    ops.rope_cache(qkv, pos, slots, cs, q, kc, vc, Hq, Hkv)
+    q_r = torch.empty(T, Hq, D, dtype=torch.bfloat16)
+    kc_r, vc_r = kc.new_zeros(kc.shape).cpu(), vc.new_zeros(vc.shape).cpu()
+    ref.rope_cache(qkv.cpu(), pos.cpu(), slots.cpu(), cs.cpu(), q_r, kc_r, vc_r, Hq, Hkv)
+    _close(q, q_r, atol=2e-2, rtol=1e-2)
+    _close(kc, kc_r, atol=2e-2, rtol=1e-2)
+    _close(vc, vc_r, atol=1e-2, rtol=1e-2)
+
+
 def _random_paged(gpu, ctx_lens, Hkv, BS, g, extra_blocks=3):
     nseq = len(ctx_lens)
     max_blocks = max((c + BS - 1) // BS for c in ctx_lens) + 1
