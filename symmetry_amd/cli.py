@@ -11,6 +11,15 @@ process per GPU, e.g. ``torchrun --nproc-per-node 8 -m symmetry_amd.cli -c
 provider.yaml``: rank 0 runs the provider node and the scheduler, the other
 ranks mirror its forward passes over RCCL.
 
+Data-parallel replicas on one node (SURVEY.md §2.5 "one provider process per
+GPU group"): ``symmetry-cli -c provider.yaml --replicas N`` (or ``replicas: N``
+in the YAML) starts N independent providers, replica i on GPUs
+[i*tp, (i+1)*tp) (``tp = tensorParallelSize``; each replica a ``torchrun``
+group when tp > 1), named ``<name>-<i>`` so each has its own identity and
+topic; the server spreads clients over them like over any set of providers.
+8 GPUs: ``--replicas 8`` for Llama-3-8B, ``tensorParallelSize: 8`` for 70B,
+``--replicas 2`` + ``tensorParallelSize: 4`` in between.
+
 Also: ``symmetry-server`` (registry/assignment server), ``symmetry-dht``
 (discovery node), ``symmetry-client`` (a chat client over the swarm).
 """
@@ -61,10 +70,95 @@ def _distributed_engine(cfg: ConfigManager):
 
     ecfg = EngineConfig.from_provider(cfg.get_all())
     engine, rank = init_tp_engine(ecfg)
+    _exit_when_orphaned()
     if rank != 0:
         engine.runner.worker_loop()
         sys.exit(0)
     return engine
+
+
+def _exit_when_orphaned(period_s: float = 1.0) -> None:
+    """A torchrun rank whose launcher (the elastic agent) is gone leaves at once: its peers are gone too, so
+    worker ranks would block in the metadata broadcast and rank 0's shutdown in its stop broadcast forever."""
+    import threading
+    import time
+
+    parent = os.getppid()
+
+    def watch():
+        while True:
+            time.sleep(period_s)
+            if os.getppid() != parent:
+                os._exit(0)
+
+    threading.Thread(target=watch, name="symmetry-orphan-watch", daemon=True).start()
+
+
+REPLICA_ENV = "SYMMETRY_REPLICA_INDEX"
+
+
+def replica_plan(cfg: dict, config_path: str, replicas: int, bootstrap: str | None = None,
+                 visible: str | None = None, port_base: int = 29600) -> list[tuple[list, dict]]:
+    """(argv, env overrides) of every replica process: its own name (identity, topic), listen / local HTTP
+    port and metrics file, and its GPUs as HIP_VISIBLE_DEVICES (a slice of ``visible`` when the launcher
+    itself was restricted)."""
+    tp = int(cfg.get("tensorParallelSize") or 1)
+    devs = [d.strip() for d in visible.split(",")] if visible else [str(d) for d in range(replicas * tp)]
+    if len(devs) < replicas * tp:
+        raise ValueError(f"{replicas} replicas x tensorParallelSize {tp} need {replicas * tp} GPUs, "
+                         f"{len(devs)} visible")
+    base = [sys.executable, "-m", "symmetry_amd.cli", "-c", config_path]
+    if bootstrap:
+        base += ["--bootstrap", bootstrap]
+    plan = []
+    for i in range(replicas):
+        env = {REPLICA_ENV: str(i), "SYMMETRY_NAME": f"{cfg.get('name') or 'provider'}-{i}"}
+        if cfg.get("listenPort"):
+            env["SYMMETRY_LISTENPORT"] = str(int(cfg["listenPort"]) + i)
+        if cfg.get("serveHttp"):
+            env["SYMMETRY_APIPORT"] = str(int(cfg["apiPort"]) + i)
+        if cfg.get("metricsFile"):
+            root, ext = os.path.splitext(str(cfg["metricsFile"]))
+            env["SYMMETRY_METRICSFILE"] = f"{root}-{i}{ext}"
+        if str(cfg.get("apiProvider", "")).lower() == "native":
+            env["HIP_VISIBLE_DEVICES"] = ",".join(devs[i * tp:(i + 1) * tp])
+        argv = base
+        if tp > 1:
+            argv = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={tp}",
+                    "--master-addr", "127.0.0.1", f"--master-port={port_base + i}", "-m", "symmetry_amd.cli",
+                    *base[3:]]
+        plan.append((argv, env))
+    return plan
+
+
+def _launch_replicas(cfg: ConfigManager, config_path: str, replicas: int, bootstrap: str | None) -> int:
+    """Run the replica providers as child processes (never an exec of this process) until they exit or
+    the launcher is interrupted; then stop exactly those children."""
+    import signal
+    import subprocess
+
+    plan = replica_plan(cfg.get_all(), config_path, replicas, bootstrap,
+                        os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES"))
+    procs = [subprocess.Popen(argv, env={**os.environ, **env}) for argv, env in plan]
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGINT)
+
+    signal.signal(signal.SIGTERM, stop)
+    try:
+        codes = [p.wait() for p in procs]
+    except KeyboardInterrupt:
+        stop()
+        codes = []
+        for p in procs:
+            try:
+                codes.append(p.wait(timeout=30))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                codes.append(p.wait())
+    return max((abs(c) for c in codes), default=0)
 
 
 def main(argv=None) -> int:
@@ -74,6 +168,8 @@ def main(argv=None) -> int:
     ap.add_argument("--bootstrap", default=None, help="discovery node(s) host:port[,host:port]")
     ap.add_argument("--init", action="store_true", help="write a default provider.yaml and exit")
     ap.add_argument("--native", action="store_true", help="with --init: apiProvider native")
+    ap.add_argument("--replicas", type=int, default=None,
+                    help="data-parallel providers on this node, one per GPU group of tensorParallelSize GPUs")
     args = ap.parse_args(argv)
     if args.init:
         return _init_config(args.config, args.native)
@@ -82,6 +178,9 @@ def main(argv=None) -> int:
     except Exception as exc:
         print(f"Error: {exc}", file=sys.stderr)
         return 1
+    replicas = int(args.replicas or cfg.get("replicas") or 1)
+    if replicas > 1 and REPLICA_ENV not in os.environ:
+        return _launch_replicas(cfg, args.config, replicas, args.bootstrap)
     engine = None
     if int(os.environ.get("WORLD_SIZE", "1")) > 1 and cfg.is_native:
         engine = _distributed_engine(cfg)

@@ -43,7 +43,7 @@ OPTIONAL_FIELDS = ("apiKey", "dataCollectionEnabled", "maxConnections", "name", 
                    "tensorParallelSize", "expertParallelSize", "maxBatchTokens", "maxModelLen", "kvCacheFraction",
                    "blockSize", "maxTokens", "seed", "device", "useGraphs", "numKvBlocks", "maxBacklog",
                    "decodeWeights", "prefillChunk", "strictServerAuth", "shareApiKey", "completionParser",
-                   "metricsInterval", "metricsFile", "bootstrap", "listenHost", "listenPort", "serveHttp")
+                   "metricsInterval", "metricsFile", "bootstrap", "listenHost", "listenPort", "serveHttp", "replicas")
 
 
 class ConfigError(Exception):
