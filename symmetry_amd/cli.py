@@ -137,8 +137,14 @@ def _launch_replicas(cfg: ConfigManager, config_path: str, replicas: int, bootst
     import signal
     import subprocess
 
-    plan = replica_plan(cfg.get_all(), config_path, replicas, bootstrap,
-                        os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES"))
+    visible = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+    if visible is None and cfg.is_native and str(cfg.get("device", "auto")) != "cpu":
+        import torch  # device_count() does not initialise the GPU runtime on this stack
+
+        n = torch.cuda.device_count()
+        if n:
+            visible = ",".join(str(d) for d in range(n))
+    plan = replica_plan(cfg.get_all(), config_path, replicas, bootstrap, visible)
     procs = [subprocess.Popen(argv, env={**os.environ, **env}) for argv, env in plan]
 
     def stop(*_):
