@@ -1,0 +1,283 @@
+// Host side of the one-shot xGMI all-reduce (csrc/kernels/xgmi_ar.hip): buffer lifetime, IPC export /
+// import of the peers' buffers, and the torch ops.
+//
+// Each TP rank allocates ONE uncached device buffer (flags + two parities x world data slots), exports it
+// with hipIpcGetMemHandle and maps every peer's buffer with hipIpcOpenMemHandle; the handles travel over
+// the gloo bootstrap group (symmetry_amd/parallel/comm.py::XgmiComm).  The collectives launch on torch's
+// current HIP stream, so they are captured into the decode hipGraph like every other kernel.
+// `xgmi_connect_local` maps buffers of the SAME process instead of IPC handles: several "ranks" on one
+// GPU in one process, for the kernel-level GPU test.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "launchers.h"
+
+namespace {
+
+using at::Tensor;
+
+#define HIP_OK(x)                                                                    \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    TORCH_CHECK(e_ == hipSuccess, "HIP error ", hipGetErrorString(e_), " at " #x);  \
+  } while (0)
+
+struct Xgmi {
+  XgmiArgs args{};
+  char* own = nullptr;
+  std::vector<char*> opened;  // IPC mappings to close
+  int device = 0;
+  long long bytes = 0;
+  bool connected = false;
+};
+
+std::mutex g_mu;
+std::vector<Xgmi*> g_x;
+// Uncached buffers are never returned to the runtime: memory freed from a hipDeviceMallocUncached
+// allocation and handed out again to ordinary hipMalloc users (the torch caching allocator) was seen
+// to lose or mix plain stores of later kernels on gfx950 (tools/xgmi_probe3.py: outputs written after
+// a communicator was destroyed read back differently from the GPU and from the host).  A destroyed
+// communicator's buffer waits here for the next communicator of the same size.
+std::vector<std::pair<long long, char*>> g_uc_pool;
+
+Xgmi* get(int64_t h) {
+  std::lock_guard<std::mutex> g(g_mu);
+  TORCH_CHECK(h >= 0 && h < (int64_t)g_x.size() && g_x[h] != nullptr, "invalid xgmi communicator");
+  return g_x[h];
+}
+
+int64_t xgmi_create(int64_t slot_bytes, int64_t world, int64_t rank, int64_t device) {
+  TORCH_CHECK(world >= 1 && world <= XG_MAX_WORLD, "xgmi: world must be 1..", XG_MAX_WORLD);
+  TORCH_CHECK(rank >= 0 && rank < world, "xgmi: bad rank");
+  TORCH_CHECK(slot_bytes > 0 && slot_bytes % 256 == 0, "xgmi: slot bytes must be a positive multiple of 256");
+  auto* x = new Xgmi();
+  x->device = (int)device;
+  HIP_OK(hipSetDevice(x->device));
+  x->bytes = xgmi_buffer_bytes((int)world, slot_bytes);
+  void* p = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    for (size_t i = 0; i < g_uc_pool.size(); ++i)
+      if (g_uc_pool[i].first == x->bytes) {
+        p = g_uc_pool[i].second;
+        g_uc_pool.erase(g_uc_pool.begin() + i);
+        break;
+      }
+  }
+  if (p == nullptr) HIP_OK(hipExtMallocWithFlags(&p, (size_t)x->bytes, hipDeviceMallocUncached));
+  HIP_OK(hipMemset(p, 0, (size_t)x->bytes));
+  x->own = (char*)p;
+  void* e = nullptr;
+  HIP_OK(hipMalloc(&e, XG_MAX_WG * sizeof(unsigned) + 64));
+  HIP_OK(hipMemset(e, 0, XG_MAX_WG * sizeof(unsigned) + 64));
+  HIP_OK(hipDeviceSynchronize());
+  x->args.epochs = (unsigned*)e;
+  x->args.err = (int*)((char*)e + XG_MAX_WG * sizeof(unsigned));
+  x->args.rank = (int)rank;
+  x->args.world = (int)world;
+  x->args.slot_bytes = slot_bytes;
+  for (int r = 0; r < XG_MAX_WORLD; ++r) x->args.bufs[r] = nullptr;
+  x->args.bufs[rank] = x->own;
+  std::lock_guard<std::mutex> g(g_mu);
+  g_x.push_back(x);
+  return (int64_t)g_x.size() - 1;
+}
+
+Tensor xgmi_ipc_handle(int64_t h) {
+  Xgmi* x = get(h);
+  hipIpcMemHandle_t ih;
+  HIP_OK(hipIpcGetMemHandle(&ih, x->own));
+  auto t = at::empty({(int64_t)sizeof(ih)}, at::kByte);
+  std::memcpy(t.data_ptr(), &ih, sizeof(ih));
+  return t;
+}
+
+// handles: uint8 [world, sizeof(hipIpcMemHandle_t)] gathered from every rank (own row ignored)
+void xgmi_open(int64_t h, const Tensor& handles) {
+  Xgmi* x = get(h);
+  const int world = x->args.world;
+  auto hc = handles.cpu().contiguous();
+  TORCH_CHECK(hc.scalar_type() == at::kByte && hc.dim() == 2 && hc.size(0) == world &&
+                  hc.size(1) == (int64_t)sizeof(hipIpcMemHandle_t),
+              "xgmi_open: handles must be uint8 [world, ", sizeof(hipIpcMemHandle_t), "]");
+  HIP_OK(hipSetDevice(x->device));
+  for (int r = 0; r < world; ++r) {
+    if (r == x->args.rank) continue;
+    hipIpcMemHandle_t ih;
+    std::memcpy(&ih, hc.data_ptr<uint8_t>() + r * sizeof(ih), sizeof(ih));
+    void* p = nullptr;
+    HIP_OK(hipIpcOpenMemHandle(&p, ih, hipIpcMemLazyEnablePeerAccess));
+    x->args.bufs[r] = (char*)p;
+    x->opened.push_back((char*)p);
+  }
+  x->connected = true;
+}
+
+// same-process "ranks" (kernel test): rank r's buffer is communicator peers[r]'s own buffer
+void xgmi_connect_local(int64_t h, std::vector<int64_t> peers) {
+  Xgmi* x = get(h);
+  TORCH_CHECK((int)peers.size() == x->args.world, "xgmi_connect_local: one communicator per rank");
+  for (int r = 0; r < x->args.world; ++r) {
+    Xgmi* p = get(peers[r]);
+    TORCH_CHECK(p->args.rank == r && p->args.world == x->args.world && p->args.slot_bytes == x->args.slot_bytes,
+                "xgmi_connect_local: peer ", r, " has a different layout");
+    x->args.bufs[r] = p->own;
+  }
+  x->connected = true;
+}
+
+void check_ready(Xgmi* x, const Tensor& t) {
+  TORCH_CHECK(x->connected, "xgmi communicator is not connected to its peers");
+  TORCH_CHECK(t.device().type() == c10::DeviceType::CUDA && t.get_device() == x->device,
+              "xgmi: tensor must live on the communicator's GPU");
+  TORCH_CHECK(t.is_contiguous(), "xgmi: tensor must be contiguous");
+}
+
+hipStream_t stream_of(const Tensor& t) { return c10::hip::getCurrentHIPStream(t.get_device()).stream(); }
+
+// out = sum over ranks of `in` (fp32 or bf16; out may alias in)
+void xgmi_all_reduce(const Tensor& in, Tensor& out, int64_t h) {
+  Xgmi* x = get(h);
+  check_ready(x, in);
+  check_ready(x, out);
+  TORCH_CHECK(in.scalar_type() == out.scalar_type() && in.numel() == out.numel(), "xgmi_all_reduce: in/out mismatch");
+  const int elem = in.scalar_type() == at::kFloat ? 0 : in.scalar_type() == at::kBFloat16 ? 1 : -1;
+  TORCH_CHECK(elem >= 0, "xgmi_all_reduce: fp32 or bf16 only");
+  const long long n = in.numel();
+  TORCH_CHECK(n % 8 == 0, "xgmi_all_reduce: element count must be a multiple of 8");
+  TORCH_CHECK(n * (long long)in.element_size() <= x->args.slot_bytes, "xgmi_all_reduce: message of ",
+              n * in.element_size(), " B exceeds the ", x->args.slot_bytes, " B slot");
+  const int chunk = xgmi_chunk(n, XG_MAX_WG);
+  TORCH_CHECK((n + chunk - 1) / chunk <= XG_MAX_WG, "xgmi_all_reduce: too many chunks");
+  launch_xgmi_all_reduce(x->args, in.data_ptr(), out.data_ptr(), n, elem, stream_of(in));
+}
+
+// resid += all_reduce(y); xw = bf16(resid * w); ss[row][part] = sum(resid^2) per column part
+void xgmi_add_prep(const Tensor& y, Tensor& resid, const Tensor& w, Tensor& xw, Tensor& ss, int64_t h) {
+  Xgmi* x = get(h);
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&y, &resid, &w, &xw, &ss}) check_ready(x, *t);
+  TORCH_CHECK(y.scalar_type() == at::kFloat && resid.scalar_type() == at::kFloat && ss.scalar_type() == at::kFloat,
+              "xgmi_add_prep: y, resid, ss fp32");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && xw.scalar_type() == at::kBFloat16, "xgmi_add_prep: w, xw bf16");
+  TORCH_CHECK(resid.dim() == 2, "xgmi_add_prep: resid [T, d]");
+  const int64_t T = resid.size(0), d = resid.size(1);
+  TORCH_CHECK(y.numel() == T * d && xw.numel() == T * d && w.numel() == d, "xgmi_add_prep: shape mismatch");
+  const int64_t P = ss.dim() == 2 ? ss.size(1) : 1;
+  TORCH_CHECK(ss.numel() >= T * P && P >= 1 && P <= 16 && d % (8 * P) == 0, "xgmi_add_prep: ss parts must divide d / 8");
+  TORCH_CHECK(T * P <= XG_MAX_WG, "xgmi_add_prep: too many rows");
+  TORCH_CHECK(T * d * 4 <= x->args.slot_bytes, "xgmi_add_prep: message exceeds the slot");
+  launch_xgmi_add_prep(x->args, y.data_ptr<float>(), resid.data_ptr<float>(),
+                       reinterpret_cast<const bf16*>(w.data_ptr()), reinterpret_cast<bf16*>(xw.data_ptr()),
+                       ss.data_ptr<float>(), (int)T, (int)d, (int)P, stream_of(y));
+}
+
+// test-only: every rank of this process in one launch (grid slice per rank; see xgmi_ar.hip)
+void xgmi_all_reduce_multi(std::vector<Tensor> ins, std::vector<Tensor> outs, std::vector<int64_t> comms) {
+  const int world = (int)comms.size();
+  TORCH_CHECK(world >= 1 && world <= XG_MULTI_MAX && (int)ins.size() == world && (int)outs.size() == world,
+              "xgmi_all_reduce_multi: one input, output and communicator per rank (<= ", XG_MULTI_MAX, ")");
+  XgmiMulti m{};
+  const long long n = ins[0].numel();
+  int elem = -1;
+  for (int r = 0; r < world; ++r) {
+    Xgmi* x = get(comms[r]);
+    TORCH_CHECK(x->args.rank == r && x->args.world == world, "xgmi_all_reduce_multi: communicator ", r, " is not rank ", r);
+    check_ready(x, ins[r]);
+    check_ready(x, outs[r]);
+    TORCH_CHECK(ins[r].numel() == n && outs[r].numel() == n && ins[r].scalar_type() == ins[0].scalar_type() &&
+                    outs[r].scalar_type() == ins[0].scalar_type(), "xgmi_all_reduce_multi: shape / dtype mismatch");
+    TORCH_CHECK(n * (long long)ins[r].element_size() <= x->args.slot_bytes, "xgmi_all_reduce_multi: message exceeds the slot");
+    m.c[r] = x->args;
+    m.in[r] = ins[r].data_ptr();
+    m.out[r] = outs[r].data_ptr();
+  }
+  elem = ins[0].scalar_type() == at::kFloat ? 0 : ins[0].scalar_type() == at::kBFloat16 ? 1 : -1;
+  TORCH_CHECK(elem >= 0 && n % 8 == 0, "xgmi_all_reduce_multi: fp32 / bf16, element count % 8");
+  launch_xgmi_all_reduce_multi(m, world, n, elem, stream_of(ins[0]));
+}
+
+void xgmi_add_prep_multi(std::vector<Tensor> ys, std::vector<Tensor> resids, const Tensor& w, std::vector<Tensor> xws,
+                         std::vector<Tensor> sss, std::vector<int64_t> comms) {
+  const int world = (int)comms.size();
+  TORCH_CHECK(world >= 1 && world <= XG_MULTI_MAX && (int)ys.size() == world && (int)resids.size() == world &&
+                  (int)xws.size() == world && (int)sss.size() == world,
+              "xgmi_add_prep_multi: one set of tensors per rank");
+  XgmiMulti m{};
+  const int64_t T = resids[0].size(0), d = resids[0].size(1);
+  const int64_t P = sss[0].dim() == 2 ? sss[0].size(1) : 1;
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.numel() == d && w.is_contiguous(), "xgmi_add_prep_multi: w bf16 [d]");
+  TORCH_CHECK(P >= 1 && P <= 16 && d % (8 * P) == 0 && T * P <= XG_MAX_WG, "xgmi_add_prep_multi: bad parts");
+  for (int r = 0; r < world; ++r) {
+    Xgmi* x = get(comms[r]);
+    TORCH_CHECK(x->args.rank == r && x->args.world == world, "xgmi_add_prep_multi: communicator ", r, " is not rank ", r);
+    for (const Tensor* t : std::initializer_list<const Tensor*>{&ys[r], &resids[r], &xws[r], &sss[r]}) check_ready(x, *t);
+    TORCH_CHECK(ys[r].scalar_type() == at::kFloat && resids[r].scalar_type() == at::kFloat &&
+                    sss[r].scalar_type() == at::kFloat && xws[r].scalar_type() == at::kBFloat16,
+                "xgmi_add_prep_multi: dtypes");
+    TORCH_CHECK(ys[r].numel() == T * d && resids[r].numel() == T * d && xws[r].numel() == T * d &&
+                    sss[r].numel() >= T * P, "xgmi_add_prep_multi: shapes");
+    TORCH_CHECK(T * d * 4 <= x->args.slot_bytes, "xgmi_add_prep_multi: message exceeds the slot");
+    m.c[r] = x->args;
+    m.in[r] = ys[r].data_ptr();
+    m.out[r] = resids[r].data_ptr();
+    m.xw[r] = xws[r].data_ptr();
+    m.ss[r] = sss[r].data_ptr<float>();
+  }
+  m.w = reinterpret_cast<const bf16*>(w.data_ptr());
+  launch_xgmi_add_prep_multi(m, world, (int)T, (int)d, (int)P, stream_of(ys[0]));
+}
+
+// reads (and clears) the error word: 1 + the source rank that never signalled within the wait limit
+int64_t xgmi_error(int64_t h) {
+  Xgmi* x = get(h);
+  int v = 0;
+  HIP_OK(hipMemcpy(&v, x->args.err, sizeof(int), hipMemcpyDeviceToHost));
+  if (v) HIP_OK(hipMemset(x->args.err, 0, sizeof(int)));
+  return v;
+}
+
+int64_t xgmi_slot_bytes(int64_t h) { return get(h)->args.slot_bytes; }
+
+void xgmi_destroy(int64_t h) {
+  Xgmi* x = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    if (h < 0 || h >= (int64_t)g_x.size() || g_x[h] == nullptr) return;
+    x = g_x[h];
+    g_x[h] = nullptr;
+  }
+  (void)hipSetDevice(x->device);
+  (void)hipDeviceSynchronize();
+  for (char* p : x->opened) (void)hipIpcCloseMemHandle(p);
+  (void)hipFree(x->args.epochs);
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    g_uc_pool.emplace_back(x->bytes, x->own);
+  }
+  delete x;
+}
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(symmetry_amd, m) {
+  m.def("xgmi_create(int slot_bytes, int world, int rank, int device) -> int", &xgmi_create);
+  m.def("xgmi_ipc_handle(int comm) -> Tensor", &xgmi_ipc_handle);
+  m.def("xgmi_open(int comm, Tensor handles) -> ()", &xgmi_open);
+  m.def("xgmi_connect_local(int comm, int[] peers) -> ()", &xgmi_connect_local);
+  m.def("xgmi_all_reduce(Tensor input, Tensor(a!) out, int comm) -> ()", &xgmi_all_reduce);
+  m.def("xgmi_add_prep(Tensor y, Tensor(a!) resid, Tensor w, Tensor(b!) xw, Tensor(c!) ss, int comm) -> ()",
+        &xgmi_add_prep);
+  m.def("xgmi_all_reduce_multi(Tensor[] inputs, Tensor(a!)[] outs, int[] comms) -> ()", &xgmi_all_reduce_multi);
+  m.def(
+      "xgmi_add_prep_multi(Tensor[] ys, Tensor(a!)[] resids, Tensor w, Tensor(b!)[] xws, Tensor(c!)[] sss, int[] comms) "
+      "-> ()",
+      &xgmi_add_prep_multi);
+  m.def("xgmi_error(int comm) -> int", &xgmi_error);
+  m.def("xgmi_slot_bytes(int comm) -> int", &xgmi_slot_bytes);
+  m.def("xgmi_destroy(int comm) -> ()", &xgmi_destroy);
+}

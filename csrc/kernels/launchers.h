@@ -175,3 +175,32 @@ void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, fl
                            int K, int S, hipStream_t s);
 void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_lo, int e_hi, const float* w, int T, int k,
                         int d, float* out, int accumulate, hipStream_t s);
+
+// xgmi_ar.hip: one-shot all-reduce over xGMI peer memory (IPC-mapped buffers of every TP rank)
+constexpr int XG_MAX_WORLD = 8;
+constexpr int XG_MAX_WG = 4096;
+struct XgmiArgs {
+  char* bufs[XG_MAX_WORLD];  // every rank's comm buffer as mapped in this process (own one included)
+  unsigned* epochs;          // [XG_MAX_WG] local per-workgroup collective counters (zeroed once)
+  int* err;                  // local error word (a peer never arrived)
+  int rank, world;
+  long long slot_bytes;      // bytes of one (parity, source rank) data slot
+};
+long long xgmi_buffer_bytes(int world, long long slot_bytes);
+int xgmi_chunk(long long n, long long max_wg);
+void launch_xgmi_all_reduce(const XgmiArgs& c, const void* in, void* out, long long n, int elem, hipStream_t s);
+void launch_xgmi_add_prep(const XgmiArgs& c, const float* y, float* resid, const bf16* w, bf16* xw, float* ss, int T,
+                          int d, int parts, hipStream_t s);
+// test-only: the ranks of one process as grid slices of ONE launch (co-resident by construction).
+// add_prep: in = y, out = resid, xw, ss per rank; w shared
+constexpr int XG_MULTI_MAX = 4;
+struct XgmiMulti {
+  XgmiArgs c[XG_MULTI_MAX];
+  const void* in[XG_MULTI_MAX];
+  void* out[XG_MULTI_MAX];
+  void* xw[XG_MULTI_MAX];
+  float* ss[XG_MULTI_MAX];
+  const bf16* w;
+};
+void launch_xgmi_all_reduce_multi(const XgmiMulti& m, int world, long long n, int elem, hipStream_t s);
+void launch_xgmi_add_prep_multi(const XgmiMulti& m, int world, int T, int d, int parts, hipStream_t s);

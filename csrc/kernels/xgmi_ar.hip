@@ -1,0 +1,220 @@
+// R1 for decode: one-shot all-reduce over xGMI peer memory (§7.4 risk 4).
+//
+// A Llama-3-70B TP=8 decode step issues 160 all-reduces of 16 KiB x batch (fp32 partials: 32 KiB x
+// batch).  At those sizes a collective is pure latency, and a ring (RCCL's default shape) pays 2(N-1)
+// dependent hops over ONE of the seven point-to-point xGMI links.  Here every rank writes its partial
+// straight into a slot of EVERY peer's buffer (seven links busy at once, one hop), raises a flag per
+// (workgroup, source rank) in each peer, waits for the world's flags of its own chunk and reduces the
+// slots in rank order -- so every rank computes bit-identical sums (TP ranks must agree on the sampled
+// token).  The reduce can carry the decode epilogue of the row-parallel projections (residual add +
+// next-norm prep, the `add_prep` of decode_gemm.hip), which removes a launch per all-reduce.
+//
+// Buffers: one per rank, hipExtMallocWithFlags(hipDeviceMallocUncached) so that stores arriving over
+// xGMI are never hidden behind a stale L2 line of the reading GPU, exported with hipIpcGetMemHandle and
+// opened by every peer (symmetry_amd/parallel/comm.py::XgmiComm).  Layout of a buffer:
+//   flags [XG_MAX_WG][XG_MAX_WORLD] u32 | data [2 parities][world][slot_bytes]
+// Epochs: workgroup g of every launch bumps its own local counter epochs[g]; all ranks run the same
+// sequence of collectives with the same grids, so the counters agree across ranks without any host
+// bookkeeping, and a captured hipGraph replays correctly.  Data slots alternate by epoch parity: a rank
+// can run at most one collective ahead of a peer (it waits for that peer's flag of the previous one),
+// so the slot it writes is never the slot the peer is still reducing.  Flags are compared with a signed
+// difference (a fast peer may already have raised the next epoch).
+// Spins are bounded: a missing peer sets the error word and the kernel exits instead of hanging.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+constexpr long long XG_FLAG_BYTES = (long long)XG_MAX_WG * XG_MAX_WORLD * 4;
+constexpr int XG_THREADS = 256;
+constexpr unsigned long long XG_WAIT_TICKS = 200000000ull;  // 2 s of the 100 MHz wall clock: a peer that
+                                                            // never arrives is an error, not a hang
+
+SYM_DEV char* xg_slot(const XgmiArgs& c, int r, int par, int src) {
+  return c.bufs[r] + XG_FLAG_BYTES + ((long long)par * c.world + src) * c.slot_bytes;
+}
+
+// Push this workgroup's chunk (nvec 16-byte vectors at byte offset `off`) into slot (parity, rank) of
+// every rank's buffer (its own included, so the reduce reads all slots from one place), signal, wait for
+// every rank's signal of the same chunk.  Returns the epoch parity (the slot set to reduce).
+SYM_DEV int xg_exchange(const XgmiArgs& c, int wg, const uint4* __restrict__ src, long long off, int nvec) {
+  __shared__ unsigned s_epoch;
+  if (threadIdx.x == 0) {
+    const unsigned e = c.epochs[wg] + 1u;
+    c.epochs[wg] = e;
+    s_epoch = e;
+  }
+  __syncthreads();
+  const unsigned epoch = s_epoch;
+  const int par = (int)(epoch & 1u);
+  for (int v = threadIdx.x; v < nvec; v += XG_THREADS) {
+    const uint4 x = src[v];
+    for (int r = 0; r < c.world; ++r) reinterpret_cast<uint4*>(xg_slot(c, r, par, c.rank) + off)[v] = x;
+  }
+  // Every wave waits for its slot stores to be acknowledged before the workgroup signals.  The buffers
+  // are uncached (MTYPE UC): the stores never sit in an L2 and the slot loads below never hit one, so
+  // no cache write-back / invalidate is needed on either side -- and none is issued: a system-scope
+  // fence also writes back and invalidates the XCD's L2 for every other workgroup's plain traffic.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x < c.world) {
+    unsigned* f = reinterpret_cast<unsigned*>(c.bufs[threadIdx.x]) + wg * XG_MAX_WORLD + c.rank;
+    __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned* mine = reinterpret_cast<const unsigned*>(c.bufs[c.rank]) + wg * XG_MAX_WORLD + threadIdx.x;
+    const unsigned long long t0 = wall_clock64();
+    while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      if (wall_clock64() - t0 > XG_WAIT_TICKS) {  // error word: 1 + the source rank that never arrived
+        __hip_atomic_store(c.err, 1 + (int)threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();  // the pollers saw every flag: the slot bytes behind them are in memory (uncached)
+  return par;
+}
+
+// Plain all-reduce (sum) of n elements, in place or out of place; ELEM: 0 = fp32, 1 = bf16.
+// Workgroup g owns elements [g * chunk, min(n, (g + 1) * chunk)), chunk a multiple of 8.
+template <int ELEM>
+SYM_DEV void xg_all_reduce_body(const XgmiArgs& c, int wg, const void* in, void* out, long long n, int chunk) {
+  const long long e0 = (long long)wg * chunk;
+  const int cnt = (int)min((long long)chunk, n - e0);
+  constexpr int ESZ = ELEM == 0 ? 4 : 2;
+  const int nvec = cnt * ESZ / 16;
+  const long long off = e0 * ESZ;
+  const int par = xg_exchange(c, wg, reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(in) + off), off,
+                              nvec);
+  for (int v = threadIdx.x; v < nvec; v += XG_THREADS) {
+    if constexpr (ELEM == 0) {
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < c.world; ++r) {
+        const float4 x = reinterpret_cast<const float4*>(xg_slot(c, c.rank, par, r) + off)[v];
+        acc[0] += x.x;
+        acc[1] += x.y;
+        acc[2] += x.z;
+        acc[3] += x.w;
+      }
+      reinterpret_cast<float4*>(reinterpret_cast<char*>(out) + off)[v] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    } else {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < c.world; ++r) {
+        float f[8];
+        load8(reinterpret_cast<const bf16*>(xg_slot(c, c.rank, par, r) + off) + 8 * v, f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += f[i];
+      }
+      store8(reinterpret_cast<bf16*>(reinterpret_cast<char*>(out) + off) + 8 * v, acc);
+    }
+  }
+}
+
+// All-reduce of fp32 row partials [T][d] fused with the decode epilogue of a row-parallel projection
+// (prep_kernel<1>): resid += sum; xw = bf16(resid * w); ss[row][part] = sum(resid^2) over the part's
+// columns.  Workgroup (row, part) of P owns columns [part d / P, (part + 1) d / P) of its row.
+SYM_DEV void xg_add_prep_body(const XgmiArgs& c, int row, int part, int P, const float* __restrict__ y,
+                              float* __restrict__ resid, const bf16* __restrict__ w, bf16* __restrict__ xw,
+                              float* __restrict__ ss, int d) {
+  __shared__ float scratch[XG_THREADS / 64];
+  const int dp = d / P;
+  const int wg = row * P + part;
+  const long long rb = (long long)row * d + (long long)part * dp;
+  const long long off = rb * 4;
+  const int par = xg_exchange(c, wg, reinterpret_cast<const uint4*>(y + rb), off, dp / 4);
+  const bf16* wp = w + (long long)part * dp;
+  float acc = 0.f;
+  for (int vi = threadIdx.x; vi < dp / 8; vi += XG_THREADS) {
+    float r[8], g[8];
+    float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < c.world; ++s) {  // the all-reduced delta first (rank order), then the residual add
+      float dd[8];
+      load8f(reinterpret_cast<const float*>(xg_slot(c, c.rank, par, s) + off) + vi * 8, dd);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sum[i] += dd[i];
+    }
+    load8f(resid + rb + vi * 8, r);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] += sum[i];
+    store8f(resid + rb + vi * 8, r);
+    load8(wp + vi * 8, g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      acc += r[i] * r[i];
+      g[i] *= r[i];
+    }
+    store8(xw + rb + vi * 8, g);
+  }
+  acc = block_sum<XG_THREADS>(acc, scratch);
+  if (threadIdx.x == 0) ss[row * P + part] = acc;
+}
+
+template <int ELEM>
+__global__ __launch_bounds__(XG_THREADS) void xgmi_all_reduce_kernel(XgmiArgs c, const void* in, void* out,
+                                                                     long long n, int chunk) {
+  xg_all_reduce_body<ELEM>(c, blockIdx.x, in, out, n, chunk);
+}
+
+__global__ __launch_bounds__(XG_THREADS) void xgmi_add_prep_kernel(XgmiArgs c, const float* __restrict__ y,
+                                                                  float* __restrict__ resid,
+                                                                  const bf16* __restrict__ w,
+                                                                  bf16* __restrict__ xw, float* __restrict__ ss,
+                                                                  int d) {
+  xg_add_prep_body(c, blockIdx.x, blockIdx.y, gridDim.y, y, resid, w, xw, ss, d);
+}
+
+// Several ranks of ONE process in one launch (grid z = rank): the GPU test of the protocol on one device.
+// Separate launches on separate streams are not guaranteed to be co-resident (streams may share a
+// hardware queue), and every rank waits on the others; the slices of one grid are.
+template <int ELEM>
+__global__ __launch_bounds__(XG_THREADS) void xgmi_all_reduce_multi_kernel(XgmiMulti m, long long n, int chunk) {
+  const int r = blockIdx.z;
+  xg_all_reduce_body<ELEM>(m.c[r], blockIdx.x, m.in[r], m.out[r], n, chunk);
+}
+
+__global__ __launch_bounds__(XG_THREADS) void xgmi_add_prep_multi_kernel(XgmiMulti m, int d) {
+  const int r = blockIdx.z;
+  xg_add_prep_body(m.c[r], blockIdx.x, blockIdx.y, gridDim.y, reinterpret_cast<const float*>(m.in[r]),
+                   reinterpret_cast<float*>(m.out[r]), m.w, reinterpret_cast<bf16*>(m.xw[r]), m.ss[r], d);
+}
+
+}  // namespace
+
+long long xgmi_buffer_bytes(int world, long long slot_bytes) { return XG_FLAG_BYTES + 2LL * world * slot_bytes; }
+
+int xgmi_chunk(long long n, long long max_wg) {
+  // >= 2048 elements per workgroup (latency-bound messages: fewer, fatter signals), multiple of 8
+  long long chunk = (n + max_wg - 1) / max_wg;
+  chunk = std::max<long long>(chunk, 2048);
+  return (int)((chunk + 7) / 8 * 8);
+}
+
+void launch_xgmi_all_reduce(const XgmiArgs& c, const void* in, void* out, long long n, int elem, hipStream_t s) {
+  if (n == 0) return;
+  const int chunk = xgmi_chunk(n, XG_MAX_WG);
+  const int grid = (int)((n + chunk - 1) / chunk);
+  if (elem == 0)
+    xgmi_all_reduce_kernel<0><<<grid, XG_THREADS, 0, s>>>(c, in, out, n, chunk);
+  else
+    xgmi_all_reduce_kernel<1><<<grid, XG_THREADS, 0, s>>>(c, in, out, n, chunk);
+}
+
+void launch_xgmi_add_prep(const XgmiArgs& c, const float* y, float* resid, const bf16* w, bf16* xw, float* ss, int T,
+                          int d, int parts, hipStream_t s) {
+  if (T == 0) return;
+  xgmi_add_prep_kernel<<<dim3(T, parts), XG_THREADS, 0, s>>>(c, y, resid, w, xw, ss, d);
+}
+
+void launch_xgmi_all_reduce_multi(const XgmiMulti& m, int world, long long n, int elem, hipStream_t s) {
+  if (n == 0) return;
+  const int chunk = xgmi_chunk(n, XG_MAX_WG);
+  const dim3 grid((unsigned)((n + chunk - 1) / chunk), 1, (unsigned)world);
+  if (elem == 0)
+    xgmi_all_reduce_multi_kernel<0><<<grid, XG_THREADS, 0, s>>>(m, n, chunk);
+  else
+    xgmi_all_reduce_multi_kernel<1><<<grid, XG_THREADS, 0, s>>>(m, n, chunk);
+}
+
+void launch_xgmi_add_prep_multi(const XgmiMulti& m, int world, int T, int d, int parts, hipStream_t s) {
+  if (T == 0) return;
+  xgmi_add_prep_multi_kernel<<<dim3(T, parts, world), XG_THREADS, 0, s>>>(m, d);
+}

@@ -310,8 +310,8 @@ class TransformerLM:
         if self._tp_active():
             y = self._buf(name + ".f32", (x.shape[0], W.shape[0]), torch.float32)
             ops.dg_f32(x, W, None, 0.0, y, wshuf=sh)
-            self.tp.all_reduce(y)
-            ops.add_prep(y, resid, w_next, xw, ss_1)
+            # all-reduce + residual add + next-norm prep (one launch on the xGMI communicator)
+            self.tp.all_reduce_add_prep(y, resid, w_next, xw, ss_1)
             return ss_1
         ops.dg_resid(x, W, resid, w_next, xw, ss_t, wshuf=sh)
         return ss_t

@@ -8,6 +8,12 @@ Two interchangeable implementations of one small interface
   into the decode hipGraph; rides xGMI on an MI355X node.
 * :class:`TorchComm` -- ``torch.distributed`` on a process group (gloo on the
   CPU for the multi-process tests; RCCL through c10d on GPUs).
+* :class:`XgmiComm` -- wraps one of the above: all-reduces that fit its slot
+  (decode-sized) run as ONE one-shot kernel over xGMI peer memory
+  (``csrc/kernels/xgmi_ar.hip``: every rank writes its partial into every
+  peer's buffer, seven links at once, one hop), optionally fused with the
+  residual add + next-norm prep of the row-parallel projections; everything
+  else goes to the wrapped communicator.
 * :class:`HostStagedComm` -- GPU tensors reduced through a gloo group on the
   host.  Not a fast path: it lets several ranks share ONE GPU (RCCL refuses
   duplicate devices), so the sharded HIP kernels of a TP/EP launch can be
@@ -38,6 +44,14 @@ class Comm:
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
         raise NotImplementedError
+
+    def all_reduce_add_prep(self, y, resid, w_next, xw, ss) -> None:
+        """resid += all_reduce(y); xw = bf16(resid * w_next); ss = row sums of resid^2 (decode epilogue
+        of a row-parallel projection, ``ops.add_prep``).  Fused into the collective by XgmiComm."""
+        from .. import ops
+
+        self.all_reduce(y)
+        ops.add_prep(y, resid, w_next, xw, ss)
 
 
 _OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
@@ -131,3 +145,63 @@ class RcclComm(Comm):
 
     def destroy(self):
         self.ops.rccl_destroy(self.handle)
+
+
+class XgmiComm(Comm):
+    """One-shot all-reduce over xGMI peer memory for decode-sized messages (see module docstring).
+
+    Every rank allocates one uncached buffer (flags + 2 x world slots of ``slot_bytes``), the IPC handles
+    are all-gathered over ``group`` (gloo) and every peer buffer is mapped (``hipIpcOpenMemHandle``).
+    Messages larger than a slot, non-sum ops and other dtypes go to ``inner`` (RCCL)."""
+
+    def __init__(self, inner: Comm, group, device, slot_bytes: int = 4 << 20):
+        from ..ops import _native
+
+        self.ops = _native.ops()
+        self.inner = inner
+        self.rank, self.world = inner.rank, inner.world
+        dev = torch.device(device)
+        self.handle = int(self.ops.xgmi_create(int(slot_bytes), self.world, self.rank, dev.index or 0))
+        self.slot_bytes = int(slot_bytes)
+        self.calls = {"all_reduce": 0, "add_prep": 0}  # collectives issued on the xGMI kernels (host count)
+        mine = self.ops.xgmi_ipc_handle(self.handle)
+        allh = [torch.zeros_like(mine) for _ in range(self.world)]
+        dist.all_gather(allh, mine, group=group)
+        self.ops.xgmi_open(self.handle, torch.stack(allh))
+        dist.barrier(group=group)  # every rank mapped every buffer before the first collective
+
+    def _fits(self, t) -> bool:
+        return (t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous()
+                and t.numel() % 8 == 0 and t.numel() * t.element_size() <= self.slot_bytes)
+
+    def all_reduce(self, t, op="sum"):
+        if op == "sum" and self._fits(t):
+            self.ops.xgmi_all_reduce(t, t, self.handle)
+            self.calls["all_reduce"] += 1
+        else:
+            self.inner.all_reduce(t, op)
+
+    def all_reduce_add_prep(self, y, resid, w_next, xw, ss):
+        if y.dtype == torch.float32 and self._fits(y) and y.numel() == resid.numel():
+            self.ops.xgmi_add_prep(y, resid, w_next, xw, ss, self.handle)
+            self.calls["add_prep"] += 1
+        else:
+            super().all_reduce_add_prep(y, resid, w_next, xw, ss)
+
+    def all_gather(self, t):
+        return self.inner.all_gather(t)
+
+    def all_to_all_rows(self, send, send_counts, recv_counts):
+        return self.inner.all_to_all_rows(send, send_counts, recv_counts)
+
+    def broadcast(self, t, src=0):
+        self.inner.broadcast(t, src)
+
+    def error(self) -> int:
+        """1 if a collective gave up waiting for a peer since the last call (cleared on read)."""
+        return int(self.ops.xgmi_error(self.handle))
+
+    def destroy(self):
+        self.ops.xgmi_destroy(self.handle)
+        if hasattr(self.inner, "destroy"):
+            self.inner.destroy()

@@ -15,7 +15,7 @@ import os
 import torch
 import torch.distributed as dist
 
-from .comm import HostStagedComm, RcclComm, TorchComm
+from .comm import HostStagedComm, RcclComm, TorchComm, XgmiComm
 
 
 def init_distributed(backend: str | None = None) -> tuple[int, int, int]:
@@ -32,15 +32,22 @@ def init_distributed(backend: str | None = None) -> tuple[int, int, int]:
     return rank, world, local
 
 
-def make_comms(on_gpu: bool):
+def make_comms(on_gpu: bool, device=None):
     """TP/EP communicator + the gloo metadata group.  ``SYMMETRY_TP_COMM=gloo`` on GPUs selects the
-    host-staged communicator (ranks sharing one GPU for kernel checks; no hipGraphs)."""
+    host-staged communicator (ranks sharing one GPU for kernel checks; no hipGraphs).  On GPUs the
+    decode-sized all-reduces run on the one-shot xGMI kernel (:class:`XgmiComm`) unless
+    ``SYMMETRY_XGMI=0``; ``SYMMETRY_XGMI_SLOT`` sets its per-rank slot (bytes, default 4 MiB)."""
     cpu_group = dist.new_group(backend="gloo")
     if not on_gpu:
         return TorchComm(cpu_group), cpu_group
     if os.environ.get("SYMMETRY_TP_COMM", "rccl").lower() == "gloo":
-        return HostStagedComm(cpu_group), cpu_group
-    return RcclComm(bootstrap_group=cpu_group), cpu_group
+        comm = HostStagedComm(cpu_group)
+    else:
+        comm = RcclComm(bootstrap_group=cpu_group)
+    if os.environ.get("SYMMETRY_XGMI", "1") != "0" and 1 < comm.world <= 8:
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        comm = XgmiComm(comm, cpu_group, dev, int(os.environ.get("SYMMETRY_XGMI_SLOT", 4 << 20)))
+    return comm, cpu_group
 
 
 def init_tp_engine(ecfg):
@@ -56,7 +63,7 @@ def init_tp_engine(ecfg):
 
     rank, world, local = init_distributed()
     on_gpu = torch.cuda.is_available() and ecfg.device != "cpu"
-    comm, cpu_group = make_comms(on_gpu)
+    comm, cpu_group = make_comms(on_gpu, torch.device("cuda", local) if on_gpu else None)
     ecfg.tp_size, ecfg.tp_rank = world, rank
     mcfg = ecfg.model_config or resolve(ecfg.model)
     ep_comm = None

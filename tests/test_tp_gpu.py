@@ -27,11 +27,11 @@ def _port():
     return p
 
 
-def _entry(model, rank, world, port, q):
+def _entry(model, rank, world, port, q, xgmi="0"):
     import traceback
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK="0", SYMMETRY_TP_COMM="gloo")
+                      LOCAL_RANK="0", SYMMETRY_TP_COMM="gloo", SYMMETRY_XGMI=xgmi)
     try:
         from symmetry_amd.engine.llm_engine import EngineConfig
         from symmetry_amd.engine.sequence import SamplingParams
@@ -40,6 +40,10 @@ def _entry(model, rank, world, port, q):
         ecfg = EngineConfig(model=model, device="cuda", max_num_seqs=4, max_model_len=512, num_kv_blocks=64,
                             use_graphs=False, weight_init="full")
         eng, r = init_tp_engine(ecfg)
+        if xgmi == "1":
+            from symmetry_amd.parallel.comm import XgmiComm
+
+            assert isinstance(eng.runner.model.tp, XgmiComm), type(eng.runner.model.tp)
         if r != 0:
             eng.runner.worker_loop()
             q.put((rank, None))
@@ -48,6 +52,10 @@ def _entry(model, rank, world, port, q):
                 for i, p in enumerate(PROMPTS)]
         while eng.has_unfinished():
             eng.step()
+        if xgmi == "1":
+            calls = eng.runner.model.tp.calls
+            assert calls["add_prep"] > 0, calls  # decode steps ran the fused peer-memory all-reduce
+            assert eng.runner.model.tp.error() == 0
         eng.shutdown()
         q.put((rank, [s.output_ids for s in seqs]))
     except Exception:
@@ -59,13 +67,13 @@ def _entry(model, rank, world, port, q):
             dist.destroy_process_group()
 
 
-def _run(model, world=2):
+def _run(model, world=2, xgmi="0"):
     import torch.multiprocessing as mp
 
     port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    procs = [ctx.Process(target=_entry, args=(model, r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_entry, args=(model, r, world, port, q, xgmi)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get() for _ in range(world))
@@ -76,13 +84,16 @@ def _run(model, world=2):
     return res[0]
 
 
+@pytest.mark.parametrize("xgmi", ["0", "1"])
 @pytest.mark.parametrize("model", ["small-llama", "tiny-mixtral"])
-def test_tp2_on_one_gpu_matches_oracle(gpu, model):
-    """small-llama: TP=2 (1 KV head per rank, down K = 1792).  tiny-mixtral: attention TP=2 + EP=2."""
+def test_tp2_on_one_gpu_matches_oracle(gpu, model, xgmi):
+    """small-llama: TP=2 (1 KV head per rank, down K = 1792).  tiny-mixtral: attention TP=2 + EP=2.
+    xgmi=1: the decode all-reduces (+ fused residual / norm prep) run on the one-shot peer-memory kernel
+    between the two processes (IPC-mapped buffers on the one GPU)."""
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
     from symmetry_amd.models import reference_model as rm
 
-    outs = _run(model)
+    outs = _run(model, xgmi=xgmi)
     ref = LLMEngine(EngineConfig(model=model, device="cpu", max_num_seqs=4, max_model_len=512, weight_init="full"))
     for p, out in zip(PROMPTS, outs):
         assert len(out) == 10

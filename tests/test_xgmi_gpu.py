@@ -1,0 +1,136 @@
+"""One-shot xGMI all-reduce kernels (csrc/kernels/xgmi_ar.hip) on ONE MI355X.
+
+Several "ranks" live in this one process: each has its own communicator (buffer, epoch counters, error
+word), the buffers are mapped to each other directly (``xgmi_connect_local``) instead of through IPC
+handles, and the ranks run as the grid slices of one launch (``*_multi`` ops: separate launches on
+separate streams may share a hardware queue and would then wait on each other forever) -- the kernel
+protocol (push into every peer's slot, per-(workgroup, source) flags, epoch parity, rank-order reduce)
+is exactly the multi-GPU one, with local HBM standing in for the xGMI links.  The two-process IPC path runs end to end in
+``test_tp_gpu.py`` (TP=2 engine on one GPU with ``SYMMETRY_XGMI=1``).  Spins are bounded, so a rank
+that never arrives shows up as the error word, not a hang.  Reference: fp32 torch sums in rank order.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _comms(ops, world, slot_bytes=1 << 20):
+    hs = [int(ops.xgmi_create(slot_bytes, world, r, 0)) for r in range(world)]
+    for h in hs:
+        ops.xgmi_connect_local(h, hs)
+    return hs
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n", [4096, 8 * 3001, 262144])
+def test_xgmi_all_reduce(gpu, world, dtype, n):
+    from symmetry_amd.ops import _native
+
+    ops = _native.ops()
+    hs = _comms(ops, world)
+    g = torch.Generator(device="cpu").manual_seed(n + world)
+    try:
+        for it in range(3):  # consecutive collectives alternate the slot parity
+            xs = [torch.randn(n, generator=g).to(gpu, dtype) for _ in range(world)]
+            outs = [torch.full_like(x, float("nan")) for x in xs]
+            ops.xgmi_all_reduce_multi(xs, outs, hs)
+            torch.cuda.synchronize()
+            ref = torch.zeros(n, dtype=torch.float32, device=gpu)
+            for x in xs:
+                ref += x.float()
+            for r in range(world):
+                assert ops.xgmi_error(hs[r]) == 0
+                torch.testing.assert_close(outs[r].float(), ref.to(dtype).float(), rtol=0, atol=0)
+                assert torch.equal(outs[r], outs[0])  # every rank bit-identical
+    finally:
+        for h in hs:
+            ops.xgmi_destroy(h)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("T,d,P", [(1, 4096, 8), (4, 8192, 8), (10, 4096, 1), (64, 4096, 4)])
+def test_xgmi_add_prep(gpu, world, T, d, P):
+    from symmetry_amd.ops import _native, reference
+
+    ops = _native.ops()
+    hs = _comms(ops, world, slot_bytes=T * d * 4 + 256)
+    g = torch.Generator(device="cpu").manual_seed(T * d + P)
+    try:
+        w = (torch.rand(d, generator=g) + 0.5).to(gpu, torch.bfloat16)
+        resid0 = torch.randn(T, d, generator=g).to(gpu)
+        for it in range(2):
+            ys = [torch.randn(T, d, generator=g).to(gpu) for _ in range(world)]
+            resids = [resid0.clone() for _ in range(world)]
+            xws = [torch.empty(T, d, dtype=torch.bfloat16, device=gpu) for _ in range(world)]
+            sss = [torch.empty(T, P, dtype=torch.float32, device=gpu) for _ in range(world)]
+            ops.xgmi_add_prep_multi(ys, resids, w, xws, sss, hs)
+            torch.cuda.synchronize()
+            ysum = torch.zeros(T, d, device=gpu)
+            for y in ys:
+                ysum += y
+            r_ref, xw_ref, ss_ref = resid0.clone(), torch.empty_like(xws[0]), torch.empty_like(sss[0])
+            reference.add_prep(ysum, r_ref, w, xw_ref, ss_ref)
+            for r in range(world):
+                assert ops.xgmi_error(hs[r]) == 0
+                torch.testing.assert_close(resids[r], r_ref, rtol=0, atol=0)
+                torch.testing.assert_close(xws[r].float(), xw_ref.float(), rtol=1e-2, atol=1e-2)
+                torch.testing.assert_close(sss[r], ss_ref, rtol=1e-4, atol=1e-3)
+                assert torch.equal(resids[r], resids[0]) and torch.equal(sss[r], sss[0])
+            resid0 = resids[0].clone()
+    finally:
+        for h in hs:
+            ops.xgmi_destroy(h)
+
+
+def test_xgmi_all_reduce_graph_replay(gpu):
+    """Captured once, replayed: the device-side epoch counters keep the ranks in step."""
+    from symmetry_amd.ops import _native
+
+    ops = _native.ops()
+    world, n = 2, 8192
+    hs = _comms(ops, world)
+    try:
+        xs = [torch.zeros(n, device=gpu) for _ in range(world)]
+        outs = [torch.zeros(n, device=gpu) for _ in range(world)]
+        ops.xgmi_all_reduce_multi(xs, outs, hs)  # warm (epoch 1)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):  # capture only: nothing runs
+            ops.xgmi_all_reduce_multi(xs, outs, hs)
+            ops.xgmi_all_reduce_multi(outs, outs, hs)
+        for it in range(4):
+            for r in range(world):
+                xs[r].fill_(float(10 * it + r + 1))
+            graph.replay()
+            torch.cuda.synchronize()
+            expect = world * sum(float(10 * it + r + 1) for r in range(world))
+            for r in range(world):
+                assert ops.xgmi_error(hs[r]) == 0
+                assert torch.all(outs[r] == expect), (it, r, outs[r][:4].tolist(), expect)
+    finally:
+        for h in hs:
+            ops.xgmi_destroy(h)
+
+
+def test_xgmi_rejects_oversized_and_bad_shapes(gpu):
+    from symmetry_amd.ops import _native
+
+    ops = _native.ops()
+    h = int(ops.xgmi_create(4096, 1, 0, 0))
+    try:
+        with pytest.raises(RuntimeError):
+            ops.xgmi_all_reduce(torch.zeros(4096, device=gpu), torch.zeros(4096, device=gpu), h)  # not connected
+        ops.xgmi_connect_local(h, [h])
+        with pytest.raises(RuntimeError):
+            ops.xgmi_all_reduce(torch.zeros(2048, device=gpu), torch.zeros(2048, device=gpu), h)  # 8 KB > slot
+        with pytest.raises(RuntimeError):
+            ops.xgmi_all_reduce(torch.zeros(12, device=gpu), torch.zeros(12, device=gpu), h)  # n % 8
+        x = torch.arange(1024, dtype=torch.float32, device=gpu)
+        out = torch.empty_like(x)
+        ops.xgmi_all_reduce(x, out, h)  # world 1: a copy
+        torch.cuda.synchronize()
+        assert torch.equal(out, x) and ops.xgmi_error(h) == 0
+    finally:
+        ops.xgmi_destroy(h)
