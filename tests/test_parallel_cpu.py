@@ -83,6 +83,19 @@ def _comm_worker(rank, world):
     b = torch.tensor([rank + 5])
     hs.broadcast(b, src=1)
     assert int(b) == 6
+    # all_reduce_add_prep (the row-parallel decode epilogue; fused on XgmiComm) == all_reduce + add_prep
+    from symmetry_amd.ops import reference
+
+    y = torch.randn(3, 64) + rank
+    resid = torch.randn(3, 64, generator=torch.Generator().manual_seed(5))
+    w = torch.rand(64, generator=torch.Generator().manual_seed(6)).to(torch.bfloat16)
+    xw, ss = torch.empty(3, 64, dtype=torch.bfloat16), torch.empty(3, 2)
+    ysum = y.clone()
+    c.all_reduce(ysum)
+    r_ref, xw_ref, ss_ref = resid.clone(), torch.empty_like(xw), torch.empty_like(ss)
+    reference.add_prep(ysum, r_ref, w, xw_ref, ss_ref)
+    c.all_reduce_add_prep(y, resid, w, xw, ss)
+    assert torch.equal(resid, r_ref) and torch.equal(xw, xw_ref) and torch.equal(ss, ss_ref)
     return t.tolist(), int(m), g.tolist(), r.tolist()
 
 
