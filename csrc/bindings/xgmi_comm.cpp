@@ -153,7 +153,7 @@ void xgmi_all_reduce(const Tensor& in, Tensor& out, int64_t h) {
   TORCH_CHECK(n * (long long)in.element_size() <= x->args.slot_bytes, "xgmi_all_reduce: message of ",
               n * in.element_size(), " B exceeds the ", x->args.slot_bytes, " B slot");
   const int chunk = xgmi_chunk(n, XG_MAX_WG);
-  TORCH_CHECK((n + chunk - 1) / chunk <= XG_MAX_WG, "xgmi_all_reduce: too many chunks");
+  TORCH_CHECK((n + chunk - 1) / chunk < XG_KEYS_WG, "xgmi_all_reduce: too many chunks");
   launch_xgmi_all_reduce(x->args, in.data_ptr(), out.data_ptr(), n, elem, stream_of(in));
 }
 
@@ -169,11 +169,23 @@ void xgmi_add_prep(const Tensor& y, Tensor& resid, const Tensor& w, Tensor& xw, 
   TORCH_CHECK(y.numel() == T * d && xw.numel() == T * d && w.numel() == d, "xgmi_add_prep: shape mismatch");
   const int64_t P = ss.dim() == 2 ? ss.size(1) : 1;
   TORCH_CHECK(ss.numel() >= T * P && P >= 1 && P <= 16 && d % (8 * P) == 0, "xgmi_add_prep: ss parts must divide d / 8");
-  TORCH_CHECK(T * P <= XG_MAX_WG, "xgmi_add_prep: too many rows");
+  TORCH_CHECK(T * P < XG_KEYS_WG, "xgmi_add_prep: too many rows");
   TORCH_CHECK(T * d * 4 <= x->args.slot_bytes, "xgmi_add_prep: message exceeds the slot");
   launch_xgmi_add_prep(x->args, y.data_ptr<float>(), resid.data_ptr<float>(),
                        reinterpret_cast<const bf16*>(w.data_ptr()), reinterpret_cast<bf16*>(xw.data_ptr()),
                        ss.data_ptr<float>(), (int)T, (int)d, (int)P, stream_of(y));
+}
+
+// vocab-parallel sampling combine: ids[i] = global argmax from every rank's packed u64 keys [B]
+void xgmi_keys_max(const Tensor& keys, Tensor& ids, int64_t h) {
+  Xgmi* x = get(h);
+  check_ready(x, keys);
+  check_ready(x, ids);
+  TORCH_CHECK(keys.scalar_type() == at::kLong && ids.scalar_type() == at::kInt, "xgmi_keys_max: keys int64, ids int32");
+  const int64_t B = keys.numel();
+  TORCH_CHECK(ids.numel() >= B && B <= 4096 && B * 8 <= x->args.slot_bytes, "xgmi_keys_max: shapes");
+  launch_xgmi_keys_max(x->args, reinterpret_cast<const unsigned long long*>(keys.data_ptr()), ids.data_ptr<int>(),
+                       (int)B, stream_of(keys));
 }
 
 // test-only: every rank of this process in one launch (grid slice per rank; see xgmi_ar.hip)
@@ -211,7 +223,7 @@ void xgmi_add_prep_multi(std::vector<Tensor> ys, std::vector<Tensor> resids, con
   const int64_t T = resids[0].size(0), d = resids[0].size(1);
   const int64_t P = sss[0].dim() == 2 ? sss[0].size(1) : 1;
   TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.numel() == d && w.is_contiguous(), "xgmi_add_prep_multi: w bf16 [d]");
-  TORCH_CHECK(P >= 1 && P <= 16 && d % (8 * P) == 0 && T * P <= XG_MAX_WG, "xgmi_add_prep_multi: bad parts");
+  TORCH_CHECK(P >= 1 && P <= 16 && d % (8 * P) == 0 && T * P < XG_KEYS_WG, "xgmi_add_prep_multi: bad parts");
   for (int r = 0; r < world; ++r) {
     Xgmi* x = get(comms[r]);
     TORCH_CHECK(x->args.rank == r && x->args.world == world, "xgmi_add_prep_multi: communicator ", r, " is not rank ", r);
@@ -277,6 +289,7 @@ TORCH_LIBRARY_FRAGMENT(symmetry_amd, m) {
       "xgmi_add_prep_multi(Tensor[] ys, Tensor(a!)[] resids, Tensor w, Tensor(b!)[] xws, Tensor(c!)[] sss, int[] comms) "
       "-> ()",
       &xgmi_add_prep_multi);
+  m.def("xgmi_keys_max(Tensor keys, Tensor(a!) ids, int comm) -> ()", &xgmi_keys_max);
   m.def("xgmi_error(int comm) -> int", &xgmi_error);
   m.def("xgmi_slot_bytes(int comm) -> int", &xgmi_slot_bytes);
   m.def("xgmi_destroy(int comm) -> ()", &xgmi_destroy);

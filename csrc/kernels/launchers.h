@@ -179,6 +179,7 @@ void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_l
 // xgmi_ar.hip: one-shot all-reduce over xGMI peer memory (IPC-mapped buffers of every TP rank)
 constexpr int XG_MAX_WORLD = 8;
 constexpr int XG_MAX_WG = 4096;
+constexpr int XG_KEYS_WG = XG_MAX_WG - 1;  // epoch / flag slot of the sampling-keys collective (others stay below)
 struct XgmiArgs {
   char* bufs[XG_MAX_WORLD];  // every rank's comm buffer as mapped in this process (own one included)
   unsigned* epochs;          // [XG_MAX_WG] local per-workgroup collective counters (zeroed once)
@@ -189,6 +190,7 @@ struct XgmiArgs {
 long long xgmi_buffer_bytes(int world, long long slot_bytes);
 int xgmi_chunk(long long n, long long max_wg);
 void launch_xgmi_all_reduce(const XgmiArgs& c, const void* in, void* out, long long n, int elem, hipStream_t s);
+void launch_xgmi_keys_max(const XgmiArgs& c, const unsigned long long* keys, int* ids, int B, hipStream_t s);
 void launch_xgmi_add_prep(const XgmiArgs& c, const float* y, float* resid, const bf16* w, bf16* xw, float* ss, int T,
                           int d, int parts, hipStream_t s);
 // test-only: the ranks of one process as grid slices of ONE launch (co-resident by construction).

@@ -37,7 +37,8 @@ SYM_DEV char* xg_slot(const XgmiArgs& c, int r, int par, int src) {
 // Push this workgroup's chunk (nvec 16-byte vectors at byte offset `off`) into slot (parity, rank) of
 // every rank's buffer (its own included, so the reduce reads all slots from one place), signal, wait for
 // every rank's signal of the same chunk.  Returns the epoch parity (the slot set to reduce).
-SYM_DEV int xg_exchange(const XgmiArgs& c, int wg, const uint4* __restrict__ src, long long off, int nvec) {
+template <typename V = uint4>
+SYM_DEV int xg_exchange(const XgmiArgs& c, int wg, const V* __restrict__ src, long long off, int nvec) {
   __shared__ unsigned s_epoch;
   if (threadIdx.x == 0) {
     const unsigned e = c.epochs[wg] + 1u;
@@ -48,8 +49,8 @@ SYM_DEV int xg_exchange(const XgmiArgs& c, int wg, const uint4* __restrict__ src
   const unsigned epoch = s_epoch;
   const int par = (int)(epoch & 1u);
   for (int v = threadIdx.x; v < nvec; v += XG_THREADS) {
-    const uint4 x = src[v];
-    for (int r = 0; r < c.world; ++r) reinterpret_cast<uint4*>(xg_slot(c, r, par, c.rank) + off)[v] = x;
+    const V x = src[v];
+    for (int r = 0; r < c.world; ++r) reinterpret_cast<V*>(xg_slot(c, r, par, c.rank) + off)[v] = x;
   }
   // Every wave waits for its slot stores to be acknowledged before the workgroup signals.  The buffers
   // are uncached (MTYPE UC): the stores never sit in an L2 and the slot loads below never hit one, so
@@ -83,8 +84,8 @@ SYM_DEV void xg_all_reduce_body(const XgmiArgs& c, int wg, const void* in, void*
   constexpr int ESZ = ELEM == 0 ? 4 : 2;
   const int nvec = cnt * ESZ / 16;
   const long long off = e0 * ESZ;
-  const int par = xg_exchange(c, wg, reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(in) + off), off,
-                              nvec);
+  const int par = xg_exchange<uint4>(c, wg, reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(in) + off),
+                                     off, nvec);
   for (int v = threadIdx.x; v < nvec; v += XG_THREADS) {
     if constexpr (ELEM == 0) {
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -120,7 +121,7 @@ SYM_DEV void xg_add_prep_body(const XgmiArgs& c, int row, int part, int P, const
   const int wg = row * P + part;
   const long long rb = (long long)row * d + (long long)part * dp;
   const long long off = rb * 4;
-  const int par = xg_exchange(c, wg, reinterpret_cast<const uint4*>(y + rb), off, dp / 4);
+  const int par = xg_exchange<uint4>(c, wg, reinterpret_cast<const uint4*>(y + rb), off, dp / 4);
   const bf16* wp = w + (long long)part * dp;
   float acc = 0.f;
   for (int vi = threadIdx.x; vi < dp / 8; vi += XG_THREADS) {
@@ -146,6 +147,23 @@ SYM_DEV void xg_add_prep_body(const XgmiArgs& c, int row, int part, int P, const
   }
   acc = block_sum<XG_THREADS>(acc, scratch);
   if (threadIdx.x == 0) ss[row * P + part] = acc;
+}
+
+// Vocab-parallel greedy / Gumbel sampling combine: every rank holds per-row packed u64 keys (order-
+// preserving value bits | inverted vocabulary index) of its vocabulary shard; the max over ranks is the
+// global argmax, and ids = 0xFFFFFFFF - low 32 bits.  One workgroup (rows <= 512), epoch slot
+// XG_KEYS_WG (the other collectives' grids stay below it).
+__global__ __launch_bounds__(XG_THREADS) void xgmi_keys_max_kernel(XgmiArgs c, const unsigned long long* keys,
+                                                                  int* __restrict__ ids, int B) {
+  const int par = xg_exchange<unsigned long long>(c, XG_KEYS_WG, keys, 0, B);
+  for (int i = threadIdx.x; i < B; i += XG_THREADS) {
+    unsigned long long best = 0;
+    for (int r = 0; r < c.world; ++r) {
+      const unsigned long long k = reinterpret_cast<const unsigned long long*>(xg_slot(c, c.rank, par, r))[i];
+      best = k > best ? k : best;
+    }
+    ids[i] = (int)(0xFFFFFFFFu - (unsigned)(best & 0xFFFFFFFFull));
+  }
 }
 
 template <int ELEM>
@@ -217,4 +235,9 @@ void launch_xgmi_all_reduce_multi(const XgmiMulti& m, int world, long long n, in
 void launch_xgmi_add_prep_multi(const XgmiMulti& m, int world, int T, int d, int parts, hipStream_t s) {
   if (T == 0) return;
   xgmi_add_prep_multi_kernel<<<dim3(T, parts, world), XG_THREADS, 0, s>>>(m, d);
+}
+
+void launch_xgmi_keys_max(const XgmiArgs& c, const unsigned long long* keys, int* ids, int B, hipStream_t s) {
+  if (B == 0) return;
+  xgmi_keys_max_kernel<<<1, XG_THREADS, 0, s>>>(c, keys, ids, B);
 }

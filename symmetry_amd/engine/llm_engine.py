@@ -175,15 +175,15 @@ class LLMEngine:
         return MAX_DECODE_ROWS if (not mcfg.is_moe and self.cfg.tp_size == 1) else FUSED_DECODE_ROWS
 
     def _graph_safe(self, tp_comm, ep_comm) -> bool:
-        """Decode hipGraphs need every collective to be capturable (our RCCL communicator) and no
-        host-side data-dependent shapes (all-to-all expert dispatch reads counts on the host)."""
+        """Decode hipGraphs need every collective to be capturable (our RCCL communicator, or the xGMI
+        kernels over it) and no host-side data-dependent shapes (all-to-all expert dispatch reads counts
+        on the host)."""
         from .. import ops
-        from ..parallel.comm import RcclComm
 
         if ops.torch_mode():  # eager torch baseline: host-synchronising reference ops
             return False
         for c in (tp_comm, ep_comm):
-            if c is not None and getattr(c, "world", 1) > 1 and not isinstance(c, RcclComm):
+            if c is not None and getattr(c, "world", 1) > 1 and not getattr(c, "capturable", False):
                 return False
         if self.model.moe is not None and self.model.moe.ep > 1 and self.model.moe.mode != "allreduce":
             return False

@@ -61,7 +61,6 @@ SPLITK_RESID_ROWS = int(os.environ.get("SYMMETRY_SPLITK_RESID_ROWS", "24"))
 # Decode batches are padded to buckets (.., 16, 24, ..), so 17..24-row steps run as 24.  0 disables.
 GENERAL_ROWS = int(os.environ.get("SYMMETRY_GENERAL_ROWS", "24"))
 MAX_STEP_SEQS = 4096  # sequences per step (rows of last_ids)
-SIGN64 = -(1 << 63)
 
 
 @dataclass
@@ -463,10 +462,6 @@ class TransformerLM:
 
     def _combine_tp(self, ids, keys, logits) -> torch.Tensor:
         if self._tp_active():
-            # keys are u64 (order-preserving); flip the sign bit so signed MAX == unsigned max
-            keys.bitwise_xor_(SIGN64)
-            self.tp.all_reduce(keys, op="max")
-            keys.bitwise_xor_(SIGN64)
-            ids.copy_((0xFFFFFFFF - (keys & 0xFFFFFFFF)).to(torch.int32))
+            self.tp.argmax_keys(keys, ids)  # global argmax over the vocabulary shards (one kernel on xGMI)
         self.last_logits = logits
         return ids

@@ -32,6 +32,7 @@ import torch.distributed as dist
 class Comm:
     rank: int = 0
     world: int = 1
+    capturable: bool = False  # every collective enqueues on the current HIP stream (hipGraph capture)
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> None:
         raise NotImplementedError
@@ -44,6 +45,15 @@ class Comm:
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
         raise NotImplementedError
+
+    def argmax_keys(self, keys: torch.Tensor, ids: torch.Tensor) -> None:
+        """Vocab-parallel sampling combine: keys int64 [B] hold each rank's packed u64 (order-preserving
+        value | inverted index) maxima; ids[:B] = the index of the global max.  Fused on XgmiComm."""
+        sign = -(1 << 63)
+        keys.bitwise_xor_(sign)  # signed MAX == unsigned max once the sign bit is flipped
+        self.all_reduce(keys, op="max")
+        keys.bitwise_xor_(sign)
+        ids[: keys.numel()].copy_((0xFFFFFFFF - (keys & 0xFFFFFFFF)).to(torch.int32))
 
     def all_reduce_add_prep(self, y, resid, w_next, xw, ss) -> None:
         """resid += all_reduce(y); xw = bf16(resid * w_next); ss = row sums of resid^2 (decode epilogue
@@ -108,6 +118,8 @@ class HostStagedComm(Comm):
 class RcclComm(Comm):
     """Graph-capturable RCCL communicator over the ranks of ``group`` (bootstrapped through it)."""
 
+    capturable = True
+
     def __init__(self, group=None, bootstrap_group=None):
         from ..ops import _native
 
@@ -160,6 +172,7 @@ class XgmiComm(Comm):
         self.ops = _native.ops()
         self.inner = inner
         self.rank, self.world = inner.rank, inner.world
+        self.capturable = inner.capturable  # the xGMI kernels are; the fallbacks are the inner ones
         dev = torch.device(device)
         self.handle = int(self.ops.xgmi_create(int(slot_bytes), self.world, self.rank, dev.index or 0))
         self.slot_bytes = int(slot_bytes)
@@ -187,6 +200,13 @@ class XgmiComm(Comm):
             self.calls["add_prep"] += 1
         else:
             super().all_reduce_add_prep(y, resid, w_next, xw, ss)
+
+    def argmax_keys(self, keys, ids):
+        if keys.is_cuda and keys.is_contiguous() and keys.numel() <= 4096:
+            self.ops.xgmi_keys_max(keys, ids, self.handle)
+            self.calls["keys"] = self.calls.get("keys", 0) + 1
+        else:
+            super().argmax_keys(keys, ids)
 
     def all_gather(self, t):
         return self.inner.all_gather(t)

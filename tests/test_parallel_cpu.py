@@ -96,6 +96,14 @@ def _comm_worker(rank, world):
     reference.add_prep(ysum, r_ref, w, xw_ref, ss_ref)
     c.all_reduce_add_prep(y, resid, w, xw, ss)
     assert torch.equal(resid, r_ref) and torch.equal(xw, xw_ref) and torch.equal(ss, ss_ref)
+    # vocab-parallel argmax combine of packed u64 keys (value bits high, inverted index low); values with
+    # the top bit set exercise the unsigned order
+    vals = [[0x80000001, 5], [0x7FFFFFFF, 9]][rank]
+    idx = [[3, 100], [1000, 2]][rank]
+    keys = torch.tensor([(v << 32) | (0xFFFFFFFF - i) for v, i in zip(vals, idx)], dtype=torch.uint64).view(torch.int64)
+    ids = torch.zeros(2, dtype=torch.int32)
+    c.argmax_keys(keys, ids)
+    assert ids.tolist() == [3, 2], ids
     return t.tolist(), int(m), g.tolist(), r.tolist()
 
 
@@ -214,3 +222,20 @@ def test_tp_graph_capture_is_mirrored_on_every_rank():
     the same order, driven by rank 0's capture commands on the metadata plane."""
     (_, a), (_, b) = _run(_capture_worker)
     assert a == b and len(a) == len(set(a)) > 4
+
+
+def test_graph_safety_follows_comm_capturability():
+    """Decode hipGraphs stay on for TP when the communicator is capturable -- including the xGMI
+    communicator wrapping RCCL (regression: a type check for RcclComm turned graphs off under it)."""
+    from types import SimpleNamespace
+
+    from symmetry_amd.engine.llm_engine import LLMEngine
+    from symmetry_amd.parallel.comm import HostStagedComm, RcclComm, TorchComm, XgmiComm
+
+    assert RcclComm.capturable and not TorchComm.capturable and not HostStagedComm.capturable
+    fake = SimpleNamespace(model=SimpleNamespace(moe=None))
+    xg = XgmiComm.__new__(XgmiComm)  # no GPU here: only the attribute XgmiComm.__init__ copies
+    xg.world, xg.capturable = 8, RcclComm.capturable
+    assert LLMEngine._graph_safe(fake, xg, None)
+    assert not LLMEngine._graph_safe(fake, SimpleNamespace(world=2, capturable=False), None)
+    assert LLMEngine._graph_safe(fake, SimpleNamespace(world=1), None)

@@ -55,6 +55,7 @@ def _entry(model, rank, world, port, q, xgmi="0"):
         if xgmi == "1":
             calls = eng.runner.model.tp.calls
             assert calls["add_prep"] > 0, calls  # decode steps ran the fused peer-memory all-reduce
+            assert calls.get("keys", 0) > 0, calls  # and the vocab-parallel sampling combine
             assert eng.runner.model.tp.error() == 0
         eng.shutdown()
         q.put((rank, [s.output_ids for s in seqs]))

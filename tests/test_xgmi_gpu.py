@@ -132,5 +132,10 @@ def test_xgmi_rejects_oversized_and_bad_shapes(gpu):
         ops.xgmi_all_reduce(x, out, h)  # world 1: a copy
         torch.cuda.synchronize()
         assert torch.equal(out, x) and ops.xgmi_error(h) == 0
+        keys = (torch.arange(5, dtype=torch.int64, device=gpu) << 32) | (0xFFFFFFFF - torch.arange(5, device=gpu) * 7)
+        ids = torch.zeros(5, dtype=torch.int32, device=gpu)
+        ops.xgmi_keys_max(keys, ids, h)  # world 1: unpack the own keys
+        torch.cuda.synchronize()
+        assert ids.tolist() == [0, 7, 14, 21, 28] and ops.xgmi_error(h) == 0
     finally:
         ops.xgmi_destroy(h)
