@@ -29,6 +29,7 @@ using at::Tensor;
 
 struct Xgmi {
   XgmiArgs args{};
+  volatile int* err_host = nullptr;  // host-mapped error word: polled after every step without a sync
   char* own = nullptr;
   std::vector<char*> opened;  // IPC mappings to close
   int device = 0;
@@ -73,11 +74,17 @@ int64_t xgmi_create(int64_t slot_bytes, int64_t world, int64_t rank, int64_t dev
   HIP_OK(hipMemset(p, 0, (size_t)x->bytes));
   x->own = (char*)p;
   void* e = nullptr;
-  HIP_OK(hipMalloc(&e, XG_MAX_WG * sizeof(unsigned) + 64));
-  HIP_OK(hipMemset(e, 0, XG_MAX_WG * sizeof(unsigned) + 64));
+  HIP_OK(hipMalloc(&e, XG_MAX_WG * sizeof(unsigned)));
+  HIP_OK(hipMemset(e, 0, XG_MAX_WG * sizeof(unsigned)));
+  void* eh = nullptr;
+  HIP_OK(hipHostMalloc(&eh, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(eh, 0, 64);
+  void* ed = nullptr;
+  HIP_OK(hipHostGetDevicePointer(&ed, eh, 0));
   HIP_OK(hipDeviceSynchronize());
   x->args.epochs = (unsigned*)e;
-  x->args.err = (int*)((char*)e + XG_MAX_WG * sizeof(unsigned));
+  x->err_host = (volatile int*)eh;
+  x->args.err = (int*)ed;
   x->args.rank = (int)rank;
   x->args.world = (int)world;
   x->args.slot_bytes = slot_bytes;
@@ -245,11 +252,11 @@ void xgmi_add_prep_multi(std::vector<Tensor> ys, std::vector<Tensor> resids, con
 }
 
 // reads (and clears) the error word: 1 + the source rank that never signalled within the wait limit
+// (host-mapped memory: no device synchronisation; a kernel still running may set it later)
 int64_t xgmi_error(int64_t h) {
   Xgmi* x = get(h);
-  int v = 0;
-  HIP_OK(hipMemcpy(&v, x->args.err, sizeof(int), hipMemcpyDeviceToHost));
-  if (v) HIP_OK(hipMemset(x->args.err, 0, sizeof(int)));
+  const int v = *x->err_host;
+  if (v) *x->err_host = 0;
   return v;
 }
 
@@ -267,6 +274,7 @@ void xgmi_destroy(int64_t h) {
   (void)hipDeviceSynchronize();
   for (char* p : x->opened) (void)hipIpcCloseMemHandle(p);
   (void)hipFree(x->args.epochs);
+  (void)hipHostFree((void*)x->err_host);
   {
     std::lock_guard<std::mutex> g(g_mu);
     g_uc_pool.emplace_back(x->bytes, x->own);

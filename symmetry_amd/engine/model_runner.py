@@ -299,6 +299,10 @@ class ModelRunner:
         if "event" in handle:
             handle["event"].synchronize()
             ids = handle["pin"].tolist()
+            check = getattr(self.model.tp, "error", None)  # xGMI collectives: host-mapped word, no sync
+            if check is not None and check():
+                raise RuntimeError("xGMI all-reduce: a peer rank never signalled within the wait limit; "
+                                   "this step's outputs are invalid")
         else:
             ids = handle["ids"]
         self.timing["forward"] += time.perf_counter() - handle["t0"]

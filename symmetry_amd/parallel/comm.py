@@ -218,7 +218,8 @@ class XgmiComm(Comm):
         self.inner.broadcast(t, src)
 
     def error(self) -> int:
-        """1 if a collective gave up waiting for a peer since the last call (cleared on read)."""
+        """1 + the source rank a collective gave up waiting for since the last call, else 0 (cleared on read;
+        host-mapped, so it costs no device synchronisation: the model runner polls it after every step)."""
         return int(self.ops.xgmi_error(self.handle))
 
     def destroy(self):
