@@ -5,7 +5,7 @@ buffers mapped to each other: the protocol (push into every rank's slot, per-(wo
 rank-order reduce) is the multi-GPU one, with local HBM in place of the xGMI links, so this is a lower
 bound on the per-collective cost (launch + push + signal + reduce), not an xGMI measurement.
 Message sizes are the TP decode all-reduces of Llama-3-70B (fp32 [rows, 8192]).
-Prints one JSON line per (world, rows, op)."""
+Prints one JSON line per (world, rows, op); add_prep_P<n>: n column parts per row (workgroups per row)."""
 import json
 import sys
 
@@ -27,10 +27,12 @@ for world in (2, 4):
         ys = [torch.randn(rows, d, device=dev) for _ in range(world)]
         resid = [torch.randn(rows, d, device=dev) for _ in range(world)]
         xw = [torch.empty(rows, d, device=dev, dtype=torch.bfloat16) for _ in range(world)]
-        ss = [torch.empty(rows, 8, device=dev) for _ in range(world)]
+        sss = {P: [torch.empty(rows, P, device=dev) for _ in range(world)] for P in (1, 2, 4, 8, 16)}
         w = torch.ones(d, device=dev, dtype=torch.bfloat16)
-        for name, fn in (("all_reduce", lambda: ops.xgmi_all_reduce_multi(ys, ys, hs)),
-                         ("add_prep", lambda: ops.xgmi_add_prep_multi(ys, resid, w, xw, ss, hs))):
+        arms = [("all_reduce", lambda: ops.xgmi_all_reduce_multi(ys, ys, hs))]
+        arms += [(f"add_prep_P{P}", (lambda P=P: ops.xgmi_add_prep_multi(ys, resid, w, xw, sss[P], hs)))
+                 for P in (1, 2, 4, 8, 16) if world * rows * P <= 1024]  # slices must be co-resident
+        for name, fn in arms:
             for _ in range(10):
                 fn()
             g = torch.cuda.CUDAGraph()

@@ -217,6 +217,10 @@ void xgmi_all_reduce_multi(std::vector<Tensor> ins, std::vector<Tensor> outs, st
   }
   elem = ins[0].scalar_type() == at::kFloat ? 0 : ins[0].scalar_type() == at::kBFloat16 ? 1 : -1;
   TORCH_CHECK(elem >= 0 && n % 8 == 0, "xgmi_all_reduce_multi: fp32 / bf16, element count % 8");
+  // the slices wait on each other: they must all be resident at once (256 CUs x a few 256-thread groups)
+  const int chunk = xgmi_chunk(n, XG_MAX_WG);
+  TORCH_CHECK(world * ((n + chunk - 1) / chunk) <= XG_MULTI_MAX_GROUPS, "xgmi_all_reduce_multi: ",
+              world * ((n + chunk - 1) / chunk), " workgroups would not be co-resident");
   launch_xgmi_all_reduce_multi(m, world, n, elem, stream_of(ins[0]));
 }
 
@@ -231,6 +235,8 @@ void xgmi_add_prep_multi(std::vector<Tensor> ys, std::vector<Tensor> resids, con
   const int64_t P = sss[0].dim() == 2 ? sss[0].size(1) : 1;
   TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.numel() == d && w.is_contiguous(), "xgmi_add_prep_multi: w bf16 [d]");
   TORCH_CHECK(P >= 1 && P <= 16 && d % (8 * P) == 0 && T * P < XG_KEYS_WG, "xgmi_add_prep_multi: bad parts");
+  TORCH_CHECK(world * T * P <= XG_MULTI_MAX_GROUPS, "xgmi_add_prep_multi: ", world * T * P,
+              " workgroups would not be co-resident");
   for (int r = 0; r < world; ++r) {
     Xgmi* x = get(comms[r]);
     TORCH_CHECK(x->args.rank == r && x->args.world == world, "xgmi_add_prep_multi: communicator ", r, " is not rank ", r);

@@ -196,6 +196,7 @@ void launch_xgmi_add_prep(const XgmiArgs& c, const float* y, float* resid, const
 // test-only: the ranks of one process as grid slices of ONE launch (co-resident by construction).
 // add_prep: in = y, out = resid, xw, ss per rank; w shared
 constexpr int XG_MULTI_MAX = 4;
+constexpr int XG_MULTI_MAX_GROUPS = 1024;  // all slices co-resident (they wait on each other)
 struct XgmiMulti {
   XgmiArgs c[XG_MULTI_MAX];
   const void* in[XG_MULTI_MAX];

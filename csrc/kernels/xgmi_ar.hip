@@ -200,9 +200,11 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_add_prep_multi_kernel(XgmiMul
 long long xgmi_buffer_bytes(int world, long long slot_bytes) { return XG_FLAG_BYTES + 2LL * world * slot_bytes; }
 
 int xgmi_chunk(long long n, long long max_wg) {
-  // >= 2048 elements per workgroup (latency-bound messages: fewer, fatter signals), multiple of 8
+  // >= 1024 elements (4 KB of fp32) per workgroup, multiple of 8: the fused add_prep's sweep of
+  // workgroups per row (profiles/xgmi_allreduce_local_r2.jsonl, 1-10 rows of 8192) was fastest with
+  // 512-1024-element parts (4 ranks: 2048-element parts 5.8-6.4 us, 1024 5.0-5.3)
   long long chunk = (n + max_wg - 1) / max_wg;
-  chunk = std::max<long long>(chunk, 2048);
+  chunk = std::max<long long>(chunk, 1024);
   return (int)((chunk + 7) / 8 * 8);
 }
 
