@@ -52,10 +52,11 @@ SYM_DEV int xg_exchange(const XgmiArgs& c, int wg, const V* __restrict__ src, lo
     const V x = src[v];
     for (int r = 0; r < c.world; ++r) reinterpret_cast<V*>(xg_slot(c, r, par, c.rank) + off)[v] = x;
   }
-  // Every wave waits for its slot stores to be acknowledged before the workgroup signals.  The buffers
-  // are uncached (MTYPE UC): the stores never sit in an L2 and the slot loads below never hit one, so
-  // no cache write-back / invalidate is needed on either side -- and none is issued: a system-scope
-  // fence also writes back and invalidates the XCD's L2 for every other workgroup's plain traffic.
+  // Every wave waits for its slot stores to be acknowledged before the workgroup signals: the AMDGPU
+  // memory model's system-scope release is `buffer_wbl2 sc0 sc1; s_waitcnt vmcnt(0)`, and the L2
+  // write-back half has nothing to do here -- the buffers are uncached (MTYPE UC), so the stores never
+  // sit in an L2 and the slot loads below never hit one (no acquire invalidate either).  A full
+  // __threadfence_system() per collective costs an L2 write-back + invalidate of the whole XCD.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < c.world) {
