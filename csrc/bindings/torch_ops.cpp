@@ -156,7 +156,8 @@ void check_cache(const Tensor& k_cache, const Tensor& v_cache) {
 }
 
 void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
-                 const Tensor& ctx_lens, Tensor& out, Tensor& tmp_o, Tensor& tmp_ml, Tensor& counters, double scale) {
+                 const Tensor& ctx_lens, Tensor& out, Tensor& tmp_o, Tensor& tmp_ml, Tensor& counters, double scale,
+                 const c10::optional<Tensor>& prefetch, int64_t prefetch_wgs) {
   check_gpu(q, "q");
   check_dtype(q, at::kBFloat16, "q");
   check_cache(k_cache, v_cache);
@@ -183,10 +184,19 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, 
   check_gpu(counters, "counters");
   check_dtype(counters, at::kInt, "counters");
   TORCH_CHECK(counters.numel() >= S * Hkv, "counters must hold num_seqs * Hkv zero-initialised ints");
+  const void* pf = nullptr;
+  long long pf_bytes = 0;
+  if (prefetch.has_value() && prefetch_wgs > 0) {  // Infinity-Cache prefetch of the next launch's weight
+    check_gpu(*prefetch, "prefetch");
+    TORCH_CHECK(prefetch->get_device() == q.get_device(), "prefetch must live on q's GPU");
+    pf = prefetch->data_ptr();
+    pf_bytes = prefetch->numel() * prefetch->element_size() / 16 * 16;  // whole 16-byte vectors only
+  }
   const at::OptionalDeviceGuard g(q.device());
   launch_attn_decode(ptr<bf16>(q), ptr<bf16>(k_cache), ptr<bf16>(v_cache), ptr<int>(block_tables), ptr<int>(ctx_lens),
                      ptr<bf16>(out), ptr<float>(tmp_o), ptr<float>(tmp_ml), ptr<int>(counters), (int)S, (int)Hq,
-                     (int)Hkv, (int)BS, (int)max_blocks, (int)max_parts, (float)scale, cur_stream(q));
+                     (int)Hkv, (int)BS, (int)max_blocks, (int)max_parts, (float)scale, cur_stream(q), pf, pf_bytes,
+                     (int)prefetch_wgs);
 }
 
 void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
@@ -799,7 +809,8 @@ TORCH_LIBRARY(symmetry_amd, m) {
       &rope_cache);
   m.def(
       "attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, Tensor(a!) out, "
-      "Tensor(b!) tmp_o, Tensor(c!) tmp_ml, Tensor(d!) counters, float scale) -> ()",
+      "Tensor(b!) tmp_o, Tensor(c!) tmp_ml, Tensor(d!) counters, float scale, Tensor? prefetch=None, "
+      "int prefetch_wgs=0) -> ()",
       &attn_decode);
   m.def(
       "attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, Tensor cu_q, "

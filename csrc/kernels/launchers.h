@@ -135,7 +135,8 @@ void launch_rope_cache(LinOut qkv, const int* positions, const int* slots, const
 // attention.hip
 void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,
                         const int* ctx_lens, bf16* out, float* tmp_o, float* tmp_ml, int* counters, int num_seqs,
-                        int Hq, int Hkv, int BS, int max_blocks, int max_parts, float scale, hipStream_t s);
+                        int Hq, int Hkv, int BS, int max_blocks, int max_parts, float scale, hipStream_t s,
+                        const void* prefetch = nullptr, long long prefetch_bytes = 0, int prefetch_wgs = 0);
 // decode attention switches to the streaming long-context kernel from this block-table span (0: never)
 void set_attn_stream_min(int tokens);
 // wide batches: one wave per (seq, kv head) from min_units units for spans of >= min_span tokens

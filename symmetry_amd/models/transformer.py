@@ -61,6 +61,9 @@ SPLITK_RESID_ROWS = int(os.environ.get("SYMMETRY_SPLITK_RESID_ROWS", "24"))
 # Decode batches are padded to buckets (.., 16, 24, ..), so 17..24-row steps run as 24.  0 disables.
 GENERAL_ROWS = int(os.environ.get("SYMMETRY_GENERAL_ROWS", "24"))
 MAX_STEP_SEQS = 4096  # sequences per step (rows of last_ids)
+# extra workgroups of the decode attention launch that stream the O weight into the Infinity Cache
+# (0 = off; csrc/kernels/attention.hip, mall_prefetch)
+ATTN_PREFETCH_WGS = int(os.environ.get("SYMMETRY_ATTN_PREFETCH", "0"))
 
 
 @dataclass
@@ -266,14 +269,16 @@ class TransformerLM:
         return y
 
     # ------------------------------------------------------------------------------------------
-    def _attention(self, b: ForwardBatch, kv: KVCache, i: int, q: torch.Tensor, attn: torch.Tensor) -> None:
+    def _attention(self, b: ForwardBatch, kv: KVCache, i: int, q: torch.Tensor, attn: torch.Tensor,
+                   prefetch: torch.Tensor | None = None) -> None:
         if b.kind == "decode":
             span = b.block_tables.shape[1] * kv.block_size
             max_parts = (span + ops.ATTN_DECODE_PART - 1) // ops.ATTN_DECODE_PART
             tmp_o = self._buf("tmp_o", (b.num_seqs, self.hq, max_parts, self.D), torch.float32)
             tmp_ml = self._buf("tmp_ml", (b.num_seqs, self.hq, max_parts, 2), torch.float32)
             cnt = self.ws.get("attn_counters", (b.num_seqs * self.hkv,), torch.int32, self.device, zeros=True)
-            ops.attn_decode(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, attn, tmp_o, tmp_ml, cnt, self.scale)
+            ops.attn_decode(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, attn, tmp_o, tmp_ml, cnt, self.scale,
+                            prefetch, ATTN_PREFETCH_WGS if prefetch is not None else 0)
         else:
             ops.attn_prefill(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, b.cu_q, b.tiles, attn, self.scale)
 
@@ -356,7 +361,9 @@ class TransformerLM:
             else:
                 ops.dg_qkv(xw, wq, ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq,
                            self.hkv, wshuf=shq)
-                self._attention(b, kv, i, q, attn)
+                # spare workgroups of the latency-bound attention launch pull the O weight into the
+                # Infinity Cache for the next launch
+                self._attention(b, kv, i, q, attn, self._dgw(i, "wo")[0] if ATTN_PREFETCH_WGS > 0 else None)
             if persistent and not block:
                 # O -> gate_up/SwiGLU -> down in one persistent launch: each phase's weight stream starts
                 # while the previous phase finishes (csrc/kernels/decode_gemm.hip, decode_mlp_kernel)

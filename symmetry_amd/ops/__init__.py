@@ -93,12 +93,14 @@ def rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv,
 ATTN_DECODE_PART = 256  # context tokens per split-KV partition of attn_decode (csrc/kernels/attn_decode.h PART)
 
 
-def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters, scale):
+def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters, scale,
+                prefetch=None, prefetch_wgs=0):
     """Split-KV paged decode attention.  ``counters``: int32 [>= num_seqs * Hkv], zero-initialised once;
-    the kernel re-arms it (graph-replay safe)."""
+    the kernel re-arms it (graph-replay safe).  ``prefetch``: a tensor (the next launch's weight) that
+    ~``prefetch_wgs`` extra workgroups of the launch stream into the Infinity Cache (GPU only)."""
     if _gpu(q):
         return _native.ops().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters,
-                                         float(scale))
+                                         float(scale), prefetch, int(prefetch_wgs))
     return reference.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, scale)
 
 
