@@ -156,6 +156,7 @@ def main() -> int:
         dist.all_gather(allt, tf)
         ttfts = sorted(torch.cat(allt).tolist())
     p50_ttft = ttfts[len(ttfts) // 2] * 1e3
+    mean_ttft, max_ttft = sum(ttfts) / len(ttfts) * 1e3, ttfts[-1] * 1e3
     ms_step = elapsed / K * 1e3
     total_tps = world * C * K / elapsed
     per_client = 1e3 / ms_step
@@ -181,6 +182,8 @@ def main() -> int:
                                "native gfx950 HIP" if torch.cuda.is_available() else "torch reference (CPU)")},
             "per_client_tokens_per_s": round(per_client, 2),
             "p50_ttft_ms": round(p50_ttft, 2),
+            "mean_ttft_ms": round(mean_ttft, 2),
+            "max_ttft_ms": round(max_ttft, 2),
             "load_s": round(t_load, 1),
             "warmup_s": round(t_cap, 1),
             "sse_events_rank0": events,

@@ -59,6 +59,9 @@ class EngineConfig:
     persistent_mlp: bool = False         # O -> gate_up -> down as one persistent launch (measured slower: profiles/)
     fused_attn_block: bool = False       # QKV -> attention -> O as one launch per layer (decode_block)
     enable_prefix_caching: bool = True   # adopt cached KV blocks of a known prompt prefix (multi-turn chats)
+    # a burst of >= 4 prompts totalling >= this many tokens, arriving while nothing decodes, prefills its
+    # first n // 2 + 1 prompts in one step and the rest in the next (0 = one step for the whole burst)
+    burst_split_tokens: int = int(os.environ.get("SYMMETRY_BURST_SPLIT", "1024"))
     model_config: ModelConfig | None = None
 
     @classmethod
@@ -75,7 +78,7 @@ class EngineConfig:
              "useGraphs": "use_graphs", "numKvBlocks": "num_kv_blocks", "decodeWeights": "decode_weights",
              "prefillChunk": "mixed_prefill_tokens",
              "persistentMlp": "persistent_mlp", "fusedAttnBlock": "fused_attn_block",
-             "enablePrefixCaching": "enable_prefix_caching"}
+             "enablePrefixCaching": "enable_prefix_caching", "burstSplitTokens": "burst_split_tokens"}
         for k, attr in m.items():
             if cfg.get(k) is not None:
                 cur, val = getattr(ec, attr), cfg[k]
@@ -137,7 +140,8 @@ class LLMEngine:
         self.scheduler = Scheduler(
             SchedulerConfig(max_num_seqs=min(cfg.max_num_seqs, self._max_decode_rows(mcfg)),
                             max_num_batched_tokens=cfg.max_num_batched_tokens, max_model_len=max_model_len,
-                            mixed_prefill_tokens=cfg.mixed_prefill_tokens),
+                            mixed_prefill_tokens=cfg.mixed_prefill_tokens,
+                            burst_split_tokens=cfg.burst_split_tokens),
             self.blocks)
         self.runner = ModelRunner(self.model, self.kv, self.scheduler.cfg.max_num_seqs, max_model_len,
                                   use_graphs=cfg.use_graphs and self._graph_safe(tp_comm, ep_comm),

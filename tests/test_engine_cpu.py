@@ -141,6 +141,29 @@ def test_scheduler_admission_limit():
     assert b.kind == "prefill" and len(b.seqs) == 2 and len(sch.waiting) == 2
 
 
+@pytest.mark.parametrize("n,plen,split,expect", [
+    (10, 128, 1024, 6),   # burst of 1280 tokens: the first n // 2 + 1 prompts, then the rest
+    (10, 128, 0, 10),     # split disabled: one step
+    (3, 512, 1024, 3),    # fewer than 4 prompts: one step
+    (6, 64, 1024, 6),     # 384 tokens: too small for the extra step overhead
+    (20, 512, 1024, 16),  # 10240 tokens > the 8192 budget: already split by the budget
+])
+def test_scheduler_burst_split(n, plen, split, expect):
+    bm = BlockManager(1024, 64)
+    sch = Scheduler(SchedulerConfig(max_num_seqs=64, max_num_batched_tokens=8192, max_model_len=2048,
+                                    burst_split_tokens=split), bm)
+    for i in range(n):
+        sch.add(Sequence(f"r{i}", list(range(plen)), SamplingParams(max_tokens=4)))
+    b = sch.schedule()
+    assert b.kind == "prefill" and len(b.seqs) == expect and all(c == plen for c in b.num_new_tokens)
+    if expect < n and split:
+        for seq in b.seqs:  # the first group's samples arrive: it decodes while the rest prefill
+            seq.num_computed = plen
+            seq.append(1, 0.0)
+        b2 = sch.schedule()
+        assert sum(1 for s in b2.seqs if s.in_prefill or s.num_computed < plen) > 0  # the rest is scheduled
+
+
 def test_detokenizer_handles_split_utf8():
     tok = ByteTokenizer(TINY_LLAMA)
     d = IncrementalDetokenizer(tok)
