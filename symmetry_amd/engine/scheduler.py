@@ -181,6 +181,7 @@ class Scheduler:
         self.blocks = blocks
         self.waiting: collections.deque[Sequence] = collections.deque()
         self.running: list[Sequence] = []
+        self._burst_rest = 0  # prompt tokens of a split burst left for the next step
 
     # ------------------------------------------------------------------------------------------
     def add(self, seq: Sequence) -> None:
@@ -229,7 +230,11 @@ class Scheduler:
             return self._schedule_prefill(self._burst_budget())
         d = self._schedule_decode()
         nd = len(d.seqs) if d is not None else 0
-        p = self._schedule_prefill(max(self.cfg.mixed_prefill_tokens - nd, 1))
+        budget = max(self.cfg.mixed_prefill_tokens - nd, 1)
+        if self._burst_rest:  # the rest of a split burst goes in ONE step, not in mixed-step chunks
+            budget = max(budget, min(self._burst_rest, self.cfg.max_num_batched_tokens - nd))
+            self._burst_rest = 0
+        p = self._schedule_prefill(budget)
         if d is None or not d.seqs:
             return p if p is not None else d
         if p is None:
@@ -243,7 +248,7 @@ class Scheduler:
         n prompts arriving together while nothing decodes would all get their first token after ONE
         prefill step of every prompt.  A step costs roughly a + b * tokens (Llama-3-8B, one MI355X:
         a ~3.5 ms, b ~13 us per token, profiles/prefill_len_sweep_r2.jsonl), so prefilling the first
-        n // 2 + 1 prompts first and the rest in the next (mixed) step moves the median request's first
+        n // 2 + 1 prompts first and the rest in the next (mixed, whole-remainder) step moves the median request's first
         token to the smaller step and lowers the mean as well: 10 x 128 tokens, p50 TTFT 21.3 -> 14.7 ms
         (profiles/ttft_burst_split_r2.jsonl); the last requests pay one step overhead more.  Only for
         bursts that would otherwise fit one step and are large enough for the overhead to be small."""
@@ -257,7 +262,9 @@ class Scheduler:
         total = sum(lens)
         if total < min_tokens or total > self.cfg.max_num_batched_tokens:
             return None
-        return sum(lens[: len(fresh) // 2 + 1])
+        first = sum(lens[: len(fresh) // 2 + 1])
+        self._burst_rest = total - first
+        return first
 
     def _schedule_prefill(self, budget: int | None = None) -> ScheduledBatch | None:
         budget = self.cfg.max_num_batched_tokens if budget is None else budget
