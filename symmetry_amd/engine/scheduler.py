@@ -252,6 +252,7 @@ class Scheduler:
         token to the smaller step and lowers the mean as well: 10 x 128 tokens, p50 TTFT 21.3 -> 14.7 ms
         (profiles/ttft_burst_split_r2.jsonl); the last requests pay one step overhead more.  Only for
         bursts that would otherwise fit one step and are large enough for the overhead to be small."""
+        self._burst_rest = 0
         min_tokens = self.cfg.burst_split_tokens
         if min_tokens <= 0 or any(s.in_prefill for s in self.running):
             return None
