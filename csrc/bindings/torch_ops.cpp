@@ -113,7 +113,7 @@ void embed_rms_norm(const Tensor& ids, const Tensor& table, Tensor& residual, co
 }
 
 void rope_cache(const Tensor& qkv, const Tensor& positions, const Tensor& slots, const Tensor& cos_sin,
-                Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t Hq, int64_t Hkv, bool perm) {
+                Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t Hq, int64_t Hkv, bool perm, bool decode) {
   check_gpu(positions, "positions");
   check_gpu(slots, "slots");
   check_gpu(cos_sin, "cos_sin");
@@ -140,7 +140,7 @@ void rope_cache(const Tensor& qkv, const Tensor& positions, const Tensor& slots,
   const at::OptionalDeviceGuard g(positions.device());
   launch_rope_cache(linout(qkv, T, (Hq + 2 * Hkv) * D, "qkv"), ptr<int>(positions), ptr<int>(slots),
                     ptr<float>(cos_sin), ptr<bf16>(q_out), ptr<bf16>(k_cache), ptr<bf16>(v_cache), (int)T, (int)Hq,
-                    (int)Hkv, (int)D, (int)BS, cur_stream(positions), perm ? 1 : 0);
+                    (int)Hkv, (int)D, (int)BS, cur_stream(positions), perm ? 1 : 0, decode ? 1 : 0);
 }
 
 void check_cache(const Tensor& k_cache, const Tensor& v_cache) {
@@ -805,7 +805,7 @@ TORCH_LIBRARY(symmetry_amd, m) {
         &embed_rms_norm);
   m.def(
       "rope_cache(Tensor qkv, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(a!) q_out, Tensor(b!) k_cache, "
-      "Tensor(c!) v_cache, int Hq, int Hkv, bool perm=False) -> ()",
+      "Tensor(c!) v_cache, int Hq, int Hkv, bool perm=False, bool decode=False) -> ()",
       &rope_cache);
   m.def(
       "attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, Tensor(a!) out, "

@@ -130,7 +130,7 @@ void launch_embed_rms_norm(const int* ids, const bf16* table, float* residual, c
 // rope_cache.hip
 void launch_rope_cache(LinOut qkv, const int* positions, const int* slots, const float* cos_sin, bf16* q_out,
                        bf16* k_cache, bf16* v_cache, int T, int Hq, int Hkv, int D, int BS, hipStream_t s,
-                       int perm = 0);
+                       int perm = 0, int decode = 0);
 
 // attention.hip
 void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,

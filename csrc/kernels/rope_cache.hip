@@ -33,7 +33,8 @@ __global__ __launch_bounds__(NT) void rope_cache_kernel(LinOut qkv, const int* _
   const float* cs = cos_sin + (long long)pos * D;
   const int rot_items = (Hq + Hkv) * gpr;
   const int v_items = Hkv * (D / 8);
-  for (int it = threadIdx.x; it < rot_items + v_items; it += NT) {
+  // gridDim.y workgroups per row: one item (8 dims of a head) per thread, one load round trip per row
+  for (int it = blockIdx.y * NT + threadIdx.x; it < rot_items + v_items; it += gridDim.y * NT) {
     if (it < rot_items) {
       const int h = it / gpr;          // 0..Hq+Hkv-1 (q heads then k heads)
       const int i0 = (it % gpr) * 8;   // pair index within the half
@@ -158,12 +159,17 @@ __global__ __launch_bounds__(NT) void rope_cache_grouped_kernel(LinOut qkv, cons
 }  // namespace
 
 void launch_rope_cache(LinOut qkv, const int* positions, const int* slots, const float* cos_sin, bf16* q_out,
-                       bf16* k_cache, bf16* v_cache, int T, int Hq, int Hkv, int D, int BS, hipStream_t s, int perm) {
+                       bf16* k_cache, bf16* v_cache, int T, int Hq, int Hkv, int D, int BS, hipStream_t s, int perm,
+                       int decode) {
   if (T == 0) return;
-  if (T >= 4 * RG && D <= NT) {  // prefill chunks: 8-row groups with 16-byte V token runs
+  // decode rows belong to different sequences (no V token runs to gain): the per-row kernel with enough
+  // workgroups per row that every thread handles one 8-dim item
+  if (!decode && T >= 4 * RG && D <= NT) {  // prefill chunks: 8-row groups with 16-byte V token runs
     rope_cache_grouped_kernel<<<dim3((T + RG - 1) / RG, RG), NT, 0, s>>>(qkv, positions, slots, cos_sin, q_out,
                                                                           k_cache, v_cache, T, Hq, Hkv, D, BS, perm);
     return;
   }
-  rope_cache_kernel<<<T, NT, 0, s>>>(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D, BS, perm);
+  const int items = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
+  rope_cache_kernel<<<dim3(T, (items + NT - 1) / NT), NT, 0, s>>>(qkv, positions, slots, cos_sin, q_out, k_cache,
+                                                                   v_cache, Hq, Hkv, D, BS, perm);
 }

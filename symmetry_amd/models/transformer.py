@@ -64,6 +64,8 @@ MAX_STEP_SEQS = 4096  # sequences per step (rows of last_ids)
 # extra workgroups of the decode attention launch that stream the O weight into the Infinity Cache
 # (0 = off; csrc/kernels/attention.hip, mall_prefetch)
 ATTN_PREFETCH_WGS = int(os.environ.get("SYMMETRY_ATTN_PREFETCH", "0"))
+# decode steps on the general path run rope_cache's per-row form (A/B knob)
+ROPE_DECODE_ROWS = os.environ.get("SYMMETRY_ROPE_DECODE_ROWS", "1") != "0"
 
 
 @dataclass
@@ -418,7 +420,7 @@ class TransformerLM:
         for i in range(cfg.num_layers):
             qkv = self._linear("qkv", x, w.layer(i, "wqkv"), wshuf=self._shuf(i, "wqkv"))
             ops.rope_cache(qkv, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq, self.hkv,
-                           perm=True)
+                           perm=True, decode=ROPE_DECODE_ROWS and b.kind == "decode")
             self._attention(b, kv, i, q, attn)
             o = self._linear("o", attn.view(T, self.hq * self.D), w.layer(i, "wo"), reduce=True,
                              wshuf=self._shuf(i, "wo"))

@@ -83,10 +83,12 @@ def embed_rms_norm(ids, table, residual, w, eps, out):
     return reference.embed_rms_norm(ids, table, residual, w, eps, out)
 
 
-def rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, perm=False):
+def rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, perm=False, decode=False):
+    """RoPE + paged K/V write.  ``decode``: rows of different sequences (a decode step): skips the prefill
+    form's 8-row V token-run grouping for more workgroups per row."""
     if _gpu(q_out):
         return _native.ops().rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, int(Hq), int(Hkv),
-                                        bool(perm))
+                                        bool(perm), bool(decode))
     return reference.rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, perm)
 
 

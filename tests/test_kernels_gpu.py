@@ -89,10 +89,12 @@ def test_rope_cache(gpu, kind):
     _close(vc, vc_r, atol=1e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("decode", [False, True])
 @pytest.mark.parametrize("kind", ["bf16", "slabs"])
-def test_rope_cache_prefill_groups(gpu, kind):
+def test_rope_cache_prefill_groups(gpu, kind, decode):
     """Prefill-sized rope_cache (8-row groups): 16-byte V token runs for aligned consecutive slots, the
-    per-token fallback for unaligned runs, scattered slots, padding rows and a ragged last group."""
+    per-token fallback for unaligned runs, scattered slots, padding rows and a ragged last group.
+    decode=True: the same rows through the per-row form (several workgroups per row)."""
     Hq, Hkv, D, BS, NB = 32, 8, 128, 64, 12
     slots_l = list(range(3 * BS + 5, 3 * BS + 5 + 37)) + list(range(5 * BS, 5 * BS + 56))
     slots_l += [9 * BS + 1, -1, 7 * BS + 63, 10 * BS + 8, -1, 11 * BS, 2 * BS + 9]
@@ -106,7 +108,7 @@ def test_rope_cache_prefill_groups(gpu, kind):
     cs = ref.rope_table(8192, D, 500000.0).to(gpu)
     q = torch.empty(T, Hq, D, device=gpu, dtype=torch.bfloat16)
     kc, vc = _make_cache(gpu, NB, Hkv, BS)
-    ops.rope_cache(qkv, pos, slots, cs, q, kc, vc, Hq, Hkv)
+    ops.rope_cache(qkv, pos, slots, cs, q, kc, vc, Hq, Hkv, decode=decode)
     q_r = torch.empty(T, Hq, D, dtype=torch.bfloat16)
     kc_r, vc_r = kc.new_zeros(kc.shape).cpu(), vc.new_zeros(vc.shape).cpu()
     ref.rope_cache(qkv.cpu(), pos.cpu(), slots.cpu(), cs.cpu(), q_r, kc_r, vc_r, Hq, Hkv)
