@@ -59,7 +59,7 @@ SPLITK_RESID_ROWS = int(os.environ.get("SYMMETRY_SPLITK_RESID_ROWS", "24"))
 # bench.py ms/step, fused vs general, 2 alternating runs each (profiles/general_rows_ab_r2.jsonl):
 # 10 rows 3.22 vs 3.90, 16 3.42 vs 3.94, 24 4.30 vs 3.98, 32 4.52 vs 4.07, 48 5.11 vs 4.37, 64 5.78 vs 4.63.
 # Decode batches are padded to buckets (.., 16, 24, ..), so 17..24-row steps run as 24.  0 disables.
-GENERAL_ROWS = int(os.environ.get("SYMMETRY_GENERAL_ROWS", "24"))
+GENERAL_ROWS = int(os.environ.get("SYMMETRY_GENERAL_ROWS", "20"))  # profiles/general_rows_ab_r2.jsonl
 MAX_STEP_SEQS = 4096  # sequences per step (rows of last_ids)
 # extra workgroups of the decode attention launch that stream the O weight into the Infinity Cache
 # (0 = off; csrc/kernels/attention.hip, mall_prefetch)
