@@ -32,6 +32,7 @@ def _check(r, n):
     assert r["higher_is_better"] is True and r["scaling"] == "weak" and r["dtype"] == "bf16"
     assert r["config"]["parallelism"] == f"dp{n}" and r["config"]["global_batch"] == 2 * n
     assert r["value"] > 0 and r["ms_per_step"] > 0 and r["p50_ttft_ms"] > 0
+    assert 0 < r["mean_ttft_ms"] <= r["max_ttft_ms"] and r["p50_ttft_ms"] <= r["max_ttft_ms"]
     # whole-job aggregate = world * clients * (1000 / ms_per_step)
     assert abs(r["value"] - n * 2 * 1e3 / r["ms_per_step"]) / r["value"] < 0.01
 
