@@ -10,6 +10,8 @@
 // sum-of-squares and the scale pass, so each byte is read once (memory bound:
 // SURVEY.md §2.6 K1).  The split-K partial slabs of the skinny decode GEMM are
 // summed here, which removes the GEMM's own reduce launch.
+#include <stdlib.h>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -71,7 +73,15 @@ void launch_mode(LinOut x, const int* ids, const bf16* table, float* residual, c
   constexpr int NT = 256;
   const int nvec = d / 8;
   dim3 grid(T);
-  if (nvec <= NT * 2) {
+  // rows of <= 4096 elements: 512 threads per row, one 8-element vector each (64-client decode step
+  // 4.680 -> 4.608 ms, profiles/norm_wide_ab_r2.jsonl); SYMMETRY_NORM_WIDE=0: 256 threads, 2 vectors
+  static const bool wide = [] {
+    const char* e = getenv("SYMMETRY_NORM_WIDE");
+    return !(e && e[0] == '0');
+  }();
+  if (wide && nvec <= 512) {
+    rms_norm_kernel<512, 1, MODE><<<grid, 512, 0, s>>>(x, ids, table, residual, w, out, d, eps);
+  } else if (nvec <= NT * 2) {
     rms_norm_kernel<NT, 2, MODE><<<grid, NT, 0, s>>>(x, ids, table, residual, w, out, d, eps);
   } else if (nvec <= NT * 4) {
     rms_norm_kernel<NT, 4, MODE><<<grid, NT, 0, s>>>(x, ids, table, residual, w, out, d, eps);
