@@ -5,26 +5,38 @@ Metric and config come from BASELINE.json ("streamed tokens/sec + p50 TTFT per
 client, Llama-3-8B provider, 1/2/4/8 MI355X"; config 3: maxConnections=10
 concurrent clients, continuous batching, greedy decode).
 
-Per GPU (one process per GPU, launched by torch.distributed.run for N > 1):
-  * a native engine serving Llama-3-8B (bf16, random-init weights of the real
-    architecture, synthetic prompts: no network for checkpoints/datasets);
-  * ``--clients`` concurrent chat requests (default 10 = maxConnections);
-  * every generated token is detokenized and encoded as one OpenAI SSE
-    ``chat.completion.chunk`` event for its client (the provider's streaming
-    path).
-Scaling is data-parallel ("weak"): each GPU runs its own provider engine and
-clients, so per-GPU work is fixed as N grows.
+One process per GPU (launched by torch.distributed.run for N > 1), bf16,
+random-init weights of the real Llama-3-8B architecture, synthetic 128-token
+prompts (no network for checkpoints/datasets).
 
-A *step* is one engine decode step (one token for every client).  The engine
-first runs its start-up warmup (one prefill per size class, hipGraph capture),
-as a provider does before it announces itself.  W warmup steps (the prefill
-of all prompts + decode steps) are untimed; then exactly K decode steps are timed between
-barrier + synchronize on both sides; the max over ranks is reported.
-p50 TTFT is measured on the prefill (all clients arrive together).
+Parallelism (``--parallel``; default ``tp`` for N > 1):
+  * ``tp``: ONE provider over all N GPUs -- Llama-3-8B tensor-parallel (TP=N,
+    Megatron column/row split, the decode all-reduces on the one-shot xGMI
+    kernel, RCCL for the rest), rank 0 schedules and streams, ranks 1..N-1
+    mirror each step from the shared-memory metadata ring (pipelined decode).
+    ``--clients`` concurrent clients in total (default 10 = maxConnections):
+    "strong" scaling -- each client's stream gets faster as GPUs are added.
+  * ``dp``: N independent providers, one per GPU, ``--clients`` each: "weak"
+    scaling of aggregate throughput.
+
+Timing (the driver contract): the engine runs its start-up warmup (prefill
+size classes, hipGraph capture); W warmup steps (the prefill of all prompts +
+decode steps) are untimed; then exactly K decode steps (one token for every
+client) are timed between sync points (every rank's GPU idle + a barrier) on
+both sides; the max over ranks is reported.  Every generated token is
+detokenized and SSE-encoded for its client inside the timed loop.
+
+Client end (``--client-end``, default on): after the timed steps the same
+engine serves as a real provider -- discovery node, Symmetry server, provider
+node and ``--clients`` swarm clients in a separate process over Noise XX +
+secretstream -- and per-client streamed tokens/s and p50 TTFT are measured on
+the client sockets (``symmetry_amd/testing/e2e.py``), reported under
+``client_end`` and as the top-level ``p50_ttft_ms`` / ``client_end_*`` fields.
 """
 from __future__ import annotations
 
 import argparse
+import asyncio
 import json
 import os
 import sys
@@ -37,15 +49,20 @@ if ROOT not in sys.path:
 METRIC = "streamed tokens/sec + p50 TTFT per client, Llama-3-8B provider, 1/2/4/8 MI355X"
 
 
-def main() -> int:
+def _args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--model", default="llama3:8b")
-    ap.add_argument("--clients", type=int, default=10, help="concurrent clients per GPU (maxConnections)")
+    ap.add_argument("--parallel", choices=("auto", "tp", "dp"), default="auto",
+                    help="tp: one provider over all GPUs (default for N > 1); dp: one provider per GPU")
+    ap.add_argument("--clients", type=int, default=10,
+                    help="concurrent clients (maxConnections): in total under tp, per GPU under dp")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--max-model-len", type=int, default=8192)
+    ap.add_argument("--client-end", type=int, default=1, help="1: also measure at the client sockets")
+    ap.add_argument("--client-tokens", type=int, default=256, help="tokens per client in the client-end run")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--persistent-mlp", action="store_true", help="O/gate_up/down as one persistent launch (A/B)")
     ap.add_argument("--attn-block", type=int, default=None, help="A/B: QKV -> attention -> O as one launch (0/1)")
@@ -53,31 +70,29 @@ def main() -> int:
     ap.add_argument("--max-batched-tokens", type=int, default=None, help="A/B: token budget of a pure-prefill step")
     ap.add_argument("--mixed-prefill-tokens", type=int, default=None, help="A/B: prompt budget of mixed steps")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra decode steps after timing (for rocprof)")
-    args = ap.parse_args()
+    return ap.parse_args()
 
+
+def main() -> int:
+    args = _args()
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if torch.cuda.is_available():
+    parallel = args.parallel if args.parallel != "auto" else ("tp" if world > 1 else "dp")
+    gpu = torch.cuda.is_available()
+    if gpu:
         torch.cuda.set_device(local % torch.cuda.device_count())
-    if world > 1:
-        # SYMMETRY_DIST_BACKEND=gloo rehearses the multi-rank flow with several ranks on one GPU (RCCL
-        # refuses two ranks on one device); the driver's multi-GPU runs use RCCL
-        backend = os.environ.get("SYMMETRY_DIST_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
-        dist.init_process_group(backend, device_id=torch.device("cuda", local)
-                                if torch.cuda.is_available() and backend == "nccl" else None)
 
     from symmetry_amd import ops
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
     from symmetry_amd.engine.sequence import SamplingParams
     from symmetry_amd.protocol import sse
 
-    if torch.cuda.is_available() and not ops.native_available():
+    if gpu and not ops.native_available():
         raise SystemExit("native kernels missing: run `python -m symmetry_amd._build` first")
-
     if args.nt_weights is not None and ops.native_available():
         from symmetry_amd.ops import _native
         _native.ops().decode_gemm_nt(int(args.nt_weights))
@@ -85,8 +100,8 @@ def main() -> int:
     C, P, W, K = args.clients, args.prompt_len, args.warmup, args.steps
     block = 64
     blocks = C * ((args.max_model_len + block - 1) // block) + 16
-    cfg = EngineConfig(model=args.model, device="auto", seed=1234 + rank, max_num_seqs=C,
-                       max_model_len=args.max_model_len, block_size=block, num_kv_blocks=blocks,
+    cfg = EngineConfig(model=args.model, device="auto", seed=1234 + (0 if parallel == "tp" else rank),
+                       max_num_seqs=C, max_model_len=args.max_model_len, block_size=block, num_kv_blocks=blocks,
                        use_graphs=not args.no_graphs, max_num_batched_tokens=max(8192, C * P),
                        persistent_mlp=args.persistent_mlp)
     if args.max_batched_tokens is not None:
@@ -95,12 +110,46 @@ def main() -> int:
         cfg.mixed_prefill_tokens = args.mixed_prefill_tokens
     if args.attn_block is not None:
         cfg.fused_attn_block = bool(args.attn_block)
+
     t0 = time.perf_counter()
-    eng = LLMEngine(cfg)
+    if parallel == "tp" and world > 1:
+        from symmetry_amd.parallel.launch import init_tp_engine
+
+        eng, rank = init_tp_engine(cfg)
+        group = eng.runner.cpu_group
+    else:
+        group = None
+        if world > 1:
+            # SYMMETRY_DIST_BACKEND=gloo rehearses the multi-rank flow with several ranks on one GPU (RCCL
+            # refuses two ranks on one device); the driver's multi-GPU runs use RCCL
+            backend = os.environ.get("SYMMETRY_DIST_BACKEND", "nccl" if gpu else "gloo")
+            dist.init_process_group(backend, device_id=torch.device("cuda", local) if gpu and backend == "nccl"
+                                    else None)
+            group = dist.new_group(backend="gloo")
+        eng = LLMEngine(cfg)
     t_load = time.perf_counter() - t0
+    tp_worker = parallel == "tp" and world > 1 and rank != 0
+    runner = eng.runner
+
+    if tp_worker:
+        # mirror rank 0 (warmup, graph capture, timed steps, client-end run) until it stops the plane
+        runner.worker_loop()
+        elapsed = runner.sync_times[1] - runner.sync_times[0] if len(runner.sync_times) >= 2 else 0.0
+        _reduce_and_exit(group, elapsed, [], world)
+        return 0
+
     # provider start-up (not timed): prefill size classes + decode hipGraph capture
     t_cap = eng.warmup([n for n in (16, 128, 512, C * P) if n <= cfg.max_num_batched_tokens])
-    sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+
+    def sync() -> float:
+        if parallel == "tp" or world == 1:
+            return runner.sync_point()
+        if gpu:
+            torch.cuda.synchronize()
+        dist.barrier(group=group)
+        if gpu:
+            torch.cuda.synchronize()
+        return time.perf_counter()
 
     # ---- clients: synthetic chat prompts of exactly P tokens, SSE-encoded streaming sinks
     g = torch.Generator().manual_seed(99 + rank)
@@ -119,50 +168,51 @@ def main() -> int:
     prefix = eng.tokenizer.apply_chat_template([{"role": "user", "content": ""}])
     seqs = []
     for i in range(C):
-        body = torch.randint(256, max(257, eng.model_cfg.vocab_size - 1024), (max(1, P - len(prefix)),), generator=g).tolist()
+        body = torch.randint(256, max(257, eng.model_cfg.vocab_size - 1024), (max(1, P - len(prefix)),),
+                             generator=g).tolist()
         seqs.append(eng.add_request(f"client-{i}", (prefix + body)[:P], params, sink(f"client-{i}")))
 
     # ---- warmup: prefill (TTFT) + W decode steps
-    steps_done = 0
     while any(s.first_token_time is None for s in seqs):
         eng.step()
-        steps_done += 1
     ttfts = sorted(s.ttft for s in seqs)
     for _ in range(W):
         eng.step()
-        steps_done += 1
-    sync()
-    if world > 1:
-        dist.barrier()
-    sync()
-    t1 = time.perf_counter()
+    t1 = sync()
     for _ in range(K):
         eng.step()
-    sync()
-    if world > 1:
-        dist.barrier()
-    sync()
-    elapsed = time.perf_counter() - t1
+    elapsed = sync() - t1
     for _ in range(args.profile_steps):
         eng.step()
-    sync()
+    for s in seqs:
+        eng.abort(s.request_id)
+    while eng.has_unfinished():
+        eng.step()
+    events = sum(len(v) for v in streams.values())
 
-    if world > 1:
-        tt = torch.tensor([elapsed], device="cuda" if torch.cuda.is_available() else "cpu", dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        tf = torch.tensor(ttfts, device=tt.device, dtype=torch.float64)
-        allt = [torch.zeros_like(tf) for _ in range(world)]
-        dist.all_gather(allt, tf)
-        ttfts = sorted(torch.cat(allt).tolist())
+    client_end = None
+    if args.client_end and rank == 0:
+        from symmetry_amd.testing.e2e import client_end_run
+
+        try:
+            client_end = asyncio.run(client_end_run(eng, args.model, C, prompt_tokens=P,
+                                                    max_tokens=args.client_tokens))
+        except Exception as exc:  # the engine-step measurement stands on its own
+            client_end = {"error": f"{type(exc).__name__}: {exc}"}
+    if parallel == "tp" and world > 1:
+        eng.shutdown()
+    elif world > 1:
+        dist.barrier(group=group)
+    elapsed, ttfts = _reduce(group, elapsed, ttfts, world, gather_ttft=parallel == "dp")
+
     p50_ttft = ttfts[len(ttfts) // 2] * 1e3
     mean_ttft, max_ttft = sum(ttfts) / len(ttfts) * 1e3, ttfts[-1] * 1e3
     ms_step = elapsed / K * 1e3
-    total_tps = world * C * K / elapsed
+    n_clients = C * (world if parallel == "dp" else 1)
+    total_tps = n_clients * K / elapsed
     per_client = 1e3 / ms_step
-    events = sum(len(v) for v in streams.values())
     if rank == 0:
-        print(json.dumps({
+        line = {
             "metric": METRIC,
             "value": round(total_tps, 2),
             "unit": "tokens/s",
@@ -171,27 +221,59 @@ def main() -> int:
             "warmup": W,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if parallel == "tp" and world > 1 else "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic prompts, random-init weights (real Llama-3-8B architecture)",
-            "config": {"model": args.model, "global_batch": world * C, "seq_len": P,
-                       "parallelism": f"dp{world}", "clients_per_gpu": C, "max_model_len": args.max_model_len,
-                       "decode": "greedy", "hipgraphs": bool(eng.runner.use_graphs),
+            "data": "synthetic 128-token prompts, random-init weights (real Llama-3-8B architecture)",
+            "config": {"model": args.model, "global_batch": n_clients, "seq_len": P,
+                       "parallelism": f"{parallel}{world}", "clients": n_clients,
+                       "clients_per_provider": C, "max_model_len": args.max_model_len,
+                       "decode": "greedy", "hipgraphs": bool(runner.use_graphs),
+                       "tp_comm": type(eng.model.tp).__name__ if eng.model.tp is not None else None,
                        "ops": ("torch-eager (baseline B1)" if ops.torch_mode() else
-                               "native gfx950 HIP" if torch.cuda.is_available() else "torch reference (CPU)")},
+                               "native gfx950 HIP" if gpu else "torch reference (CPU)")},
             "per_client_tokens_per_s": round(per_client, 2),
-            "p50_ttft_ms": round(p50_ttft, 2),
-            "mean_ttft_ms": round(mean_ttft, 2),
-            "max_ttft_ms": round(max_ttft, 2),
+            "engine_p50_ttft_ms": round(p50_ttft, 2),
+            "engine_mean_ttft_ms": round(mean_ttft, 2),
+            "engine_max_ttft_ms": round(max_ttft, 2),
             "load_s": round(t_load, 1),
             "warmup_s": round(t_cap, 1),
             "sse_events_rank0": events,
-        }), flush=True)
+        }
+        if client_end is not None:
+            line["client_end"] = client_end
+            line["p50_ttft_ms"] = client_end.get("p50_ttft_ms")
+            line["client_end_per_client_tokens_per_s"] = client_end.get("per_client_tokens_per_s_median")
+        else:
+            line["p50_ttft_ms"] = round(p50_ttft, 2)
+        print(json.dumps(line), flush=True)
     if world > 1:
-        dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def _reduce(group, elapsed, ttfts, world, gather_ttft):
+    """Max elapsed over ranks; all ranks' TTFTs (dp: every rank has its own clients)."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return elapsed, ttfts
+    tt = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
+    if gather_ttft:
+        tf = torch.tensor(ttfts, dtype=torch.float64)
+        allt = [torch.zeros_like(tf) for _ in range(world)]
+        dist.all_gather(allt, tf, group=group)
+        ttfts = sorted(torch.cat(allt).tolist())
+    return float(tt.item()), ttfts
+
+
+def _reduce_and_exit(group, elapsed, ttfts, world):
+    import torch.distributed as dist
+
+    _reduce(group, elapsed, ttfts, world, gather_ttft=False)
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

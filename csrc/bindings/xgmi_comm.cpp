@@ -41,7 +41,7 @@ std::mutex g_mu;
 std::vector<Xgmi*> g_x;
 // Uncached buffers are never returned to the runtime: memory freed from a hipDeviceMallocUncached
 // allocation and handed out again to ordinary hipMalloc users (the torch caching allocator) was seen
-// to lose or mix plain stores of later kernels on gfx950 (tools/xgmi_probe3.py: outputs written after
+// to lose or mix plain stores of later kernels on gfx950 (a round-2 probe: outputs written after
 // a communicator was destroyed read back differently from the GPU and from the host).  A destroyed
 // communicator's buffer waits here for the next communicator of the same size.
 std::vector<std::pair<long long, char*>> g_uc_pool;
@@ -73,16 +73,12 @@ int64_t xgmi_create(int64_t slot_bytes, int64_t world, int64_t rank, int64_t dev
   if (p == nullptr) HIP_OK(hipExtMallocWithFlags(&p, (size_t)x->bytes, hipDeviceMallocUncached));
   HIP_OK(hipMemset(p, 0, (size_t)x->bytes));
   x->own = (char*)p;
-  void* e = nullptr;
-  HIP_OK(hipMalloc(&e, XG_MAX_WG * sizeof(unsigned)));
-  HIP_OK(hipMemset(e, 0, XG_MAX_WG * sizeof(unsigned)));
   void* eh = nullptr;
   HIP_OK(hipHostMalloc(&eh, 64, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(eh, 0, 64);
   void* ed = nullptr;
   HIP_OK(hipHostGetDevicePointer(&ed, eh, 0));
   HIP_OK(hipDeviceSynchronize());
-  x->args.epochs = (unsigned*)e;
   x->err_host = (volatile int*)eh;
   x->args.err = (int*)ed;
   x->args.rank = (int)rank;
@@ -196,11 +192,14 @@ void xgmi_keys_max(const Tensor& keys, Tensor& ids, int64_t h) {
 }
 
 // test-only: every rank of this process in one launch (grid slice per rank; see xgmi_ar.hip)
-void xgmi_all_reduce_multi(std::vector<Tensor> ins, std::vector<Tensor> outs, std::vector<int64_t> comms) {
+void xgmi_all_reduce_multi(std::vector<Tensor> ins, std::vector<Tensor> outs, std::vector<int64_t> comms,
+                           int64_t delay_rank, int64_t delay_us) {
   const int world = (int)comms.size();
   TORCH_CHECK(world >= 1 && world <= XG_MULTI_MAX && (int)ins.size() == world && (int)outs.size() == world,
               "xgmi_all_reduce_multi: one input, output and communicator per rank (<= ", XG_MULTI_MAX, ")");
   XgmiMulti m{};
+  m.delay_rank = (int)delay_rank;
+  m.delay_ticks = (unsigned long long)std::max<int64_t>(delay_us, 0) * 100ull;  // 100 MHz wall clock
   const long long n = ins[0].numel();
   int elem = -1;
   for (int r = 0; r < world; ++r) {
@@ -225,12 +224,14 @@ void xgmi_all_reduce_multi(std::vector<Tensor> ins, std::vector<Tensor> outs, st
 }
 
 void xgmi_add_prep_multi(std::vector<Tensor> ys, std::vector<Tensor> resids, const Tensor& w, std::vector<Tensor> xws,
-                         std::vector<Tensor> sss, std::vector<int64_t> comms) {
+                         std::vector<Tensor> sss, std::vector<int64_t> comms, int64_t delay_rank, int64_t delay_us) {
   const int world = (int)comms.size();
   TORCH_CHECK(world >= 1 && world <= XG_MULTI_MAX && (int)ys.size() == world && (int)resids.size() == world &&
                   (int)xws.size() == world && (int)sss.size() == world,
               "xgmi_add_prep_multi: one set of tensors per rank");
   XgmiMulti m{};
+  m.delay_rank = (int)delay_rank;
+  m.delay_ticks = (unsigned long long)std::max<int64_t>(delay_us, 0) * 100ull;
   const int64_t T = resids[0].size(0), d = resids[0].size(1);
   const int64_t P = sss[0].dim() == 2 ? sss[0].size(1) : 1;
   TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.numel() == d && w.is_contiguous(), "xgmi_add_prep_multi: w bf16 [d]");
@@ -257,6 +258,30 @@ void xgmi_add_prep_multi(std::vector<Tensor> ys, std::vector<Tensor> resids, con
   launch_xgmi_add_prep_multi(m, world, (int)T, (int)d, (int)P, stream_of(ys[0]));
 }
 
+void xgmi_keys_max_multi(std::vector<Tensor> keys, std::vector<Tensor> ids, std::vector<int64_t> comms,
+                         int64_t delay_rank, int64_t delay_us) {
+  const int world = (int)comms.size();
+  TORCH_CHECK(world >= 1 && world <= XG_MULTI_MAX && (int)keys.size() == world && (int)ids.size() == world,
+              "xgmi_keys_max_multi: one keys / ids tensor and communicator per rank");
+  XgmiMulti m{};
+  m.delay_rank = (int)delay_rank;
+  m.delay_ticks = (unsigned long long)std::max<int64_t>(delay_us, 0) * 100ull;
+  const int64_t B = keys[0].numel();
+  for (int r = 0; r < world; ++r) {
+    Xgmi* x = get(comms[r]);
+    TORCH_CHECK(x->args.rank == r && x->args.world == world, "xgmi_keys_max_multi: communicator ", r, " is not rank ", r);
+    check_ready(x, keys[r]);
+    check_ready(x, ids[r]);
+    TORCH_CHECK(keys[r].scalar_type() == at::kLong && ids[r].scalar_type() == at::kInt && keys[r].numel() == B &&
+                    ids[r].numel() >= B && B <= 4096 && B * 8 <= x->args.slot_bytes,
+                "xgmi_keys_max_multi: keys int64 [B], ids int32 [>= B]");
+    m.c[r] = x->args;
+    m.in[r] = keys[r].data_ptr();
+    m.out[r] = ids[r].data_ptr();
+  }
+  launch_xgmi_keys_max_multi(m, world, (int)B, stream_of(keys[0]));
+}
+
 // reads (and clears) the error word: 1 + the source rank that never signalled within the wait limit
 // (host-mapped memory: no device synchronisation; a kernel still running may set it later)
 int64_t xgmi_error(int64_t h) {
@@ -279,7 +304,6 @@ void xgmi_destroy(int64_t h) {
   (void)hipSetDevice(x->device);
   (void)hipDeviceSynchronize();
   for (char* p : x->opened) (void)hipIpcCloseMemHandle(p);
-  (void)hipFree(x->args.epochs);
   (void)hipHostFree((void*)x->err_host);
   {
     std::lock_guard<std::mutex> g(g_mu);
@@ -298,12 +322,15 @@ TORCH_LIBRARY_FRAGMENT(symmetry_amd, m) {
   m.def("xgmi_all_reduce(Tensor input, Tensor(a!) out, int comm) -> ()", &xgmi_all_reduce);
   m.def("xgmi_add_prep(Tensor y, Tensor(a!) resid, Tensor w, Tensor(b!) xw, Tensor(c!) ss, int comm) -> ()",
         &xgmi_add_prep);
-  m.def("xgmi_all_reduce_multi(Tensor[] inputs, Tensor(a!)[] outs, int[] comms) -> ()", &xgmi_all_reduce_multi);
+  m.def("xgmi_all_reduce_multi(Tensor[] inputs, Tensor(a!)[] outs, int[] comms, int delay_rank=-1, int delay_us=0) -> ()",
+        &xgmi_all_reduce_multi);
   m.def(
-      "xgmi_add_prep_multi(Tensor[] ys, Tensor(a!)[] resids, Tensor w, Tensor(b!)[] xws, Tensor(c!)[] sss, int[] comms) "
-      "-> ()",
+      "xgmi_add_prep_multi(Tensor[] ys, Tensor(a!)[] resids, Tensor w, Tensor(b!)[] xws, Tensor(c!)[] sss, int[] comms, "
+      "int delay_rank=-1, int delay_us=0) -> ()",
       &xgmi_add_prep_multi);
   m.def("xgmi_keys_max(Tensor keys, Tensor(a!) ids, int comm) -> ()", &xgmi_keys_max);
+  m.def("xgmi_keys_max_multi(Tensor[] keys, Tensor(a!)[] ids, int[] comms, int delay_rank=-1, int delay_us=0) -> ()",
+        &xgmi_keys_max_multi);
   m.def("xgmi_error(int comm) -> int", &xgmi_error);
   m.def("xgmi_slot_bytes(int comm) -> int", &xgmi_slot_bytes);
   m.def("xgmi_destroy(int comm) -> ()", &xgmi_destroy);

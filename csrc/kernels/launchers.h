@@ -180,10 +180,10 @@ void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_l
 // xgmi_ar.hip: one-shot all-reduce over xGMI peer memory (IPC-mapped buffers of every TP rank)
 constexpr int XG_MAX_WORLD = 8;
 constexpr int XG_MAX_WG = 4096;
-constexpr int XG_KEYS_WG = XG_MAX_WG - 1;  // epoch / flag slot of the sampling-keys collective (others stay below)
+constexpr int XG_KEYS_WG = XG_MAX_WG - 1;  // flag word of the sampling-keys collective (others stay below)
 struct XgmiArgs {
-  char* bufs[XG_MAX_WORLD];  // every rank's comm buffer as mapped in this process (own one included)
-  unsigned* epochs;          // [XG_MAX_WG] local per-workgroup collective counters (zeroed once)
+  char* bufs[XG_MAX_WORLD];  // every rank's comm buffer as mapped in this process (own one included; its
+                             // header holds this rank's collective counter)
   int* err;                  // local error word (a peer never arrived)
   int rank, world;
   long long slot_bytes;      // bytes of one (parity, source rank) data slot
@@ -196,7 +196,7 @@ void launch_xgmi_add_prep(const XgmiArgs& c, const float* y, float* resid, const
                           int d, int parts, hipStream_t s);
 // test-only: the ranks of one process as grid slices of ONE launch (co-resident by construction).
 // add_prep: in = y, out = resid, xw, ss per rank; w shared
-constexpr int XG_MULTI_MAX = 4;
+constexpr int XG_MULTI_MAX = 8;
 constexpr int XG_MULTI_MAX_GROUPS = 1024;  // all slices co-resident (they wait on each other)
 struct XgmiMulti {
   XgmiArgs c[XG_MULTI_MAX];
@@ -205,6 +205,9 @@ struct XgmiMulti {
   void* xw[XG_MULTI_MAX];
   float* ss[XG_MULTI_MAX];
   const bf16* w;
+  int delay_rank;                  // this slice waits delay_ticks (100 MHz wall clock) before pushing (-1: none)
+  unsigned long long delay_ticks;
 };
 void launch_xgmi_all_reduce_multi(const XgmiMulti& m, int world, long long n, int elem, hipStream_t s);
 void launch_xgmi_add_prep_multi(const XgmiMulti& m, int world, int T, int d, int parts, hipStream_t s);
+void launch_xgmi_keys_max_multi(const XgmiMulti& m, int world, int B, hipStream_t s);

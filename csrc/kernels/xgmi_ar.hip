@@ -12,20 +12,26 @@
 // Buffers: one per rank, hipExtMallocWithFlags(hipDeviceMallocUncached) so that stores arriving over
 // xGMI are never hidden behind a stale L2 line of the reading GPU, exported with hipIpcGetMemHandle and
 // opened by every peer (symmetry_amd/parallel/comm.py::XgmiComm).  Layout of a buffer:
-//   flags [XG_MAX_WG][XG_MAX_WORLD] u32 | data [2 parities][world][slot_bytes]
-// Epochs: workgroup g of every launch bumps its own local counter epochs[g]; all ranks run the same
-// sequence of collectives with the same grids, so the counters agree across ranks without any host
-// bookkeeping, and a captured hipGraph replays correctly.  Data slots alternate by epoch parity: a rank
-// can run at most one collective ahead of a peer (it waits for that peer's flag of the previous one),
-// so the slot it writes is never the slot the peer is still reducing.  Flags are compared with a signed
-// difference (a fast peer may already have raised the next epoch).
+//   header (local collective counter) | flags [XG_MAX_WG][XG_MAX_WORLD] u32 | data [2 parities][world][slot_bytes]
+// Epochs: ONE counter per communicator numbers its collectives.  Every workgroup of a launch reads it on
+// entry and counts itself in; the last one to arrive bumps it, after every workgroup has read it, and
+// the next collective on the stream starts only after this launch retired -- so all workgroups of one
+// collective share one epoch whatever the grid, and all ranks (running the same sequence of
+// collectives) agree on it without host bookkeeping; a captured hipGraph replays correctly.  The data
+// slots alternate by epoch parity.  A rank can finish collective e+1 only after every peer has entered
+// e+1 (it waits for their flags), i.e. after every peer has finished reducing e: so a rank two
+// collectives ahead can never overwrite the parity of e while a peer still reads it, however the two
+// collectives split their bytes over workgroups (add_prep parts, all-reduce chunks and the keys
+// collective all address the same slot bytes differently).  Flags are compared with a signed
+// difference (a fast peer may already have raised a later epoch in the same flag word).
 // Spins are bounded: a missing peer sets the error word and the kernel exits instead of hanging.
 #include "common.h"
 #include "launchers.h"
 
 namespace {
 
-constexpr long long XG_FLAG_BYTES = (long long)XG_MAX_WG * XG_MAX_WORLD * 4;
+constexpr long long XG_HDR_BYTES = 256;  // [0] collective counter, [32] arrivals of the current collective
+constexpr long long XG_FLAG_BYTES = XG_HDR_BYTES + (long long)XG_MAX_WG * XG_MAX_WORLD * 4;
 constexpr int XG_THREADS = 256;
 constexpr unsigned long long XG_WAIT_TICKS = 200000000ull;  // 2 s of the 100 MHz wall clock: a peer that
                                                             // never arrives is an error, not a hang
@@ -37,16 +43,40 @@ SYM_DEV char* xg_slot(const XgmiArgs& c, int r, int par, int src) {
 // Push this workgroup's chunk (nvec 16-byte vectors at byte offset `off`) into slot (parity, rank) of
 // every rank's buffer (its own included, so the reduce reads all slots from one place), signal, wait for
 // every rank's signal of the same chunk.  Returns the epoch parity (the slot set to reduce).
-template <typename V = uint4>
-SYM_DEV int xg_exchange(const XgmiArgs& c, int wg, const V* __restrict__ src, long long off, int nvec) {
+// This workgroup's epoch of the current collective (nwg workgroups per rank in the launch).
+SYM_DEV unsigned xg_epoch(const XgmiArgs& c, int nwg) {
   __shared__ unsigned s_epoch;
   if (threadIdx.x == 0) {
-    const unsigned e = c.epochs[wg] + 1u;
-    c.epochs[wg] = e;
+    unsigned* ctr = reinterpret_cast<unsigned*>(c.bufs[c.rank]);
+    const unsigned e = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    // acq_rel: the counter load above is ordered before this workgroup counts itself in
+    const unsigned n = __hip_atomic_fetch_add(ctr + 8, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (n == (unsigned)nwg - 1u) {  // last to arrive: every workgroup has read the counter
+      __hip_atomic_store(ctr + 8, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
     s_epoch = e;
   }
   __syncthreads();
-  const unsigned epoch = s_epoch;
+  return s_epoch;
+}
+
+// Test hook: hold this rank's workgroups back before they push (a slow peer), `delay` wall-clock ticks.
+SYM_DEV void xg_delay(unsigned long long delay) {
+  if (delay == 0) return;
+  const unsigned long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < delay) __builtin_amdgcn_s_sleep(8);
+}
+
+// Push this workgroup's chunk (nvec vectors at byte offset `off`) into slot (parity, rank) of every rank's
+// buffer (its own included, so the reduce reads all slots from one place), raise flag (wg, rank) in every
+// rank, wait for every rank's flag (wg, src).  `wg` indexes flags only; `nwg` = workgroups of this rank in
+// the launch (epoch accounting).  Returns the epoch parity (the slot set to reduce).
+template <typename V = uint4>
+SYM_DEV int xg_exchange(const XgmiArgs& c, int wg, int nwg, const V* __restrict__ src, long long off, int nvec,
+                        unsigned long long delay = 0) {
+  const unsigned epoch = xg_epoch(c, nwg);
+  xg_delay(delay);
   const int par = (int)(epoch & 1u);
   for (int v = threadIdx.x; v < nvec; v += XG_THREADS) {
     const V x = src[v];
@@ -60,9 +90,10 @@ SYM_DEV int xg_exchange(const XgmiArgs& c, int wg, const V* __restrict__ src, lo
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < c.world) {
-    unsigned* f = reinterpret_cast<unsigned*>(c.bufs[threadIdx.x]) + wg * XG_MAX_WORLD + c.rank;
+    unsigned* f = reinterpret_cast<unsigned*>(c.bufs[threadIdx.x] + XG_HDR_BYTES) + wg * XG_MAX_WORLD + c.rank;
     __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const unsigned* mine = reinterpret_cast<const unsigned*>(c.bufs[c.rank]) + wg * XG_MAX_WORLD + threadIdx.x;
+    const unsigned* mine =
+        reinterpret_cast<const unsigned*>(c.bufs[c.rank] + XG_HDR_BYTES) + wg * XG_MAX_WORLD + threadIdx.x;
     const unsigned long long t0 = wall_clock64();
     while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       if (wall_clock64() - t0 > XG_WAIT_TICKS) {  // error word: 1 + the source rank that never arrived
@@ -77,16 +108,18 @@ SYM_DEV int xg_exchange(const XgmiArgs& c, int wg, const V* __restrict__ src, lo
 }
 
 // Plain all-reduce (sum) of n elements, in place or out of place; ELEM: 0 = fp32, 1 = bf16.
-// Workgroup g owns elements [g * chunk, min(n, (g + 1) * chunk)), chunk a multiple of 8.
+// Workgroup g of nwg owns elements [g * chunk, min(n, (g + 1) * chunk)), chunk a multiple of 8.
 template <int ELEM>
-SYM_DEV void xg_all_reduce_body(const XgmiArgs& c, int wg, const void* in, void* out, long long n, int chunk) {
+SYM_DEV void xg_all_reduce_body(const XgmiArgs& c, int wg, int nwg, const void* in, void* out, long long n, int chunk,
+                                unsigned long long delay = 0) {
   const long long e0 = (long long)wg * chunk;
   const int cnt = (int)min((long long)chunk, n - e0);
   constexpr int ESZ = ELEM == 0 ? 4 : 2;
   const int nvec = cnt * ESZ / 16;
   const long long off = e0 * ESZ;
-  const int par = xg_exchange<uint4>(c, wg, reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(in) + off),
-                                     off, nvec);
+  const int par = xg_exchange<uint4>(c, wg, nwg,
+                                     reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(in) + off), off, nvec,
+                                     delay);
   for (int v = threadIdx.x; v < nvec; v += XG_THREADS) {
     if constexpr (ELEM == 0) {
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -113,16 +146,16 @@ SYM_DEV void xg_all_reduce_body(const XgmiArgs& c, int wg, const void* in, void*
 
 // All-reduce of fp32 row partials [T][d] fused with the decode epilogue of a row-parallel projection
 // (prep_kernel<1>): resid += sum; xw = bf16(resid * w); ss[row][part] = sum(resid^2) over the part's
-// columns.  Workgroup (row, part) of P owns columns [part d / P, (part + 1) d / P) of its row.
-SYM_DEV void xg_add_prep_body(const XgmiArgs& c, int row, int part, int P, const float* __restrict__ y,
+// columns.  Workgroup (row, part) of T x P owns columns [part d / P, (part + 1) d / P) of its row.
+SYM_DEV void xg_add_prep_body(const XgmiArgs& c, int row, int part, int T, int P, const float* __restrict__ y,
                               float* __restrict__ resid, const bf16* __restrict__ w, bf16* __restrict__ xw,
-                              float* __restrict__ ss, int d) {
+                              float* __restrict__ ss, int d, unsigned long long delay = 0) {
   __shared__ float scratch[XG_THREADS / 64];
   const int dp = d / P;
   const int wg = row * P + part;
   const long long rb = (long long)row * d + (long long)part * dp;
   const long long off = rb * 4;
-  const int par = xg_exchange<uint4>(c, wg, reinterpret_cast<const uint4*>(y + rb), off, dp / 4);
+  const int par = xg_exchange<uint4>(c, wg, T * P, reinterpret_cast<const uint4*>(y + rb), off, dp / 4, delay);
   const bf16* wp = w + (long long)part * dp;
   float acc = 0.f;
   for (int vi = threadIdx.x; vi < dp / 8; vi += XG_THREADS) {
@@ -152,11 +185,10 @@ SYM_DEV void xg_add_prep_body(const XgmiArgs& c, int row, int part, int P, const
 
 // Vocab-parallel greedy / Gumbel sampling combine: every rank holds per-row packed u64 keys (order-
 // preserving value bits | inverted vocabulary index) of its vocabulary shard; the max over ranks is the
-// global argmax, and ids = 0xFFFFFFFF - low 32 bits.  One workgroup (rows <= 512), epoch slot
-// XG_KEYS_WG (the other collectives' grids stay below it).
-__global__ __launch_bounds__(XG_THREADS) void xgmi_keys_max_kernel(XgmiArgs c, const unsigned long long* keys,
-                                                                  int* __restrict__ ids, int B) {
-  const int par = xg_exchange<unsigned long long>(c, XG_KEYS_WG, keys, 0, B);
+// global argmax, and ids = 0xFFFFFFFF - low 32 bits.  One workgroup (rows <= 4096) on flag word XG_KEYS_WG.
+SYM_DEV void xg_keys_max_body(const XgmiArgs& c, const unsigned long long* keys, int* __restrict__ ids, int B,
+                              unsigned long long delay = 0) {
+  const int par = xg_exchange<unsigned long long>(c, XG_KEYS_WG, 1, keys, 0, B, delay);
   for (int i = threadIdx.x; i < B; i += XG_THREADS) {
     unsigned long long best = 0;
     for (int r = 0; r < c.world; ++r) {
@@ -167,10 +199,15 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_keys_max_kernel(XgmiArgs c, c
   }
 }
 
+__global__ __launch_bounds__(XG_THREADS) void xgmi_keys_max_kernel(XgmiArgs c, const unsigned long long* keys,
+                                                                  int* __restrict__ ids, int B) {
+  xg_keys_max_body(c, keys, ids, B);
+}
+
 template <int ELEM>
 __global__ __launch_bounds__(XG_THREADS) void xgmi_all_reduce_kernel(XgmiArgs c, const void* in, void* out,
                                                                      long long n, int chunk) {
-  xg_all_reduce_body<ELEM>(c, blockIdx.x, in, out, n, chunk);
+  xg_all_reduce_body<ELEM>(c, blockIdx.x, gridDim.x, in, out, n, chunk);
 }
 
 __global__ __launch_bounds__(XG_THREADS) void xgmi_add_prep_kernel(XgmiArgs c, const float* __restrict__ y,
@@ -178,22 +215,34 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_add_prep_kernel(XgmiArgs c, c
                                                                   const bf16* __restrict__ w,
                                                                   bf16* __restrict__ xw, float* __restrict__ ss,
                                                                   int d) {
-  xg_add_prep_body(c, blockIdx.x, blockIdx.y, gridDim.y, y, resid, w, xw, ss, d);
+  xg_add_prep_body(c, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, y, resid, w, xw, ss, d);
 }
 
 // Several ranks of ONE process in one launch (grid z = rank): the GPU test of the protocol on one device.
 // Separate launches on separate streams are not guaranteed to be co-resident (streams may share a
-// hardware queue), and every rank waits on the others; the slices of one grid are.
+// hardware queue), and every rank waits on the others; the slices of one grid are.  Slice
+// m.delay_rank is held back by m.delay_ticks before it pushes (a slow peer).
+SYM_DEV unsigned long long xg_multi_delay(const XgmiMulti& m, int r) {
+  return r == m.delay_rank ? m.delay_ticks : 0ull;
+}
+
 template <int ELEM>
 __global__ __launch_bounds__(XG_THREADS) void xgmi_all_reduce_multi_kernel(XgmiMulti m, long long n, int chunk) {
   const int r = blockIdx.z;
-  xg_all_reduce_body<ELEM>(m.c[r], blockIdx.x, m.in[r], m.out[r], n, chunk);
+  xg_all_reduce_body<ELEM>(m.c[r], blockIdx.x, gridDim.x, m.in[r], m.out[r], n, chunk, xg_multi_delay(m, r));
 }
 
 __global__ __launch_bounds__(XG_THREADS) void xgmi_add_prep_multi_kernel(XgmiMulti m, int d) {
   const int r = blockIdx.z;
-  xg_add_prep_body(m.c[r], blockIdx.x, blockIdx.y, gridDim.y, reinterpret_cast<const float*>(m.in[r]),
-                   reinterpret_cast<float*>(m.out[r]), m.w, reinterpret_cast<bf16*>(m.xw[r]), m.ss[r], d);
+  xg_add_prep_body(m.c[r], blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, reinterpret_cast<const float*>(m.in[r]),
+                   reinterpret_cast<float*>(m.out[r]), m.w, reinterpret_cast<bf16*>(m.xw[r]), m.ss[r], d,
+                   xg_multi_delay(m, r));
+}
+
+__global__ __launch_bounds__(XG_THREADS) void xgmi_keys_max_multi_kernel(XgmiMulti m, int B) {
+  const int r = blockIdx.z;
+  xg_keys_max_body(m.c[r], reinterpret_cast<const unsigned long long*>(m.in[r]), reinterpret_cast<int*>(m.out[r]), B,
+                   xg_multi_delay(m, r));
 }
 
 }  // namespace
@@ -225,6 +274,11 @@ void launch_xgmi_add_prep(const XgmiArgs& c, const float* y, float* resid, const
   xgmi_add_prep_kernel<<<dim3(T, parts), XG_THREADS, 0, s>>>(c, y, resid, w, xw, ss, d);
 }
 
+void launch_xgmi_keys_max(const XgmiArgs& c, const unsigned long long* keys, int* ids, int B, hipStream_t s) {
+  if (B == 0) return;
+  xgmi_keys_max_kernel<<<1, XG_THREADS, 0, s>>>(c, keys, ids, B);
+}
+
 void launch_xgmi_all_reduce_multi(const XgmiMulti& m, int world, long long n, int elem, hipStream_t s) {
   if (n == 0) return;
   const int chunk = xgmi_chunk(n, XG_MAX_WG);
@@ -240,7 +294,7 @@ void launch_xgmi_add_prep_multi(const XgmiMulti& m, int world, int T, int d, int
   xgmi_add_prep_multi_kernel<<<dim3(T, parts, world), XG_THREADS, 0, s>>>(m, d);
 }
 
-void launch_xgmi_keys_max(const XgmiArgs& c, const unsigned long long* keys, int* ids, int B, hipStream_t s) {
+void launch_xgmi_keys_max_multi(const XgmiMulti& m, int world, int B, hipStream_t s) {
   if (B == 0) return;
-  xgmi_keys_max_kernel<<<1, XG_THREADS, 0, s>>>(c, keys, ids, B);
+  xgmi_keys_max_multi_kernel<<<dim3(1, 1, world), XG_THREADS, 0, s>>>(m, B);
 }

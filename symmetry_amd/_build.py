@@ -9,6 +9,9 @@ travel with the repo snapshot to the GPU box:
   WITHOUT torch headers (fast); only ``csrc/bindings/torch_ops.cpp`` sees the
   ATen headers.  No hipify step, no CUDA sources: the kernels are HIP written
   for CDNA4 directly.
+* ``symmetry_amd/runtime/_runtime.so`` -- native runtime pieces around the
+  GPU path (``csrc/runtime``): the shared-memory step-metadata ring that
+  drives tensor-parallel workers (R4).
 * ``symmetry_amd/net/_native.so`` -- the C++ P2P plane (crypto over OpenSSL
   libcrypto, Noise XX, secretstream framing, epoll transport), the
   MI355X-box equivalent of the reference's native deps sodium-native and
@@ -39,6 +42,7 @@ HIPCC = os.path.join(ROCM, "bin", "hipcc")
 
 KERNEL_SO = os.path.join(PKG, "_C.so")
 NET_SO = os.path.join(PKG, "net", "_native.so")
+RUNTIME_SO = os.path.join(PKG, "runtime", "_runtime.so")
 
 
 def _torch_paths():
@@ -155,6 +159,32 @@ def build_net(verbose: bool = False, force: bool = False) -> str:
     return NET_SO
 
 
+def build_runtime(verbose: bool = False, force: bool = False) -> str:
+    """csrc/runtime/*.cpp -> symmetry_amd/runtime/_runtime.so (pybind11, host C++ only)."""
+    import pybind11
+
+    os.makedirs(OBJ, exist_ok=True)
+    rdir = os.path.join(CSRC, "runtime")
+    sources = sorted(glob.glob(os.path.join(rdir, "*.cpp")))
+    headers = glob.glob(os.path.join(rdir, "*.h"))
+    pyinc = sysconfig.get_paths()["include"]
+    cxx = shutil.which("g++") or "c++"
+    flags = ["-O2", "-g", "-std=c++17", "-fPIC", "-Wall", "-fvisibility=hidden"]
+    extra = os.environ.get("SYMMETRY_AMD_RUNTIME_CXXFLAGS", "").split()
+    jobs, objs = [], []
+    for src in sources:
+        obj = os.path.join(OBJ, "rt_" + os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _newer(obj, [src] + headers):
+            jobs.append([cxx, "-c", src, "-o", obj, "-I", rdir, "-I", pybind11.get_include(), "-I", pyinc]
+                        + flags + extra)
+    for c in jobs:
+        _run(c, verbose)
+    if force or jobs or _newer(RUNTIME_SO, objs):
+        _run([cxx, "-shared", "-o", RUNTIME_SO] + objs + ["-lrt", "-lpthread"] + extra, verbose)
+    return RUNTIME_SO
+
+
 SELFTEST = os.path.join(ROOT, "build", "net_selftest_asan")
 
 
@@ -175,6 +205,7 @@ def build_selftest(verbose: bool = False, force: bool = False) -> str:
 
 def build_all(verbose: bool = False, force: bool = False):
     net = build_net(verbose, force)
+    build_runtime(verbose, force)
     ker = build_kernels(verbose, force)
     return ker, net
 
@@ -187,5 +218,7 @@ if __name__ == "__main__":
         print(build_net(verbose, force))
     if not what or "kernels" in what:
         print(build_kernels(verbose, force))
+    if not what or "runtime" in what:
+        print(build_runtime(verbose, force))
     if "selftest" in what:
         print(build_selftest(verbose, force))

@@ -145,12 +145,15 @@ class LLMEngine:
             self.blocks)
         self.runner = ModelRunner(self.model, self.kv, self.scheduler.cfg.max_num_seqs, max_model_len,
                                   use_graphs=cfg.use_graphs and self._graph_safe(tp_comm, ep_comm),
-                                  tp_rank=cfg.tp_rank, tp_size=cfg.tp_size, cpu_group=cpu_group)
+                                  tp_rank=cfg.tp_rank, tp_size=cfg.tp_size, cpu_group=cpu_group,
+                                  max_num_tokens=max(cfg.max_num_batched_tokens, 8192))
         self.requests: dict[str, tuple] = {}
         self.lock = threading.Lock()
         self._inflight: dict | None = None
         self._last_done = 0.0
-        self.pipeline = cfg.pipeline and cfg.tp_size == 1
+        # pipelined decode on one GPU and under TP (the workers poll the shared-memory metadata ring and
+        # never synchronise: parallel/metaplane.py)
+        self.pipeline = cfg.pipeline
         self._profiler = None
         self._profile_left = int(os.environ.get("SYMMETRY_PROFILE_STEPS", "20"))
         self.profile_trace: str | None = None
@@ -247,7 +250,7 @@ class LLMEngine:
     def step(self) -> list[RequestOutput]:
         """One engine iteration; returns the outputs that completed in it.
 
-        Pipelined decode (single-GPU engines): step N+1 is scheduled and enqueued on the GPU before
+        Pipelined decode (single-GPU and TP engines): step N+1 is scheduled and enqueued on the GPU before
         step N's sampled ids are copied back -- its pending input tokens are gathered on the device
         from step N's output buffer -- and only then does the host wait for, detokenize and stream
         step N.  Host scheduling, detokenization and the provider's socket writes thus overlap the GPU,

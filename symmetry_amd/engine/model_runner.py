@@ -10,9 +10,12 @@
   block-table width and therefore the split-KV grid of decode attention, so
   short chats do not launch thousands of empty partition workgroups.  Padded
   rows write no cache (slot -1) and read only the reserved block 0.
-* Tensor parallel: rank 0 runs the scheduler; :meth:`execute` broadcasts the
-  packed metadata to the other ranks (R4) which replay the
-  same forward via :meth:`worker_loop`.
+* Tensor parallel: rank 0 runs the scheduler; :meth:`launch` sends the
+  packed metadata to the other ranks through the step-metadata plane (R4,
+  SURVEY.md §2.6; a shared-memory ring, ``parallel/metaplane.py``) and the
+  workers replay the same forward via :meth:`worker_loop` without ever
+  synchronising their stream, so the TP decode loop is pipelined like the
+  single-GPU one: every rank enqueues step N+1 while step N runs.
 """
 from __future__ import annotations
 
@@ -30,7 +33,7 @@ DECODE_BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 25
 MAX_DECODE_ROWS = 256  # dense single-GPU models (general path on the medium-M GEMM); others: FUSED_DECODE_ROWS
 FUSED_DECODE_ROWS = 64
 CTX_BUCKETS = (512, 2048, 8192, 32768, 131072)  # tokens (multiples of the 512-token attention partition)
-CMD_STOP, CMD_CAPTURE = -1, 2  # control headers of the rank-0 -> worker metadata plane
+CMD_STOP, CMD_CAPTURE, CMD_SYNC = -1, 2, 3  # control headers of the rank-0 -> worker metadata plane
 HEADER_LEN = 7  # kind, T, rows, max_blocks, prefill tiles, real seqs, filtered-sampling flag
 _SEED_MIX = 0x9E3779B97F4A7C15
 
@@ -99,7 +102,8 @@ class _Layout:
 
 class ModelRunner:
     def __init__(self, model: TransformerLM, kv: KVCache, max_num_seqs: int, max_model_len: int,
-                 use_graphs: bool = True, tp_group=None, tp_rank: int = 0, tp_size: int = 1, cpu_group=None):
+                 use_graphs: bool = True, tp_group=None, tp_rank: int = 0, tp_size: int = 1, cpu_group=None,
+                 max_num_tokens: int = 8192):
         self.model = model
         self.kv = kv
         self.device = model.device
@@ -121,6 +125,18 @@ class ModelRunner:
         self.step_counter = 0
         self._parity = 0
         self.timing = {"h2d": 0.0, "forward": 0.0, "d2h": 0.0, "steps": 0}
+        self.meta = None
+        if tp_size > 1:
+            from ..parallel.metaplane import make_metaplane
+
+            n = max(max_num_tokens, max_num_seqs)
+            nseq = max(max_num_seqs, 1)
+            ints = 4 * n + 12 * nseq + 2 * (n // 64 + nseq) + nseq * self.max_blocks + 64 + HEADER_LEN
+            self.meta = make_metaplane(cpu_group, tp_rank, tp_size, HEADER_LEN, 4 * (ints + ints // 4) + 4096)
+        self._wslots: list = []  # worker: ring of (pinned buffer, event) for the H2D copies in flight
+        self._wnext = 0
+        self._stop_sent = False
+        self.sync_times: list[float] = []  # worker: host times of rank 0's sync points
 
     # ------------------------------------------------------------------------------------------
     def _host(self, n: int, key: str) -> torch.Tensor:
@@ -385,39 +401,75 @@ class ModelRunner:
     # ------------------------------------------------------------------------------------------
     # tensor-parallel metadata plane (R4)
     def _broadcast(self, header: np.ndarray, host_t: torch.Tensor) -> None:
-        import torch.distributed as dist
-
-        h = torch.from_numpy(np.concatenate([header, [host_t.numel()]]).astype(np.int32))
-        dist.broadcast(h, src=0, group=self.cpu_group)
-        n = int(h[-1])
-        dist.broadcast(host_t[:n].contiguous() if n else torch.zeros(1, dtype=torch.int32), src=0,
-                       group=self.cpu_group)
+        self.meta.send(header, host_t.numpy() if host_t.numel() else None)
 
     def broadcast_stop(self) -> None:
-        if self.tp_size > 1:
-            import torch.distributed as dist
+        if self.tp_size > 1 and self.meta is not None and self.tp_rank == 0 and not self._stop_sent:
+            self._stop_sent = True
+            self.meta.send(np.array([CMD_STOP] + [0] * (HEADER_LEN - 1), dtype=np.int32), None)
+            self.meta.close()
 
-            h = torch.tensor([CMD_STOP] + [0] * HEADER_LEN, dtype=torch.int32)
-            dist.broadcast(h, src=0, group=self.cpu_group)
-
-    def worker_loop(self) -> None:
-        """Ranks 1..tp-1: mirror rank 0's steps until it broadcasts stop."""
+    def sync_point(self) -> float:
+        """Every rank's GPU idle + a barrier over the bootstrap group; returns this rank's host time.  Under
+        TP rank 0 sends CMD_SYNC so the workers (in :meth:`worker_loop`) meet it (bench timing brackets)."""
         import torch.distributed as dist
 
+        if self.tp_size > 1 and self.tp_rank == 0:
+            self.meta.send(np.array([CMD_SYNC] + [0] * (HEADER_LEN - 1), dtype=np.int32), None)
+        if self.is_gpu:
+            torch.cuda.synchronize()
+        if self.tp_size > 1:
+            dist.barrier(group=self.cpu_group)
+        if self.is_gpu:
+            torch.cuda.synchronize()
+        return time.perf_counter()
+
+    WORKER_SLOTS = 4  # pinned metadata buffers a worker cycles through (H2D copies still in flight)
+
+    def _worker_host(self, n: int) -> torch.Tensor:
+        """A pinned buffer whose previous H2D copy (WORKER_SLOTS steps ago) has completed."""
+        if not self._wslots:
+            self._wslots = [[None, None] for _ in range(self.WORKER_SLOTS)]
+        slot = self._wslots[self._wnext]
+        self._wnext = (self._wnext + 1) % self.WORKER_SLOTS
+        if slot[1] is not None:
+            slot[1].synchronize()  # normally long done: the GPU is at most a step or two behind
+        if slot[0] is None or slot[0].numel() < n:
+            slot[0] = torch.empty(max(n, 1024), dtype=torch.int32, pin_memory=self.is_gpu)
+        self._wslot = slot
+        return slot[0][:n]
+
+    def worker_loop(self) -> None:
+        """Ranks 1..tp-1: mirror rank 0's steps until it sends stop.  Never synchronises the stream: the
+        next step's metadata is popped and enqueued while the GPU still runs this one (the xGMI
+        collectives keep the ranks in step on the device).  A collective that gave up waiting for a peer
+        (the communicator's host-mapped error word) ends the worker with an error: its partial sums would
+        be garbage."""
+        check = getattr(self.model.tp, "error", None)
         while True:
-            h = torch.zeros(HEADER_LEN + 1, dtype=torch.int32)
-            dist.broadcast(h, src=0, group=self.cpu_group)
-            header = h.numpy()
+            msg = self.meta.recv()
+            if msg is None:
+                return
+            header, payload = msg
             if header[0] == CMD_STOP:
                 return
-            n = int(header[HEADER_LEN])
-            host_t = self._host(max(n, 1), "worker")
-            buf = torch.zeros(max(n, 1), dtype=torch.int32)
-            dist.broadcast(buf, src=0, group=self.cpu_group)
-            host_t.copy_(buf)
+            if header[0] == CMD_SYNC:
+                self.sync_times.append(self.sync_point())
+                continue
+            n = int(payload.size)
+            host_t = self._worker_host(max(n, 1))
+            if n:
+                host_t.numpy()[:n] = payload
             if header[0] == CMD_CAPTURE:
                 self._capture(int(header[1]), int(header[3]), bool(header[6]))
                 continue
             self._run(header[:HEADER_LEN], host_t)
             if self.is_gpu:
-                torch.cuda.current_stream().synchronize()
+                ev = torch.cuda.Event()
+                ev.record()
+                self._wslot[1] = ev
+            if not self.is_gpu:
+                continue
+            err = check() if check is not None else 0
+            if err:
+                raise RuntimeError(f"TP rank {self.tp_rank}: xGMI collective timed out waiting for rank {err - 1}")

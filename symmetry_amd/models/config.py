@@ -90,6 +90,10 @@ TINY_LLAMA = ModelConfig(
     num_kv_heads=2, rope_theta=10000.0, max_position=2048, bos_token_id=500, eos_token_ids=(501, 502),
 )
 TINY_MIXTRAL = TINY_LLAMA.replace(name="tiny-mixtral", num_experts=4, top_k=2)
+# 8 KV heads like Llama-3-70B / Mixtral: TP=8 leaves one KV head (and two q heads) per rank, the 70B TP=8
+# shard geometry; the MoE variant has 8 experts, one per rank at EP=8
+TINY_LLAMA_KV8 = TINY_LLAMA.replace(name="tiny-llama-kv8", num_heads=16, num_kv_heads=8, intermediate_size=2048)
+TINY_MIXTRAL_E8 = TINY_LLAMA_KV8.replace(name="tiny-mixtral-e8", num_experts=8, top_k=2)
 SMALL_LLAMA = ModelConfig(
     name="small-llama", vocab_size=32768, hidden_size=1024, intermediate_size=3584, num_layers=4, num_heads=8,
     num_kv_heads=2, max_position=8192, bos_token_id=32000, eos_token_ids=(32001, 32002),
@@ -97,7 +101,8 @@ SMALL_LLAMA = ModelConfig(
 
 _REGISTRY = {
     c.name: c
-    for c in (LLAMA3_8B, LLAMA31_8B, LLAMA3_70B, LLAMA31_70B, MIXTRAL_8X7B, TINY_LLAMA, TINY_MIXTRAL, SMALL_LLAMA)
+    for c in (LLAMA3_8B, LLAMA31_8B, LLAMA3_70B, LLAMA31_70B, MIXTRAL_8X7B, TINY_LLAMA, TINY_MIXTRAL, SMALL_LLAMA,
+              TINY_LLAMA_KV8, TINY_MIXTRAL_E8)
 }
 _ALIASES = {
     "llama3": "llama3:8b",

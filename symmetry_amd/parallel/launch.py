@@ -22,6 +22,8 @@ def init_distributed(backend: str | None = None) -> tuple[int, int, int]:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        local = local % torch.cuda.device_count()  # several ranks per GPU: host-staged rehearsal
     if world > 1 and not dist.is_initialized():
         if torch.cuda.is_available():
             torch.cuda.set_device(local)
@@ -36,17 +38,24 @@ def make_comms(on_gpu: bool, device=None):
     """TP/EP communicator + the gloo metadata group.  ``SYMMETRY_TP_COMM=gloo`` on GPUs selects the
     host-staged communicator (ranks sharing one GPU for kernel checks; no hipGraphs).  On GPUs the
     decode-sized all-reduces run on the one-shot xGMI kernel (:class:`XgmiComm`) unless
-    ``SYMMETRY_XGMI=0``; ``SYMMETRY_XGMI_SLOT`` sets its per-rank slot (bytes, default 4 MiB)."""
+    ``SYMMETRY_XGMI=0``; ``SYMMETRY_XGMI_SLOT`` sets its per-rank slot (bytes, default 4 MiB).
+
+    Over the host-staged communicator the xGMI kernels are opt-in (``SYMMETRY_XGMI=1``): ranks sharing one
+    GPU only make progress if their spinning kernels are co-resident, which separate processes do not
+    guarantee (a miss costs the kernel's 2 s wait limit, then an error).  ``SYMMETRY_XGMI_GRAPHS=1``
+    additionally lets such a rehearsal capture decode hipGraphs (every decode collective then runs on the
+    xGMI kernels; a host-staged fallback inside a capture fails loudly)."""
     cpu_group = dist.new_group(backend="gloo")
     if not on_gpu:
         return TorchComm(cpu_group), cpu_group
-    if os.environ.get("SYMMETRY_TP_COMM", "rccl").lower() == "gloo":
-        comm = HostStagedComm(cpu_group)
-    else:
-        comm = RcclComm(bootstrap_group=cpu_group)
-    if os.environ.get("SYMMETRY_XGMI", "1") != "0" and 1 < comm.world <= 8:
+    staged = os.environ.get("SYMMETRY_TP_COMM", "rccl").lower() == "gloo"
+    comm = HostStagedComm(cpu_group) if staged else RcclComm(bootstrap_group=cpu_group)
+    want = os.environ.get("SYMMETRY_XGMI", "auto")
+    if (want == "1" or (want == "auto" and not staged)) and 1 < comm.world <= 8:
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         comm = XgmiComm(comm, cpu_group, dev, int(os.environ.get("SYMMETRY_XGMI_SLOT", 4 << 20)))
+        if staged and os.environ.get("SYMMETRY_XGMI_GRAPHS", "0") == "1":
+            comm.capturable = True
     return comm, cpu_group
 
 

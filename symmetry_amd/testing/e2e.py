@@ -1,0 +1,151 @@
+"""Client-end measurement of the BASELINE.json metric: streamed tokens/s + p50 TTFT per client, read on
+the clients' swarm sockets ("per-client streamed tok/s over the swarm socket, p50 TTFT from
+the ``inference`` write to the first content event").
+
+Process layout (everything on 127.0.0.1):
+  * this process: discovery node + Symmetry server + the provider node (``symmetry-cli`` equivalent, native
+    backend on the given, already warmed-up engine -- under TP, rank 0's engine with the workers mirroring);
+  * a separate client process: C Symmetry clients, each ``requestProvider`` (model-based assignment by the
+    server), join the provider's topic (Noise XX + secretstream), send ``newConversation`` + ``inference``,
+    then read the ``symmetryEmitterKey`` header, one SSE event per token and ``inferenceEnded``
+    (the reference's stream shape, ``/root/reference/src/provider.ts:234-262``).
+
+Per client: TTFT = ``inference`` write -> first content delta on the client's socket; tokens/s =
+(content events - 1) / (last event - first event).  Used by ``bench.py`` (its ``client_end`` fields) and
+``bench/e2e.py``.
+"""
+from __future__ import annotations
+
+import asyncio
+import multiprocessing as mp
+import os
+import statistics
+import tempfile
+import time
+
+# chat-template tokens around a single user message (byte tokenizer, llama3 format): begin, header(user),
+# "\n\n" + content, eot, header(assistant) "\n\n"
+_TEMPLATE_TOKENS = 23
+
+
+def prompt_text(i: int, tokens: int) -> str:
+    """ASCII user content that makes a ``tokens``-token chat prompt under the byte tokenizer."""
+    n = max(1, tokens - _TEMPLATE_TOKENS)
+    base = "".join(chr(0x61 + (i * 7 + k * 13) % 26) if (k + i) % 6 else " " for k in range(n))
+    return base[:n]
+
+
+def _client_proc(boot, server_key, model, n, prompt_tokens, max_tokens, out_q, start_evt):
+    async def one(i):
+        from symmetry_amd.testing.mock_client import SymmetryClient
+
+        c = SymmetryClient(boot, server_key)
+        await c.start()
+        try:
+            det = await c.request_provider(model)
+            conn = await c.connect_provider(det["discoveryKey"])
+            await ready.wait()
+            r = await c.chat(conn, [{"role": "user", "content": prompt_text(i, prompt_tokens)}],
+                             extra={"max_tokens": max_tokens, "ignore_eos": True, "temperature": 0.0},
+                             timeout=600)
+            return {"ttft_ms": None if r.ttft_s is None else r.ttft_s * 1e3, "tokens_per_s": r.tokens_per_s,
+                    "events": r.content_events, "ended": r.ended, "error": r.error,
+                    "wall_s": r.t_end - r.t_start}
+        finally:
+            await c.stop()
+
+    async def main():
+        nonlocal ready
+        ready = asyncio.Event()
+        tasks = [asyncio.create_task(one(i)) for i in range(n)]
+        # every client has its provider connection before any sends: all requests arrive together
+        await asyncio.to_thread(start_evt.wait)
+        await asyncio.sleep(0.2)
+        ready.set()
+        return await asyncio.gather(*tasks)
+
+    ready = None
+    try:
+        out_q.put(asyncio.run(main()))
+    except Exception as exc:  # report, never hang the parent
+        import traceback
+
+        out_q.put(f"client process failed: {exc}\n{traceback.format_exc()}")
+
+
+async def client_end_run(engine, model: str, clients: int, prompt_tokens: int = 128, max_tokens: int = 256,
+                         data_collection: bool = False, public: bool = True, timeout: float = 600.0) -> dict:
+    """Serve ``engine`` as a provider and measure ``clients`` concurrent streamed chats at the client end."""
+    import yaml
+
+    from ..backends.native import NativeBackend
+    from ..net import DiscoveryServer
+    from ..provider.node import SymmetryProvider
+    from .mock_server import SymmetryServer
+
+    ds = DiscoveryServer()
+    await ds.start()
+    boot = [ds.address]
+    server = SymmetryServer(bootstrap=boot, ping_interval=5.0)
+    await server.start()
+    tmp = tempfile.mkdtemp(prefix="symmetry-e2e-")
+    cfg = {"apiHostname": "127.0.0.1", "apiPath": "/v1/chat/completions", "apiPort": 0, "apiProtocol": "http",
+           "apiProvider": "native", "dataCollectionEnabled": bool(data_collection),
+           "maxConnections": clients, "modelName": model, "name": "e2e-provider",
+           "path": os.path.join(tmp, "data"), "public": bool(public), "serverKey": server.server_key,
+           "metricsInterval": 0}
+    path = os.path.join(tmp, "provider.yaml")
+    with open(path, "w") as f:
+        yaml.safe_dump(cfg, f)
+    provider = SymmetryProvider(path, backend=NativeBackend(cfg, engine=engine), bootstrap=boot)
+    await provider.init()
+    for _ in range(200):
+        if server.providers(model):
+            break
+        await asyncio.sleep(0.05)
+    ctx = mp.get_context("spawn")
+    q, start_evt = ctx.Queue(), ctx.Event()
+    p = ctx.Process(target=_client_proc, args=(boot, server.server_key, model, clients, prompt_tokens,
+                                               max_tokens, q, start_evt), daemon=True)
+    p.start()
+    try:
+        await asyncio.sleep(0.5)
+        engine.metrics = type(engine.metrics)()
+        t1 = time.perf_counter()
+        start_evt.set()
+        res = await asyncio.wait_for(asyncio.to_thread(q.get), timeout)
+        wall = time.perf_counter() - t1
+    finally:
+        p.join(30)
+        if p.is_alive():
+            p.kill()
+        stats = provider.stats()
+        saved = len(provider.saved_files)
+        # the provider's backend stop would shut the engine down: detach it (the caller owns the engine)
+        backend = provider.backend
+        if getattr(backend, "aengine", None) is not None:
+            ae, backend.aengine = backend.aengine, None
+            ae._stop = True
+            ae._wake.set()
+            if ae._started:
+                await asyncio.to_thread(ae._thread.join, 10)
+        await provider.destroy()
+        await server.stop()
+        await ds.stop()
+    if isinstance(res, str):
+        raise RuntimeError(res)
+    ttfts = sorted(r["ttft_ms"] for r in res if r["ttft_ms"] is not None)
+    tps = [r["tokens_per_s"] for r in res]
+    total_events = sum(r["events"] for r in res)
+    return {
+        "clients": clients, "prompt_tokens": prompt_tokens, "max_tokens": max_tokens,
+        "p50_ttft_ms": round(statistics.median(ttfts), 2) if ttfts else None,
+        "p90_ttft_ms": round(ttfts[int(0.9 * (len(ttfts) - 1))], 2) if ttfts else None,
+        "per_client_tokens_per_s_median": round(statistics.median(tps), 2) if tps else None,
+        "per_client_tokens_per_s_min": round(min(tps), 2) if tps else None,
+        "aggregate_tokens_per_s": round(total_events / wall, 2),
+        "all_ended": all(r["ended"] and not r["error"] for r in res),
+        "content_events": total_events,
+        "data_collection_files": saved,
+        "engine": {k: stats.get(k) for k in ("mean_decode_batch", "p50_itl_ms", "decode_steps", "step_phase_ms")},
+    }

@@ -1,5 +1,6 @@
 """bench.py contract (driver-facing): one JSON line from rank 0 with the BASELINE metric, whole-job value,
-max-over-ranks timing; single process and a 2-rank torchrun (gloo on CPU, tiny model)."""
+max-over-ranks timing; single process, a 2-rank torchrun in the default tensor-parallel mode (one provider
+over both ranks, strong scaling) and in data-parallel mode (gloo on CPU, tiny model)."""
 import json
 import os
 import socket
@@ -7,8 +8,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ARGS = ["--model", "tiny-llama", "--steps", "3", "--warmup", "1", "--clients", "2", "--prompt-len", "16",
-        "--max-model-len", "128"]
+ARGS = ["--model", "tiny-llama", "--steps", "3", "--warmup", "1", "--clients", "2", "--prompt-len", "32",
+        "--max-model-len", "128", "--client-tokens", "8"]
 
 
 def _free_port():
@@ -26,22 +27,36 @@ def _run(cmd):
     return json.loads(lines[0])
 
 
-def _check(r, n):
+def _check(r, n, mode):
     assert r["metric"].startswith("streamed tokens/sec + p50 TTFT per client")
     assert r["n_gpus"] == n and r["steps"] == 3 and r["warmup"] == 1
-    assert r["higher_is_better"] is True and r["scaling"] == "weak" and r["dtype"] == "bf16"
-    assert r["config"]["parallelism"] == f"dp{n}" and r["config"]["global_batch"] == 2 * n
-    assert r["value"] > 0 and r["ms_per_step"] > 0 and r["p50_ttft_ms"] > 0
-    assert 0 < r["mean_ttft_ms"] <= r["max_ttft_ms"] and r["p50_ttft_ms"] <= r["max_ttft_ms"]
-    # whole-job aggregate = world * clients * (1000 / ms_per_step)
-    assert abs(r["value"] - n * 2 * 1e3 / r["ms_per_step"]) / r["value"] < 0.01
+    assert r["higher_is_better"] is True and r["dtype"] == "bf16"
+    assert r["scaling"] == ("strong" if mode == "tp" and n > 1 else "weak")
+    clients = 2 * n if mode == "dp" else 2
+    assert r["config"]["parallelism"] == f"{mode}{n}" and r["config"]["global_batch"] == clients
+    assert r["value"] > 0 and r["ms_per_step"] > 0
+    assert 0 < r["engine_mean_ttft_ms"] <= r["engine_max_ttft_ms"]
+    assert r["engine_p50_ttft_ms"] <= r["engine_max_ttft_ms"]
+    # whole-job aggregate = clients * (1000 / ms_per_step)
+    assert abs(r["value"] - clients * 1e3 / r["ms_per_step"]) / r["value"] < 0.01
+    # the client-end run: every client streamed over the swarm and got its inferenceEnded
+    ce = r["client_end"]
+    assert ce["all_ended"] and ce["clients"] == 2 and ce["p50_ttft_ms"] > 0, ce
+    assert r["p50_ttft_ms"] == ce["p50_ttft_ms"] and r["client_end_per_client_tokens_per_s"] > 0
 
 
 def test_bench_single_process():
-    _check(_run([sys.executable, "bench.py", "--gpus", "1"] + ARGS), 1)
+    _check(_run([sys.executable, "bench.py", "--gpus", "1"] + ARGS), 1, "dp")
 
 
-def test_bench_torchrun_two_ranks():
+def test_bench_torchrun_two_ranks_tp():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2"] + ARGS
-    _check(_run(cmd), 2)
+    _check(_run(cmd), 2, "tp")
+
+
+def test_bench_torchrun_two_ranks_dp():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--parallel", "dp"] + ARGS
+    _check(_run(cmd), 2, "dp")

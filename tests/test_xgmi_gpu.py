@@ -22,13 +22,15 @@ def _comms(ops, world, slot_bytes=1 << 20):
     return hs
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("n", [4096, 8 * 3001, 262144])
 def test_xgmi_all_reduce(gpu, world, dtype, n):
     from symmetry_amd.ops import _native
 
     ops = _native.ops()
+    if world * -(-n // 1024) > 1024:
+        pytest.skip("the grid slices of one launch would not all be co-resident")
     hs = _comms(ops, world)
     g = torch.Generator(device="cpu").manual_seed(n + world)
     try:
@@ -49,7 +51,7 @@ def test_xgmi_all_reduce(gpu, world, dtype, n):
             ops.xgmi_destroy(h)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("T,d,P", [(1, 4096, 8), (4, 8192, 8), (10, 4096, 1), (64, 4096, 4)])
 def test_xgmi_add_prep(gpu, world, T, d, P):
     from symmetry_amd.ops import _native, reference
@@ -139,3 +141,62 @@ def test_xgmi_rejects_oversized_and_bad_shapes(gpu):
         assert ids.tolist() == [0, 7, 14, 21, 28] and ops.xgmi_error(h) == 0
     finally:
         ops.xgmi_destroy(h)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_xgmi_mixed_geometry_with_slow_rank(gpu, world):
+    """The decode sequence of a TP layer stack, every collective with a different workgroup split of the same
+    slot bytes -- add_prep with 8 parts per row, add_prep with 4 parts, the sampling keys (one workgroup at
+    byte 0), a plain chunked all-reduce -- repeated, with one rank's slice held back 50 us before it pushes
+    (rotating).  The per-communicator collective counter keeps every collective on its own slot parity
+    whatever the split (the per-workgroup epochs of round 2 could alias them); results are bit-exact."""
+    from symmetry_amd.ops import _native, reference
+
+    ops = _native.ops()
+    d = 4096
+    hs = _comms(ops, world, slot_bytes=24 * d * 4 + 256)
+    g = torch.Generator(device="cpu").manual_seed(world)
+    w = (torch.rand(d, generator=g) + 0.5).to(gpu, torch.bfloat16)
+    try:
+        for it in range(4):
+            slow = it % world
+            for T, P in ((4, 8), (24, 4)):
+                ys = [torch.randn(T, d, generator=g).to(gpu) for _ in range(world)]
+                r0 = torch.randn(T, d, generator=g).to(gpu)
+                resids = [r0.clone() for _ in range(world)]
+                xws = [torch.empty(T, d, dtype=torch.bfloat16, device=gpu) for _ in range(world)]
+                sss = [torch.empty(T, P, dtype=torch.float32, device=gpu) for _ in range(world)]
+                ops.xgmi_add_prep_multi(ys, resids, w, xws, sss, hs, slow, 50)
+                ysum = torch.zeros(T, d, device=gpu)
+                for y in ys:
+                    ysum += y
+                r_ref, xw_ref, ss_ref = r0.clone(), torch.empty_like(xws[0]), torch.empty_like(sss[0])
+                reference.add_prep(ysum, r_ref, w, xw_ref, ss_ref)
+                torch.cuda.synchronize()
+                for r in range(world):
+                    torch.testing.assert_close(resids[r], r_ref, rtol=0, atol=0)
+                    assert torch.equal(resids[r], resids[0]) and torch.equal(sss[r], sss[0])
+            B = 10
+            vals = [torch.randint(0, 1 << 30, (B,), generator=g) for _ in range(world)]
+            idx = [torch.randint(0, 1 << 20, (B,), generator=g) for _ in range(world)]
+            keys = [((v << 32) | (0xFFFFFFFF - i)).to(gpu) for v, i in zip(vals, idx)]
+            ids = [torch.full((B,), -1, dtype=torch.int32, device=gpu) for _ in range(world)]
+            ops.xgmi_keys_max_multi(keys, ids, hs, (slow + 1) % world, 50)
+            stacked = torch.stack([k.cpu() for k in keys])
+            best = stacked.max(0).values
+            expect = (0xFFFFFFFF - (best & 0xFFFFFFFF)).to(torch.int32)
+            n = 32 * 1024
+            xs = [torch.randn(n, generator=g).to(gpu) for _ in range(world)]
+            outs = [torch.empty_like(x) for x in xs]
+            ops.xgmi_all_reduce_multi(xs, outs, hs, slow, 50)
+            ref = torch.zeros(n, device=gpu)
+            for x in xs:
+                ref += x
+            torch.cuda.synchronize()
+            for r in range(world):
+                assert ops.xgmi_error(hs[r]) == 0
+                assert torch.equal(ids[r].cpu(), expect), (it, r)
+                torch.testing.assert_close(outs[r], ref, rtol=0, atol=0)
+    finally:
+        for h in hs:
+            ops.xgmi_destroy(h)
