@@ -348,8 +348,91 @@ void moe_route_permute(const Tensor& logits, const Tensor& x, int64_t k, int64_t
   TORCH_CHECK(ld >= E, "moe: logits narrower than E");
   launch_moe_route(linout(logits, T, ld, "logits"), (int)ld, (int)T, (int)E, (int)k, ptr<int>(ids), ptr<float>(w), s);
   launch_moe_align(ptr<int>(ids), (int)(T * k), (int)E, ptr<int>(counts), ptr<int>(offsets), ptr<int>(cursor), s);
-  launch_moe_scatter(ptr<bf16>(x), (int)T, (int)d, (int)k, ptr<int>(ids), ptr<int>(offsets), ptr<int>(cursor),
-                     ptr<bf16>(xs), ptr<int>(dst), nullptr, s);
+  launch_moe_scatter(ptr<bf16>(x), (int)T, (int)d, (int)k, (int)E, ptr<int>(ids), ptr<int>(offsets), ptr<int>(cursor),
+                     ptr<bf16>(xs), (int)(T * k), ptr<int>(dst), nullptr, s);
+}
+
+// Routing only: logits LinOut [T][E] -> top-k ids [T*k] + softmax-renormalised weights [T*k].
+void moe_route(const Tensor& logits, int64_t T, int64_t k, int64_t E, Tensor& ids, Tensor& w) {
+  check_gpu(ids, "ids");
+  check_dtype(ids, at::kInt, "ids");
+  check_gpu(w, "w");
+  check_dtype(w, at::kFloat, "w");
+  TORCH_CHECK(E >= 1 && E <= 64 && k >= 1 && k <= 8 && k <= E, "moe_route: need 1 <= k <= E <= 64, k <= 8");
+  TORCH_CHECK(ids.numel() >= T * k && w.numel() >= T * k, "moe_route: outputs too small");
+  const int64_t ld = logits.size(logits.dim() - 1);
+  TORCH_CHECK(ld >= E, "moe_route: logits narrower than E");
+  const at::OptionalDeviceGuard g(ids.device());
+  launch_moe_route(linout(logits, T, ld, "logits"), (int)ld, (int)T, (int)E, (int)k, ptr<int>(ids), ptr<float>(w),
+                   cur_stream(ids));
+}
+
+// Segment ids into groups: counts [G] + offsets [G+1] (exclusive prefix sum) + cursor [G] zeroed, from
+// ids [n] (ids outside [0, G) ignored).
+void moe_align(const Tensor& ids, int64_t G, Tensor& counts, Tensor& offsets, Tensor& cursor) {
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&ids, &counts, &offsets, &cursor}) {
+    check_gpu(*t, "moe_align tensor");
+    check_dtype(*t, at::kInt, "moe_align tensor");
+  }
+  TORCH_CHECK(G >= 1 && G <= 64 && counts.numel() >= G && offsets.numel() >= G + 1 && cursor.numel() >= G,
+              "moe_align: 1 <= G <= 64 groups");
+  const at::OptionalDeviceGuard g(ids.device());
+  launch_moe_align(ptr<int>(ids), (int)ids.numel(), (int)G, ptr<int>(counts), ptr<int>(offsets), ptr<int>(cursor),
+                   cur_stream(ids));
+}
+
+// Row scatter into group segments: for assignment a = t * k + j with group g = ids[a] in [0, G):
+// row = offsets[g] + (running count of g); xs[row] = x[t]; dst[a] = row (src_tok[row] = t if given).
+// Assignments with g outside [0, G) are skipped (dst[a] left as is).  cursor [G] must be zero; the
+// segments may be any fixed starts (e.g. one capacity block per destination rank), rows past xs are dropped.
+void moe_scatter(const Tensor& x, const Tensor& ids, int64_t k, int64_t G, const Tensor& offsets, Tensor& cursor,
+                 Tensor& xs, Tensor& dst, const c10::optional<Tensor>& src_tok) {
+  check_gpu(x, "x");
+  check_dtype(x, at::kBFloat16, "x");
+  check_gpu(xs, "xs");
+  check_dtype(xs, at::kBFloat16, "xs");
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&ids, &offsets, &cursor, &dst}) {
+    check_gpu(*t, "moe_scatter index");
+    check_dtype(*t, at::kInt, "moe_scatter index");
+  }
+  TORCH_CHECK(x.dim() == 2 && xs.dim() == 2 && xs.size(1) == x.size(1), "moe_scatter: x [T, d], xs [R, d]");
+  const int64_t T = x.size(0), d = x.size(1);
+  TORCH_CHECK(d % 8 == 0 && k >= 1 && ids.numel() >= T * k && dst.numel() >= T * k, "moe_scatter: shapes");
+  TORCH_CHECK(G >= 1 && offsets.numel() >= G + 1 && cursor.numel() >= G, "moe_scatter: offsets / cursor");
+  int* st = nullptr;
+  if (src_tok.has_value()) {
+    check_gpu(*src_tok, "src_tok");
+    check_dtype(*src_tok, at::kInt, "src_tok");
+    TORCH_CHECK(src_tok->numel() >= xs.size(0), "moe_scatter: src_tok too small");
+    st = ptr<int>(*src_tok);
+  }
+  const at::OptionalDeviceGuard g(x.device());
+  launch_moe_scatter(ptr<bf16>(x), (int)T, (int)d, (int)k, (int)G, ptr<int>(ids), ptr<int>(offsets), ptr<int>(cursor),
+                     ptr<bf16>(xs), (int)xs.size(0), ptr<int>(dst), st, cur_stream(x));
+}
+
+// Grouped MFMA GEMM over expert segments (any routed row count; segment bounds read on the device).
+// mode 0: y bf16 [R, N]; 1: y fp32 [R, N]; 2: SwiGLU, W [E, 2N, K] = [gate; up] rows, y = act bf16 [R, N].
+void grouped_gemm(const Tensor& xs, const Tensor& W, const Tensor& offsets, int64_t e0, Tensor& y, int64_t mode) {
+  check_gpu(xs, "xs");
+  check_gpu(W, "W");
+  check_gpu(offsets, "offsets");
+  check_gpu(y, "y");
+  check_dtype(xs, at::kBFloat16, "xs");
+  check_dtype(W, at::kBFloat16, "W");
+  check_dtype(offsets, at::kInt, "offsets");
+  check_dtype(y, mode == 1 ? at::kFloat : at::kBFloat16, "y");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "grouped_gemm: mode 0 (bf16), 1 (fp32), 2 (SwiGLU)");
+  TORCH_CHECK(W.dim() == 3 && xs.dim() == 2 && y.dim() == 2 && xs.is_contiguous() && W.is_contiguous() &&
+                  y.is_contiguous(), "grouped_gemm: W [E, N, K], xs [R, K], y [R, N], contiguous");
+  const int64_t E = W.size(0), K = W.size(2), R = xs.size(0);
+  const int64_t N = mode == 2 ? W.size(1) / 2 : W.size(1);
+  TORCH_CHECK(xs.size(1) == K && y.size(0) >= R && y.size(1) == N, "grouped_gemm: shape mismatch");
+  TORCH_CHECK(K % 64 == 0 && (mode == 2 ? N % 64 == 0 : N % 128 == 0), "grouped_gemm: K % 64, N % 128 (SwiGLU: F % 64)");
+  TORCH_CHECK(E >= 1 && E <= 64 && e0 >= 0 && offsets.numel() >= e0 + E + 1, "grouped_gemm: offsets must cover e0..e0+E");
+  const at::OptionalDeviceGuard g(xs.device());
+  launch_grouped_gemm(ptr<bf16>(xs), ptr<bf16>(W), ptr<int>(offsets), y.data_ptr(), (int)R, (int)E, (int)e0, (int)N,
+                      (int)K, (int)mode, cur_stream(xs));
 }
 
 void grouped_skinny(const Tensor& xs, const Tensor& W, const Tensor& offsets, int64_t e0, Tensor& y) {
@@ -869,6 +952,13 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("decode_gemm_variant(int v) -> ()", [](int64_t v) { set_decode_gemm_variant((int)v); });
   m.def("decode_gemm_nt(int on) -> ()", [](int64_t on) { set_decode_gemm_nt((int)on); });
   m.def("grouped_skinny(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y) -> ()", &grouped_skinny);
+  m.def("grouped_gemm(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y, int mode) -> ()", &grouped_gemm);
+  m.def("moe_route(Tensor logits, int T, int k, int E, Tensor(a!) ids, Tensor(b!) w) -> ()", &moe_route);
+  m.def("moe_align(Tensor ids, int G, Tensor(a!) counts, Tensor(b!) offsets, Tensor(c!) cursor) -> ()", &moe_align);
+  m.def(
+      "moe_scatter(Tensor x, Tensor ids, int k, int G, Tensor offsets, Tensor(a!) cursor, Tensor(b!) xs, Tensor(c!) dst, "
+      "Tensor(d!)? src_tok=None) -> ()",
+      &moe_scatter);
   m.def(
       "moe_combine(Tensor y, Tensor dst, Tensor ids, int e_lo, int e_hi, Tensor w, int k, Tensor(a!) out, "
       "bool accumulate) -> ()",

@@ -170,8 +170,10 @@ void launch_swiglu(LinOut gu, bf16* out, int T, int F, hipStream_t s, int interl
 // moe.hip
 void launch_moe_route(LinOut logits, int ld, int T, int E, int k, int* ids, float* w, hipStream_t s);
 void launch_moe_align(const int* ids, int n, int E, int* counts, int* offsets, int* cursor, hipStream_t s);
-void launch_moe_scatter(const bf16* x, int T, int d, int k, const int* ids, const int* offsets, int* cursor,
-                        bf16* xs, int* dst, int* src_tok, hipStream_t s);
+void launch_moe_scatter(const bf16* x, int T, int d, int k, int E, const int* ids, const int* offsets, int* cursor,
+                        bf16* xs, int R, int* dst, int* src_tok, hipStream_t s);
+void launch_grouped_gemm(const bf16* xs, const bf16* W, const int* offsets, void* y, int R, int E, int e0, int N,
+                         int K, int out, hipStream_t s);
 void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, float* y, int R, int E, int e0, int N,
                            int K, int S, hipStream_t s);
 void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_lo, int e_hi, const float* w, int T, int k,

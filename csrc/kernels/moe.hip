@@ -6,6 +6,10 @@
 //   grouped_skinny  Y[rows of expert e] = Xs[rows of e] . W[e]^T on MFMA, one weight tile per
 //                 workgroup, reading the segment bounds from device memory (graph-capturable,
 //                 no host sync); fp32 split-K slabs like the dense skinny GEMM
+//   grouped_gemm  the same for any number of routed rows (prefill): 128 x 128 MFMA tiles over the
+//                 concatenated expert segments, the tile -> (expert, row block) map computed on the
+//                 device from the segment offsets (no host sync, graph-capturable); optional fused
+//                 SwiGLU epilogue (gate and up columns of one tile meet through LDS)
 //   moe_combine   out[t] = sum_j w[t][j] * Y[dst[t][j]]  (fixed slot order -> deterministic)
 //
 // Rows inside an expert segment are placed by atomics (order varies run to run) but every row
@@ -83,14 +87,16 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__
   }
 }
 
-// one 256-thread block per (token, slot); cursor[E] zeroed by the op
-__global__ __launch_bounds__(256) void moe_scatter_kernel(const bf16* __restrict__ x, int d, int k, int R,
+// one 256-thread block per (token, slot); cursor[E] zeroed by the op.  Assignments with an expert id
+// outside [0, E) (empty slots of an expert-parallel receive buffer) are skipped.
+__global__ __launch_bounds__(256) void moe_scatter_kernel(const bf16* __restrict__ x, int d, int k, int R, int E,
                                                           const int* __restrict__ ids, const int* __restrict__ offsets,
                                                           int* __restrict__ cursor, bf16* __restrict__ xs,
                                                           int* __restrict__ dst, int* __restrict__ src_tok) {
   const int a = blockIdx.x;  // assignment t * k + j
   const int t = a / k;
   const int e = ids[a];
+  if (e < 0 || e >= E) return;
   __shared__ int row;
   if (threadIdx.x == 0) {
     row = offsets[e] + atomicAdd(&cursor[e], 1);
@@ -162,6 +168,172 @@ __global__ __launch_bounds__(256) void grouped_skinny_kernel(const bf16* __restr
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// Grouped GEMM for prefill-sized routed batches (K12): Y[rows of expert e] = Xs[rows of e] . W[e]^T.
+//
+// Tiles of 128 routed rows x 128 weight rows, BK = 64, 256 threads = 4 waves in a 2 x 2 grid of 64 x 64
+// wave tiles, v_mfma_f32_16x16x32_bf16 with the WEIGHT fragment as the A operand (a lane then holds four
+// consecutive output columns of one row: 16-B fp32 / 8-B bf16 stores).  Both operand tiles are staged
+// global -> LDS by LDS-DMA (global_load_lds_dwordx4, 16 B per lane, double-buffered: the next k-tile's
+// DMA overlaps this one's MFMAs); the LDS images are [128 rows][8 chunks of 16 B] with chunk
+// c stored at c ^ ((row >> 1) & 7) (pre-swizzled on the per-lane GLOBAL address, the LDS side of a DMA
+// being lane-linear), so the 16-row x 4-chunk fragment reads are bank-conflict free.
+//
+// Grid: x = weight-row tiles, y = an upper bound on the row tiles (ceil(R / 128) + experts); workgroup
+// (x, y) walks the device-side segment offsets to find which expert's which row block y is (or exits).
+// SWIGLU: weight rows are [gate (F) ; up (F)]; x-tile j covers output columns f = 64 j .. 64 j + 63 and
+// stages gate rows 64 j.. as tile rows 0-63 and up rows F + 64 j.. as rows 64-127, so waves wn = 0 / 1
+// hold gate / up of the same (row, f); the up waves hand theirs over through LDS and the gate waves store
+// act = bf16(silu(gate) * up) -- the [R, 2F] intermediate never exists.
+// OUT: 0 = bf16 Y, 1 = fp32 Y, 2 = SwiGLU act (bf16 [R][F]).
+// ---------------------------------------------------------------------------------------------------
+constexpr int GG_BM = 128, GG_BN = 128, GG_BK = 64, GG_THREADS = 256;
+constexpr int GG_TILE_BYTES = GG_BM * GG_BK * 2;  // 16 KB per operand tile
+
+SYM_DEV void gg_glds16(const bf16* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+SYM_DEV int gg_swz(int row) { return (row >> 1) & 7; }
+
+template <int OUT>
+__global__ __launch_bounds__(GG_THREADS, 2) void grouped_gemm_kernel(const bf16* __restrict__ xs,
+                                                                     const bf16* __restrict__ W,
+                                                                     const int* __restrict__ offsets,
+                                                                     void* __restrict__ y, int R, int N, int K,
+                                                                     int E, int e0) {
+  extern __shared__ __attribute__((aligned(16))) char gg_smem[];
+  // ---- which expert / row block is this workgroup (device-side segment walk, E <= 64)
+  int e = -1, rb = 0, r0 = 0, n_e = 0;
+  {
+    int cum = 0;
+    for (int i = 0; i < E; ++i) {
+      const int a = offsets[e0 + i], b = min(offsets[e0 + i + 1], R);
+      const int n = max(0, b - a);
+      const int t = (n + GG_BM - 1) / GG_BM;
+      if ((int)blockIdx.y < cum + t) {
+        e = i;
+        rb = blockIdx.y - cum;
+        r0 = a + rb * GG_BM;
+        n_e = min(GG_BM, b - r0);
+        break;
+      }
+      cum += t;
+    }
+  }
+  if (e < 0) return;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  // ---- DMA source addresses: wave w stages rows 8 (4 i + w) + lane / 8 of each 128-row tile, i = 0..3,
+  // chunk (lane & 7) of the LDS row <- global chunk (lane & 7) ^ swz(row)
+  const bf16* asrc[4];
+  const bf16* bsrc[4];
+  const long long Nw = OUT == 2 ? 2LL * N : N;  // weight rows per expert (SwiGLU: N = F output columns)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (4 * i + wid) + (lane >> 3);
+    const int ch = (lane & 7) ^ gg_swz(row);
+    const int m = r0 + min(row, n_e - 1);  // rows past the segment re-read its last row (never stored)
+    asrc[i] = xs + (long long)m * K + 8 * ch;
+    long long wrow;
+    if constexpr (OUT == 2) wrow = row < 64 ? 64LL * blockIdx.x + row : (long long)N + 64LL * blockIdx.x + (row - 64);
+    else wrow = (long long)GG_BN * blockIdx.x + row;
+    bsrc[i] = W + (long long)e * Nw * K + wrow * K + 8 * ch;  // W holds the local experts only
+  }
+  auto stage = [&](int kt, int buf) {
+    char* base = gg_smem + buf * 2 * GG_TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      gg_glds16(asrc[i] + kt * GG_BK, base + (4 * i + wid) * 1024);
+      gg_glds16(bsrc[i] + kt * GG_BK, base + GG_TILE_BYTES + (4 * i + wid) * 1024);
+    }
+  };
+  f32x4 acc[4][4];  // [n subtile][m subtile]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int r16 = lane & 15, h = lane >> 4;
+  const int nk = K / GG_BK;
+  stage(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // tile kt landed for every wave; every wave finished reading buffer (kt + 1) & 1
+    if (kt + 1 < nk) stage(kt + 1, (kt + 1) & 1);
+    const char* A = gg_smem + (kt & 1) * 2 * GG_TILE_BYTES;  // routed rows
+    const char* B = A + GG_TILE_BYTES;                        // weight rows
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = 4 * ks + h;  // 16-B chunk of the fragment (k = 32 ks + 8 h ..)
+      Pack8 bf[4], af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 64 * wn + 16 * i + r16;
+        bf[i].u = *reinterpret_cast<const uint4*>(B + row * 128 + 16 * (c ^ gg_swz(row)));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = 64 * wm + 16 * j + r16;
+        af[j].u = *reinterpret_cast<const uint4*>(A + row * 128 + 16 * (c ^ gg_swz(row)));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bf[i].v, af[j].v, acc[i][j]);
+    }
+  }
+  // ---- epilogue: lane (r16, h) of acc[i][j] holds output row m = 64 wm + 16 j + r16, weight columns
+  // 64 wn + 16 i + 4 h .. + 3 of the tile
+  if constexpr (OUT == 2) {
+    __syncthreads();  // staging buffers are free: the up waves hand over their accumulators
+    f32x4* xch = reinterpret_cast<f32x4*>(gg_smem);
+    if (wn == 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xch[((wm * 4 + i) * 4 + j) * 64 + lane] = acc[i][j];
+    }
+    __syncthreads();
+    if (wn == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = 64 * wm + 16 * j + r16;
+        if (m >= n_e) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f32x4 u = xch[((wm * 4 + i) * 4 + j) * 64 + lane];
+          const f32x4 g = acc[i][j];
+          float o[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = g[q] / (1.f + __expf(-g[q])) * u[q];
+          bf16* yp = reinterpret_cast<bf16*>(y) + (long long)(r0 + m) * N + 64 * blockIdx.x + 16 * i + 4 * h;
+          bf16x4 pk = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+          *reinterpret_cast<bf16x4*>(yp) = pk;
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = 64 * wm + 16 * j + r16;
+      if (m >= n_e) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long long off = (long long)(r0 + m) * N + GG_BN * blockIdx.x + 64 * wn + 16 * i + 4 * h;
+        const f32x4 v = acc[i][j];
+        if constexpr (OUT == 1) {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(y) + off) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          bf16x4 pk = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(y) + off) = pk;
+        }
+      }
+    }
+  }
+}
+
 // out[t] (fp32 [T][d]) = sum_j w[t][j] * y[dst[t][j]] over assignments whose expert is in
 // [e_lo, e_hi) (the experts this rank computed); y is a LinOut over R rows
 __global__ __launch_bounds__(256) void moe_combine_kernel(LinOut y, int R, const int* __restrict__ dst,
@@ -203,10 +375,10 @@ void launch_moe_align(const int* ids, int n, int E, int* counts, int* offsets, i
   moe_align_kernel<<<1, 1024, 0, s>>>(ids, n, E, counts, offsets, cursor);
 }
 
-void launch_moe_scatter(const bf16* x, int T, int d, int k, const int* ids, const int* offsets, int* cursor,
-                        bf16* xs, int* dst, int* src_tok, hipStream_t s) {
+void launch_moe_scatter(const bf16* x, int T, int d, int k, int E, const int* ids, const int* offsets, int* cursor,
+                        bf16* xs, int R, int* dst, int* src_tok, hipStream_t s) {
   if (T == 0) return;
-  moe_scatter_kernel<<<T * k, 256, 0, s>>>(x, d, k, T * k, ids, offsets, cursor, xs, dst, src_tok);
+  moe_scatter_kernel<<<T * k, 256, 0, s>>>(x, d, k, R, E, ids, offsets, cursor, xs, dst, src_tok);
 }
 
 void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, float* y, int R, int E, int e0, int N,
@@ -214,6 +386,21 @@ void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, fl
   if (R == 0) return;
   dim3 grid(N / 16, E, S);
   grouped_skinny_kernel<<<grid, 256, 0, s>>>(xs, W, offsets, y, R, N, K, K / S, e0);
+}
+
+// out: 0 bf16 [R][N], 1 fp32 [R][N], 2 SwiGLU act bf16 [R][N] with W holding 2N rows per expert
+void launch_grouped_gemm(const bf16* xs, const bf16* W, const int* offsets, void* y, int R, int E, int e0, int N,
+                         int K, int out, hipStream_t s) {
+  if (R == 0) return;
+  const int ntile = out == 2 ? N / 64 : N / GG_BN;
+  const dim3 grid(ntile, (R + GG_BM - 1) / GG_BM + E);
+  const size_t lds = 4 * GG_TILE_BYTES;
+  if (out == 2)
+    grouped_gemm_kernel<2><<<grid, GG_THREADS, lds, s>>>(xs, W, offsets, y, R, N, K, E, e0);
+  else if (out == 1)
+    grouped_gemm_kernel<1><<<grid, GG_THREADS, lds, s>>>(xs, W, offsets, y, R, N, K, E, e0);
+  else
+    grouped_gemm_kernel<0><<<grid, GG_THREADS, lds, s>>>(xs, W, offsets, y, R, N, K, E, e0);
 }
 
 void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_lo, int e_hi, const float* w, int T, int k,

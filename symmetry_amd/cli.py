@@ -6,10 +6,12 @@ config ``~/.config/symmetry/provider.yaml``, ``--version`` prints ``1.0.0``
 ``--bootstrap host:port`` (discovery nodes; also ``bootstrap:`` in the YAML),
 ``--init`` (write the install script's default provider.yaml).
 
-Multi-GPU native providers (``tensorParallelSize > 1``) are launched one
-process per GPU, e.g. ``torchrun --nproc-per-node 8 -m symmetry_amd.cli -c
-provider.yaml``: rank 0 runs the provider node and the scheduler, the other
-ranks mirror its forward passes over RCCL.
+Multi-GPU native providers (``tensorParallelSize > 1``) run one process per
+GPU: plain ``symmetry-cli -c provider.yaml`` checks the visible GPUs and
+starts them as one ``torchrun`` child (or launch ``torchrun --nproc-per-node 8
+-m symmetry_amd.cli -c provider.yaml`` yourself): rank 0 runs the provider
+node and the scheduler, the other ranks mirror its forward passes (SURVEY.md
+§3.6).  A mismatch fails at start-up, before the provider announces itself.
 
 Data-parallel replicas on one node (SURVEY.md §2.5 "one provider process per
 GPU group"): ``symmetry-cli -c provider.yaml --replicas N`` (or ``replicas: N``
@@ -68,6 +70,10 @@ def _distributed_engine(cfg: ConfigManager):
     from .engine.llm_engine import EngineConfig
     from .parallel.launch import init_tp_engine
 
+    tp = int(cfg.get("tensorParallelSize") or 1)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if tp > 1 and tp != world:
+        raise SystemExit(f"Error: tensorParallelSize {tp} but the launcher started {world} ranks")
     ecfg = EngineConfig.from_provider(cfg.get_all())
     engine, rank = init_tp_engine(ecfg)
     _exit_when_orphaned()
@@ -167,6 +173,54 @@ def _launch_replicas(cfg: ConfigManager, config_path: str, replicas: int, bootst
     return max((abs(c) for c in codes), default=0)
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def tp_launch_plan(cfg: dict, config_path: str, bootstrap: str | None, port: int | None = None) -> list:
+    """argv of the torchrun child that runs a ``tensorParallelSize > 1`` provider started as a plain
+    ``symmetry-cli`` (one rank per GPU; rank 0 announces itself only once every shard is built)."""
+    tp = int(cfg.get("tensorParallelSize") or 1)
+    argv = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={tp}",
+            "--master-addr", "127.0.0.1", f"--master-port={port or _free_port()}", "-m", "symmetry_amd.cli",
+            "-c", config_path]
+    if bootstrap:
+        argv += ["--bootstrap", bootstrap]
+    return argv
+
+
+def _launch_tp(cfg: ConfigManager, config_path: str, bootstrap: str | None) -> int:
+    """``tensorParallelSize > 1`` outside torchrun: check the GPUs at start-up (the reference validates its
+    config before it goes online, ``src/config.ts:19-45``), then run the ranks as ONE torchrun child --
+    started before this process touches the GPU, never an exec -- and exit with its code."""
+    import subprocess
+
+    tp = int(cfg.get("tensorParallelSize") or 1)
+    if str(cfg.get("device", "auto")) != "cpu":
+        import torch  # device_count() does not initialise the GPU runtime on this stack
+
+        n = torch.cuda.device_count()
+        if n < tp:
+            print(f"Error: tensorParallelSize {tp} needs {tp} GPUs, {n} visible", file=sys.stderr)
+            return 1
+    p = subprocess.Popen(tp_launch_plan(cfg.get_all(), config_path, bootstrap))
+    try:
+        return abs(p.wait())
+    except KeyboardInterrupt:
+        import signal
+
+        p.send_signal(signal.SIGINT)
+        try:
+            return abs(p.wait(timeout=30))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            return abs(p.wait())
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="symmetry-cli", description="symmetry cli")
     ap.add_argument("-c", "--config", default=DEFAULT_CONFIG_PATH, help="Path to config file")
@@ -188,7 +242,10 @@ def main(argv=None) -> int:
     if replicas > 1 and REPLICA_ENV not in os.environ:
         return _launch_replicas(cfg, args.config, replicas, args.bootstrap)
     engine = None
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and cfg.is_native:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and cfg.is_native and int(cfg.get("tensorParallelSize") or 1) > 1:
+        return _launch_tp(cfg, args.config, args.bootstrap)
+    if world > 1 and cfg.is_native:
         engine = _distributed_engine(cfg)
     try:
         asyncio.run(_run_provider(cfg, args.bootstrap, engine))

@@ -113,6 +113,9 @@ _PROFILE_DIR = os.environ.get("SYMMETRY_PROFILE")
 class LLMEngine:
     def __init__(self, cfg: EngineConfig, tp_comm=None, ep_comm=None, cpu_group=None):
         self.cfg = cfg
+        if cfg.tp_size > 1 and tp_comm is None:
+            raise ValueError(f"tp_size {cfg.tp_size} needs a TP communicator: build TP engines with "
+                             "parallel.launch.init_tp_engine under torchrun (symmetry-cli starts it)")
         self.device = _pick_device(cfg.device)
         self.model_cfg = cfg.model_config or self._model_config(cfg)
         mcfg = self.model_cfg
@@ -183,8 +186,8 @@ class LLMEngine:
 
     def _graph_safe(self, tp_comm, ep_comm) -> bool:
         """Decode hipGraphs need every collective to be capturable (our RCCL communicator, or the xGMI
-        kernels over it) and no host-side data-dependent shapes (all-to-all expert dispatch reads counts
-        on the host)."""
+        kernels over it).  The MoE block reads nothing on the host (device-side segment offsets, fixed-
+        capacity expert all-to-all), whichever EP mode it runs."""
         from .. import ops
 
         if ops.torch_mode():  # eager torch baseline: host-synchronising reference ops
@@ -192,8 +195,6 @@ class LLMEngine:
         for c in (tp_comm, ep_comm):
             if c is not None and getattr(c, "world", 1) > 1 and not getattr(c, "capturable", False):
                 return False
-        if self.model.moe is not None and self.model.moe.ep > 1 and self.model.moe.mode != "allreduce":
-            return False
         return True
 
     def _auto_blocks(self, max_model_len: int) -> int:

@@ -259,6 +259,9 @@ class Scheduler:
         fresh = list(itertools.islice(self.waiting, max(0, self.cfg.max_num_seqs - len(self.running))))
         if len(fresh) < 4:
             return None
+        for s in fresh:  # prefix-cache hits first (take() would adopt them anyway): split uncached work
+            if not s.block_table and not s.num_computed:
+                self.blocks.match_prefix(s)
         lens = [s.prefill_target - s.num_computed for s in fresh]
         total = sum(lens)
         if total < min_tokens or total > self.cfg.max_num_batched_tokens:

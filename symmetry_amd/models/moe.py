@@ -1,32 +1,43 @@
 """Mixtral sparse-MoE block (K10-K12) with expert parallelism (R3).
 
-Routing, permutation into expert segments, the per-expert GEMMs and the
-weighted combine run as HIP kernels (``csrc/kernels/moe.hip``); small routed
-batches (<= 64 rows: every decode step) use the grouped skinny MFMA GEMM,
-which reads the segment bounds from device memory -- no host sync, so the
-decode step stays hipGraph-capturable.  Larger (prefill) batches read the
-segment offsets once and run one library GEMM per expert.
+Routing, permutation into expert segments, the per-expert GEMMs and the weighted combine run as HIP
+kernels (``csrc/kernels/moe.hip``) whose segment bounds live in device memory: no host sync anywhere in
+the block, so every step (decode and prefill, with or without expert parallelism) is hipGraph-capturable.
+Small routed batches (<= 64 rows: decode steps) use the grouped skinny MFMA GEMM; larger ones the grouped
+128 x 128 MFMA GEMM (``ops.grouped_gemm``) with SwiGLU fused into the gate/up epilogue.
 
-Expert parallelism, ``ep_size = N`` ranks each owning ``E/N`` experts:
+Expert parallelism, ``ep_size = N`` ranks each owning ``E / N`` experts (attention is tensor-parallel, so
+every rank holds the same T tokens when the block starts):
 
-* ``mode="allreduce"`` (with tensor-parallel attention: every rank holds the
-  same tokens) -- each rank applies only its own experts to all routed rows
-  and the partial outputs are summed with one all-reduce (graph-capturable);
-* ``mode="a2a"`` (with data-parallel attention: ranks hold different tokens)
-  -- tokens are dispatched to the ranks owning their experts and the results
-  combined back with two all-to-all exchanges over RCCL (``Comm.all_to_all_rows``).
+* all-reduce combine (``mode="allreduce"``, and ``"auto"`` below ``A2A_ROWS`` rows -- decode steps): each
+  rank applies its own experts to all routed rows and one all-reduce sums the partial outputs (on the
+  one-shot xGMI kernel at decode sizes);
+* expert all-to-all (``mode="a2a"``, and ``"auto"`` from ``A2A_ROWS`` rows -- prefill): rank r takes token
+  slice r (ceil(T / N) rows), routes it, DISPATCHES each routed row to the rank owning its expert, the
+  owners run their grouped GEMMs, the results RETURN to the slice owners, who combine their slice; an
+  all-gather rebuilds the [T, d] output on every rank.  Exchanges use fixed capacity blocks (a rank sends
+  at most ceil(T / N) * k rows to any one owner) with the expert id travelling beside each row (-1 marks
+  an empty slot), so no counts are ever read on the host: the dispatch and return are graph-capturable
+  collectives of host-known size (RCCL send/recv groups on GPUs).  Per rank the exchange moves
+  ~T k d / N rows each way + the gathered output, instead of the all-reduce's full [T, d] fp32 partials.
+* :meth:`MoEBlock.forward_tokens` is the same exchange for ranks that hold DIFFERENT tokens (data-parallel
+  attention in front of expert-parallel MoE): dispatch, expert GEMMs, return, combine, no gather.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
 from .. import ops
 
 SKINNY_ROWS = 64
+# "auto": expert all-to-all from this many tokens (prefill); decode steps (<= 64 rows under MoE) all-reduce
+A2A_ROWS = int(os.environ.get("SYMMETRY_MOE_A2A_ROWS", "128"))
 
 
 class MoEBlock:
-    def __init__(self, model, ep_comm=None, mode: str = "allreduce"):
+    def __init__(self, model, ep_comm=None, mode: str | None = None):
         self.m = model
         cfg = model.cfg
         shard = model.w.shard
@@ -36,8 +47,9 @@ class MoEBlock:
         self.e_lo = self.ep_rank * self.E_local
         self.e_hi = self.e_lo + self.E_local
         self.comm = ep_comm if ep_comm is not None else model.tp
-        self.mode = mode
+        self.mode = mode or os.environ.get("SYMMETRY_MOE_MODE", "auto")
         self.F = cfg.intermediate_size
+        self.calls = {"allreduce": 0, "a2a": 0}
         # router rows padded to a multiple of 16 for the skinny GEMM (padded logits are never read)
         self.router = {}
         Ep = (self.E + 15) // 16 * 16
@@ -50,9 +62,16 @@ class MoEBlock:
     def _buf(self, name, shape, dtype):
         return self.m._buf("moe." + name, shape, dtype)
 
+    def use_a2a(self, T: int) -> bool:
+        if self.ep <= 1:
+            return False
+        return self.mode == "a2a" or (self.mode == "auto" and T >= A2A_ROWS)
+
     def forward(self, i: int, x: torch.Tensor) -> torch.Tensor:
-        if self.ep > 1 and self.mode == "a2a":
+        if self.use_a2a(x.shape[0]):
+            self.calls["a2a"] += 1
             return self.forward_a2a(i, x)
+        self.calls["allreduce"] += 1
         return self._forward_local(i, x, reduce=self.ep > 1)
 
     # ------------------------------------------------------------------------------------------
@@ -71,8 +90,12 @@ class MoEBlock:
         ops.moe_route_permute(logits, x, k, E, ids, w, counts, offsets, cursor, xs, dst)
         return ids, w, dst, offsets, xs
 
-    def _experts(self, i, xs, offsets, e_lo, n_local):
-        """Apply experts [e_lo, e_lo + n_local) to their segments of xs; returns a LinOut [.., R, d]."""
+    def _grouped_ok(self, d: int) -> bool:
+        return d % 128 == 0 and d % 64 == 0 and self.F % 64 == 0
+
+    def _experts(self, i, xs, offsets, e_lo, n_local, out_f32: bool = False):
+        """Apply experts [e_lo, e_lo + n_local) to their segments of xs (segment bounds: ``offsets``, device
+        memory, global expert numbering); returns a LinOut [.., R, d]."""
         R, d = xs.shape
         w13 = self.m.w.layer(i, "w13")
         w2 = self.m.w.layer(i, "w2")
@@ -87,6 +110,13 @@ class MoEBlock:
             y2 = self._buf("y2", (s2, R, d), torch.float32)
             ops.grouped_skinny(act, w2, offsets, e_lo, y2)
             return y2
+        if self._grouped_ok(d):
+            # prefill-sized: grouped MFMA GEMMs, SwiGLU fused into the gate/up epilogue
+            ops.grouped_gemm(xs, w13, offsets, e_lo, act, ops.GROUPED_SWIGLU)
+            y2 = self._buf("y2f" if out_f32 else "y2b", (R, d), torch.float32 if out_f32 else torch.bfloat16)
+            ops.grouped_gemm(act, w2, offsets, e_lo, y2, ops.GROUPED_F32 if out_f32 else ops.GROUPED_BF16)
+            return y2
+        # shapes outside the grouped kernel's tiling (not the registered models): per-expert library GEMMs
         offs = offsets.tolist()
         y1 = self._buf("y1b", (R, 2 * F), torch.bfloat16)
         y2 = self._buf("y2b", (R, d), torch.bfloat16)
@@ -104,7 +134,7 @@ class MoEBlock:
     def _forward_local(self, i, x, reduce: bool) -> torch.Tensor:
         T, d = x.shape
         ids, w, dst, offsets, xs = self._route(i, x)
-        y2 = self._experts(i, xs, offsets, self.e_lo, self.E_local)
+        y2 = self._experts(i, xs, offsets, self.e_lo, self.E_local, out_f32=True)
         out = self._buf("out", (T, d), torch.float32)
         ops.moe_combine(y2, dst, ids, self.e_lo, self.e_hi, w, self.k, out)
         if reduce:
@@ -113,35 +143,76 @@ class MoEBlock:
 
     # ------------------------------------------------------------------------------------------
     def forward_a2a(self, i: int, x: torch.Tensor) -> torch.Tensor:
-        """Dispatch/combine over all-to-all.  x holds THIS rank's tokens (data-parallel attention)."""
+        """Expert all-to-all over token slices (x [T, d] identical on every rank; see the module note)."""
         T, d = x.shape
-        k, ep = self.k, self.ep
-        ids, w, dst, offsets, xs = self._route(i, x)
-        R = T * k
-        # xs rows are grouped by expert == grouped by owner rank (owners own contiguous expert ranges)
-        offs = offsets.to("cpu", torch.int64)
-        bounds = [int(offs[r * self.E_local]) for r in range(ep)] + [R]
-        send_counts = [bounds[r + 1] - bounds[r] for r in range(ep)]
-        cnt = torch.tensor(send_counts, dtype=torch.int64, device=x.device).view(ep, 1)
-        recv_cnt = self.comm.all_to_all_rows(cnt, [1] * ep, [1] * ep).view(-1).tolist()
-        # expert id of every sent row (rows of xs are sorted by expert)
-        row_expert = torch.repeat_interleave(torch.arange(self.E, device=x.device),
-                                             (offs[1:] - offs[:-1]).to(x.device))
-        x_recv = self.comm.all_to_all_rows(xs[:R], send_counts, recv_cnt)
-        e_recv = self.comm.all_to_all_rows(row_expert.view(-1, 1).to(torch.int64), send_counts, recv_cnt).view(-1)
-        # local expert segments of the received rows (stable sort keeps per-source order)
-        order = torch.argsort(e_recv, stable=True)
-        xr = x_recv.index_select(0, order).contiguous()
-        local = e_recv.index_select(0, order) - self.e_lo
-        cnt_local = torch.bincount(local, minlength=self.E_local)[: self.E_local]
-        loc_off = torch.zeros(self.E + 1, dtype=torch.int32, device=x.device)
-        loc_off[self.e_lo + 1 : self.e_lo + self.E_local + 1] = torch.cumsum(cnt_local, 0).to(torch.int32)
-        loc_off[self.e_lo + self.E_local + 1 :] = loc_off[self.e_lo + self.E_local]
-        yl = self._experts(i, xr, loc_off, self.e_lo, self.E_local)
-        ylf = ops.reference.linout_sum(yl) if yl.dim() == 3 else yl.float()
-        y_sorted_back = torch.empty_like(ylf)
-        y_sorted_back[order] = ylf  # undo the local sort: rows back in received order
-        y_back = self.comm.all_to_all_rows(y_sorted_back.contiguous(), recv_cnt, send_counts)
-        out = self._buf("out", (T, d), torch.float32)
-        ops.moe_combine(y_back, dst, ids, 0, self.E, w, k, out)
+        N, r = self.ep, self.ep_rank
+        S = -(-T // N)
+        lo, hi = min(T, r * S), min(T, (r + 1) * S)
+        out_s = self.forward_tokens(i, x[lo:hi], S)
+        full = self._buf("a2a.slice", (S, d), torch.float32)
+        if hi > lo:
+            full[: hi - lo].copy_(out_s)
+        g = self.comm.all_gather(full)  # [N * S, d]
+        return g[:T]
+
+    def forward_tokens(self, i: int, x: torch.Tensor, S: int) -> torch.Tensor:
+        """Dispatch -> owners' expert GEMMs -> return -> combine for THIS rank's tokens x [T_r <= S, d] (ranks
+        may hold different tokens; S: the per-rank row bound every rank uses, which fixes the capacity)."""
+        Tr, d = x.shape
+        N, k, E, El = self.ep, self.k, self.E, self.E_local
+        cap = S * k                       # rows this rank can send to one owner
+        dev = x.device
+        R = Tr * k
+        # ---- route my tokens; group the routed rows by OWNER rank into fixed capacity blocks
+        ids = self._buf("a2a.ids", (max(R, 1),), torch.int32)
+        w = self._buf("a2a.w", (max(R, 1),), torch.float32)
+        dst = self._buf("a2a.dst", (max(R, 1),), torch.int32)
+        send = self._buf("a2a.send", (N * cap, d), torch.bfloat16)
+        send_e = self._buf("a2a.send_e", (N * cap, 1), torch.int32)
+        send_e.fill_(-1)
+        if Tr > 0:
+            logits = self.m._linear("router", x, self.router[i])
+            ops.moe_route(logits, Tr, k, E, ids, w)
+            owner = self._buf("a2a.owner", (R,), torch.int32)
+            torch.floor_divide(ids[:R], El, out=owner)
+            blocks = self._blocks(N, cap, dev)
+            cursor = self._buf("a2a.cursor", (N,), torch.int32)
+            cursor.zero_()
+            ops.moe_scatter(x, owner, k, N, blocks, cursor, send, dst)
+            send_e.view(-1).index_copy_(0, dst[:R].long(), ids[:R])
+        # ---- dispatch: block q of every rank's send buffer goes to rank q
+        splits = [cap] * N
+        recv = self.comm.all_to_all_rows(send, splits, splits)            # [N * cap, d]  (src-major)
+        recv_e = self.comm.all_to_all_rows(send_e, splits, splits).view(-1)  # expert id per slot, -1 = empty
+        # ---- group the received rows by local expert, run the grouped GEMMs
+        counts = self._buf("a2a.counts", (E,), torch.int32)
+        offsets = self._buf("a2a.offsets", (E + 1,), torch.int32)
+        cursor_e = self._buf("a2a.cursor_e", (E,), torch.int32)
+        ops.moe_align(recv_e, E, counts, offsets, cursor_e)
+        xs = self._buf("a2a.xs", (N * cap, d), torch.bfloat16)
+        ldst = self._buf("a2a.ldst", (N * cap,), torch.int32)
+        ldst.zero_()  # empty slots keep row 0 (returned, never combined)
+        ops.moe_scatter(recv, recv_e, 1, E, offsets, cursor_e, xs, ldst)
+        y = self._experts(i, xs, offsets, self.e_lo, El, out_f32=True)
+        if y.dim() == 3:  # skinny-path slabs -> [N * cap, d] fp32, rows in local expert order
+            yl = self._buf("a2a.ysum", (N * cap, d), torch.float32)
+            torch.sum(y, 0, out=yl)
+        else:
+            yl = y
+        # ---- return: every received slot's result goes back to the slot it came from
+        back = self._buf("a2a.back", (N * cap, d), torch.float32)
+        torch.index_select(yl, 0, ldst.long(), out=back)
+        ret = self.comm.all_to_all_rows(back, splits, splits)             # [N * cap, d]: my slots' results
+        out = self._buf("a2a.out", (max(Tr, 1), d), torch.float32)[:Tr]
+        if Tr > 0:
+            ops.moe_combine(ret, dst, ids, 0, E, w, k, out)
         return out
+
+    def _blocks(self, N: int, cap: int, dev) -> torch.Tensor:
+        """Fixed segment starts q * cap of the per-owner send blocks (built once per capacity)."""
+        key = ("moe.a2a.blocks", N, cap)
+        b = self.m.ws.buffers.get(key)
+        if b is None:
+            b = torch.arange(N + 1, dtype=torch.int32, device=dev) * cap
+            self.m.ws.buffers[key] = b
+        return b

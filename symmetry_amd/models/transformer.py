@@ -178,6 +178,7 @@ class TransformerLM:
         self.dgw = self._decode_copies(decode_weights)
         self.persistent_mlp = persistent_mlp
         self.fused_attn_block = fused_attn_block
+        self.tp_reduced_bytes: dict[str, int] = {}  # bytes per rank of the last general-path all-reduce
 
     def _decode_copies(self, mode: str) -> dict:
         """MFMA-preshuffled copies of the decode-GEMM weights (1 KB contiguous per wave load:
@@ -267,6 +268,13 @@ class TransformerLM:
             y = self._buf(name + ".bf16", (T, N), torch.bfloat16)
             ops.linear(x, w, out=y)
         if reduce and self.tp is not None and self.tp_size > 1:
+            if y.dim() == 3 and y.shape[0] > 1:
+                # sum the split-K slabs locally first: the collective then moves one [T, N] fp32 partial per
+                # rank instead of S of them (S x fewer bytes over xGMI on every row-parallel projection)
+                ys = self._buf(name + ".red", (1, T, N), torch.float32)
+                torch.sum(y, dim=0, keepdim=True, out=ys)
+                y = ys
+            self.tp_reduced_bytes[name] = y.numel() * y.element_size()
             self.tp.all_reduce(y)
         return y
 

@@ -241,6 +241,35 @@ def moe_route_permute(logits, x, k, E, ids, w, counts, offsets, cursor, xs, dst)
     return reference.moe_route_permute(logits, x, k, E, ids, w, counts, offsets, cursor, xs, dst)
 
 
+def moe_route(logits, T, k, E, ids, w):
+    if _gpu(ids):
+        return _native.ops().moe_route(logits, int(T), int(k), int(E), ids, w)
+    return reference.moe_route(logits, T, k, E, ids, w)
+
+
+def moe_align(ids, G, counts, offsets, cursor):
+    if _gpu(ids):
+        return _native.ops().moe_align(ids, int(G), counts, offsets, cursor)
+    return reference.moe_align(ids, G, counts, offsets, cursor)
+
+
+def moe_scatter(x, ids, k, G, offsets, cursor, xs, dst, src_tok=None):
+    """Rows of x into group segments starting at offsets[g] (``cursor`` zero); dst[a] = row of assignment a."""
+    if _gpu(x):
+        return _native.ops().moe_scatter(x, ids, int(k), int(G), offsets, cursor, xs, dst, src_tok)
+    return reference.moe_scatter(x, ids, k, G, offsets, cursor, xs, dst, src_tok)
+
+
+GROUPED_BF16, GROUPED_F32, GROUPED_SWIGLU = 0, 1, 2
+
+
+def grouped_gemm(xs, W, offsets, e0, y, mode):
+    """Grouped MFMA GEMM over expert segments for any routed row count (segment bounds on the device)."""
+    if _gpu(xs):
+        return _native.ops().grouped_gemm(xs, W, offsets, int(e0), y, int(mode))
+    return reference.grouped_gemm(xs, W, offsets, e0, y, mode)
+
+
 def grouped_skinny(xs, W, offsets, e0, y):
     if _gpu(xs):
         return _native.ops().grouped_skinny(xs, W, offsets, int(e0), y)

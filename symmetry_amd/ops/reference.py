@@ -379,6 +379,55 @@ def moe_route_permute(logits, x, k: int, E: int, ids, w, counts, offsets, cursor
     xs[rows] = x[torch.arange(T * k) // k].to(xs.dtype)
 
 
+def moe_route(logits, T: int, k: int, E: int, ids, w) -> None:
+    lg = linout_sum(logits)[:T, :E]
+    topv, topi = torch.topk(lg, k, dim=-1)  # ties -> lower index first (same as the kernel)
+    ids[: T * k].copy_(topi.reshape(-1).to(ids.dtype))
+    w[: T * k].copy_(torch.softmax(topv, dim=-1).reshape(-1))
+
+
+def moe_align(ids, G: int, counts, offsets, cursor) -> None:
+    v = ids.long()
+    v = v[(v >= 0) & (v < G)]
+    cnt = torch.bincount(v, minlength=G)[:G]
+    counts[:G].copy_(cnt.to(counts.dtype))
+    off = torch.zeros(G + 1, dtype=torch.int64)
+    off[1:] = torch.cumsum(cnt, 0)
+    offsets[: G + 1].copy_(off.to(offsets.dtype))
+    cursor[:G].zero_()
+
+
+def moe_scatter(x, ids, k: int, G: int, offsets, cursor, xs, dst, src_tok=None) -> None:
+    """Rows into group segments in assignment order (the kernel's order within a segment varies; every
+    consumer indexes through dst, so results agree)."""
+    T = x.shape[0]
+    R = xs.shape[0]
+    for a in range(T * k):
+        g = int(ids[a])
+        if g < 0 or g >= G:
+            continue
+        row = int(offsets[g]) + int(cursor[g])
+        cursor[g] += 1
+        dst[a] = row
+        if 0 <= row < R:
+            xs[row] = x[a // k].to(xs.dtype)
+            if src_tok is not None:
+                src_tok[row] = a // k
+
+
+def grouped_gemm(xs, W, offsets, e0: int, y, mode: int) -> None:
+    """Y[rows of e] = Xs[rows of e] . W[e]^T (mode 0 bf16 / 1 fp32), or SwiGLU of the [gate; up] product."""
+    for e in range(W.shape[0]):
+        a, b = int(offsets[e0 + e]), int(offsets[e0 + e + 1])
+        if b <= a:
+            continue
+        p = _mm(xs[a:b], W[e])
+        if mode == 2:
+            F = p.shape[1] // 2
+            p = torch.nn.functional.silu(p[:, :F]) * p[:, F:]
+        y[a:b] = p.to(y.dtype)
+
+
 def grouped_skinny(xs, W, offsets, e0: int, y) -> None:
     S = y.shape[0]
     y.zero_()

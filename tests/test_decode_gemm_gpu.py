@@ -74,7 +74,8 @@ def test_dg_swiglu(gpu, M, F, K):
 
 
 @pytest.mark.parametrize("M", MS)
-@pytest.mark.parametrize("Hq,Hkv,K", [(32, 8, 4096), (4, 1, 512), (2, 1, 256)])
+# (8, 1, 8192): the Llama-3-70B TP=8 shard (64 / 8 q heads, ONE kv head per rank, d = 8192)
+@pytest.mark.parametrize("Hq,Hkv,K", [(32, 8, 4096), (4, 1, 512), (2, 1, 256), (8, 1, 8192)])
 def test_dg_qkv(gpu, M, Hq, Hkv, K):
     D, BS, NB = 128, 32, 8
     N = (Hq + 2 * Hkv) * D

@@ -454,3 +454,24 @@ def test_prefix_cache_is_scoped_per_client():
     while eng.has_unfinished():
         eng.step()
     assert eng.blocks.hit_tokens - h0 == (len(p) - 1) // 16 * 16  # same client: adopted
+
+
+def test_scheduler_burst_split_counts_uncached_tokens():
+    """A burst whose prompts hit the prefix cache is split on the UNCACHED remainders: the first step
+    holds exactly the first n // 2 + 1 prompts (not more because cached tokens inflated the budget)."""
+    bm = BlockManager(1024, 64, prefix_caching=True)
+    sch = Scheduler(SchedulerConfig(max_num_seqs=64, max_num_batched_tokens=8192, max_model_len=4096,
+                                    burst_split_tokens=1024), bm)
+    shared = list(range(1000, 1000 + 512))  # 8 full blocks of a known conversation prefix
+    warm = Sequence("warm", shared + [7], SamplingParams(max_tokens=1))
+    sch.add(warm)
+    b = sch.schedule()
+    warm.num_computed = len(warm.token_ids)
+    bm.register(warm)
+    sch.finish(warm, warm.status.__class__.FINISHED_STOPPED)
+    n = 10
+    for i in range(n):  # every prompt: the cached 512-token prefix + 200 new tokens
+        sch.add(Sequence(f"r{i}", shared + list(range(i * 300, i * 300 + 200)), SamplingParams(max_tokens=4)))
+    b = sch.schedule()
+    assert b.kind == "prefill" and len(b.seqs) == n // 2 + 1
+    assert all(c == 200 for c in b.num_new_tokens)  # the cached 512 tokens are skipped

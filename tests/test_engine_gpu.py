@@ -317,3 +317,94 @@ def test_prefix_cache_multi_turn_on_gpu_matches_oracle(gpu, model):
     assert eng.blocks.hit_tokens - hits0 >= (len(turn1) // 32) * 32
     _agree(eng.weights, turn1, out1, tol=0.08)
     _agree(eng.weights, turn2, out2, tol=0.08)
+
+
+@pytest.mark.parametrize("path", ["fused", "general"])
+def test_llama3_8b_shapes_two_layers_match_oracle(gpu, monkeypatch, path):
+    """The headline model's real shapes (d = 4096, F = 14336, Hq / Hkv = 32 / 8, V = 128256) with two
+    layers, through prefill, the decode hipGraphs and either decode path (fused decode GEMMs, or the
+    general mgemm + consumer path that wide batches take), against the fp32 oracle."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+    from symmetry_amd.models import transformer
+    from symmetry_amd.models.config import LLAMA3_8B
+
+    if path == "general":
+        monkeypatch.setattr(transformer, "GENERAL_ROWS", 1)
+    mcfg = LLAMA3_8B.replace(num_layers=2)
+    eng = LLMEngine(EngineConfig(model="llama3:8b", model_config=mcfg, device="cuda:0", max_num_seqs=8,
+                                 max_model_len=1024, num_kv_blocks=64, use_graphs=True))
+    eng.warmup([16, 128])
+    prompts = [eng.tokenizer.apply_chat_template([{"role": "user", "content": f"shape check {i} " * (2 * i + 1)}])
+               for i in range(6)]
+    seqs = [eng.add_request(f"s{i}", p, SamplingParams(max_tokens=8, ignore_eos=True))
+            for i, p in enumerate(prompts)]
+    while eng.has_unfinished():
+        eng.step()
+    assert eng.runner.graphs, "decode steps must replay captured hipGraphs"
+    for p, s in zip(prompts, seqs):
+        assert len(s.output_ids) == 8
+        _agree(eng.weights, p, s.output_ids, tol=0.1)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("counts", [(300, 0, 129, 1, 640, 77, 0, 200), (3, 2, 1, 0, 0, 0, 0, 300)])
+def test_grouped_gemm_vs_fp32(gpu, mode, counts):
+    """Grouped MFMA GEMM (K12) over uneven expert segments (empty ones, a 1-row one, multi-tile ones) with
+    the segment bounds read on the device: bf16 / fp32 outputs and the fused SwiGLU epilogue, against fp32
+    products; rows outside every segment are never written."""
+    E, d, F = 8, 512, 384
+    g = torch.Generator(device=gpu).manual_seed(sum(counts) + mode)
+    R = sum(counts)
+    off = torch.zeros(E + 1, dtype=torch.int32)
+    off[1:] = torch.cumsum(torch.tensor(counts), 0)
+    offsets = off.to(gpu)
+    xs = torch.randn(R + 16, d, device=gpu, generator=g).bfloat16()
+    N = F if mode == 2 else 2 * F
+    W = (torch.randn(E, 2 * F, d, device=gpu, generator=g) * 0.05).bfloat16()
+    e0, El = (2, 4) if mode == 1 else (0, E)  # mode 1: an expert-parallel shard (experts 2..5)
+    Wl = W[e0:e0 + El].contiguous()
+    dt = torch.float32 if mode == 1 else torch.bfloat16
+    y = torch.full((R + 16, N), 7.0, device=gpu, dtype=dt)
+    ops.grouped_gemm(xs, Wl, offsets, e0, y, mode)
+    torch.cuda.synchronize()
+    yc, xc, Wc = y.float().cpu(), xs.float().cpu(), Wl.float().cpu()
+    written = torch.zeros(R + 16, dtype=torch.bool)
+    for e in range(El):
+        a, b = int(off[e0 + e]), int(off[e0 + e + 1])
+        if b <= a:
+            continue
+        p = xc[a:b] @ Wc[e].t()
+        if mode == 2:
+            p = torch.nn.functional.silu(p[:, :F]) * p[:, F:]
+        tol = 2e-2 if mode != 1 else 2e-3
+        torch.testing.assert_close(yc[a:b], p, atol=tol, rtol=tol)
+        written[a:b] = True
+    assert torch.all(yc[~written] == 7.0)
+
+
+def test_mixtral_prefill_grouped_path_matches_oracle(gpu):
+    """tiny-mixtral prefill of more than 64 routed rows: the grouped MFMA GEMM path (no host sync) end to
+    end against the fp32 oracle, with the decode steps in hipGraphs."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+
+    eng = LLMEngine(EngineConfig(model="tiny-mixtral", device="cuda:0", max_num_seqs=4, max_model_len=1024,
+                                 num_kv_blocks=64, use_graphs=True))
+    prompts = [list(range(40 + 7 * i, 40 + 7 * i + 90 + 20 * i)) for i in range(3)]  # 90..130 tokens each
+    calls = []
+    orig = ops.grouped_gemm
+    import symmetry_amd.models.moe as moe_mod
+
+    moe_mod.ops.grouped_gemm = lambda *a, **k: calls.append(a[0].shape[0]) or orig(*a, **k)
+    try:
+        seqs = [eng.add_request(f"m{i}", p, SamplingParams(max_tokens=6, ignore_eos=True))
+                for i, p in enumerate(prompts)]
+        while eng.has_unfinished():
+            eng.step()
+    finally:
+        moe_mod.ops.grouped_gemm = orig
+    assert calls and max(calls) > 64
+    for p, s in zip(prompts, seqs):
+        assert len(s.output_ids) == 6
+        _agree(eng.weights, p, s.output_ids, tol=0.08)

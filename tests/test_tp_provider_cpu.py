@@ -9,6 +9,7 @@ import socket
 import subprocess
 import sys
 
+import pytest
 import yaml
 
 from symmetry_amd.net import DiscoveryServer
@@ -26,7 +27,9 @@ def _port():
     return p
 
 
-def test_tp2_provider_over_torchrun_streams_like_tp1(tmp_path):
+@pytest.mark.parametrize("launch", ["torchrun", "plain"])
+def test_tp2_provider_over_torchrun_streams_like_tp1(tmp_path, launch):
+    """``plain``: ``symmetry-cli -c provider.yaml`` with tensorParallelSize 2 starts the torchrun ranks itself."""
     async def main():
         ds = DiscoveryServer()
         await ds.start()
@@ -44,6 +47,8 @@ def test_tp2_provider_over_torchrun_streams_like_tp1(tmp_path):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m", "symmetry_amd.cli", "-c",
                str(path), "--bootstrap", f"{boot[0][0]}:{boot[0][1]}"]
+        if launch == "plain":
+            cmd = [sys.executable, "-m", "symmetry_amd.cli", "-c", str(path), "--bootstrap", f"{boot[0][0]}:{boot[0][1]}"]
         proc = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
                                 start_new_session=True)
         try:
@@ -81,3 +86,28 @@ def test_tp2_provider_over_torchrun_streams_like_tp1(tmp_path):
                        SamplingParams(max_tokens=8, ignore_eos=True))
     # same weights (seeded full init), same greedy decode: TP=2 over gloo reproduces the TP=1 text
     assert text == ref.tokenizer.decode(ids), (text, ref.tokenizer.decode(ids))
+
+
+def test_tp_config_fails_at_startup_without_gpus(tmp_path):
+    """tensorParallelSize 2 on a box with fewer GPUs: symmetry-cli exits non-zero before announcing."""
+    from symmetry_amd import cli
+
+    cfg = {"apiHostname": "127.0.0.1", "apiPath": "/v1/chat/completions", "apiPort": 0, "apiProtocol": "http",
+           "apiProvider": "native", "modelName": "tiny-llama", "name": "tp", "path": str(tmp_path),
+           "public": True, "serverKey": "00" * 32, "tensorParallelSize": 2}
+    path = tmp_path / "provider.yaml"
+    path.write_text(yaml.safe_dump(cfg))
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("this box has the GPUs")
+    assert cli.main(["-c", str(path)]) == 1
+    plan = cli.tp_launch_plan(cfg, str(path), None)
+    assert "--nproc-per-node=2" in plan and plan[-2:] == ["-c", str(path)]
+
+
+def test_engine_refuses_tp_without_communicator():
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+
+    with pytest.raises(ValueError, match="communicator"):
+        LLMEngine(EngineConfig(model="tiny-llama", device="cpu", tp_size=2, max_model_len=128))
