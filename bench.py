@@ -240,6 +240,11 @@ def main() -> int:
             "warmup_s": round(t_cap, 1),
             "sse_events_rank0": events,
         }
+        if parallel == "tp" and world > 1:
+            tp = eng.model.tp
+            line["tp"] = {"xgmi_calls": dict(getattr(tp, "calls", {})),
+                          "prefill_allreduce_bytes_per_rank": dict(eng.model.tp_reduced_bytes),
+                          "metadata_plane": type(runner.meta).__name__}
         if client_end is not None:
             line["client_end"] = client_end
             line["p50_ttft_ms"] = client_end.get("p50_ttft_ms")

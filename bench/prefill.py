@@ -22,20 +22,44 @@ def main():
     ap.add_argument("--clients", type=int, default=10)
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--ab-moe-grouped", action="store_true",
+                    help="MoE: alternate grouped MFMA GEMMs / per-expert library GEMMs (host sync) per rep")
     args = ap.parse_args()
-    import torch
-
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
-    from symmetry_amd.engine.sequence import SamplingParams
 
     C, L = args.clients, args.prompt_len
     eng = LLMEngine(EngineConfig(model=args.model, max_num_seqs=max(C, 1), max_model_len=max(2048, L + 64),
                                  max_num_batched_tokens=max(8192, C * L)))
     eng.warmup([16, 128, 512, C * L] if C * L > 512 else None)
+    from symmetry_amd.models import moe as moe_mod
+
+    arms = [True, False] if args.ab_moe_grouped else [moe_mod.GROUPED]
+    res = {}
+    for arm in arms:
+        moe_mod.GROUPED = arm
+        res[arm] = _run(eng, args, C, L, salt=len(res))
     cfg = eng.model_cfg
+    toks = C * L
+    vd = cfg.vocab_size * cfg.hidden_size
+    body = cfg.num_params() - vd - (0 if cfg.tie_embeddings else vd)  # layers only: embedding is a gather
+    flops = 2 * body * toks + 2 * vd * C + 4 * cfg.num_layers * cfg.num_heads * cfg.head_dim * C * L * L / 2
+    for arm, t in res.items():
+        out = {"model": args.model, "clients": C, "prompt_len": L, "ttft_ms": round(t * 1e3, 2),
+               "prefill_tokens_per_s": round(toks / t), "tflops": round(flops / t / 1e12, 1)}
+        if cfg.is_moe:
+            out["moe_grouped_gemm"] = arm
+        print(json.dumps(out), flush=True)
+
+
+def _run(eng, args, C, L, salt=0):
+    """Median TTFT of ``args.reps`` bursts (``salt`` keeps the arms' prompts apart: no prefix-cache hits)."""
+    import torch
+
+    from symmetry_amd.engine.sequence import SamplingParams
+
     times = []
     for r in range(args.reps):
-        seqs = [eng.add_request(f"p{r}-{i}", [(97 * i + 13 * k + r) % 30000 + 300 for k in range(L)],
+        seqs = [eng.add_request(f"p{salt}-{r}-{i}", [(97 * i + 13 * k + r + 1009 * salt) % 30000 + 300 for k in range(L)],
                                 SamplingParams(max_tokens=1, ignore_eos=True)) for i in range(C)]
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -46,13 +70,7 @@ def main():
         while eng.has_unfinished():
             eng.step()
     times.sort()
-    t = times[len(times) // 2]
-    toks = C * L
-    vd = cfg.vocab_size * cfg.hidden_size
-    body = cfg.num_params() - vd - (0 if cfg.tie_embeddings else vd)  # layers only: embedding is a gather
-    flops = 2 * body * toks + 2 * vd * C + 4 * cfg.num_layers * cfg.num_heads * cfg.head_dim * C * L * L / 2
-    print(json.dumps({"model": args.model, "clients": C, "prompt_len": L, "ttft_ms": round(t * 1e3, 2),
-                      "prefill_tokens_per_s": round(toks / t), "tflops": round(flops / t / 1e12, 1)}))
+    return times[len(times) // 2]
 
 
 if __name__ == "__main__":

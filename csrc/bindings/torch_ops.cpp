@@ -96,7 +96,7 @@ void add_rms_norm(const Tensor& delta, Tensor& residual, const Tensor& w, double
 }
 
 void embed_rms_norm(const Tensor& ids, const Tensor& table, Tensor& residual, const Tensor& w, double eps,
-                    Tensor& out) {
+                    Tensor& out, const c10::optional<Tensor>& src, const c10::optional<Tensor>& prev) {
   check_gpu(ids, "ids");
   check_gpu(table, "table");
   check_gpu(residual, "residual");
@@ -107,9 +107,21 @@ void embed_rms_norm(const Tensor& ids, const Tensor& table, Tensor& residual, co
   const int64_t T = ids.numel(), d = table.size(1);
   TORCH_CHECK(residual.numel() == T * d && out.numel() == T * d && w.numel() == d, "embed_rms_norm: shape mismatch");
   TORCH_CHECK(d % 8 == 0 && d <= 16384, "embed_rms_norm: bad d");
+  TORCH_CHECK(src.has_value() == prev.has_value(), "embed_rms_norm: src and prev go together");
+  const int* sp = nullptr;
+  const int* pp = nullptr;
+  if (src.has_value()) {
+    check_gpu(*src, "src");
+    check_gpu(*prev, "prev");
+    check_dtype(*src, at::kInt, "src");
+    check_dtype(*prev, at::kInt, "prev");
+    TORCH_CHECK(src->numel() >= T, "embed_rms_norm: src shorter than ids");
+    sp = ptr<int>(*src);
+    pp = ptr<int>(*prev);
+  }
   const at::OptionalDeviceGuard g(ids.device());
   launch_embed_rms_norm(ptr<int>(ids), ptr<bf16>(table), ptr<float>(residual), ptr<bf16>(w), ptr<bf16>(out), (int)T,
-                        (int)d, (float)eps, cur_stream(ids));
+                        (int)d, (float)eps, cur_stream(ids), sp, pp);
 }
 
 void rope_cache(const Tensor& qkv, const Tensor& positions, const Tensor& slots, const Tensor& cos_sin,
@@ -884,7 +896,8 @@ void rownorm(const Tensor& xw, const Tensor& ss, double eps, Tensor& out) {
 TORCH_LIBRARY(symmetry_amd, m) {
   m.def("rms_norm(Tensor x, Tensor w, float eps, Tensor(a!) out) -> ()", &rms_norm);
   m.def("add_rms_norm(Tensor delta, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out) -> ()", &add_rms_norm);
-  m.def("embed_rms_norm(Tensor ids, Tensor table, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out) -> ()",
+  m.def("embed_rms_norm(Tensor ids, Tensor table, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out, "
+        "Tensor? src=None, Tensor? prev=None) -> ()",
         &embed_rms_norm);
   m.def(
       "rope_cache(Tensor qkv, Tensor positions, Tensor slots, Tensor cos_sin, Tensor(a!) q_out, Tensor(b!) k_cache, "

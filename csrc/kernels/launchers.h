@@ -125,7 +125,7 @@ void launch_rms_norm(LinOut x, const bf16* w, bf16* out, int T, int d, float eps
 void launch_add_rms_norm(LinOut delta, float* residual, const bf16* w, bf16* out, int T, int d, float eps,
                          hipStream_t s);
 void launch_embed_rms_norm(const int* ids, const bf16* table, float* residual, const bf16* w, bf16* out, int T,
-                           int d, float eps, hipStream_t s);
+                           int d, float eps, hipStream_t s, const int* src = nullptr, const int* prev = nullptr);
 
 // rope_cache.hip
 void launch_rope_cache(LinOut qkv, const int* positions, const int* slots, const float* cos_sin, bf16* q_out,

@@ -2,7 +2,9 @@
 //
 //   mode 0 (norm):      out = rmsnorm(x) * w                 x: LinOut (bf16 or fp32 slabs)
 //   mode 1 (add_norm):  residual += delta; out = rmsnorm(residual) * w
-//   mode 2 (embed_norm): residual = table[ids]; out = rmsnorm(residual) * w
+//   mode 2 (embed_norm): residual = table[tok]; out = rmsnorm(residual) * w, tok = src[row] >= 0 ?
+//                        prev[src[row]] : ids[row] (src/prev optional: a pipelined decode row's token is the
+//                        previous step's on-device sample)
 //
 // The residual stream is kept in fp32 ([T][d]) for accuracy; activations fed
 // to the projections are bf16.  One 256-thread workgroup per row, 16 B per
@@ -22,7 +24,8 @@ __global__ __launch_bounds__(NT) void rms_norm_kernel(LinOut x, const int* __res
                                                       const bf16* __restrict__ table,
                                                       float* __restrict__ residual,
                                                       const bf16* __restrict__ w,
-                                                      bf16* __restrict__ out, int d, float eps) {
+                                                      bf16* __restrict__ out, int d, float eps,
+                                                      const int* __restrict__ src, const int* __restrict__ prev) {
   __shared__ float scratch[NT / 64];
   const int row = blockIdx.x;
   const int nvec = d >> 3;
@@ -44,7 +47,8 @@ __global__ __launch_bounds__(NT) void rms_norm_kernel(LinOut x, const int* __res
         for (int i = 0; i < 8; ++i) v[k][i] += r[i];
         store8f(residual + off, v[k]);
       } else {
-        const long long tok = ids[row];
+        const int sr = src ? src[row] : -1;
+        const long long tok = sr >= 0 ? prev[sr] : ids[row];
         load8(table + tok * d + vi * 8, v[k]);
         store8f(residual + off, v[k]);
       }
@@ -69,7 +73,7 @@ __global__ __launch_bounds__(NT) void rms_norm_kernel(LinOut x, const int* __res
 
 template <int MODE>
 void launch_mode(LinOut x, const int* ids, const bf16* table, float* residual, const bf16* w, bf16* out,
-                 int T, int d, float eps, hipStream_t s) {
+                 int T, int d, float eps, hipStream_t s, const int* src = nullptr, const int* prev = nullptr) {
   constexpr int NT = 256;
   const int nvec = d / 8;
   dim3 grid(T);
@@ -80,13 +84,13 @@ void launch_mode(LinOut x, const int* ids, const bf16* table, float* residual, c
     return !(e && e[0] == '0');
   }();
   if (wide && nvec <= 512) {
-    rms_norm_kernel<512, 1, MODE><<<grid, 512, 0, s>>>(x, ids, table, residual, w, out, d, eps);
+    rms_norm_kernel<512, 1, MODE><<<grid, 512, 0, s>>>(x, ids, table, residual, w, out, d, eps, src, prev);
   } else if (nvec <= NT * 2) {
-    rms_norm_kernel<NT, 2, MODE><<<grid, NT, 0, s>>>(x, ids, table, residual, w, out, d, eps);
+    rms_norm_kernel<NT, 2, MODE><<<grid, NT, 0, s>>>(x, ids, table, residual, w, out, d, eps, src, prev);
   } else if (nvec <= NT * 4) {
-    rms_norm_kernel<NT, 4, MODE><<<grid, NT, 0, s>>>(x, ids, table, residual, w, out, d, eps);
+    rms_norm_kernel<NT, 4, MODE><<<grid, NT, 0, s>>>(x, ids, table, residual, w, out, d, eps, src, prev);
   } else {
-    rms_norm_kernel<NT, 8, MODE><<<grid, NT, 0, s>>>(x, ids, table, residual, w, out, d, eps);
+    rms_norm_kernel<NT, 8, MODE><<<grid, NT, 0, s>>>(x, ids, table, residual, w, out, d, eps, src, prev);
   }
 }
 
@@ -102,9 +106,9 @@ void launch_add_rms_norm(LinOut delta, float* residual, const bf16* w, bf16* out
 }
 
 void launch_embed_rms_norm(const int* ids, const bf16* table, float* residual, const bf16* w, bf16* out, int T,
-                           int d, float eps, hipStream_t s) {
+                           int d, float eps, hipStream_t s, const int* src, const int* prev) {
   LinOut none{nullptr, 0, 1, 0};
-  launch_mode<2>(none, ids, table, residual, w, out, T, d, eps, s);
+  launch_mode<2>(none, ids, table, residual, w, out, T, d, eps, s, src, prev);
 }
 
 // rownorm: out = xw * rsqrt(sum(ss[m][:]) / d + eps)  -- materialises a normalised activation from the

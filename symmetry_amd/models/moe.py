@@ -34,6 +34,7 @@ from .. import ops
 SKINNY_ROWS = 64
 # "auto": expert all-to-all from this many tokens (prefill); decode steps (<= 64 rows under MoE) all-reduce
 A2A_ROWS = int(os.environ.get("SYMMETRY_MOE_A2A_ROWS", "128"))
+GROUPED = os.environ.get("SYMMETRY_MOE_GROUPED", "1") != "0"  # A/B: 0 = per-expert library GEMMs (host sync)
 
 
 class MoEBlock:
@@ -91,7 +92,9 @@ class MoEBlock:
         return ids, w, dst, offsets, xs
 
     def _grouped_ok(self, d: int) -> bool:
-        return d % 128 == 0 and d % 64 == 0 and self.F % 64 == 0
+        return d % 128 == 0 and self.F % 64 == 0 and GROUPED
+
+
 
     def _experts(self, i, xs, offsets, e_lo, n_local, out_f32: bool = False):
         """Apply experts [e_lo, e_lo + n_local) to their segments of xs (segment bounds: ``offsets``, device

@@ -15,11 +15,14 @@ def _rms(x, w, eps):
     return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps) * w.float()
 
 
-def _moe(cfg, w, i, h):
+def _moe(cfg, w, i, h, gaps=None):
     router = w.layer(i, "router").float()
     w13 = w.layer(i, "w13").float()
     w2 = w.layer(i, "w2").float()
     logits = h @ router.t()
+    if gaps is not None and cfg.top_k < cfg.num_experts:  # margin of the k-th choice over the (k+1)-th
+        top = logits.topk(cfg.top_k + 1, dim=-1).values
+        gaps.append(top[:, cfg.top_k - 1] - top[:, cfg.top_k])
     topv, topi = logits.topk(cfg.top_k, dim=-1)
     gates = torch.softmax(topv, dim=-1)
     out = torch.zeros_like(h)
@@ -34,8 +37,10 @@ def _moe(cfg, w, i, h):
 
 
 @torch.no_grad()
-def forward_logits(w: ModelWeights, ids: list[int]) -> torch.Tensor:
-    """Logits [len(ids), V] for a single sequence (tp=1 weights)."""
+def forward_logits(w: ModelWeights, ids: list[int], router_gaps: list | None = None) -> torch.Tensor:
+    """Logits [len(ids), V] for a single sequence (tp=1 weights).  ``router_gaps`` (MoE): receives, per
+    layer, each position's router margin between its k-th and (k+1)-th expert -- a near-zero margin is a
+    routing near-tie that bf16 activations may resolve the other way."""
     from .layout import natural_tensors
 
     if getattr(w, "layout", "natural") != "natural":
@@ -67,7 +72,7 @@ def forward_logits(w: ModelWeights, ids: list[int]) -> torch.Tensor:
         x = x + o @ w.layer(i, "wo").float().t()
         h = _rms(x, w.layer(i, "ln2"), cfg.rms_eps)
         if cfg.is_moe:
-            x = x + _moe(cfg, w, i, h)
+            x = x + _moe(cfg, w, i, h, router_gaps)
         else:
             gu = h @ w.layer(i, "w_gu").float().t()
             F = gu.shape[-1] // 2

@@ -421,10 +421,10 @@ class TransformerLM:
         x = self._buf("x", (T, d), torch.bfloat16)
         q = self._buf("q", (T, self.hq, self.D), torch.bfloat16)
         attn = self._buf("attn", (T, self.hq, self.D), torch.bfloat16)
-        tok = b.input_ids
-        if b.src is not None and b.kind == "decode":  # pipelined decode rows (prefill never has pending ids)
-            tok = reference.resolve_ids(b.input_ids, b.src, self.last_ids).to(torch.int32)
-        ops.embed_rms_norm(tok, w["embed"], resid, w.layer(0, "ln1"), eps, x)
+        # pipelined decode rows read their token from the previous step's samples on the device
+        src = b.src if b.src is not None and b.kind == "decode" else None
+        ops.embed_rms_norm(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), eps, x, src,
+                           self.last_ids if src is not None else None)
         for i in range(cfg.num_layers):
             qkv = self._linear("qkv", x, w.layer(i, "wqkv"), wshuf=self._shuf(i, "wqkv"))
             ops.rope_cache(qkv, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq, self.hkv,

@@ -77,10 +77,11 @@ def add_rms_norm(delta, residual, w, eps, out):
     return reference.add_rms_norm(delta, residual, w, eps, out)
 
 
-def embed_rms_norm(ids, table, residual, w, eps, out):
+def embed_rms_norm(ids, table, residual, w, eps, out, src=None, prev=None):
+    """``src``/``prev``: rows with src >= 0 take the token prev[src] (the previous step's on-device sample)."""
     if _gpu(residual):
-        return _native.ops().embed_rms_norm(ids, table, residual, w, float(eps), out)
-    return reference.embed_rms_norm(ids, table, residual, w, eps, out)
+        return _native.ops().embed_rms_norm(ids, table, residual, w, float(eps), out, src, prev)
+    return reference.embed_rms_norm(reference.resolve_ids(ids, src, prev), table, residual, w, eps, out)
 
 
 def rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, perm=False, decode=False):

@@ -11,14 +11,26 @@ from symmetry_amd.ops import reference as ref
 pytestmark = pytest.mark.gpu
 
 
-def _agree(weights, prompt, out, tol):
+def _agree(weights, prompt, out, tol, router_tie=0.005):
+    """Every generated token within ``tol`` of the fp32 oracle's best logit.  MoE: the check stops at the
+    first position whose oracle routing has a near-tie (k-th vs (k+1)-th expert margin < ``router_tie`` in
+    some layer, at or before it): bf16 activations may pick the other expert there, and the sequences
+    legitimately diverge from that point on."""
     from symmetry_amd.models import reference_model as rm
-    from symmetry_amd.models.weights import ModelWeights
 
     cpu = weights.to("cpu")
-    lg = rm.forward_logits(cpu, prompt + out[:-1])
+    gaps = []
+    lg = rm.forward_logits(cpu, prompt + out[:-1], router_gaps=gaps)
+    tie = None
+    if gaps:
+        g = torch.stack(gaps).min(0).values  # [positions]
+        hit = (g < router_tie).nonzero()
+        tie = int(hit[0]) if hit.numel() else None
     for j, t in enumerate(out):
-        row = lg[len(prompt) - 1 + j]
+        pos = len(prompt) - 1 + j
+        if tie is not None and pos >= tie:
+            break
+        row = lg[pos]
         assert float(row.max() - row[t]) <= tol, (j, t, int(row.argmax()), float(row.max() - row[t]))
 
 

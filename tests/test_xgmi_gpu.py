@@ -57,6 +57,8 @@ def test_xgmi_add_prep(gpu, world, T, d, P):
     from symmetry_amd.ops import _native, reference
 
     ops = _native.ops()
+    if world * T * P > 1024:
+        pytest.skip("the grid slices of one launch would not all be co-resident")
     hs = _comms(ops, world, slot_bytes=T * d * 4 + 256)
     g = torch.Generator(device="cpu").manual_seed(T * d + P)
     try:
