@@ -166,7 +166,7 @@ class XgmiComm(Comm):
     are all-gathered over ``group`` (gloo) and every peer buffer is mapped (``hipIpcOpenMemHandle``).
     Messages larger than a slot, non-sum ops and other dtypes go to ``inner`` (RCCL)."""
 
-    def __init__(self, inner: Comm, group, device, slot_bytes: int = 4 << 20):
+    def __init__(self, inner: Comm, group, device, slot_bytes: int = 4 << 20, barrier: bool = True):
         from ..ops import _native
 
         self.ops = _native.ops()
@@ -174,14 +174,23 @@ class XgmiComm(Comm):
         self.rank, self.world = inner.rank, inner.world
         self.capturable = inner.capturable  # the xGMI kernels are; the fallbacks are the inner ones
         dev = torch.device(device)
-        self.handle = int(self.ops.xgmi_create(int(slot_bytes), self.world, self.rank, dev.index or 0))
         self.slot_bytes = int(slot_bytes)
         self.calls = {"all_reduce": 0, "add_prep": 0}  # collectives issued on the xGMI kernels (host count)
-        mine = self.ops.xgmi_ipc_handle(self.handle)
-        allh = [torch.zeros_like(mine) for _ in range(self.world)]
-        dist.all_gather(allh, mine, group=group)
+        try:
+            self.handle = int(self.ops.xgmi_create(int(slot_bytes), self.world, self.rank, dev.index or 0))
+            mine = self.ops.xgmi_ipc_handle(self.handle)
+        except Exception:  # noqa: BLE001 -- still take part in the exchange below, then fail
+            mine = None
+            if not hasattr(self, "handle"):
+                self.handle = None
+        ref = mine if mine is not None else torch.zeros(64, dtype=torch.uint8)
+        allh = [torch.zeros_like(ref) for _ in range(self.world)]
+        dist.all_gather(allh, ref, group=group)  # every rank takes part, even one that failed to export
+        if mine is None:
+            raise RuntimeError("xgmi: hipIpcGetMemHandle failed")
         self.ops.xgmi_open(self.handle, torch.stack(allh))
-        dist.barrier(group=group)  # every rank mapped every buffer before the first collective
+        if barrier:
+            dist.barrier(group=group)  # every rank mapped every buffer before the first collective
 
     def _fits(self, t) -> bool:
         return (t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous()
@@ -222,7 +231,8 @@ class XgmiComm(Comm):
         host-mapped, so it costs no device synchronisation: the model runner polls it after every step)."""
         return int(self.ops.xgmi_error(self.handle))
 
-    def destroy(self):
-        self.ops.xgmi_destroy(self.handle)
-        if hasattr(self.inner, "destroy"):
+    def destroy(self, inner_too: bool = True):
+        if self.handle is not None:
+            self.ops.xgmi_destroy(self.handle)
+        if inner_too and hasattr(self.inner, "destroy"):
             self.inner.destroy()

@@ -53,10 +53,35 @@ def make_comms(on_gpu: bool, device=None):
     want = os.environ.get("SYMMETRY_XGMI", "auto")
     if (want == "1" or (want == "auto" and not staged)) and 1 < comm.world <= 8:
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-        comm = XgmiComm(comm, cpu_group, dev, int(os.environ.get("SYMMETRY_XGMI_SLOT", 4 << 20)))
-        if staged and os.environ.get("SYMMETRY_XGMI_GRAPHS", "0") == "1":
-            comm.capturable = True
+        xg = _try_xgmi(comm, cpu_group, dev)
+        if xg is not None:
+            comm = xg
+            if staged and os.environ.get("SYMMETRY_XGMI_GRAPHS", "0") == "1":
+                comm.capturable = True
     return comm, cpu_group
+
+
+def _try_xgmi(inner, group, dev):
+    """The xGMI communicator on every rank, or on none: a rank whose peer-memory mapping fails (IPC refused,
+    no peer access) votes no over the gloo group and every rank keeps the plain RCCL communicator."""
+    import sys
+
+    xg, err = None, None
+    try:
+        xg = XgmiComm(inner, group, dev, int(os.environ.get("SYMMETRY_XGMI_SLOT", 4 << 20)), barrier=False)
+    except Exception as exc:  # noqa: BLE001 -- any failure means: no one-shot kernels on this node
+        err = exc
+    ok = torch.tensor([0 if xg is None else 1], dtype=torch.int32)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+    if int(ok[0]) == 1:
+        dist.barrier(group=group)  # every rank mapped every buffer before the first collective
+        return xg
+    if err is not None:
+        print(f"symmetry: xGMI one-shot collectives unavailable ({type(err).__name__}: {err}); using RCCL",
+              file=sys.stderr, flush=True)
+    if xg is not None:
+        xg.destroy(inner_too=False)
+    return None
 
 
 def init_tp_engine(ecfg):
