@@ -126,7 +126,9 @@ class ModelRunner:
         self._parity = 0
         self.timing = {"h2d": 0.0, "forward": 0.0, "d2h": 0.0, "steps": 0}
         self.meta = None
-        if tp_size > 1:
+        # (tp_size > 1 without a bootstrap group: ONE rank's shard alone, no workers -- the TP shard timing
+        # simulation of bench/tp_shard.py)
+        if tp_size > 1 and cpu_group is not None:
             from ..parallel.metaplane import make_metaplane
 
             n = max(max_num_tokens, max_num_seqs)
@@ -296,7 +298,7 @@ class ModelRunner:
         self._fill(lay, host, seqs, counts, prev_rows)
         header = np.array([0 if batch.kind == "decode" else 1, lay.T, lay.nseq, lay.max_blocks, lay.ntiles, nseq,
                            int(self._filtered(seqs))], dtype=np.int32)
-        if self.tp_size > 1:
+        if self.meta is not None:
             self._broadcast(header, host_t)
         ids = self._run(header, host_t)
         handle = {"nseq": nseq, "t0": t0}
@@ -392,7 +394,7 @@ class ModelRunner:
             for mb in sorted(self.ctx_blocks, reverse=True):
                 for b in sorted(self.buckets, reverse=True):
                     if (b, mb, False) not in self.graphs:
-                        if self.tp_size > 1:
+                        if self.meta is not None:
                             self._broadcast(np.array([CMD_CAPTURE, b, b, mb, 0, b, 0], dtype=np.int32),
                                             torch.zeros(0, dtype=torch.int32))
                         self._capture(b, mb)
@@ -414,11 +416,11 @@ class ModelRunner:
         TP rank 0 sends CMD_SYNC so the workers (in :meth:`worker_loop`) meet it (bench timing brackets)."""
         import torch.distributed as dist
 
-        if self.tp_size > 1 and self.tp_rank == 0:
+        if self.meta is not None and self.tp_rank == 0:
             self.meta.send(np.array([CMD_SYNC] + [0] * (HEADER_LEN - 1), dtype=np.int32), None)
         if self.is_gpu:
             torch.cuda.synchronize()
-        if self.tp_size > 1:
+        if self.meta is not None:
             dist.barrier(group=self.cpu_group)
         if self.is_gpu:
             torch.cuda.synchronize()
