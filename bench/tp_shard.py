@@ -24,6 +24,9 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+PUSH = os.environ.get("SYMMETRY_XGMI_PUSH", "1") != "0"
+
+
 class LocalXgmi:
     """The XgmiComm interface over a world-1 xGMI communicator (every collective a real kernel launch)."""
 
@@ -34,13 +37,16 @@ class LocalXgmi:
 
         self.ops = _native.ops()
         self.rank, self.world = 0, world
+        self.slot_bytes = slot_bytes
         self.handle = int(self.ops.xgmi_create(slot_bytes, 1, 0, device.index or 0))
         self.ops.xgmi_connect_local(self.handle, [self.handle])
         self.calls = {"all_reduce": 0, "add_prep": 0, "keys": 0}
 
     def all_reduce(self, t, op="sum"):
-        self.ops.xgmi_all_reduce(t, t, self.handle)
-        self.calls["all_reduce"] += 1
+        # prefill-sized messages go to RCCL on a real node; a world-1 sum is the identity (not timed here)
+        if op == "sum" and t.numel() * t.element_size() <= self.slot_bytes and t.numel() % 8 == 0:
+            self.ops.xgmi_all_reduce(t, t, self.handle)
+            self.calls["all_reduce"] += 1
 
     def all_reduce_add_prep(self, y, resid, w_next, xw, ss):
         self.ops.xgmi_add_prep(y, resid, w_next, xw, ss, self.handle)
@@ -49,6 +55,13 @@ class LocalXgmi:
     def argmax_keys(self, keys, ids):
         self.ops.xgmi_keys_max(keys, ids, self.handle)
         self.calls["keys"] += 1
+
+    def gemm_add_prep(self, x, W, wshuf, resid, w_next, xw, ss) -> bool:
+        if not PUSH or x.shape[0] * resid.shape[1] * 4 > self.slot_bytes:
+            return False
+        self.ops.xgmi_gemm_add_prep(x, W, bool(wshuf), resid, w_next, xw, ss, self.handle)
+        self.calls["gemm_add_prep"] = self.calls.get("gemm_add_prep", 0) + 1
+        return True
 
     def all_gather(self, t):
         import torch
@@ -83,10 +96,14 @@ def main():
                        num_kv_blocks=blocks, tp_size=args.tp, tp_rank=0, weight_init="shard",
                        max_num_batched_tokens=max(8192, C * P))
     eng = LLMEngine(cfg, tp_comm=comm)
+    print(f"loaded {args.model} TP={args.tp} shard", flush=True)
     eng.warmup([16, 128, C * P])
+    print("warm", flush=True)
     params = SamplingParams(max_tokens=args.steps + args.warmup + 4, temperature=0.0, ignore_eos=True)
     seqs = [eng.add_request(f"c{i}", [(31 * i + 7 * k) % 100000 + 300 for k in range(P)], params) for i in range(C)]
     while any(s.first_token_time is None for s in seqs):
+        if any(s.status.finished for s in seqs):
+            raise SystemExit("a request failed (see the engine's traceback)")
         eng.step()
     for _ in range(args.warmup):
         eng.step()

@@ -64,11 +64,32 @@ SYM_DEV void store4bf_sc1(bf16* p, float a, float b, float c, float d) {
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- XPUSH (row-parallel projection under TP, xgmi_ar.hip protocol): the collective's epoch is this
+// rank's counter + 1 (read here, bumped by the reduce kernel that follows on the stream); tiles are stored
+// into slot (epoch parity, this rank) of every rank's buffer, then flag (tile, this rank) is raised in
+// every rank once the storing wave's stores are acknowledged (uncached buffers: no cache maintenance).
+SYM_DEV unsigned xp_epoch(const XgmiPush& xp) {
+  return __hip_atomic_load(reinterpret_cast<const unsigned*>(xp.bufs[xp.rank]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT) + 1u;
+}
+
+SYM_DEV void xp_flag(const XgmiPush& xp, int r, int tile, unsigned epoch) {
+  unsigned* f = reinterpret_cast<unsigned*>(xp.bufs[r] + XG_HDR_BYTES) + tile * XG_MAX_WORLD + xp.rank;
+  __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <int EPI>
-SYM_DEV void epilogue(const DecodeEpi& e, f32x4 v, int tile, int m, bool mok, int h, int N) {
+SYM_DEV void epilogue(const DecodeEpi& e, f32x4 v, int tile, int m, bool mok, int h, int N, unsigned xep = 0) {
   const int n0 = tile * 16;
   if constexpr (EPI == DECODE_EPI_F32) {
     if (mok) *reinterpret_cast<float4*>(e.y + (long long)m * N + n0 + 4 * h) = make_float4(v[0], v[1], v[2], v[3]);
+  } else if constexpr (EPI == DECODE_EPI_XPUSH) {
+    if (mok) {
+      const long long off = XG_FLAG_BYTES + ((long long)(xep & 1u) * e.xp.world + e.xp.rank) * e.xp.slot_bytes +
+                            ((long long)m * N + n0 + 4 * h) * 4;
+      const float4 val = make_float4(v[0], v[1], v[2], v[3]);
+      for (int r = 0; r < e.xp.world; ++r) *reinterpret_cast<float4*>(e.xp.bufs[r] + off) = val;
+    }
   } else if constexpr (EPI == DECODE_EPI_QKV) {
     const int D = 128;
     const int head = n0 / D, jj = (n0 % D) / 16;
@@ -238,6 +259,8 @@ SYM_DEV void gemm_tile(const bf16* __restrict__ x, const bf16* __restrict__ W, i
 
   __shared__ f32x4 red[NW][RT * MT][64];
   __shared__ float rn_s[64];
+  unsigned xep = 0;
+  if constexpr (EPI == DECODE_EPI_XPUSH) xep = xp_epoch(e.xp);
 
   f32x4 acc[RT][MT];
 #pragma unroll
@@ -362,7 +385,13 @@ SYM_DEV void gemm_tile(const bf16* __restrict__ x, const bf16* __restrict__ W, i
     const float sc = (e.ss_in && mok) ? rn_s[m] : 1.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] *= sc;
-    epilogue<EPI>(e, v, tile0 + rt, m, mok, h, N);
+    epilogue<EPI>(e, v, tile0 + rt, m, mok, h, N, xep);
+  }
+  if constexpr (EPI == DECODE_EPI_XPUSH) {  // every wave's slot stores acknowledged, then the tile flags
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int tid = threadIdx.x;
+    if (tid < RT * e.xp.world) xp_flag(e.xp, tid % e.xp.world, tile0 + tid / e.xp.world, xep);
   }
 }
 
@@ -796,6 +825,8 @@ __global__ __launch_bounds__(1024) void decode_gemm_xres_kernel(const bf16* __re
     }
   }
   __shared__ f32x4 red[2][NW][64];
+  unsigned xep = 0;
+  if constexpr (EPI == DECODE_EPI_XPUSH) xep = xp_epoch(e.xp);
   int buf = 0;
   for (;;) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -829,7 +860,11 @@ __global__ __launch_bounds__(1024) void decode_gemm_xres_kernel(const bf16* __re
       const float sc = (e.ss_in && mok) ? rn_s[m] : 1.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] *= sc;
-      epilogue<EPI>(e, v, t, m, mok, h, N);
+      epilogue<EPI>(e, v, t, m, mok, h, N, xep);
+      if constexpr (EPI == DECODE_EPI_XPUSH) {  // wave 0 stored the whole tile: acknowledged, then flag it
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane < e.xp.world) xp_flag(e.xp, lane, t, xep);
+      }
     }
     buf ^= 1;
     if (tn >= ntiles) break;
@@ -972,6 +1007,7 @@ void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int
     case DECODE_EPI_QKV: launch_epi<DECODE_EPI_QKV>(x, W, M, N, K, e, s); break;
     case DECODE_EPI_RESID: launch_epi<DECODE_EPI_RESID>(x, W, M, N, K, e, s); break;
     case DECODE_EPI_SWIGLU: launch_epi<DECODE_EPI_SWIGLU>(x, W, M, N, K, e, s); break;
+    case DECODE_EPI_XPUSH: launch_epi<DECODE_EPI_XPUSH>(x, W, M, N, K, e, s); break;
     default: launch_epi<DECODE_EPI_ARGMAX>(x, W, M, N, K, e, s); break;
   }
 }

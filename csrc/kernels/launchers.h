@@ -9,7 +9,28 @@
 #include "common.h"
 
 // decode_gemm.hip -- fused decode projections (see the file header)
-enum { DECODE_EPI_F32 = 0, DECODE_EPI_QKV = 1, DECODE_EPI_RESID = 2, DECODE_EPI_SWIGLU = 3, DECODE_EPI_ARGMAX = 4 };
+enum {
+  DECODE_EPI_F32 = 0,
+  DECODE_EPI_QKV = 1,
+  DECODE_EPI_RESID = 2,
+  DECODE_EPI_SWIGLU = 3,
+  DECODE_EPI_ARGMAX = 4,
+  DECODE_EPI_XPUSH = 5,  // fp32 tile straight into every TP rank's xGMI slot + a per-tile flag (row-parallel)
+};
+
+// xGMI communicator buffer layout (xgmi_ar.hip): header (collective counter) | flags [XG_MAX_WG][XG_MAX_WORLD]
+// u32 | data [2 parities][world][slot_bytes]
+constexpr int XG_MAX_WORLD = 8;
+constexpr int XG_MAX_WG = 4096;
+constexpr int XG_KEYS_WG = XG_MAX_WG - 1;  // flag word of the sampling-keys collective (others stay below)
+constexpr long long XG_HDR_BYTES = 256;   // [0] collective counter, [32] arrivals of the current collective
+constexpr long long XG_FLAG_BYTES = XG_HDR_BYTES + (long long)XG_MAX_WG * XG_MAX_WORLD * 4;
+// DECODE_EPI_XPUSH target: every rank's mapped buffer; the GEMM reads (never bumps) this rank's counter
+struct XgmiPush {
+  char* bufs[XG_MAX_WORLD] = {};
+  int rank = 0, world = 0;
+  long long slot_bytes = 0;
+};
 struct DecodeEpi {
   // weight layout: 0 = row-major [N][K]; 1 = MFMA-preshuffled (models/layout.py::preshuffle): each
   // 16-row x 32-k block is 1 KB contiguous in lane order, so one load instruction reads 1 KB and a
@@ -44,6 +65,8 @@ struct DecodeEpi {
   const long long* step = nullptr;
   unsigned long long* keys = nullptr;
   int n_offset = 0;
+  // XPUSH (row-parallel projection under TP): y tiles go to slot (parity, rank) of every rank's buffer
+  XgmiPush xp;
 };
 // Persistent decode MLP block (O-proj + residual + ln2 prep -> gate_up + SwiGLU -> down + residual + next
 // norm prep), M <= 16, every K % 512 == 0.  ctl: DECODE_MLP_CTL_INTS ints, zero-initialised once, re-armed by the kernel.
@@ -179,10 +202,8 @@ void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, fl
 void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_lo, int e_hi, const float* w, int T, int k,
                         int d, float* out, int accumulate, hipStream_t s);
 
-// xgmi_ar.hip: one-shot all-reduce over xGMI peer memory (IPC-mapped buffers of every TP rank)
-constexpr int XG_MAX_WORLD = 8;
-constexpr int XG_MAX_WG = 4096;
-constexpr int XG_KEYS_WG = XG_MAX_WG - 1;  // flag word of the sampling-keys collective (others stay below)
+// xgmi_ar.hip: one-shot all-reduce over xGMI peer memory (IPC-mapped buffers of every TP rank); the
+// constants and the push descriptor live at the top of this header (the decode GEMMs push into the slots)
 struct XgmiArgs {
   char* bufs[XG_MAX_WORLD];  // every rank's comm buffer as mapped in this process (own one included; its
                              // header holds this rank's collective counter)
@@ -213,3 +234,8 @@ struct XgmiMulti {
 void launch_xgmi_all_reduce_multi(const XgmiMulti& m, int world, long long n, int elem, hipStream_t s);
 void launch_xgmi_add_prep_multi(const XgmiMulti& m, int world, int T, int d, int parts, hipStream_t s);
 void launch_xgmi_keys_max_multi(const XgmiMulti& m, int world, int B, hipStream_t s);
+// the reduce half of a GEMM-pushed row-parallel all-reduce (DECODE_EPI_XPUSH): wait for every rank's tile
+// flags of this part's columns, sum the slots in rank order + residual add + next-norm prep (add_prep)
+void launch_xgmi_reduce_add_prep(const XgmiArgs& c, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d,
+                                 int parts, hipStream_t s);
+void launch_xgmi_reduce_add_prep_multi(const XgmiMulti& m, int world, int T, int d, int parts, hipStream_t s);

@@ -30,8 +30,6 @@
 
 namespace {
 
-constexpr long long XG_HDR_BYTES = 256;  // [0] collective counter, [32] arrivals of the current collective
-constexpr long long XG_FLAG_BYTES = XG_HDR_BYTES + (long long)XG_MAX_WG * XG_MAX_WORLD * 4;
 constexpr int XG_THREADS = 256;
 constexpr unsigned long long XG_WAIT_TICKS = 200000000ull;  // 2 s of the 100 MHz wall clock: a peer that
                                                             // never arrives is an error, not a hang
@@ -183,6 +181,70 @@ SYM_DEV void xg_add_prep_body(const XgmiArgs& c, int row, int part, int T, int P
   if (threadIdx.x == 0) ss[row * P + part] = acc;
 }
 
+// Reduce half of a GEMM-pushed row-parallel all-reduce: the decode GEMM (DECODE_EPI_XPUSH, same epoch:
+// it reads the counter this kernel bumps) already stored its fp32 [T][d] tile columns into slot (parity,
+// rank) of every rank and raised flag (tile, rank) per 16-column tile.  Workgroup (row, part) waits for
+// every source's flags of the tiles covering its columns, then sums the slots in rank order and applies
+// the residual add + next-norm prep exactly like xg_add_prep_body (bit-identical results on every rank).
+SYM_DEV void xg_reduce_add_prep_body(const XgmiArgs& c, int row, int part, int T, int P, float* __restrict__ resid,
+                                     const bf16* __restrict__ w, bf16* __restrict__ xw, float* __restrict__ ss,
+                                     int d, unsigned long long delay = 0) {
+  __shared__ float scratch[XG_THREADS / 64];
+  const unsigned epoch = xg_epoch(c, T * P);
+  xg_delay(delay);
+  const int par = (int)(epoch & 1u);
+  const int dp = d / P;
+  const int t0 = part * dp / 16, nt = dp / 16;
+  const unsigned* flags = reinterpret_cast<const unsigned*>(c.bufs[c.rank] + XG_HDR_BYTES);
+  for (int i = threadIdx.x; i < nt * c.world; i += XG_THREADS) {
+    const int tile = t0 + i / c.world, src = i % c.world;
+    const unsigned* f = flags + tile * XG_MAX_WORLD + src;
+    const unsigned long long w0 = wall_clock64();
+    while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      if (wall_clock64() - w0 > XG_WAIT_TICKS) {
+        __hip_atomic_store(c.err, 1 + src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  const long long rb = (long long)row * d + (long long)part * dp;
+  const long long off = rb * 4;
+  const bf16* wp = w + (long long)part * dp;
+  float acc = 0.f;
+  for (int vi = threadIdx.x; vi < dp / 8; vi += XG_THREADS) {
+    float r[8], g[8];
+    float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < c.world; ++s) {
+      float dd[8];
+      load8f(reinterpret_cast<const float*>(xg_slot(c, c.rank, par, s) + off) + vi * 8, dd);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sum[i] += dd[i];
+    }
+    load8f(resid + rb + vi * 8, r);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] += sum[i];
+    store8f(resid + rb + vi * 8, r);
+    load8(wp + vi * 8, g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      acc += r[i] * r[i];
+      g[i] *= r[i];
+    }
+    store8(xw + rb + vi * 8, g);
+  }
+  acc = block_sum<XG_THREADS>(acc, scratch);
+  if (threadIdx.x == 0) ss[row * P + part] = acc;
+}
+
+__global__ __launch_bounds__(XG_THREADS) void xgmi_reduce_add_prep_kernel(XgmiArgs c, float* __restrict__ resid,
+                                                                         const bf16* __restrict__ w,
+                                                                         bf16* __restrict__ xw,
+                                                                         float* __restrict__ ss, int d) {
+  xg_reduce_add_prep_body(c, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, resid, w, xw, ss, d);
+}
+
 // Vocab-parallel greedy / Gumbel sampling combine: every rank holds per-row packed u64 keys (order-
 // preserving value bits | inverted vocabulary index) of its vocabulary shard; the max over ranks is the
 // global argmax, and ids = 0xFFFFFFFF - low 32 bits.  One workgroup (rows <= 4096) on flag word XG_KEYS_WG.
@@ -239,6 +301,12 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_add_prep_multi_kernel(XgmiMul
                    xg_multi_delay(m, r));
 }
 
+__global__ __launch_bounds__(XG_THREADS) void xgmi_reduce_add_prep_multi_kernel(XgmiMulti m, int d) {
+  const int r = blockIdx.z;
+  xg_reduce_add_prep_body(m.c[r], blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, reinterpret_cast<float*>(m.out[r]),
+                          m.w, reinterpret_cast<bf16*>(m.xw[r]), m.ss[r], d, xg_multi_delay(m, r));
+}
+
 __global__ __launch_bounds__(XG_THREADS) void xgmi_keys_max_multi_kernel(XgmiMulti m, int B) {
   const int r = blockIdx.z;
   xg_keys_max_body(m.c[r], reinterpret_cast<const unsigned long long*>(m.in[r]), reinterpret_cast<int*>(m.out[r]), B,
@@ -292,6 +360,17 @@ void launch_xgmi_all_reduce_multi(const XgmiMulti& m, int world, long long n, in
 void launch_xgmi_add_prep_multi(const XgmiMulti& m, int world, int T, int d, int parts, hipStream_t s) {
   if (T == 0) return;
   xgmi_add_prep_multi_kernel<<<dim3(T, parts, world), XG_THREADS, 0, s>>>(m, d);
+}
+
+void launch_xgmi_reduce_add_prep(const XgmiArgs& c, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d,
+                                 int parts, hipStream_t s) {
+  if (T == 0) return;
+  xgmi_reduce_add_prep_kernel<<<dim3(T, parts), XG_THREADS, 0, s>>>(c, resid, w, xw, ss, d);
+}
+
+void launch_xgmi_reduce_add_prep_multi(const XgmiMulti& m, int world, int T, int d, int parts, hipStream_t s) {
+  if (T == 0) return;
+  xgmi_reduce_add_prep_multi_kernel<<<dim3(T, parts, world), XG_THREADS, 0, s>>>(m, d);
 }
 
 void launch_xgmi_keys_max_multi(const XgmiMulti& m, int world, int B, hipStream_t s) {

@@ -25,6 +25,8 @@ issues exactly two per layer and keeps them inside the captured graph.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -176,6 +178,9 @@ class XgmiComm(Comm):
         dev = torch.device(device)
         self.slot_bytes = int(slot_bytes)
         self.calls = {"all_reduce": 0, "add_prep": 0}  # collectives issued on the xGMI kernels (host count)
+        # row-parallel decode projections push their tiles from the GEMM epilogue (SYMMETRY_XGMI_PUSH=0: GEMM
+        # into a local fp32 buffer + the fused all-reduce / add_prep launch)
+        self.push = os.environ.get("SYMMETRY_XGMI_PUSH", "1") != "0"
         try:
             self.handle = int(self.ops.xgmi_create(int(slot_bytes), self.world, self.rank, dev.index or 0))
             mine = self.ops.xgmi_ipc_handle(self.handle)
@@ -209,6 +214,20 @@ class XgmiComm(Comm):
             self.calls["add_prep"] += 1
         else:
             super().all_reduce_add_prep(y, resid, w_next, xw, ss)
+
+    def gemm_add_prep(self, x, W, wshuf, resid, w_next, xw, ss) -> bool:
+        """Row-parallel decode projection + all-reduce + residual add + next-norm prep as ONE GEMM launch
+        whose epilogue pushes its fp32 tiles into every rank's slot, then one reduce launch
+        (``xgmi_gemm_add_prep``).  Returns False when the shapes do not fit (the caller runs GEMM + add_prep)."""
+        if not self.push or not x.is_cuda or x.shape[0] > 64 or W.shape[0] % 16 or x.shape[1] % 256:
+            return False
+        P = ss.shape[1] if ss.dim() == 2 else 1
+        d = resid.shape[1]
+        if x.shape[0] * d * 4 > self.slot_bytes or d % (16 * P) or W.shape[0] != d:
+            return False
+        self.ops.xgmi_gemm_add_prep(x, W, bool(wshuf), resid, w_next, xw, ss, self.handle)
+        self.calls["gemm_add_prep"] = self.calls.get("gemm_add_prep", 0) + 1
+        return True
 
     def argmax_keys(self, keys, ids):
         if keys.is_cuda and keys.is_contiguous() and keys.numel() <= 4096:
