@@ -24,7 +24,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
-PUSH = os.environ.get("SYMMETRY_XGMI_PUSH", "1") != "0"
+PUSH = os.environ.get("SYMMETRY_XGMI_PUSH", "0") == "1"
 
 
 class LocalXgmi:

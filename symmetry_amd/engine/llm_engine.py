@@ -62,6 +62,12 @@ class EngineConfig:
     # a burst of >= 4 prompts totalling >= this many tokens, arriving while nothing decodes, prefills its
     # first n // 2 + 1 prompts in one step and the rest in the next (0 = one step for the whole burst)
     burst_split_tokens: int = int(os.environ.get("SYMMETRY_BURST_SPLIT", "1024"))
+    # an idle engine that receives a request waits until no further request has arrived for
+    # arrival_quiet_us (at most arrival_window_us) before its first step, so requests sent together by many
+    # clients -- spread over a millisecond or two by the network and the per-peer decryption -- prefill as one
+    # burst instead of one lone prompt followed by the rest (0 = off)
+    arrival_quiet_us: int = int(os.environ.get("SYMMETRY_ARRIVAL_QUIET_US", "300"))
+    arrival_window_us: int = int(os.environ.get("SYMMETRY_ARRIVAL_WINDOW_US", "2000"))
     model_config: ModelConfig | None = None
 
     @classmethod
@@ -78,7 +84,8 @@ class EngineConfig:
              "useGraphs": "use_graphs", "numKvBlocks": "num_kv_blocks", "decodeWeights": "decode_weights",
              "prefillChunk": "mixed_prefill_tokens",
              "persistentMlp": "persistent_mlp", "fusedAttnBlock": "fused_attn_block",
-             "enablePrefixCaching": "enable_prefix_caching", "burstSplitTokens": "burst_split_tokens"}
+             "enablePrefixCaching": "enable_prefix_caching", "burstSplitTokens": "burst_split_tokens",
+             "arrivalQuietUs": "arrival_quiet_us", "arrivalWindowUs": "arrival_window_us"}
         for k, attr in m.items():
             if cfg.get(k) is not None:
                 cur, val = getattr(ec, attr), cfg[k]
@@ -151,6 +158,7 @@ class LLMEngine:
                                   tp_rank=cfg.tp_rank, tp_size=cfg.tp_size, cpu_group=cpu_group,
                                   max_num_tokens=max(cfg.max_num_batched_tokens, 8192))
         self.requests: dict[str, tuple] = {}
+        self.last_arrival = 0.0  # perf_counter of the latest add_request (arrival coalescing)
         self.lock = threading.Lock()
         self._inflight: dict | None = None
         self._last_done = 0.0
@@ -222,6 +230,7 @@ class LLMEngine:
             self.scheduler.add(seq)
             self.requests[request_id] = (seq, IncrementalDetokenizer(self.tokenizer), callback)
             self.metrics.on_arrival()
+            self.last_arrival = time.perf_counter()
         return seq
 
     def add_chat_request(self, request_id: str, messages: list, params: SamplingParams | None = None,
@@ -465,13 +474,31 @@ class AsyncEngine:
             self._thread.start()
 
     def _loop(self) -> None:
+        idle = True
         while not self._stop:
             if not self.engine.has_unfinished():
+                idle = True
                 self._wake.wait(0.05)
                 self._wake.clear()
                 continue
+            if idle:
+                self._coalesce()
+                idle = False
             self.engine.step()
             self._flush()
+
+    def _coalesce(self) -> None:
+        """Idle -> busy: let a burst of simultaneous requests finish arriving (EngineConfig.arrival_*)."""
+        cfg = self.engine.cfg
+        quiet, window = cfg.arrival_quiet_us * 1e-6, cfg.arrival_window_us * 1e-6
+        if quiet <= 0:
+            return
+        t0 = time.perf_counter()
+        while not self._stop:
+            now = time.perf_counter()
+            if now - self.engine.last_arrival >= quiet or now - t0 >= window:
+                return
+            time.sleep(min(quiet, 1e-4))
 
     def _flush(self) -> None:
         """Hand this step's outputs to their event loops, one call per loop."""

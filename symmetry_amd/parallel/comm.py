@@ -178,9 +178,12 @@ class XgmiComm(Comm):
         dev = torch.device(device)
         self.slot_bytes = int(slot_bytes)
         self.calls = {"all_reduce": 0, "add_prep": 0}  # collectives issued on the xGMI kernels (host count)
-        # row-parallel decode projections push their tiles from the GEMM epilogue (SYMMETRY_XGMI_PUSH=0: GEMM
-        # into a local fp32 buffer + the fused all-reduce / add_prep launch)
-        self.push = os.environ.get("SYMMETRY_XGMI_PUSH", "1") != "0"
+        # SYMMETRY_XGMI_PUSH=1: row-parallel decode projections push their tiles into the peers' slots from the
+        # GEMM epilogue (+ one reduce launch) instead of GEMM into a local fp32 buffer + the fused all-reduce /
+        # add_prep launch.  Off by default: on one GPU (world-1 communicator, no link latency) it measured
+        # 1.535 vs 1.522 ms per TP=8-shard step (profiles/r3/tp_shard_push_ab.jsonl); its point -- the remote
+        # stores overlapping the GEMM -- needs real xGMI links to show
+        self.push = os.environ.get("SYMMETRY_XGMI_PUSH", "0") == "1"
         try:
             self.handle = int(self.ops.xgmi_create(int(slot_bytes), self.world, self.rank, dev.index or 0))
             mine = self.ops.xgmi_ipc_handle(self.handle)

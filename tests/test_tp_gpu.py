@@ -48,16 +48,20 @@ def _entry(model, rank, world, port, q, xgmi="0"):
             eng.runner.worker_loop()
             q.put((rank, None))
             return
-        seqs = [eng.add_request(f"t{i}", p, SamplingParams(max_tokens=10, ignore_eos=True))
-                for i, p in enumerate(PROMPTS)]
-        while eng.has_unfinished():
-            eng.step()
+        try:
+            seqs = [eng.add_request(f"t{i}", p, SamplingParams(max_tokens=10, ignore_eos=True))
+                    for i, p in enumerate(PROMPTS)]
+            while eng.has_unfinished():
+                eng.step()
+        finally:
+            eng.shutdown()  # the worker leaves its loop whatever happened here
         if xgmi == "1":
             calls = eng.runner.model.tp.calls
-            assert calls["add_prep"] > 0, calls  # decode steps ran the fused peer-memory all-reduce
+            # decode steps ran the peer-memory all-reduce: fused into the row-parallel GEMMs (XPUSH epilogue
+            # + reduce launch) for the dense model, the fused add_prep kernel around the MoE block
+            assert calls.get("gemm_add_prep", 0) + calls["add_prep"] > 0, calls
             assert calls.get("keys", 0) > 0, calls  # and the vocab-parallel sampling combine
             assert eng.runner.model.tp.error() == 0
-        eng.shutdown()
         q.put((rank, [s.output_ids for s in seqs]))
     except Exception:
         q.put((rank, traceback.format_exc()))
