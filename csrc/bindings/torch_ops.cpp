@@ -492,17 +492,44 @@ struct DGShape {
   int64_t M, N, K;
 };
 
-DGShape dg_check(const Tensor& x, const Tensor& W) {
+DGShape dg_check(const Tensor& x, const Tensor& W, bool mg = false) {
   check_gpu(x, "x");
   check_gpu(W, "W");
   check_dtype(x, at::kBFloat16, "x");
   check_dtype(W, at::kBFloat16, "W");
   TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && x.size(1) == W.size(1), "decode_gemm: x [M,K], W [N,K]");
   const int64_t M = x.size(0), K = x.size(1), N = W.size(0);
-  TORCH_CHECK(M >= 1 && M <= 64, "decode_gemm: M must be in [1, 64]");
+  TORCH_CHECK(M >= 1 && M <= (mg ? 256 : 64), "decode_gemm: M must be in [1, 64] (mgemm: 256)");
   TORCH_CHECK(N % 16 == 0, "decode_gemm: N % 16");
-  TORCH_CHECK(K % 256 == 0, "decode_gemm: K must be a multiple of 256 (4 waves x 64)");
+  TORCH_CHECK(K % (mg ? 64 : 256) == 0, "decode_gemm: K must be a multiple of 256 (4 waves x 64)");
   return {M, N, K};
+}
+
+// The decode GEMM (M <= 64) or, with an mgemm slab given, the medium-M GEMM with the same fused epilogue
+// (in-launch split-K reduction; weights MFMA-preshuffled): slab [S, M, N] fp32 scratch, counters [N / (64 rw)]
+// ints zeroed once (re-armed by the kernel).
+void launch_dg(int epi, const Tensor& x, const Tensor& W, const DGShape& sh, DecodeEpi& e,
+               const c10::optional<Tensor>& slab, const c10::optional<Tensor>& counters, int64_t rw) {
+  const at::OptionalDeviceGuard g(x.device());
+  if (!slab.has_value()) {
+    launch_decode_gemm(epi, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, e, cur_stream(x));
+    return;
+  }
+  TORCH_CHECK(e.wshuf, "mgemm epilogue: the weights must be the MFMA-preshuffled copy");
+  TORCH_CHECK(counters.has_value(), "mgemm epilogue: counters required");
+  check_gpu(*slab, "slab");
+  check_dtype(*slab, at::kFloat, "slab");
+  check_gpu(*counters, "counters");
+  check_dtype(*counters, at::kInt, "counters");
+  const int64_t S = slab->dim() == 3 ? slab->size(0) : 0;
+  TORCH_CHECK(S >= 1 && slab->size(1) == sh.M && slab->size(2) == sh.N && slab->is_contiguous(),
+              "mgemm epilogue: slab [S, M, N]");
+  TORCH_CHECK(rw >= 1 && rw <= 4 && (sh.M <= 128 || rw <= 2) && sh.N % (64 * rw) == 0 && sh.K % (S * 64) == 0,
+              "mgemm epilogue: rw / split shape");
+  TORCH_CHECK(counters->numel() >= sh.N / (64 * rw), "mgemm epilogue: counters too small");
+  TORCH_CHECK((sh.M + 255) * sh.K * 2 < (1LL << 31) && sh.N * sh.K * 2 < (1LL << 31), "mgemm: operands exceed 2 GB");
+  launch_mgemm_epi(epi, ptr<bf16>(x), ptr<bf16>(W), ptr<float>(*slab), (int)sh.M, (int)sh.N, (int)sh.K, (int)S,
+                   (int)rw, e, ptr<int>(*counters), cur_stream(x));
 }
 
 void dg_norm_in(DecodeEpi& e, const c10::optional<Tensor>& ss_in, int64_t M, int64_t K, double eps) {
@@ -531,8 +558,9 @@ void dg_f32(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in
 
 void dg_qkv(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, const Tensor& positions,
             const Tensor& slots, const Tensor& cos_sin, Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t Hq,
-            int64_t Hkv, bool wshuf) {
-  auto sh = dg_check(x, W);
+            int64_t Hkv, bool wshuf, const c10::optional<Tensor>& mg_slab, const c10::optional<Tensor>& mg_counters,
+            int64_t mg_rw) {
+  auto sh = dg_check(x, W, mg_slab.has_value());
   for (auto* t : {&positions, &slots}) {
     check_gpu(*t, "index tensor");
     check_dtype(*t, at::kInt, "index tensor");
@@ -559,12 +587,12 @@ void dg_qkv(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in
   e.Hq = (int)Hq;
   e.Hkv = (int)Hkv;
   e.BS = (int)k_cache.size(2);
-  const at::OptionalDeviceGuard g(x.device());
-  launch_decode_gemm(DECODE_EPI_QKV, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, e, cur_stream(x));
+  launch_dg(DECODE_EPI_QKV, x, W, sh, e, mg_slab, mg_counters, mg_rw);
 }
 
-void dg_resid(const Tensor& x, const Tensor& W, Tensor& resid, const Tensor& w_next, Tensor& xw_out, Tensor& ss_out, bool wshuf) {
-  auto sh = dg_check(x, W);
+void dg_resid(const Tensor& x, const Tensor& W, Tensor& resid, const Tensor& w_next, Tensor& xw_out, Tensor& ss_out, bool wshuf,
+              const c10::optional<Tensor>& mg_slab, const c10::optional<Tensor>& mg_counters, int64_t mg_rw) {
+  auto sh = dg_check(x, W, mg_slab.has_value());
   check_gpu(resid, "resid");
   check_dtype(resid, at::kFloat, "resid");
   check_gpu(w_next, "w_next");
@@ -582,12 +610,12 @@ void dg_resid(const Tensor& x, const Tensor& W, Tensor& resid, const Tensor& w_n
   e.w_next = ptr<bf16>(w_next);
   e.xw_out = ptr<bf16>(xw_out);
   e.ss_out = ptr<float>(ss_out);
-  const at::OptionalDeviceGuard g(x.device());
-  launch_decode_gemm(DECODE_EPI_RESID, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, e, cur_stream(x));
+  launch_dg(DECODE_EPI_RESID, x, W, sh, e, mg_slab, mg_counters, mg_rw);
 }
 
-void dg_swiglu(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, Tensor& act, bool wshuf) {
-  auto sh = dg_check(x, W);
+void dg_swiglu(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, Tensor& act, bool wshuf,
+               const c10::optional<Tensor>& mg_slab, const c10::optional<Tensor>& mg_counters, int64_t mg_rw) {
+  auto sh = dg_check(x, W, mg_slab.has_value());
   check_gpu(act, "act");
   check_dtype(act, at::kBFloat16, "act");
   TORCH_CHECK(act.numel() == sh.M * sh.N / 2, "dg_swiglu: act must be [M, N/2]");
@@ -595,9 +623,7 @@ void dg_swiglu(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss
   e.wshuf = wshuf ? 1 : 0;
   dg_norm_in(e, ss_in, sh.M, sh.K, eps);
   e.act = ptr<bf16>(act);
-  const at::OptionalDeviceGuard g(x.device());
-  launch_decode_gemm(DECODE_EPI_SWIGLU, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, e,
-                     cur_stream(x));
+  launch_dg(DECODE_EPI_SWIGLU, x, W, sh, e, mg_slab, mg_counters, mg_rw);
 }
 
 void dg_argmax(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, const Tensor& temps,
@@ -930,11 +956,17 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("dg_f32(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor(a!) y, bool wshuf=False) -> ()", &dg_f32);
   m.def(
       "dg_qkv(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor positions, Tensor slots, Tensor cos_sin, "
-      "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, bool wshuf=False) -> ()",
+      "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, bool wshuf=False, "
+      "Tensor(d!)? mg_slab=None, Tensor(e!)? mg_counters=None, int mg_rw=0) -> ()",
       &dg_qkv);
-  m.def("dg_resid(Tensor x, Tensor W, Tensor(a!) resid, Tensor w_next, Tensor(b!) xw_out, Tensor(c!) ss_out, bool wshuf=False) -> ()",
-        &dg_resid);
-  m.def("dg_swiglu(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor(a!) act, bool wshuf=False) -> ()", &dg_swiglu);
+  m.def(
+      "dg_resid(Tensor x, Tensor W, Tensor(a!) resid, Tensor w_next, Tensor(b!) xw_out, Tensor(c!) ss_out, "
+      "bool wshuf=False, Tensor(d!)? mg_slab=None, Tensor(e!)? mg_counters=None, int mg_rw=0) -> ()",
+      &dg_resid);
+  m.def(
+      "dg_swiglu(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor(a!) act, bool wshuf=False, "
+      "Tensor(d!)? mg_slab=None, Tensor(e!)? mg_counters=None, int mg_rw=0) -> ()",
+      &dg_swiglu);
   m.def(
       "dg_argmax(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor temps, Tensor seeds, Tensor step, "
       "Tensor(a!) tile_keys, Tensor(b!) out_keys, Tensor(c!) out_ids, int n_offset, Tensor(d!)? logits, bool wshuf=False) -> ()",

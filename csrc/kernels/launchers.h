@@ -141,6 +141,11 @@ void launch_rownorm(const bf16* xw, const float* ss, int ss_tiles, float eps, bf
 // mgemm.hip -- medium-M (65..256 tokens) projection into fp32 split-K slabs y[S][M][N]; W is the
 // MFMA-preshuffled weight copy, 64 * rw | N, 64 * S | K
 void launch_mgemm(const bf16* x, const bf16* Wshuf, float* y, int M, int N, int K, int S, int rw, hipStream_t s);
+// mgemm with a fused consumer epilogue (DECODE_EPI_QKV / RESID / SWIGLU / F32 of decode_epi.h): y is the
+// [S][M][N] fp32 slab scratch (S > 1: in-launch split-K reduction by the last workgroup of each column group),
+// counters [N / (64 rw)] ints, zero before the first launch (re-armed by the kernel)
+void launch_mgemm_epi(int epi, const bf16* x, const bf16* Wshuf, float* y, int M, int N, int K, int S, int rw,
+                      const DecodeEpi& e, int* counters, hipStream_t s);
 void set_mgemm_nt(int on);  // non-temporal weight DMA (A/B knob)
 
 // norm.hip

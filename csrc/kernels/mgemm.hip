@@ -24,6 +24,7 @@
 //   * the 16x16 accumulator of (weight tile, token tile) holds 4 consecutive features of one token per
 //     lane: one float4 store per accumulator into the slab.
 #include "common.h"
+#include "decode_epi.h"
 #include "launchers.h"
 
 namespace {
@@ -62,9 +63,17 @@ struct MgCfg {
 
 // MT: 16-token tiles (M <= 16 MT); RW: 16-row weight tiles per wave.  Weights MFMA-preshuffled
 // (models/layout.py::preshuffle): block (t, kb) = 16 rows x 32 k, 1 KB in fragment order.
-template <int MT, int RW, bool WNT>
+// EPI < 0: the k split's fp32 slab is the output (the consumer kernel sums the slabs).  EPI >= 0: a fused
+// consumer (decode_epi.h): with one split the accumulators go straight to epilogue<EPI>; with S splits every
+// workgroup stores its slab, and the LAST of the S workgroups of a column group (agent-scope release /
+// acquire around a per-group counter, cdna_hip_programming.md §5 "In-launch split-K reduction") sums the S
+// slabs of its columns in the accumulator layout, applies the deferred-RMSNorm row scale (e.ss_in) and runs
+// the epilogue -- the separate rope_cache / add+RMSNorm / SwiGLU launches of the slab path disappear.
+// `counters` [N / (64 RW)] start at zero and are re-armed by the last arriver (graph-replay safe).
+template <int MT, int RW, bool WNT, int EPI>
 __global__ __launch_bounds__(MG_THR, 1) void mgemm_kernel(const bf16* __restrict__ x, const bf16* __restrict__ W,
-                                                           float* __restrict__ y, int M, int N, int K, int kslice) {
+                                                           float* __restrict__ y, int M, int N, int K, int kslice,
+                                                           DecodeEpi e, int* __restrict__ counters) {
   using C = MgCfg<MT, RW>;
   __shared__ __attribute__((aligned(1024))) char smem[C::SLOTS * C::SLOT];
   asm volatile("" ::: "a0");  // accumulators may live in AGPRs
@@ -155,43 +164,122 @@ __global__ __launch_bounds__(MG_THR, 1) void mgemm_kernel(const bf16* __restrict
   }
 
   // ---- epilogue: lane holds features 16 t + 4 (lane >> 4) .. + 3 of token 16 mt + (lane & 15)
+  const int S = gridDim.y;
   float* ys = y + (long long)split * M * N;
+  if (EPI < 0 || S > 1) {
 #pragma unroll
-  for (int rt = 0; rt < RW; ++rt) {
-    const int n = 16 * (tile0 + rt) + 4 * (lane >> 4);
+    for (int rt = 0; rt < RW; ++rt) {
+      const int n = 16 * (tile0 + rt) + 4 * (lane >> 4);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int m = 16 * mt + (lane & 15);
-      if (m < M)
-        *reinterpret_cast<float4*>(ys + (long long)m * N + n) =
-            make_float4(acc[rt][mt][0], acc[rt][mt][1], acc[rt][mt][2], acc[rt][mt][3]);
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = 16 * mt + (lane & 15);
+        if (m < M)
+          *reinterpret_cast<float4*>(ys + (long long)m * N + n) =
+              make_float4(acc[rt][mt][0], acc[rt][mt][1], acc[rt][mt][2], acc[rt][mt][3]);
+      }
+    }
+  }
+  if constexpr (EPI >= 0) {
+    // LDS ring is free once every wave is past its last compute: row scales + the "last arriver" word
+    __syncthreads();
+    float* rn = reinterpret_cast<float*>(smem);
+    int* last = reinterpret_cast<int*>(smem + 1024 * 4);
+    if (S > 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores are out
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int got = __hip_atomic_fetch_add(counters + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int is_last = got == S - 1;
+        if (is_last) {
+          __hip_atomic_store(counters + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *last = is_last;
+      }
+      __syncthreads();
+      if (!*last) return;
+    }
+    // deferred-RMSNorm row scales of the input rows (the producer's sum-of-squares partials)
+    if (e.ss_in) {
+      for (int m = wid; m < M; m += 4) {
+        float sacc = 0.f;
+        for (int i = lane; i < e.ss_tiles; i += 64) sacc += e.ss_in[(long long)m * e.ss_tiles + i];
+        sacc = wave_sum(sacc);
+        if (lane == 0) rn[m] = rsqrtf(sacc * e.inv_d + e.eps);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int rt = 0; rt < RW; ++rt) {
+      const int n = 16 * (tile0 + rt) + 4 * (lane >> 4);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = 16 * mt + (lane & 15);
+        const bool mok = m < M;
+        f32x4 v = acc[rt][mt];
+        if (S > 1) {
+          v = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (mok)
+            for (int sp = 0; sp < S; ++sp) {  // fixed split order: bitwise reproducible
+              const float4 p = *reinterpret_cast<const float4*>(y + ((long long)sp * M + m) * N + n);
+              v[0] += p.x;
+              v[1] += p.y;
+              v[2] += p.z;
+              v[3] += p.w;
+            }
+        }
+        const float sc = (e.ss_in && mok) ? rn[m] : 1.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] *= sc;
+        epilogue<EPI>(e, v, tile0 + rt, m, mok, lane >> 4, N);
+      }
     }
   }
 }
 
 int g_mgemm_nt = 0;
 
-template <int MT, int RW>
-void launch_mt_rw(const bf16* x, const bf16* W, float* y, int M, int N, int K, int S, hipStream_t s) {
-  if (g_mgemm_nt)
-    mgemm_kernel<MT, RW, true><<<dim3(N / (64 * RW), S), dim3(MG_THR), 0, s>>>(x, W, y, M, N, K, K / S);
+template <int MT, int RW, int EPI>
+void launch_mt_rw(const bf16* x, const bf16* W, float* y, int M, int N, int K, int S, const DecodeEpi& e,
+                  int* counters, hipStream_t s) {
+  if (g_mgemm_nt && EPI < 0)
+    mgemm_kernel<MT, RW, true, EPI><<<dim3(N / (64 * RW), S), dim3(MG_THR), 0, s>>>(x, W, y, M, N, K, K / S, e,
+                                                                                   counters);
   else
-    mgemm_kernel<MT, RW, false><<<dim3(N / (64 * RW), S), dim3(MG_THR), 0, s>>>(x, W, y, M, N, K, K / S);
+    mgemm_kernel<MT, RW, false, EPI><<<dim3(N / (64 * RW), S), dim3(MG_THR), 0, s>>>(x, W, y, M, N, K, K / S, e,
+                                                                                    counters);
 }
 
-template <int MT>
-void launch_mt(const bf16* x, const bf16* W, float* y, int M, int N, int K, int S, int rw, hipStream_t s) {
+template <int MT, int EPI>
+void launch_mt(const bf16* x, const bf16* W, float* y, int M, int N, int K, int S, int rw, const DecodeEpi& e,
+               int* counters, hipStream_t s) {
   if constexpr (MT > 8) {  // 256 rows: at most 2 weight tiles per wave (accumulators + LDS ring)
-    if (rw == 1) launch_mt_rw<MT, 1>(x, W, y, M, N, K, S, s);
-    else launch_mt_rw<MT, 2>(x, W, y, M, N, K, S, s);
+    if (rw == 1) launch_mt_rw<MT, 1, EPI>(x, W, y, M, N, K, S, e, counters, s);
+    else launch_mt_rw<MT, 2, EPI>(x, W, y, M, N, K, S, e, counters, s);
     return;
   }
   switch (rw) {
-    case 1: launch_mt_rw<MT, 1>(x, W, y, M, N, K, S, s); break;
-    case 3: launch_mt_rw<MT, 3>(x, W, y, M, N, K, S, s); break;
-    case 4: launch_mt_rw<MT, 4>(x, W, y, M, N, K, S, s); break;
-    default: launch_mt_rw<MT, 2>(x, W, y, M, N, K, S, s); break;
+    case 1: launch_mt_rw<MT, 1, EPI>(x, W, y, M, N, K, S, e, counters, s); break;
+    case 3: launch_mt_rw<MT, 3, EPI>(x, W, y, M, N, K, S, e, counters, s); break;
+    case 4: launch_mt_rw<MT, 4, EPI>(x, W, y, M, N, K, S, e, counters, s); break;
+    default: launch_mt_rw<MT, 2, EPI>(x, W, y, M, N, K, S, e, counters, s); break;
   }
+}
+
+template <int EPI>
+void launch_epi_m(const bf16* x, const bf16* W, float* y, int M, int N, int K, int S, int rw, const DecodeEpi& e,
+                  int* counters, hipStream_t s) {
+  if (M <= 32)
+    launch_mt<2, EPI>(x, W, y, M, N, K, S, rw, e, counters, s);
+  else if (M <= 64)
+    launch_mt<4, EPI>(x, W, y, M, N, K, S, rw, e, counters, s);
+  else if (M <= 128)
+    launch_mt<8, EPI>(x, W, y, M, N, K, S, rw, e, counters, s);
+  else
+    launch_mt<16, EPI>(x, W, y, M, N, K, S, rw, e, counters, s);
 }
 
 }  // namespace
@@ -199,12 +287,15 @@ void launch_mt(const bf16* x, const bf16* W, float* y, int M, int N, int K, int 
 void set_mgemm_nt(int on) { g_mgemm_nt = on; }
 
 void launch_mgemm(const bf16* x, const bf16* Wshuf, float* y, int M, int N, int K, int S, int rw, hipStream_t s) {
-  if (M <= 32)
-    launch_mt<2>(x, Wshuf, y, M, N, K, S, rw, s);
-  else if (M <= 64)
-    launch_mt<4>(x, Wshuf, y, M, N, K, S, rw, s);
-  else if (M <= 128)
-    launch_mt<8>(x, Wshuf, y, M, N, K, S, rw, s);
-  else
-    launch_mt<16>(x, Wshuf, y, M, N, K, S, rw, s);
+  launch_epi_m<-1>(x, Wshuf, y, M, N, K, S, rw, DecodeEpi{}, nullptr, s);
+}
+
+void launch_mgemm_epi(int epi, const bf16* x, const bf16* Wshuf, float* y, int M, int N, int K, int S, int rw,
+                      const DecodeEpi& e, int* counters, hipStream_t s) {
+  switch (epi) {
+    case DECODE_EPI_QKV: launch_epi_m<DECODE_EPI_QKV>(x, Wshuf, y, M, N, K, S, rw, e, counters, s); break;
+    case DECODE_EPI_RESID: launch_epi_m<DECODE_EPI_RESID>(x, Wshuf, y, M, N, K, S, rw, e, counters, s); break;
+    case DECODE_EPI_SWIGLU: launch_epi_m<DECODE_EPI_SWIGLU>(x, Wshuf, y, M, N, K, S, rw, e, counters, s); break;
+    default: launch_epi_m<DECODE_EPI_F32>(x, Wshuf, y, M, N, K, S, rw, e, counters, s); break;
+  }
 }

@@ -66,6 +66,10 @@ MAX_STEP_SEQS = 4096  # sequences per step (rows of last_ids)
 ATTN_PREFETCH_WGS = int(os.environ.get("SYMMETRY_ATTN_PREFETCH", "0"))
 # decode steps on the general path run rope_cache's per-row form (A/B knob)
 ROPE_DECODE_ROWS = os.environ.get("SYMMETRY_ROPE_DECODE_ROWS", "1") != "0"
+# decode steps on the general path run their four projections on mgemm with the fused decode epilogues
+# (in-launch split-K reduction; RoPE + KV write, residual + norm prep, SwiGLU in the GEMM) when every
+# projection has an mgemm pick: 5 launches per layer instead of 9 (0 = the slab + consumer-kernel path)
+MG_FUSED = os.environ.get("SYMMETRY_MG_FUSED", "1") != "0"
 
 
 @dataclass
@@ -297,7 +301,30 @@ class TransformerLM:
         """Run one step; returns sampled token ids [num_seqs] int32 (device)."""
         if self.fused and b.num_tokens <= SKINNY_MAX_M and not self._general_rows(b.num_tokens):
             return self._forward_fused(b, kv)
+        mgs = self._mg_plan(b)
+        if mgs is not None:
+            return self._forward_general_fused(b, kv, mgs)
         return self._forward_general(b, kv)
+
+    def _mg_plan(self, b: ForwardBatch):
+        """mgemm (rw, split) + scratch per projection for the fused general path, or None."""
+        if not (MG_FUSED and b.kind == "decode" and self.dgw and self.device.type != "cpu" and not self.cfg.is_moe
+                and not self._tp_active() and b.num_tokens <= 256):
+            return None
+        T, d, dq = b.num_tokens, self.cfg.hidden_size, self.hq * self.D
+        wgu = self.w.layer(0, "w_gu")
+        shapes = {"qkv": (self.w.layer(0, "wqkv").shape[0], d), "o": (d, dq), "gu": (wgu.shape[0], d),
+                  "down": (d, wgu.shape[0] // 2)}
+        plan = {}
+        for name, (N, K) in shapes.items():
+            pick = ops.choose_mgemm(T, N, K)
+            if pick is None:
+                return None
+            rw, S = pick
+            slab = self._buf("mg.slab", (S, T, N), torch.float32)
+            cnt = self.ws.get("mg.cnt." + name, (N // 64,), torch.int32, self.device, zeros=True)
+            plan[name] = (slab, cnt, rw)
+        return plan
 
     def _general_rows(self, T: int) -> bool:
         """Steps of GENERAL_ROWS..64 rows take the general path (medium-M projections + consumer kernels)
@@ -414,6 +441,45 @@ class TransformerLM:
         ops.dg_argmax(xl, w["lm_head"], sl, eps, b.temps, b.seeds, b.step, tk, keys, ids,
                       self.tp_rank * self.vocab_shard, logits)
         return self._finish_sampling(b, ids, keys, logits)
+
+    def _forward_general_fused(self, b: ForwardBatch, kv: KVCache, mgs: dict) -> torch.Tensor:
+        """Decode steps of 20..256 rows: the fused path's dataflow (deferred RMSNorm, epilogues in the GEMMs) on
+        the medium-M GEMM -- qkv (+ RoPE, paged K/V write) -> attention -> o (+ residual, ln2 prep) -> gate_up
+        (+ SwiGLU) -> down (+ residual, next-ln1 prep), each projection ONE mgemm launch whose last k-split
+        workgroup per column group reduces the fp32 split slabs and runs the epilogue."""
+        cfg, w = self.cfg, self.w
+        T, d, eps = b.num_tokens, cfg.hidden_size, cfg.rms_eps
+        resid = self._buf("resid", (T, d), torch.float32)
+        xw = self._buf("xw", (T, d), torch.bfloat16)
+        ss_t = self._buf("ss_t", (T, d // 16), torch.float32)
+        ss_1 = self._buf("ss_1", (T, 1), torch.float32)
+        q = self._buf("q", (T, self.hq, self.D), torch.bfloat16)
+        attn = self._buf("attn", (T, self.hq, self.D), torch.bfloat16)
+        ops.embed_prep(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), xw, ss_1, b.src, self.last_ids)
+        ss = ss_1
+        for i in range(cfg.num_layers):
+            nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
+            ops.dg_qkv(xw, self.dgw[(i, "wqkv")], ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i],
+                       kv.v[i], self.hq, self.hkv, wshuf=True, mg=mgs["qkv"])
+            self._attention(b, kv, i, q, attn)
+            ops.dg_resid(attn.view(T, self.hq * self.D), self.dgw[(i, "wo")], resid, w.layer(i, "ln2"), xw, ss_t,
+                         wshuf=True, mg=mgs["o"])
+            w_gu = self.dgw[(i, "w_gu")]
+            act = self._buf("act", (T, w_gu.shape[0] // 2), torch.bfloat16)
+            ops.dg_swiglu(xw, w_gu, ss_t, eps, act, wshuf=True, mg=mgs["gu"])
+            ops.dg_resid(act, self.dgw[(i, "w_down")], resid, nxt, xw, ss_t, wshuf=True, mg=mgs["down"])
+            ss = ss_t
+        n = b.num_seqs
+        ids = self.last_ids[:n]
+        keys = self._buf("keys", (n,), torch.int64)
+        if n <= SKINNY_MAX_M:
+            tk = self._buf("tile_keys", (n * (self.vocab_shard // 16),), torch.int64)
+            logits = self._buf("logits", (n, self.vocab_shard), torch.float32) if b.need_logits or b.filtered else None
+            ops.dg_argmax(xw, w["lm_head"], ss, eps, b.temps, b.seeds, b.step, tk, keys, ids, 0, logits)
+            return self._finish_sampling(b, ids, keys, logits)
+        x = self._buf("x", (T, d), torch.bfloat16)
+        ops.rownorm(xw, ss, eps, x)
+        return self.sample(b, x)
 
     # ------------------------------------------------------------------------------------------
     def _forward_general(self, b: ForwardBatch, kv: KVCache) -> torch.Tensor:

@@ -187,23 +187,28 @@ def dg_f32(x, W, ss_in, eps, y, wshuf=False):
     return reference.dg_f32(x, reference.unshuffled(W, wshuf), ss_in, eps, y)
 
 
-def dg_qkv(x, W, ss_in, eps, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, wshuf=False):
+# mg: (slab [S, M, N] fp32, counters int32, rw) -> run the projection on the medium-M GEMM (mgemm, up to 256
+# rows, preshuffled weights) with the same fused epilogue after an in-launch split-K reduction
+def dg_qkv(x, W, ss_in, eps, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, wshuf=False, mg=None):
     if _gpu(x):
+        slab, cnt, rw = mg if mg is not None else (None, None, 0)
         return _native.ops().dg_qkv(x, W, ss_in, float(eps), positions, slots, cos_sin, q_out, k_cache, v_cache,
-                                    int(Hq), int(Hkv), bool(wshuf))
+                                    int(Hq), int(Hkv), bool(wshuf), slab, cnt, int(rw))
     return reference.dg_qkv(x, reference.unshuffled(W, wshuf), ss_in, eps, positions, slots, cos_sin, q_out,
                             k_cache, v_cache, Hq, Hkv)
 
 
-def dg_resid(x, W, resid, w_next, xw_out, ss_out, wshuf=False):
+def dg_resid(x, W, resid, w_next, xw_out, ss_out, wshuf=False, mg=None):
     if _gpu(x):
-        return _native.ops().dg_resid(x, W, resid, w_next, xw_out, ss_out, bool(wshuf))
+        slab, cnt, rw = mg if mg is not None else (None, None, 0)
+        return _native.ops().dg_resid(x, W, resid, w_next, xw_out, ss_out, bool(wshuf), slab, cnt, int(rw))
     return reference.dg_resid(x, reference.unshuffled(W, wshuf), resid, w_next, xw_out, ss_out)
 
 
-def dg_swiglu(x, W, ss_in, eps, act, wshuf=False):
+def dg_swiglu(x, W, ss_in, eps, act, wshuf=False, mg=None):
     if _gpu(x):
-        return _native.ops().dg_swiglu(x, W, ss_in, float(eps), act, bool(wshuf))
+        slab, cnt, rw = mg if mg is not None else (None, None, 0)
+        return _native.ops().dg_swiglu(x, W, ss_in, float(eps), act, bool(wshuf), slab, cnt, int(rw))
     return reference.dg_swiglu(x, reference.unshuffled(W, wshuf), ss_in, eps, act)
 
 

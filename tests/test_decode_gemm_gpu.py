@@ -394,3 +394,73 @@ def test_decode_block_fused_equals_three_launches(gpu, M, Hq, Hkv, d, shuf):
                 assert torch.equal(gr[k], bf[k]), k
     finally:
         nat.decode_gemm_variant(-1)
+
+
+def _mg(gpu, M, N, K):
+    """(slab, counters, rw) for the mgemm-with-epilogue form of a projection (ops.choose_mgemm's pick, or a
+    forced 4-way split when the chooser declines: the in-launch reduction is what is under test)."""
+    pick = ops.choose_mgemm(M, N, K) or (1, 4 if K % 256 == 0 else 1)
+    rw, S = pick
+    return (torch.full((S, M, N), float("nan"), device=gpu), torch.zeros(N // 64, dtype=torch.int32, device=gpu),
+            rw), S
+
+
+@pytest.mark.parametrize("M", [1, 20, 33, 64, 100])
+@pytest.mark.parametrize("kind", ["qkv", "resid", "swiglu"])
+def test_mgemm_fused_epilogues(gpu, M, kind):
+    """mgemm with the fused decode epilogues (the general decode path of 20-256 rows): the last k-split
+    workgroup of each column group reduces the fp32 slabs in split order and runs the same epilogue as the
+    decode GEMMs, against the fp32 references; run twice (the counters re-arm themselves)."""
+    from symmetry_amd.models.layout import preshuffle
+
+    if kind == "qkv":
+        Hq, Hkv, K, D = 32, 8, 4096, 128
+        N = (Hq + 2 * Hkv) * D
+    elif kind == "resid":
+        N, K = 4096, 4096
+    else:
+        N, K = 2 * 1792, 4096
+    x, W, s = _inputs(gpu, M, N, K, seed=7)
+    if kind == "qkv":
+        W = W[qkv_perm(Hq, Hkv, D).to(gpu)].contiguous()
+    elif kind == "swiglu":
+        W = W[gu_perm(N // 2).to(gpu)].contiguous()
+    Ws = preshuffle(W)
+    mg, S = _mg(gpu, M, N, K)
+    for rep in range(2):
+        if kind == "qkv":
+            BS, NB = 32, 16
+            cs = ref.rope_table(1024, D, 500000.0, device=gpu)
+            g = torch.Generator(device=gpu).manual_seed(5)
+            pos = torch.randint(0, 1024, (M,), device=gpu, generator=g, dtype=torch.int32)
+            slots = torch.randperm(NB * BS, device=gpu, generator=g)[:M].int()
+            slots[0] = -1
+            q = torch.empty(M, Hq, D, device=gpu, dtype=torch.bfloat16)
+            kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=torch.bfloat16)
+            vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=torch.bfloat16)
+            ops.dg_qkv(x, Ws, s, 1e-5, pos, slots, cs, q, kc, vc, Hq, Hkv, wshuf=True, mg=mg)
+            q_r, kc_r, vc_r = torch.empty(M, Hq, D, dtype=torch.bfloat16), torch.zeros_like(kc.cpu()), torch.zeros_like(vc.cpu())
+            ref.dg_qkv(x.cpu(), W.cpu(), s.cpu(), 1e-5, pos.cpu(), slots.cpu(), cs.cpu(), q_r, kc_r, vc_r, Hq, Hkv)
+            _close(q, q_r, atol=2e-2, rtol=2e-2)
+            _close(kc, kc_r, atol=2e-2, rtol=2e-2)
+            _close(vc, vc_r, atol=2e-2, rtol=2e-2)
+        elif kind == "resid":
+            g = torch.Generator(device=gpu).manual_seed(2)
+            resid = torch.randn(M, N, device=gpu, generator=g)
+            wn = (torch.randn(N, device=gpu, generator=g) * 0.1 + 1).bfloat16()
+            xw = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+            ss = torch.empty(M, N // 16, device=gpu)
+            r_ref, xw_ref, ss_ref = resid.cpu().clone(), torch.empty(M, N, dtype=torch.bfloat16), torch.empty(M, N // 16)
+            ops.dg_resid(x, Ws, resid, wn, xw, ss, wshuf=True, mg=mg)
+            ref.dg_resid(x.cpu(), W.cpu(), r_ref, wn.cpu(), xw_ref, ss_ref)
+            _close(resid, r_ref, atol=2e-3, rtol=1e-3)
+            _close(xw, xw_ref, atol=2e-2, rtol=1e-2)
+            _close(ss, ss_ref, atol=1e-2, rtol=1e-3)
+        else:
+            act = torch.empty(M, N // 2, device=gpu, dtype=torch.bfloat16)
+            ops.dg_swiglu(x, Ws, s, 1e-5, act, wshuf=True, mg=mg)
+            act_ref = torch.empty(M, N // 2, dtype=torch.bfloat16)
+            ref.dg_swiglu(x.cpu(), W.cpu(), s.cpu(), 1e-5, act_ref)
+            _close(act, act_ref, atol=1e-2, rtol=2e-2)
+        torch.cuda.synchronize()
+        assert int(mg[1].abs().sum()) == 0, "split-K counters must re-arm to zero"

@@ -1,0 +1,14 @@
+#!/bin/bash
+# A/B of the fused general decode path (mgemm + in-launch split-K reduction + decode epilogues) against the
+# slab + consumer-kernel path, alternating arms, at wide client counts (bench.py, engine-side timing).
+set -o pipefail
+out=gpurun_out/mg_fused_ab.jsonl
+for c in ${CLIENTS:-64 32 20}; do
+  for rep in 1 2; do
+    for mg in 1 0; do
+      SYMMETRY_MG_FUSED=$mg timeout -k 10 240 python -u bench.py --clients $c --steps 64 --warmup 8 --client-end 0 \
+        --max-model-len 1024 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'clients': $c, 'mg_fused': $mg, 'rep': $rep, 'ms_per_step': d['ms_per_step'], 'tokens_per_s': d['value'], 'p50_ttft_ms': d['p50_ttft_ms']}))" >> $out || exit $?
+      tail -1 $out
+    done
+  done
+done
