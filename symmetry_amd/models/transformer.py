@@ -70,6 +70,9 @@ ROPE_DECODE_ROWS = os.environ.get("SYMMETRY_ROPE_DECODE_ROWS", "1") != "0"
 # (in-launch split-K reduction; RoPE + KV write, residual + norm prep, SwiGLU in the GEMM) when every
 # projection has an mgemm pick: 5 launches per layer instead of 9 (0 = the slab + consumer-kernel path)
 MG_FUSED = os.environ.get("SYMMETRY_MG_FUSED", "1") != "0"
+# projections of the FUSED decode path (below GENERAL_ROWS rows) that run on mgemm with their epilogue
+# instead of the decode GEMM (comma list of qkv, o, gu, down; A/B knob)
+MG_PROJ = tuple(p for p in os.environ.get("SYMMETRY_MG_PROJ", "").split(",") if p)
 
 
 @dataclass
@@ -306,10 +309,12 @@ class TransformerLM:
             return self._forward_general_fused(b, kv, mgs)
         return self._forward_general(b, kv)
 
-    def _mg_plan(self, b: ForwardBatch):
+    def _mg_plan(self, b: ForwardBatch, names=("qkv", "o", "gu", "down"), need_all: bool = True):
         """mgemm (rw, split) + scratch per projection for the fused general path, or None."""
+        # under TP only the column-parallel projections (qkv, gate_up: no collective in their epilogue)
+        tp_ok = not self._tp_active() or set(names) <= {"qkv", "gu"}
         if not (MG_FUSED and b.kind == "decode" and self.dgw and self.device.type != "cpu" and not self.cfg.is_moe
-                and not self._tp_active() and b.num_tokens <= 256):
+                and tp_ok and b.num_tokens <= 256):
             return None
         T, d, dq = b.num_tokens, self.cfg.hidden_size, self.hq * self.D
         wgu = self.w.layer(0, "w_gu")
@@ -317,9 +322,13 @@ class TransformerLM:
                   "down": (d, wgu.shape[0] // 2)}
         plan = {}
         for name, (N, K) in shapes.items():
+            if name not in names:
+                continue
             pick = ops.choose_mgemm(T, N, K)
             if pick is None:
-                return None
+                if need_all:
+                    return None
+                continue
             rw, S = pick
             slab = self._buf("mg.slab", (S, T, N), torch.float32)
             cnt = self.ws.get("mg.cnt." + name, (N // 64,), torch.int32, self.device, zeros=True)
@@ -335,10 +344,13 @@ class TransformerLM:
     def _tp_active(self) -> bool:
         return self.tp is not None and self.tp_size > 1
 
-    def _resid_proj(self, name, x, Wsh, resid, w_next, xw, ss_t, ss_1, w_row=None) -> torch.Tensor:
+    def _resid_proj(self, name, x, Wsh, resid, w_next, xw, ss_t, ss_1, w_row=None, mg=None) -> torch.Tensor:
         """Row-parallel projection + residual add + next-norm prep; returns the ss partials to use."""
         W, sh = Wsh
         M = x.shape[0]
+        if mg is not None and sh and not self._tp_active():
+            ops.dg_resid(x, W, resid, w_next, xw, ss_t, wshuf=True, mg=mg)
+            return ss_t
         if w_row is not None and not self._tp_active() and 0 < SPLITK_RESID_ROWS <= M:
             N, K = w_row.shape
             y = self._buf(name + ".slab", (ops.choose_splits(N, K), M, N), torch.float32)
@@ -377,6 +389,8 @@ class TransformerLM:
         attn = self._buf("attn", (T, self.hq, self.D), torch.bfloat16)
         ops.embed_prep(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), xw, ss_1, b.src, self.last_ids)
         ss = ss_1
+        proj = MG_PROJ if not self._tp_active() else tuple(p for p in MG_PROJ if p in ("qkv", "gu"))
+        mgp = (self._mg_plan(b, proj, need_all=False) or {}) if proj else {}
         persistent = self._persistent_mlp_ok(T)
         ctl = self.ws.get("mlp_ctl", (ops.DECODE_MLP_CTL,), torch.int32, self.device, zeros=True) if persistent else None
         block = self._attn_block_ok(b)
@@ -401,7 +415,7 @@ class TransformerLM:
                 ss = ss_t
             else:
                 ops.dg_qkv(xw, wq, ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq,
-                           self.hkv, wshuf=shq)
+                           self.hkv, wshuf=shq, mg=mgp.get("qkv") if shq else None)
                 # spare workgroups of the latency-bound attention launch pull the O weight into the
                 # Infinity Cache for the next launch
                 self._attention(b, kv, i, q, attn, self._dgw(i, "wo")[0] if ATTN_PREFETCH_WGS > 0 else None)
@@ -416,7 +430,7 @@ class TransformerLM:
                 continue
             if not block:
                 ss = self._resid_proj("o", attn2d, self._dgw(i, "wo"), resid, w.layer(i, "ln2"), xw, ss_t, ss_1,
-                                     w.layer(i, "wo"))
+                                     w.layer(i, "wo"), mg=mgp.get("o"))
             if cfg.is_moe:
                 # router + experts are not decode GEMMs: materialise RMSNorm(resid) (one bf16 rounding)
                 xn = self._buf("x", (T, d), torch.bfloat16)
@@ -426,9 +440,9 @@ class TransformerLM:
             else:
                 w_gu, shg = self._dgw(i, "w_gu")
                 act = self._buf("act", (T, w_gu.shape[0] // 2), torch.bfloat16)
-                ops.dg_swiglu(xw, w_gu, ss, eps, act, wshuf=shg)
+                ops.dg_swiglu(xw, w_gu, ss, eps, act, wshuf=shg, mg=mgp.get("gu") if shg else None)
                 ss = self._resid_proj("down", act, self._dgw(i, "w_down"), resid, nxt, xw, ss_t, ss_1,
-                                     w.layer(i, "w_down"))
+                                     w.layer(i, "w_down"), mg=mgp.get("down"))
         n = b.num_seqs
         if b.kind == "decode":
             xl, sl = xw, ss
