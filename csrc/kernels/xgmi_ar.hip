@@ -31,8 +31,10 @@
 namespace {
 
 constexpr int XG_THREADS = 256;
-constexpr unsigned long long XG_WAIT_TICKS = 200000000ull;  // 2 s of the 100 MHz wall clock: a peer that
-                                                            // never arrives is an error, not a hang
+// 30 s of the 100 MHz wall clock: a peer that never arrives is an error, not a hang.  Long enough for the
+// first collectives of a provider start-up, where ranks can drift by the time each one spends loading
+// library GEMM code objects before its first prefill.
+constexpr unsigned long long XG_WAIT_TICKS = 3000000000ull;
 
 SYM_DEV char* xg_slot(const XgmiArgs& c, int r, int par, int src) {
   return c.bufs[r] + XG_FLAG_BYTES + ((long long)par * c.world + src) * c.slot_bytes;

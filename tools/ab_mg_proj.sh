@@ -3,7 +3,7 @@
 # epilogue (in-launch split-K reduction, all 256 CUs) than on the decode GEMMs.  Alternating arms.
 set -o pipefail
 out=gpurun_out/mg_proj_10_ab.jsonl
-for rep in 1 2 3; do
+for rep in $(seq 1 ${REPS:-3}); do
   for proj in none qkv qkv,o o; do
     p=$proj; [ "$p" = none ] && p=""
     SYMMETRY_MG_PROJ=$p timeout -k 10 240 python -u bench.py --clients 10 --steps 96 --warmup 8 --client-end 0 \
