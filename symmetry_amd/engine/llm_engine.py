@@ -27,7 +27,7 @@ from ..models.config import ModelConfig, resolve
 from ..models.transformer import KVCache, TransformerLM
 from ..models.weights import ModelWeights, ShardSpec, load_hf_weights, random_weights
 from ..utils.metrics import EngineMetrics
-from .model_runner import FUSED_DECODE_ROWS, MAX_DECODE_ROWS, ModelRunner
+from .model_runner import MAX_DECODE_ROWS, ModelRunner
 from .scheduler import BlockManager, Scheduler, SchedulerConfig
 from .sequence import SamplingParams, Sequence, SeqStatus
 from .tokenizer import IncrementalDetokenizer, load_tokenizer
@@ -185,12 +185,11 @@ class LLMEngine:
         return resolve(cfg.model)
 
     def _max_decode_rows(self, mcfg: ModelConfig) -> int:
-        """Concurrent sequences per decode step on the GPU: up to MAX_DECODE_ROWS for a dense model on one
-        GPU (rows past the fused decode kernels run the general path on the medium-M GEMM, one graph per
-        bucket), FUSED_DECODE_ROWS under TP / for MoE (the CPU reference path: MAX_DECODE_ROWS)."""
-        if self.device.type == "cpu":
-            return MAX_DECODE_ROWS
-        return MAX_DECODE_ROWS if (not mcfg.is_moe and self.cfg.tp_size == 1) else FUSED_DECODE_ROWS
+        """Concurrent sequences per decode step: up to MAX_DECODE_ROWS (rows past the fused decode kernels run
+        the general path -- medium-M GEMMs with fused epilogues on one GPU; under TP the slab path whose
+        all-reduces are capturable; for MoE the grouped GEMMs whose segment bounds stay on the device -- one
+        hipGraph per bucket)."""
+        return MAX_DECODE_ROWS
 
     def _graph_safe(self, tp_comm, ep_comm) -> bool:
         """Decode hipGraphs need every collective to be capturable (our RCCL communicator, or the xGMI

@@ -30,7 +30,7 @@ from ..models.transformer import ForwardBatch, KVCache, TransformerLM
 from .scheduler import ScheduledBatch
 
 DECODE_BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256)
-MAX_DECODE_ROWS = 256  # dense single-GPU models (general path on the medium-M GEMM); others: FUSED_DECODE_ROWS
+MAX_DECODE_ROWS = 256  # decode rows per step (past FUSED_DECODE_ROWS: the general path, one graph per bucket)
 FUSED_DECODE_ROWS = 64
 CTX_BUCKETS = (512, 2048, 8192, 32768, 131072)  # tokens (multiples of the 512-token attention partition)
 CMD_STOP, CMD_CAPTURE, CMD_SYNC = -1, 2, 3  # control headers of the rank-0 -> worker metadata plane

@@ -147,6 +147,46 @@ def _tp_e8_worker(rank, world):
     return _tp_worker(rank, world, model="tiny-mixtral-e8")
 
 
+def _tp_wide_batch_worker(rank, world):
+    """TP=2 with 70 concurrent sequences: decode steps past 64 rows run the general path under TP."""
+    from symmetry_amd.engine.llm_engine import EngineConfig
+    from symmetry_amd.engine.sequence import SamplingParams
+    from symmetry_amd.parallel.launch import init_tp_engine
+
+    ecfg = EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=70, max_model_len=128, block_size=16,
+                        weight_init="full", num_kv_blocks=70 * 8 + 8)
+    eng, r = init_tp_engine(ecfg)
+    if r != 0:
+        eng.runner.worker_loop()
+        return None
+    assert eng.scheduler.cfg.max_num_seqs == 70
+    prompts = [list(range(5 + i, 15 + i)) for i in range(70)]
+    seqs = [eng.add_request(f"w{i}", p, SamplingParams(max_tokens=4, ignore_eos=True)) for i, p in enumerate(prompts)]
+    widest = 0
+    while eng.has_unfinished():
+        eng.step()
+        widest = max(widest, sum(1 for s in seqs if s.output_ids and not s.status.finished))
+    eng.shutdown()
+    return {"outs": [seqs[i].output_ids for i in (0, 33, 69)], "prompts": [prompts[i] for i in (0, 33, 69)],
+            "widest": widest}
+
+
+def test_tp_decode_past_64_rows():
+    res = _run(_tp_wide_batch_worker, world=2)
+    r = res[0][1]
+    assert r["widest"] > 64
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.models import reference_model as rm
+
+    eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_model_len=128, weight_init="full"))
+    for p, out in zip(r["prompts"], r["outs"]):
+        assert len(out) == 4
+        lg = rm.forward_logits(eng.weights, p + out[:-1])
+        for j, t in enumerate(out):
+            row = lg[len(p) - 1 + j]
+            assert float(row.max() - row[t]) <= 0.05
+
+
 def _check_against_oracle(model, tp_out):
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
     from symmetry_amd.models import reference_model as rm
