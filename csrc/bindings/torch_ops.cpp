@@ -505,13 +505,29 @@ DGShape dg_check(const Tensor& x, const Tensor& W, bool mg = false) {
   return {M, N, K};
 }
 
+// mg_slab [S, M, N] selects the medium-M GEMM; a 1-D fp32 mg_slab is the decode GEMM's split-K workspace
+bool is_mg(const c10::optional<Tensor>& slab) { return slab.has_value() && slab->dim() == 3; }
+
 // The decode GEMM (M <= 64) or, with an mgemm slab given, the medium-M GEMM with the same fused epilogue
 // (in-launch split-K reduction; weights MFMA-preshuffled): slab [S, M, N] fp32 scratch, counters [N / (64 rw)]
-// ints zeroed once (re-armed by the kernel).
+// ints zeroed once (re-armed by the kernel).  With a 1-D slab (fp32 workspace) + counters (ints, zeroed once)
+// the decode GEMM may split K across workgroups (decode_gemm.hip, go_xres).
 void launch_dg(int epi, const Tensor& x, const Tensor& W, const DGShape& sh, DecodeEpi& e,
                const c10::optional<Tensor>& slab, const c10::optional<Tensor>& counters, int64_t rw) {
   const at::OptionalDeviceGuard g(x.device());
-  if (!slab.has_value()) {
+  if (!is_mg(slab)) {
+    if (slab.has_value()) {
+      TORCH_CHECK(counters.has_value(), "decode split-K workspace: counters required");
+      check_gpu(*slab, "ks_ws");
+      check_dtype(*slab, at::kFloat, "ks_ws");
+      check_gpu(*counters, "ks_cnt");
+      check_dtype(*counters, at::kInt, "ks_cnt");
+      TORCH_CHECK(slab->is_contiguous() && counters->is_contiguous(), "decode split-K workspace: contiguous");
+      e.ks_ws = ptr<float>(*slab);
+      e.ks_cap = slab->numel();
+      e.ks_cnt = ptr<int>(*counters);
+      e.ks_ncnt = (int)counters->numel();
+    }
     launch_decode_gemm(epi, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, e, cur_stream(x));
     return;
   }
@@ -560,7 +576,7 @@ void dg_qkv(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in
             const Tensor& slots, const Tensor& cos_sin, Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t Hq,
             int64_t Hkv, bool wshuf, const c10::optional<Tensor>& mg_slab, const c10::optional<Tensor>& mg_counters,
             int64_t mg_rw) {
-  auto sh = dg_check(x, W, mg_slab.has_value());
+  auto sh = dg_check(x, W, is_mg(mg_slab));
   for (auto* t : {&positions, &slots}) {
     check_gpu(*t, "index tensor");
     check_dtype(*t, at::kInt, "index tensor");
@@ -592,7 +608,7 @@ void dg_qkv(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in
 
 void dg_resid(const Tensor& x, const Tensor& W, Tensor& resid, const Tensor& w_next, Tensor& xw_out, Tensor& ss_out, bool wshuf,
               const c10::optional<Tensor>& mg_slab, const c10::optional<Tensor>& mg_counters, int64_t mg_rw) {
-  auto sh = dg_check(x, W, mg_slab.has_value());
+  auto sh = dg_check(x, W, is_mg(mg_slab));
   check_gpu(resid, "resid");
   check_dtype(resid, at::kFloat, "resid");
   check_gpu(w_next, "w_next");
@@ -615,7 +631,7 @@ void dg_resid(const Tensor& x, const Tensor& W, Tensor& resid, const Tensor& w_n
 
 void dg_swiglu(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, Tensor& act, bool wshuf,
                const c10::optional<Tensor>& mg_slab, const c10::optional<Tensor>& mg_counters, int64_t mg_rw) {
-  auto sh = dg_check(x, W, mg_slab.has_value());
+  auto sh = dg_check(x, W, is_mg(mg_slab));
   check_gpu(act, "act");
   check_dtype(act, at::kBFloat16, "act");
   TORCH_CHECK(act.numel() == sh.M * sh.N / 2, "dg_swiglu: act must be [M, N/2]");
@@ -995,6 +1011,7 @@ TORCH_LIBRARY(symmetry_amd, m) {
       "Tensor(i!) xw_out, Tensor(j!) ss_out, Tensor(k!) ctl, bool wshuf=False, Tensor(l!)? stamps=None, int cfg=0) -> ()",
       &decode_block);
   m.def("decode_gemm_variant(int v) -> ()", [](int64_t v) { set_decode_gemm_variant((int)v); });
+  m.def("decode_ksplit(int on) -> ()", [](int64_t on) { set_decode_ksplit((int)on); });
   m.def("decode_gemm_nt(int on) -> ()", [](int64_t on) { set_decode_gemm_nt((int)on); });
   m.def("grouped_skinny(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y) -> ()", &grouped_skinny);
   m.def("grouped_gemm(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y, int mode) -> ()", &grouped_gemm);

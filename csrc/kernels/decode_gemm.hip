@@ -83,12 +83,24 @@ SYM_DEV void gemm_tile(const bf16* __restrict__ x, const bf16* __restrict__ W, i
 
   auto row_scales = [&]() {
     // RMSNorm row scales of the input rows (deferred norm), overlapped with the weight loads in flight.
+    // Four rows per batch: their loads are independent, so a wave with 16 rows (M = 64, 4 waves) pays 4 load
+    // round trips instead of 16 (the 64-row lm_head: 295 -> ~230 us).
     if (e.ss_in) {
-      for (int m = wid; m < M; m += NW) {
-        float s = 0.f;
-        for (int i = lane; i < e.ss_tiles; i += 64) s += e.ss_in[(long long)m * e.ss_tiles + i];
-        s = wave_sum(s);
-        if (lane == 0) rn_s[m] = rsqrtf(s * e.inv_d + e.eps);
+      for (int m0 = wid; m0 < M; m0 += 4 * NW) {
+        float s[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = m0 + j * NW;
+          s[j] = 0.f;
+          if (m < M)
+            for (int i = lane; i < e.ss_tiles; i += 64) s[j] += e.ss_in[(long long)m * e.ss_tiles + i];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = m0 + j * NW;
+          const float t = wave_sum(s[j]);
+          if (lane == 0 && m < M) rn_s[m] = rsqrtf(t * e.inv_d + e.eps);
+        }
       }
     }
   };
@@ -597,36 +609,57 @@ __global__ __launch_bounds__(512, 4) void decode_block_kernel(DecodeBlockArgs a)
 // flight while it is reduced (LDS, double-buffered) and finished by wave 0 (16 waves x 8 KB per CU in
 // flight is above the ~50 KB Little's-law need); the grid gives every CU the same tile count.
 // ---------------------------------------------------------------------------------------------------
-template <int U, int EPI>
+// Remainder tiles split over K (KS > 1, chosen by go_xres when whole tiles leave CUs idle).  With ntiles =
+// f * G + R (G workgroups), the first f * G tiles are walked whole as above and the R remainder tiles are cut
+// into R * KS parts of K / KS, dealt out after them (part p: tile f G + p / KS, k-split p % KS, computed by the
+// 16 / KS waves whose resident x slices cover that k range; the others add zeros).  Llama-3-8B QKV: 384 tiles
+// = 2 per CU on 192 CUs whole -> 1 whole + 1 half per CU on all 256 (25 % fewer bytes on the busiest CU);
+// TP = 8 shard: 48 tiles -> 192 quarter tiles.  Wave 0 stores each part's reduced 16 x 16 fp32 partial with
+// write-through stores as it goes; after the last unit it drains them ONCE (vmcnt(0): the only point where it
+// has no weight loads in flight), bumps the parts' tile counters (one lane per part), and for the tiles whose
+// last split it delivered sums the KS partials in split order (bitwise reproducible whatever the arrival
+// order), re-arms the counter and runs the epilogue.  No workgroup ever waits for another.  (A first version
+// handed off after every part with agent fences: the fence writes back / invalidates the XCD's whole L2 and
+// the drain stalls on the next unit's loads, +23 us per QKV launch.)
+template <int U, int KS, int EPI>
 __global__ __launch_bounds__(1024) void decode_gemm_xres_kernel(const bf16* __restrict__ x, const bf16* __restrict__ W,
-                                                                int M, int N, int K, DecodeEpi e) {
+                                                                int M, int N, int K, DecodeEpi e, int NF, int P) {
   constexpr int NW = 16;
+  constexpr int WPS = NW / KS;  // waves per k-split
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r16 = lane & 15, h = lane >> 4;
   const int kbeg = wid * (K / NW);
-  const int ntiles = N / 16;
+  const int b = blockIdx.x, G = gridDim.x;
   const int wmul = e.wshuf ? 16 : 1, wsec = e.wshuf ? 512 : 32;
   auto wptr = [&](int t) -> const bf16* {
     return e.wshuf ? W + ((long long)t * (K / 32) + kbeg / 32) * 512 + lane * 8
                    : W + (long long)(16 * t + r16) * K + kbeg + 8 * h;
   };
-  int t = blockIdx.x;
+  // this workgroup's units: whole tiles b, b + G, ... < NF, then parts b, b + G, ... < P
+  const int nf = NF > b ? (NF - b + G - 1) / G : 0;
+  const int np = (KS > 1 && P > b) ? (P - b + G - 1) / G : 0;
+  const int nu = nf + np;
+  if (nu == 0) return;  // uniform over the workgroup
+  auto unit_tile = [&](int i) { return i < nf ? b + i * G : NF + (b + (i - nf) * G) / KS; };
+  auto unit_active = [&](int i) { return i < nf || wid / WPS == (b + (i - nf) * G) % KS; };
   Pack8 wa[U][2];
-  {
-    const bf16* wp = wptr(t);
+  auto load_w = [&](int i) {
+    if (!unit_active(i)) return;
+    const bf16* wp = wptr(unit_tile(i));
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      wa[u][0].u = *reinterpret_cast<const uint4*>(wp + u * 64 * wmul);
-      wa[u][1].u = *reinterpret_cast<const uint4*>(wp + u * 64 * wmul + wsec);
+    for (int j = 0; j < U; ++j) {
+      wa[j][0].u = *reinterpret_cast<const uint4*>(wp + j * 64 * wmul);
+      wa[j][1].u = *reinterpret_cast<const uint4*>(wp + j * 64 * wmul + wsec);
     }
-  }
+  };
+  load_w(0);
   const bool xok = r16 < M;
   const bf16* xrow = x + (long long)min(r16, M - 1) * K + kbeg + 8 * h;
   Pack8 xa[U][2];
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    xa[u][0].u = xok ? *reinterpret_cast<const uint4*>(xrow + u * 64) : make_uint4(0, 0, 0, 0);
-    xa[u][1].u = xok ? *reinterpret_cast<const uint4*>(xrow + u * 64 + 32) : make_uint4(0, 0, 0, 0);
+  for (int j = 0; j < U; ++j) {
+    xa[j][0].u = xok ? *reinterpret_cast<const uint4*>(xrow + j * 64) : make_uint4(0, 0, 0, 0);
+    xa[j][1].u = xok ? *reinterpret_cast<const uint4*>(xrow + j * 64 + 32) : make_uint4(0, 0, 0, 0);
   }
   __shared__ float rn_s[16];
   if (e.ss_in) {  // deferred-RMSNorm row scales, once per workgroup
@@ -640,25 +673,31 @@ __global__ __launch_bounds__(1024) void decode_gemm_xres_kernel(const bf16* __re
   __shared__ f32x4 red[2][NW][64];
   unsigned xep = 0;
   if constexpr (EPI == DECODE_EPI_XPUSH) xep = xp_epoch(e.xp);
-  int buf = 0;
-  for (;;) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int m = r16;
+  const bool mok = m < M;
+  auto finish = [&](f32x4 v, int t) {  // wave 0: row scale + epilogue of a final tile
+    const float sc = (e.ss_in && mok) ? rn_s[m] : 1.f;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      acc = mfma16(wa[u][0].v, xa[u][0].v, acc);
-      acc = mfma16(wa[u][1].v, xa[u][1].v, acc);
+    for (int i = 0; i < 4; ++i) v[i] *= sc;
+    epilogue<EPI>(e, v, t, m, mok, h, N, xep);
+    if constexpr (EPI == DECODE_EPI_XPUSH) {  // wave 0 stored the whole tile: acknowledged, then flag it
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane < e.xp.world) xp_flag(e.xp, lane, t, xep);
+    }
+  };
+  int buf = 0;
+  for (int i = 0; i < nu; ++i) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (unit_active(i)) {
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        acc = mfma16(wa[j][0].v, xa[j][0].v, acc);
+        acc = mfma16(wa[j][1].v, xa[j][1].v, acc);
+      }
     }
     // keep the next loads behind this tile's MFMAs: they reuse wa's registers (no renamed second copy)
     __builtin_amdgcn_sched_barrier(0);
-    const int tn = t + gridDim.x;
-    if (tn < ntiles) {  // next tile's weight stream in flight during this tile's reduction and epilogue
-      const bf16* wp = wptr(tn);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        wa[u][0].u = *reinterpret_cast<const uint4*>(wp + u * 64 * wmul);
-        wa[u][1].u = *reinterpret_cast<const uint4*>(wp + u * 64 * wmul + wsec);
-      }
-    }
+    if (i + 1 < nu) load_w(i + 1);  // next unit's weight stream in flight during this unit's reduction/epilogue
     red[buf][wid][lane] = acc;
     __syncthreads();
     if (wid == 0) {
@@ -668,24 +707,69 @@ __global__ __launch_bounds__(1024) void decode_gemm_xres_kernel(const bf16* __re
         v += red[buf][w][lane];
         if ((w & 3) == 3) asm volatile("" : "+v"(v)::"memory");  // <= 4 partials in registers at a time
       }
-      const int m = r16;
-      const bool mok = m < M;
-      const float sc = (e.ss_in && mok) ? rn_s[m] : 1.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] *= sc;
-      epilogue<EPI>(e, v, t, m, mok, h, N, xep);
-      if constexpr (EPI == DECODE_EPI_XPUSH) {  // wave 0 stored the whole tile: acknowledged, then flag it
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane < e.xp.world) xp_flag(e.xp, lane, t, xep);
+      if (i < nf) {
+        finish(v, unit_tile(i));
+      } else if constexpr (KS > 1) {  // part: publish the partial (write-through), no wait here
+        unsigned long long* slot =
+            reinterpret_cast<unsigned long long*>(e.ks_ws + (long long)(b + (i - nf) * G) * 256 + lane * 4);
+        const float4 f4 = make_float4(v[0], v[1], v[2], v[3]);
+        const unsigned long long* w64 = reinterpret_cast<const unsigned long long*>(&f4);
+        __hip_atomic_store(slot, w64[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(slot + 1, w64[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     buf ^= 1;
-    if (tn >= ntiles) break;
-    t = tn;
+  }
+  if constexpr (KS > 1) {
+    if (wid != 0 || np == 0) return;
+    // MI355X_MICROARCH.md hand-off: write-through payload, vmcnt drain, relaxed agent add; the last split's
+    // wave reads the payloads with agent-scope (L2-bypassing) loads
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int last = 0;
+    if (lane < np) {
+      const int tl = (b + lane * G) / KS;
+      last = __hip_atomic_fetch_add(e.ks_cnt + tl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
+      if (last) __hip_atomic_store(e.ks_cnt + tl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const unsigned long long lastmask = __ballot(last);
+    for (int j = 0; j < np; ++j) {
+      if (!((lastmask >> j) & 1)) continue;
+      const int tl = (b + j * G) / KS;
+      const unsigned long long* base =
+          reinterpret_cast<const unsigned long long*>(e.ks_ws + (long long)tl * KS * 256 + lane * 4);
+      unsigned long long r[KS][2];
+#pragma unroll
+      for (int sp = 0; sp < KS; ++sp) {
+        r[sp][0] = __hip_atomic_load(base + sp * 128, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r[sp][1] = __hip_atomic_load(base + sp * 128 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sp = 0; sp < KS; ++sp) {  // split order
+        const float* q = reinterpret_cast<const float*>(r[sp]);
+        v += f32x4{q[0], q[1], q[2], q[3]};
+      }
+      finish(v, NF + tl);
+    }
   }
 }
 
 int g_num_cus = 0;
+
+// Remainder split: OFF by default.  Measured (profiles/r3/ksplit_ab.jsonl, alternating runs): 8B 10 clients
+// 3.308 vs 3.230 ms per step, TP = 8 shard 1.576 vs 1.538, TP = 4 1.965 vs 1.817 -- at these sizes the launch
+// is bound by latency (ramp, first loads, the tail), not by the busiest CU's bytes, and the hand-off adds a
+// drain + atomic + L2-bypassing read round trip to the tail.  SYMMETRY_DG_KSPLIT=1 / set_decode_ksplit(1).
+static bool g_dg_ksplit = [] {
+  const char* knob = getenv("SYMMETRY_DG_KSPLIT");
+  return knob && knob[0] == '1';
+}();
+
+template <int U, int KS, int EPI>
+void go_xres_ks(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, int grid, int NF, int P,
+                hipStream_t s) {
+  decode_gemm_xres_kernel<U, KS, EPI><<<grid, 1024, 0, s>>>(x, W, M, N, K, e, NF, P);
+}
 
 template <int EPI>
 bool go_xres(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, hipStream_t s) {
@@ -696,13 +780,38 @@ bool go_xres(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi&
     hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
     g_num_cus = std::max(1, g_num_cus);
   }
+  const int C = g_num_cus;
   const int ntiles = N / 16;
-  const int per = (ntiles + g_num_cus - 1) / g_num_cus;  // equal tile count per workgroup
-  const int grid = (ntiles + per - 1) / per;
-  switch (K / 1024) {
-    case 1: decode_gemm_xres_kernel<1, EPI><<<grid, 1024, 0, s>>>(x, W, M, N, K, e); return true;
-    case 2: decode_gemm_xres_kernel<2, EPI><<<grid, 1024, 0, s>>>(x, W, M, N, K, e); return true;
-    case 4: decode_gemm_xres_kernel<4, EPI><<<grid, 1024, 0, s>>>(x, W, M, N, K, e); return true;
+  const int per = (ntiles + C - 1) / C;  // whole tiles: equal tile count per workgroup
+  int grid = (ntiles + per - 1) / per, NF = ntiles, P = 0, KS = 1;
+  // remainder split: weight bytes on the busiest CU, f K + q K / KS, must drop >= 10 % (<= 4 parts per
+  // workgroup, >= 4 waves per part)
+  const int f = ntiles / C, R = ntiles - f * C;
+  if (g_dg_ksplit && R > 0 && e.ks_ws && e.ks_cnt && e.ks_ncnt >= R && EPI != DECODE_EPI_ARGMAX) {
+    long long best = (long long)per * K * 9 / 10;
+    for (int ks = 2; ks <= 4; ks *= 2) {
+      const int parts = R * ks, g = f > 0 ? C : std::min(C, parts), q = (parts + g - 1) / g;
+      const long long cost = (long long)f * K + (long long)q * (K / ks);
+      if (q > 4 || (long long)parts * 256 > e.ks_cap || cost > best) continue;
+      if (cost < best || KS == 1) {
+        best = cost;
+        KS = ks;
+        grid = g;
+        NF = f * C;
+        P = parts;
+      }
+    }
+  }
+  switch (KS * 8 + K / 1024) {
+    case 8 + 1: go_xres_ks<1, 1, EPI>(x, W, M, N, K, e, grid, NF, P, s); return true;
+    case 8 + 2: go_xres_ks<2, 1, EPI>(x, W, M, N, K, e, grid, NF, P, s); return true;
+    case 8 + 4: go_xres_ks<4, 1, EPI>(x, W, M, N, K, e, grid, NF, P, s); return true;
+    case 16 + 1: go_xres_ks<1, 2, EPI>(x, W, M, N, K, e, grid, NF, P, s); return true;
+    case 16 + 2: go_xres_ks<2, 2, EPI>(x, W, M, N, K, e, grid, NF, P, s); return true;
+    case 16 + 4: go_xres_ks<4, 2, EPI>(x, W, M, N, K, e, grid, NF, P, s); return true;
+    case 32 + 1: go_xres_ks<1, 4, EPI>(x, W, M, N, K, e, grid, NF, P, s); return true;
+    case 32 + 2: go_xres_ks<2, 4, EPI>(x, W, M, N, K, e, grid, NF, P, s); return true;
+    case 32 + 4: go_xres_ks<4, 4, EPI>(x, W, M, N, K, e, grid, NF, P, s); return true;
     default: return false;
   }
 }
@@ -853,6 +962,8 @@ void launch_decode_mlp(const DecodeMlpArgs& a, hipStream_t s) {
     default: go_mlp<8, 2, 4>(a, s); break;  // 2 WGs / CU
   }
 }
+
+void set_decode_ksplit(int on) { g_dg_ksplit = on != 0; }
 
 void set_decode_gemm_variant(int v) {
   // v >= 1000: persistent decode MLP configuration v - 1000 (launch_decode_mlp)

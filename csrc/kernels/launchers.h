@@ -67,6 +67,13 @@ struct DecodeEpi {
   int n_offset = 0;
   // XPUSH (row-parallel projection under TP): y tiles go to slot (parity, rank) of every rank's buffer
   XgmiPush xp;
+  // split-K workspace of the x-resident decode GEMM (decode_gemm.hip, go_xres): ks_ws fp32 partial tiles
+  // (256 floats per (tile, split)), ks_cnt one arrival counter per 16-row tile (zero, re-armed in-launch);
+  // nullptr -> whole-K tiles only
+  float* ks_ws = nullptr;
+  int* ks_cnt = nullptr;
+  long long ks_cap = 0;  // floats in ks_ws
+  int ks_ncnt = 0;       // ints in ks_cnt
 };
 // Persistent decode MLP block (O-proj + residual + ln2 prep -> gate_up + SwiGLU -> down + residual + next
 // norm prep), M <= 16, every K % 512 == 0.  ctl: DECODE_MLP_CTL_INTS ints, zero-initialised once, re-armed by the kernel.
@@ -127,6 +134,7 @@ struct DecodeBlockArgs {
 };
 void launch_decode_block(const DecodeBlockArgs& a, hipStream_t s);
 void set_decode_gemm_variant(int v);  // -1: default heuristic
+void set_decode_ksplit(int on);       // x-resident decode GEMM remainder split over K (default off)
 void set_decode_gemm_nt(int on);      // non-temporal weight-stream loads (keeps the variant choice)
 void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e,
                         hipStream_t s);

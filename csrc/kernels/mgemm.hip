@@ -145,10 +145,47 @@ __global__ __launch_bounds__(MG_THR, 1) void mgemm_kernel(const bf16* __restrict
     }
   };
 
+  // deferred-RMSNorm row scales (EPI >= 0 with e.ss_in): tpr threads per row sum the producer's partials.
+  // Loads issued before the DMA prologue, summed after it (the DMAs stay in flight); the scale lives in one
+  // register until the epilogue.  (Computed in the epilogue with one wave-serial loop per row, it cost
+  // ~13 us per launch at 64 rows: 16 dependent load round trips per wave.)
+  float rn_reg = 1.f;
+  int rn_row = -1;
+  float rn_part = 0.f;
+  int tpr = 1;
+  if constexpr (EPI >= 0) {
+    if (e.ss_in) {
+      while (tpr < 64 && tpr * 2 * M <= MG_THR) tpr *= 2;
+      const int row = threadIdx.x / tpr, sub = threadIdx.x % tpr;
+      if (row < M) {
+        rn_row = row;
+        const float* sp = e.ss_in + (long long)row * e.ss_tiles;
+        if (e.ss_tiles % (4 * tpr) == 0) {
+          const float4* s4 = reinterpret_cast<const float4*>(sp);
+#pragma unroll 8
+          for (int i = sub; i < e.ss_tiles / 4; i += tpr) {
+            const float4 q = s4[i];
+            rn_part += (q.x + q.y) + (q.z + q.w);
+          }
+        } else {
+#pragma unroll 8
+          for (int i = sub; i < e.ss_tiles; i += tpr) rn_part += sp[i];
+        }
+      }
+    }
+  }
+
   // prologue: chunks 0 .. D-1 in flight
 #pragma unroll
   for (int c = 0; c < C::D; ++c)
     if (c < nch) issue(c, c);
+
+  if constexpr (EPI >= 0) {
+    if (e.ss_in) {  // tpr consecutive lanes of one wave (tpr divides 64)
+      for (int o = 1; o < tpr; o *= 2) rn_part += __shfl_xor(rn_part, o, 64);
+      rn_reg = rsqrtf(rn_part * e.inv_d + e.eps);
+    }
+  }
 
   // chunk c lives in ring slot c % SLOTS.  Before computing it: wait until this wave's DMAs of chunk c
   // have landed (the D - 1 younger chunks stay in flight), barrier (every wave's x rows of the chunk are
@@ -173,9 +210,16 @@ __global__ __launch_bounds__(MG_THR, 1) void mgemm_kernel(const bf16* __restrict
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int m = 16 * mt + (lane & 15);
-        if (m < M)
-          *reinterpret_cast<float4*>(ys + (long long)m * N + n) =
-              make_float4(acc[rt][mt][0], acc[rt][mt][1], acc[rt][mt][2], acc[rt][mt][3]);
+        if (m >= M) continue;
+        const float4 f4 = make_float4(acc[rt][mt][0], acc[rt][mt][1], acc[rt][mt][2], acc[rt][mt][3]);
+        if constexpr (EPI >= 0) {  // read back in this launch by the last split: write-through (see below)
+          unsigned long long* q = reinterpret_cast<unsigned long long*>(ys + (long long)m * N + n);
+          const unsigned long long* w64 = reinterpret_cast<const unsigned long long*>(&f4);
+          __hip_atomic_store(q, w64[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(q + 1, w64[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          *reinterpret_cast<float4*>(ys + (long long)m * N + n) = f4;
+        }
       }
     }
   }
@@ -187,29 +231,22 @@ __global__ __launch_bounds__(MG_THR, 1) void mgemm_kernel(const bf16* __restrict
     if (S > 1) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores are out
       __syncthreads();
+      // hand-off without L2 maintenance (MI355X_MICROARCH.md): write-through slab stores drained above,
+      // relaxed agent add, the last split reads the slabs with agent-scope (L2-bypassing) loads.  Agent
+      // fences here wrote back / invalidated the XCD's whole L2 once per workgroup: the fused general path
+      // ran 6.22 vs 4.43 ms per 64-client step (profiles/r3/mg_fused_ab.jsonl).
       if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int got = __hip_atomic_fetch_add(counters + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int is_last = got == S - 1;
-        if (is_last) {
-          __hip_atomic_store(counters + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        if (is_last) __hip_atomic_store(counters + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *last = is_last;
       }
       __syncthreads();
       if (!*last) return;
     }
-    // deferred-RMSNorm row scales of the input rows (the producer's sum-of-squares partials)
+    // deferred-RMSNorm row scales of the input rows (summed before the main loop)
     if (e.ss_in) {
-      for (int m = wid; m < M; m += 4) {
-        float sacc = 0.f;
-        for (int i = lane; i < e.ss_tiles; i += 64) sacc += e.ss_in[(long long)m * e.ss_tiles + i];
-        sacc = wave_sum(sacc);
-        if (lane == 0) rn[m] = rsqrtf(sacc * e.inv_d + e.eps);
-      }
+      if (rn_row >= 0 && threadIdx.x % tpr == 0) rn[rn_row] = rn_reg;
       __syncthreads();
     }
 #pragma unroll
@@ -224,11 +261,16 @@ __global__ __launch_bounds__(MG_THR, 1) void mgemm_kernel(const bf16* __restrict
           v = f32x4{0.f, 0.f, 0.f, 0.f};
           if (mok)
             for (int sp = 0; sp < S; ++sp) {  // fixed split order: bitwise reproducible
-              const float4 p = *reinterpret_cast<const float4*>(y + ((long long)sp * M + m) * N + n);
-              v[0] += p.x;
-              v[1] += p.y;
-              v[2] += p.z;
-              v[3] += p.w;
+              const unsigned long long* q =
+                  reinterpret_cast<const unsigned long long*>(y + ((long long)sp * M + m) * N + n);
+              unsigned long long r[2];
+              r[0] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              r[1] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const float* p = reinterpret_cast<const float*>(r);
+              v[0] += p[0];
+              v[1] += p[1];
+              v[2] += p[2];
+              v[3] += p[3];
             }
         }
         const float sc = (e.ss_in && mok) ? rn[m] : 1.f;

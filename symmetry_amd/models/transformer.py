@@ -66,10 +66,16 @@ MAX_STEP_SEQS = 4096  # sequences per step (rows of last_ids)
 ATTN_PREFETCH_WGS = int(os.environ.get("SYMMETRY_ATTN_PREFETCH", "0"))
 # decode steps on the general path run rope_cache's per-row form (A/B knob)
 ROPE_DECODE_ROWS = os.environ.get("SYMMETRY_ROPE_DECODE_ROWS", "1") != "0"
-# decode steps on the general path run their four projections on mgemm with the fused decode epilogues
-# (in-launch split-K reduction; RoPE + KV write, residual + norm prep, SwiGLU in the GEMM) when every
-# projection has an mgemm pick: 5 launches per layer instead of 9 (0 = the slab + consumer-kernel path)
-MG_FUSED = os.environ.get("SYMMETRY_MG_FUSED", "1") != "0"
+# general path (20-256 rows): which projections run on mgemm with the fused decode epilogue (in-launch split-K
+# reduction; RoPE + KV write, residual + norm prep, SwiGLU in the GEMM) instead of slabs + a consumer kernel.
+#   "all": all four (5 launches per layer instead of 9), "gu" (default): gate_up + SwiGLU only (o's consumer
+#   becomes add_prep: deferred norm for gate_up), "0": none.  profiles/r3/mg_fused_ab.jsonl (alternating
+#   runs): 64 clients 4.84 / 4.30-4.33 / 4.46 ms per step, 32 clients 3.95 / 3.80 / 3.91 for all / gu / 0:
+#   the in-launch reduction's tail (one of S workgroups per column group sums the slabs) costs o / down /
+#   qkv more than the separate consumer kernel they save.
+MG_FUSED_MODE = os.environ.get("SYMMETRY_MG_FUSED", "gu")
+MG_FUSED = MG_FUSED_MODE in ("1", "all")
+MG_FUSED_GU = MG_FUSED_MODE == "gu"
 # projections of the FUSED decode path (below GENERAL_ROWS rows) that run on mgemm with their epilogue
 # instead of the decode GEMM (comma list of qkv, o, gu, down; A/B knob)
 MG_PROJ = tuple(p for p in os.environ.get("SYMMETRY_MG_PROJ", "").split(",") if p)
@@ -182,6 +188,8 @@ class TransformerLM:
         # samples here and the next step's embedding reads pending input tokens from here (src map),
         # so the host can enqueue step N+1 before it has seen step N's tokens (pipelined decode).
         self.last_ids = torch.zeros(MAX_STEP_SEQS, dtype=torch.int32, device=self.device)
+        if self.device.type != "cpu":
+            ops.decode_ks_ws(self.device)  # allocated before any graph capture (stable address)
         self.dgw = self._decode_copies(decode_weights)
         self.persistent_mlp = persistent_mlp
         self.fused_attn_block = fused_attn_block
@@ -309,12 +317,13 @@ class TransformerLM:
             return self._forward_general_fused(b, kv, mgs)
         return self._forward_general(b, kv)
 
-    def _mg_plan(self, b: ForwardBatch, names=("qkv", "o", "gu", "down"), need_all: bool = True):
+    def _mg_plan(self, b: ForwardBatch, names=("qkv", "o", "gu", "down"), need_all: bool = True,
+                 any_kind: bool = False):
         """mgemm (rw, split) + scratch per projection for the fused general path, or None."""
         # under TP only the column-parallel projections (qkv, gate_up: no collective in their epilogue)
         tp_ok = not self._tp_active() or set(names) <= {"qkv", "gu"}
-        if not (MG_FUSED and b.kind == "decode" and self.dgw and self.device.type != "cpu" and not self.cfg.is_moe
-                and tp_ok and b.num_tokens <= 256):
+        if not ((MG_FUSED or any_kind) and (b.kind == "decode" or any_kind) and self.dgw
+                and self.device.type != "cpu" and not self.cfg.is_moe and tp_ok and b.num_tokens <= 256):
             return None
         T, d, dq = b.num_tokens, self.cfg.hidden_size, self.hq * self.D
         wgu = self.w.layer(0, "w_gu")
@@ -483,14 +492,8 @@ class TransformerLM:
             ops.dg_swiglu(xw, w_gu, ss_t, eps, act, wshuf=True, mg=mgs["gu"])
             ops.dg_resid(act, self.dgw[(i, "w_down")], resid, nxt, xw, ss_t, wshuf=True, mg=mgs["down"])
             ss = ss_t
-        n = b.num_seqs
-        ids = self.last_ids[:n]
-        keys = self._buf("keys", (n,), torch.int64)
-        if n <= SKINNY_MAX_M:
-            tk = self._buf("tile_keys", (n * (self.vocab_shard // 16),), torch.int64)
-            logits = self._buf("logits", (n, self.vocab_shard), torch.float32) if b.need_logits or b.filtered else None
-            ops.dg_argmax(xw, w["lm_head"], ss, eps, b.temps, b.seeds, b.step, tk, keys, ids, 0, logits)
-            return self._finish_sampling(b, ids, keys, logits)
+        # normalise first: the lm_head's own row-scale prologue (4 waves x 16 rows of partial sums behind its weight
+        # loads) cost 295 vs 230 us at 64 rows (profiles/r3/prof_all64.csv)
         x = self._buf("x", (T, d), torch.bfloat16)
         ops.rownorm(xw, ss, eps, x)
         return self.sample(b, x)
@@ -509,6 +512,12 @@ class TransformerLM:
         src = b.src if b.src is not None and b.kind == "decode" else None
         ops.embed_rms_norm(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), eps, x, src,
                            self.last_ids if src is not None else None)
+        gu_plan = None
+        if MG_FUSED_GU and self.dgw and self.device.type != "cpu" and not cfg.is_moe and T <= 256:
+            gu_plan = (self._mg_plan(b, names=("gu",), need_all=False, any_kind=True) or {}).get("gu")
+        if gu_plan is not None:
+            xw = self._buf("xw", (T, d), torch.bfloat16)
+            ss_p = self._buf("ss_pgu", (T, 4 if d % 32 == 0 else 1), torch.float32)
         for i in range(cfg.num_layers):
             qkv = self._linear("qkv", x, w.layer(i, "wqkv"), wshuf=self._shuf(i, "wqkv"))
             ops.rope_cache(qkv, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq, self.hkv,
@@ -516,10 +525,18 @@ class TransformerLM:
             self._attention(b, kv, i, q, attn)
             o = self._linear("o", attn.view(T, self.hq * self.D), w.layer(i, "wo"), reduce=True,
                              wshuf=self._shuf(i, "wo"))
-            ops.add_rms_norm(o, resid, w.layer(i, "ln2"), eps, x)
-            if cfg.is_moe:
+            if gu_plan is not None:
+                # deferred norm into gate_up + SwiGLU epilogue (one mgemm launch instead of GEMM + swiglu)
+                ops.add_prep(o, resid, w.layer(i, "ln2"), xw, ss_p)
+                w_gu = self.dgw[(i, "w_gu")]
+                act = self._buf("act", (T, w_gu.shape[0] // 2), torch.bfloat16)
+                ops.dg_swiglu(xw, w_gu, ss_p, eps, act, wshuf=True, mg=gu_plan)
+                mlp = self._linear("down", act, w.layer(i, "w_down"), reduce=True, wshuf=self._shuf(i, "w_down"))
+            elif cfg.is_moe:
+                ops.add_rms_norm(o, resid, w.layer(i, "ln2"), eps, x)
                 mlp = self.moe.forward(i, x)
             else:
+                ops.add_rms_norm(o, resid, w.layer(i, "ln2"), eps, x)
                 gu = self._linear("gu", x, w.layer(i, "w_gu"), wshuf=self._shuf(i, "w_gu"))
                 F = gu.shape[-1] // 2
                 act = self._buf("act", (T, F), torch.bfloat16)

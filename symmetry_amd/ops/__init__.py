@@ -187,11 +187,31 @@ def dg_f32(x, W, ss_in, eps, y, wshuf=False):
     return reference.dg_f32(x, reference.unshuffled(W, wshuf), ss_in, eps, y)
 
 
+_KS_WS = {}
+KS_WS_FLOATS = 1 << 20  # 4 MB: 4096 (tile, split) partials
+KS_WS_TILES = 1 << 14
+
+
+def decode_ks_ws(device):
+    """The decode GEMMs' split-K workspace on ``device`` (fp32 partials + per-tile arrival counters, zeroed
+    once and re-armed by the kernel): one per device for the process, so its address is stable across hipGraph
+    captures.  Call it before capturing (the engine's model init does)."""
+    key = (device.type, device.index)
+    ws = _KS_WS.get(key)
+    if ws is None:
+        ws = (torch.empty(KS_WS_FLOATS, dtype=torch.float32, device=device),
+              torch.zeros(KS_WS_TILES, dtype=torch.int32, device=device), 0)
+        _KS_WS[key] = ws
+    return ws
+
+
 # mg: (slab [S, M, N] fp32, counters int32, rw) -> run the projection on the medium-M GEMM (mgemm, up to 256
-# rows, preshuffled weights) with the same fused epilogue after an in-launch split-K reduction
+# rows, preshuffled weights) with the same fused epilogue after an in-launch split-K reduction.  Without mg the
+# decode GEMM gets the device's split-K workspace (decode_gemm.hip go_xres: k split across workgroups where
+# whole 16-row tiles would leave CUs idle).
 def dg_qkv(x, W, ss_in, eps, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, wshuf=False, mg=None):
     if _gpu(x):
-        slab, cnt, rw = mg if mg is not None else (None, None, 0)
+        slab, cnt, rw = mg if mg is not None else decode_ks_ws(x.device)
         return _native.ops().dg_qkv(x, W, ss_in, float(eps), positions, slots, cos_sin, q_out, k_cache, v_cache,
                                     int(Hq), int(Hkv), bool(wshuf), slab, cnt, int(rw))
     return reference.dg_qkv(x, reference.unshuffled(W, wshuf), ss_in, eps, positions, slots, cos_sin, q_out,
@@ -200,14 +220,14 @@ def dg_qkv(x, W, ss_in, eps, positions, slots, cos_sin, q_out, k_cache, v_cache,
 
 def dg_resid(x, W, resid, w_next, xw_out, ss_out, wshuf=False, mg=None):
     if _gpu(x):
-        slab, cnt, rw = mg if mg is not None else (None, None, 0)
+        slab, cnt, rw = mg if mg is not None else decode_ks_ws(x.device)
         return _native.ops().dg_resid(x, W, resid, w_next, xw_out, ss_out, bool(wshuf), slab, cnt, int(rw))
     return reference.dg_resid(x, reference.unshuffled(W, wshuf), resid, w_next, xw_out, ss_out)
 
 
 def dg_swiglu(x, W, ss_in, eps, act, wshuf=False, mg=None):
     if _gpu(x):
-        slab, cnt, rw = mg if mg is not None else (None, None, 0)
+        slab, cnt, rw = mg if mg is not None else decode_ks_ws(x.device)
         return _native.ops().dg_swiglu(x, W, ss_in, float(eps), act, bool(wshuf), slab, cnt, int(rw))
     return reference.dg_swiglu(x, reference.unshuffled(W, wshuf), ss_in, eps, act)
 

@@ -464,3 +464,95 @@ def test_mgemm_fused_epilogues(gpu, M, kind):
             _close(act, act_ref, atol=1e-2, rtol=2e-2)
         torch.cuda.synchronize()
         assert int(mg[1].abs().sum()) == 0, "split-K counters must re-arm to zero"
+
+
+@pytest.mark.parametrize("M", [1, 10, 16])
+# (32, 8): Llama-3-8B QKV (384 tiles -> 768 half-K units); (4, 1): its TP=8 shard (48 tiles -> 192 quarter-K
+# units); (16, 4, 2048): K = 2048 (U = 1 per split)
+@pytest.mark.parametrize("Hq,Hkv,K", [(32, 8, 4096), (4, 1, 4096), (16, 4, 2048)])
+def test_dg_qkv_ksplit_xres(gpu, M, Hq, Hkv, K):
+    """x-resident decode GEMM with K split across workgroups (in-launch last-arriver reduction, decode_gemm.hip
+    go_xres): same outputs as the fp32 reference and as the whole-K kernel, repeated launches (counters re-arm)."""
+    from symmetry_amd.models.layout import preshuffle
+
+    D, BS, NB = 128, 32, 8
+    N = (Hq + 2 * Hkv) * D
+    x, W, s = _inputs(gpu, M, N, K, seed=21)
+    W = W[qkv_perm(Hq, Hkv, D).to(gpu)].contiguous()
+    Ws = preshuffle(W)
+    cs = ref.rope_table(1024, D, 500000.0, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(22)
+    pos = torch.randint(0, 1024, (M,), device=gpu, generator=g, dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device=gpu, generator=g)[:M].int()
+
+    def run(mg):
+        q = torch.empty(M, Hq, D, device=gpu, dtype=torch.bfloat16)
+        kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=torch.bfloat16)
+        vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=torch.bfloat16)
+        ops.dg_qkv(x, Ws, s, 1e-5, pos, slots, cs, q, kc, vc, Hq, Hkv, wshuf=True, mg=mg)
+        return q, kc, vc
+
+    from symmetry_amd.ops import _native
+
+    whole = run((None, None, 0))
+    _native.ops().decode_ksplit(1)
+    try:
+        for _ in range(3):
+            split = run(None)  # the device workspace: remainder tiles split over K
+            for a, b in zip(split, whole):
+                _close(a, b, atol=2e-2, rtol=2e-2)
+    finally:
+        _native.ops().decode_ksplit(0)
+    assert int(ops.decode_ks_ws(x.device)[1].abs().sum()) == 0  # every tile's counter re-armed
+    q_r, kc_r, vc_r = torch.empty(M, Hq, D, dtype=torch.bfloat16), torch.zeros(NB, Hkv, BS, D, dtype=torch.bfloat16), \
+        torch.zeros(NB, Hkv, D, BS, dtype=torch.bfloat16)
+    ref.dg_qkv(x.cpu(), W.cpu(), s.cpu(), 1e-5, pos.cpu(), slots.cpu(), cs.cpu(), q_r, kc_r, vc_r, Hq, Hkv)
+    for a, b in zip(split, (q_r, kc_r, vc_r)):
+        _close(a, b, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 10])
+def test_dg_resid_swiglu_ksplit_xres(gpu, M):
+    """RESID / SWIGLU epilogues on the split-K x-resident kernel: N = 2048 at K = 4096 is 128 whole tiles (half
+    the CUs) or 256 half-K units."""
+    from symmetry_amd.models.layout import preshuffle
+
+    F, K = 1024, 4096
+    x, W, s = _inputs(gpu, M, 2 * F, K, seed=23)
+    W = W[gu_perm(F).to(gpu)].contiguous()
+    Ws = preshuffle(W)
+    outs = []
+    from symmetry_amd.ops import _native
+
+    lib = _native.ops()
+    for mg in ((None, None, 0), None):
+        act = torch.empty(M, F, device=gpu, dtype=torch.bfloat16)
+        lib.decode_ksplit(int(mg is None))
+        try:
+            ops.dg_swiglu(x, Ws, s, 1e-5, act, wshuf=True, mg=mg)
+        finally:
+            lib.decode_ksplit(0)
+        outs.append(act)
+    act_ref = torch.empty(M, F, dtype=torch.bfloat16)
+    ref.dg_swiglu(x.cpu(), W.cpu(), s.cpu(), 1e-5, act_ref)
+    for a in outs:
+        _close(a, act_ref, atol=1e-2, rtol=2e-2)
+    N = 2048
+    x, W, _ = _inputs(gpu, M, N, K, seed=24)
+    g = torch.Generator(device=gpu).manual_seed(25)
+    resid0 = torch.randn(M, N, device=gpu, generator=g)
+    wn = (torch.randn(N, device=gpu, generator=g) * 0.1 + 1).bfloat16()
+    r_ref, xw_ref, ss_ref = resid0.cpu().clone(), torch.empty(M, N, dtype=torch.bfloat16), torch.empty(M, N // 16)
+    ref.dg_resid(x.cpu(), W.cpu(), r_ref, wn.cpu(), xw_ref, ss_ref)
+    for mg in ((None, None, 0), None):
+        resid = resid0.clone()
+        xw = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        ss = torch.empty(M, N // 16, device=gpu)
+        lib.decode_ksplit(int(mg is None))
+        try:
+            ops.dg_resid(x, preshuffle(W), resid, wn, xw, ss, wshuf=True, mg=mg)
+        finally:
+            lib.decode_ksplit(0)
+        _close(resid, r_ref, atol=2e-3, rtol=1e-3)
+        _close(xw, xw_ref, atol=2e-2, rtol=1e-2)
+        _close(ss, ss_ref, atol=1e-2, rtol=1e-3)

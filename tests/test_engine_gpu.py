@@ -78,26 +78,29 @@ def test_splitk_resid_path_native(gpu, monkeypatch, graphs):
 
 
 @pytest.mark.parametrize("graphs", [False, True])
-@pytest.mark.parametrize("mg_fused", [False, True])
+@pytest.mark.parametrize("mg_fused", ["0", "all", "gu"])
 def test_general_rows_decode_native(gpu, monkeypatch, graphs, mg_fused):
     """Decode steps on the general path, as wide batches run it, against the fp32 oracle; the threshold is
-    lowered so a small batch takes it.  mg_fused=False: mgemm projections -> rope_cache / add_rms_norm /
-    swiglu summing the slabs -> decode lm_head on normalised rows.  mg_fused=True (default): each projection
-    one mgemm launch with the decode epilogue fused after an in-launch split-K reduction."""
+    lowered so a small batch takes it.  "0": mgemm projections -> rope_cache / add_rms_norm / swiglu summing
+    the slabs -> decode lm_head on normalised rows.  "all": each projection one mgemm launch with the decode
+    epilogue fused after an in-launch split-K reduction.  "gu": only gate_up fused (SwiGLU epilogue, deferred
+    norm from add_prep)."""
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
     from symmetry_amd.engine.sequence import SamplingParams
     from symmetry_amd.models import transformer
 
     calls = []
-    if mg_fused:
-        orig = ops.dg_qkv
-        monkeypatch.setattr(ops, "dg_qkv", lambda *a, **k: (calls.append(a[0].shape[0]) if k.get("mg") else None)
+    if mg_fused != "0":
+        name = "dg_qkv" if mg_fused == "all" else "dg_swiglu"
+        orig = getattr(ops, name)
+        monkeypatch.setattr(ops, name, lambda *a, **k: (calls.append(a[0].shape[0]) if k.get("mg") else None)
                             or orig(*a, **k))
     else:
         orig = ops.mgemm
         monkeypatch.setattr(ops, "mgemm", lambda *a, **k: calls.append(a[0].shape[0]) or orig(*a, **k))
     monkeypatch.setattr(transformer, "GENERAL_ROWS", 1)
-    monkeypatch.setattr(transformer, "MG_FUSED", mg_fused)
+    monkeypatch.setattr(transformer, "MG_FUSED", mg_fused == "all")
+    monkeypatch.setattr(transformer, "MG_FUSED_GU", mg_fused == "gu")
     eng = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", max_num_seqs=6, max_model_len=1024,
                                  num_kv_blocks=64, use_graphs=graphs))
     prompts = [list(range(700 + 9 * i, 720 + 11 * i)) for i in range(5)]
