@@ -29,6 +29,10 @@ def main():
     ap.add_argument("--row-major", action="store_true")
     ap.add_argument("--cfgs", type=int, nargs="+", default=[-1],
                     help="persistent configurations (launch_decode_mlp; -1 = default)")
+    ap.add_argument("--xcfgs", type=int, nargs="+", default=[],
+                    help="x-resident persistent kernel A/B knob bits (decode_gemm.hip g_mlp_xcfg)")
+    ap.add_argument("--stamps", action="store_true",
+                    help="x-resident kernel: per-phase s_memrealtime stamps of the last layer (us from launch start)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     d, F, L = args.d, args.F, args.layers
@@ -63,8 +67,13 @@ def main():
         res = {"M": M, "layers": L, "layout": "preshuffled" if shuf else "row-major"}
         lib = ops._native.ops()
         runs = [("three_launches", seq, None)] + [(f"persistent{'' if c < 0 else c}", per, c) for c in args.cfgs]
+        runs += [(f"xres_x{x}", per, -1 - 1000 * (x + 1)) for x in args.xcfgs]
         for name, fn, c in runs:
-            if c is not None:
+            if c is not None and c <= -1000:
+                lib.decode_gemm_variant(-1)
+                lib.decode_gemm_variant(2000 + (-c // 1000 - 1))
+            elif c is not None:
+                lib.decode_gemm_variant(2000)
                 lib.decode_gemm_variant(1000 + c if c >= 0 else -1)
             s = torch.cuda.Stream()
             with torch.cuda.stream(s):
@@ -86,6 +95,22 @@ def main():
             res[f"{name}_TBps"] = round(byts / L / (us * 1e-6) / 1e12, 2)
             res[f"{name}_ctl_ok"] = not bool(ctl.any())
         lib.decode_gemm_variant(-1)
+        lib.decode_gemm_variant(2000)
+        if args.stamps:
+            st = torch.zeros(1024, 8, dtype=torch.int64, device=dev)
+            lib.decode_mlp_stamps(st)
+            for _ in range(2):
+                per()
+            torch.cuda.synchronize()
+            lib.decode_mlp_stamps(None)
+            st = st.cpu()
+            st = st[st[:, 0] > 0]
+            t0 = int(st[:, 0].min())
+            names = ["start", "o_done", "gu_wait_done", "gu_done", "d_wait_done", "end"]
+            q = torch.tensor([0.0, 0.1, 0.5, 0.9, 1.0])
+            res["stamps_us_p0_10_50_90_100"] = {
+                n: [round(v, 2) for v in (torch.quantile((st[:, k] - t0).double(), q.double()) * 0.01).tolist()]
+                for k, n in enumerate(names)}
         print(json.dumps(res), flush=True)
 
 

@@ -957,6 +957,9 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) y, int variant=0) -> ()", &skinny_gemm);
   m.def("mgemm(Tensor x, Tensor w, Tensor(a!) y, int rw) -> ()", &mgemm);
   m.def("mgemm_nt(int on) -> ()", [](int64_t on) { set_mgemm_nt((int)on); });
+  m.def("decode_mlp_stamps(Tensor? stamps) -> ()", [](const c10::optional<Tensor>& t) {
+    set_decode_mlp_stamps(t.has_value() ? reinterpret_cast<long long*>(t->data_ptr()) : nullptr);
+  });
   m.def("attn_stream_min(int tokens) -> ()", [](int64_t t) { set_attn_stream_min((int)t); });
   m.def("attn_wave(int min_units, int min_span) -> ()",
         [](int64_t u, int64_t span) { set_attn_wave((int)u, (int)span); });

@@ -376,6 +376,294 @@ __global__ __launch_bounds__(NW * 64, WPE) void decode_mlp_kernel(DecodeMlpArgs 
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Persistent decode MLP on x-resident bodies: O -> gate_up -> down of one layer in ONE launch, one 16-wave
+// workgroup per CU (M <= 16, dq = d = 1024 U, F % 1024 == 0).
+//
+// decode_mlp_kernel above ran every phase on 8-wave gemm_tile bodies (10-38 spilled VGPRs) and lost to the
+// three launches.  Here O and gate_up run the decode_gemm_xres_kernel body (each wave loads its k-slice of x
+// once per phase, the next tile's weights are in flight during a tile's reduction and epilogue) and down runs
+// 16 waves splitting K = F in rounds of U k-blocks.
+//
+// Where the launches lose time is where HBM idles: the latency-bound O projection (33.5 MB in ~10 us, half
+// the chip's rate), the launch boundaries and every launch's ramp and tail.  So the weights of the NEXT
+// phase's first round are staged into LDS by LDS-DMA early, with nothing waiting on them: gate_up tile 0
+// (128 KB per CU at U = 4, 32 MB chip-wide) from the first instruction of the launch, behind the O loads;
+// the down tile's first U k-blocks of every wave from gate_up tile 1 on (the LDS slice is free once tile
+// 0's fragments are in registers).  A phase then starts on bytes that are already on chip.  Measured
+// variants: profiles/r3/mlp_xres_*.jsonl (bench/kernels/bench_decode_mlp.py --xcfgs, --stamps).
+//
+// Hand-offs (MI355X_MICROARCH.md hand-off table, first row): wave 0 runs every epilogue of its workgroup and
+// stores write-through (sc1); after the workgroup's last tile of a phase it drains vmcnt and ONE lane adds
+// to the workgroup's counter line (b % 64); wave 0 keeps no weight loads of its own in flight across a
+// publish or a poll (its slice of a next round is issued after them), so neither waits on the stream.  The
+// consumer's wave 0 polls the 64 lines with sc1 loads, a workgroup barrier follows, then every read of
+// handed-off bytes (xw, the ss partials, act, the residual) is an sc1 (L1-bypassing) load -- 16-B buffer
+// loads (aux 16): the 8-B atomic form doubled the request count and cost 9 us per layer at M = 10.  No acquire
+// fence: its buffer_inv + vmcnt(0) would wait for the weight stream in flight.  Write-after-read is safe by
+// the edges: xw / ss are rewritten by the down epilogue only after every workgroup has published its
+// gate_up phase, i.e. finished reading them.
+// Deadlock freedom: grid = #CUs with one resident workgroup per CU (checked at the first launch).  Spins are
+// bounded (error word); the last workgroup out re-arms the counter lines (graph-replay safe).
+// O and gate_up are bitwise equal to the x-resident launches; down sums K in a different order than the
+// 4-wave standalone kernel (fp32-close).
+// ---------------------------------------------------------------------------------------------------
+// 16 B from a buffer resource; aux 16 = sc1 (L1-bypassing: bytes written by another CU in this launch)
+SYM_DEV uint4 ldbuf16_sc1(__amdgpu_buffer_rsrc_t r, int off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+SYM_DEV __amdgpu_buffer_rsrc_t mk_rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+int g_mlp_xcfg = 0;  // A/B knobs of decode_mlp_xres_kernel (set_decode_gemm_variant(2000 + bits)):
+                     // 8 = no down-tile LDS staging, 16 = no gate_up-tile LDS staging
+
+template <int U>
+__global__ __launch_bounds__(1024) void decode_mlp_xres_kernel(DecodeMlpArgs a) {
+  constexpr int NW = 16;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, h = lane >> 4;
+  const int b = blockIdx.x, G = gridDim.x;
+  const int M = a.M, d = a.d, F = a.F;
+  const int nO = d / 16, nG = 2 * F / 16, nD = d / 16;
+  const int tO = nO > b ? (nO - b + G - 1) / G : 0;  // this workgroup's tiles per phase: b, b + G, ...
+  const int tG = nG > b ? (nG - b + G - 1) / G : 0;
+  const int tD = nD > b ? (nD - b + G - 1) / G : 0;
+  const int nb = F / 1024;  // down k-blocks per wave
+  const bool stage_g = !(a.xcfg & 16) && tG > 0, stage_d = !(a.xcfg & 8) && tD > 0 && tG > 1;
+  int* ctl = a.ctl;
+  const int wmul = a.wshuf ? 16 : 1, wsec = a.wshuf ? 512 : 32;
+  const int m = r16;
+  const bool mok = m < M;
+  const int mr = min(r16, M - 1);
+  auto wptr = [&](const bf16* W, int K, int t) -> const bf16* {  // this wave's k-slice of 16-row tile t
+    const int kbeg = wid * (K / NW);
+    return a.wshuf ? W + ((long long)t * (K / 32) + kbeg / 32) * 512 + lane * 8
+                   : W + (long long)(16 * t + r16) * K + kbeg + 8 * h;
+  };
+  Pack8 wa[U][2];
+  auto load_w = [&](const bf16* wp, int j0, int n) {  // k-blocks j0 .. j0 + U - 1 (< n) of a slice
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (j0 + j < n) {
+        wa[j][0].u = *reinterpret_cast<const uint4*>(wp + (j0 + j) * 64 * wmul);
+        wa[j][1].u = *reinterpret_cast<const uint4*>(wp + (j0 + j) * 64 * wmul + wsec);
+      }
+  };
+  // per-wave LDS staging slice (U k-blocks x 2 halves x 1 KB) filled by LDS-DMA: lane l's 16 B land at l * 16
+  __shared__ __attribute__((aligned(1024))) char pf[NW][U][2][1024];
+  __shared__ f32x4 red[2][NW - 1][64];  // waves 1..15's partials (wave 0 keeps its own in registers)
+  auto stage = [&](const bf16* wp, int n) {  // the first min(U, n) k-blocks of a slice -> this wave's pf
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (j < n) {
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(wp + j * 64 * wmul + hf * wsec),
+              (__attribute__((address_space(3))) void*)&pf[wid][j][hf][0], 16, 0, 0);
+      }
+  };
+  auto unstage = [&](int n) {  // staged k-blocks -> wa (the wave's own DMAs: vmcnt covers them)
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (j < n) {
+        wa[j][0].u = *reinterpret_cast<const uint4*>(&pf[wid][j][0][lane * 16]);
+        wa[j][1].u = *reinterpret_cast<const uint4*>(&pf[wid][j][1][lane * 16]);
+      }
+  };
+  DecodeEpi eo, eg, ed;
+  eo.resid = ed.resid = a.resid;
+  eo.w_next = a.ln2;
+  eo.xw_out = ed.xw_out = a.xw;
+  eo.ss_out = ed.ss_out = a.ss;
+  eo.sc1 = 1;  // resid / xw / ss read by other CUs of this launch
+  eg.act = a.act;
+  eg.sc1 = 1;
+  ed.w_next = a.w_next;
+  ed.resid_sc1 = 1;  // the residual was rewritten by the O phase of this launch
+  int buf = 0;
+  long long* st = a.stamps ? a.stamps + 8 * b : nullptr;  // phase stamps (timing only)
+  auto stamp = [&](int k) {
+    if (st && threadIdx.x == 0) st[k] = (long long)__builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  // wave 0 reduces a tile's 16 partials (same order as decode_gemm_xres_kernel: bitwise-equal results)
+  auto reduce = [&](f32x4 acc) -> f32x4 {
+    if (wid != 0) red[buf][wid - 1][lane] = acc;
+    __syncthreads();
+    f32x4 v = acc;
+    if (wid == 0) {
+#pragma unroll
+      for (int w = 1; w < NW; ++w) {
+        v += red[buf][w - 1][lane];
+        if ((w & 3) == 3) asm volatile("" : "+v"(v)::"memory");
+      }
+    }
+    buf ^= 1;
+    return v;
+  };
+  auto publish = [&](int* lines) {  // wave 0 only: its write-through stores acknowledged, then one add
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+      __hip_atomic_fetch_add(lines + (b % MLP_LINES) * MLP_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto mma = [&](const Pack8 (&xa)[U][2], int n) -> f32x4 {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (j < n) {
+        acc = mfma16(wa[j][0].v, xa[j][0].v, acc);
+        acc = mfma16(wa[j][1].v, xa[j][1].v, acc);
+      }
+    return acc;
+  };
+
+  // ---- phase O: attn [M, d] (previous launch's output: plain loads) x Wo -> resid, xw, ss (sc1) ----
+  if (tO > 0) load_w(wptr(a.Wo, d, b), 0, U);
+  {
+    Pack8 xa[U][2];
+    const bf16* xrow = a.attn + (long long)mr * d + wid * (d / NW) + 8 * h;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      xa[j][0].u = mok ? *reinterpret_cast<const uint4*>(xrow + j * 64) : make_uint4(0, 0, 0, 0);
+      xa[j][1].u = mok ? *reinterpret_cast<const uint4*>(xrow + j * 64 + 32) : make_uint4(0, 0, 0, 0);
+    }
+    if (stage_g) stage(wptr(a.Wgu, d, b), U);  // gate_up tile 0 streams in behind the O loads
+    for (int i = 0; i < tO; ++i) {
+      const int t = b + i * G;
+      const f32x4 acc = mma(xa, U);
+      __builtin_amdgcn_sched_barrier(0);
+      if (i + 1 < tO) load_w(wptr(a.Wo, d, t + G), 0, U);
+      const f32x4 v = reduce(acc);
+      if (wid == 0) epilogue<DECODE_EPI_RESID>(eo, v, t, m, mok, h, d);
+    }
+  }
+  stamp(1);
+  if (wid == 0) publish(ctl + MLP_CNT_O);
+
+  // ---- phase gate_up: xw (sc1) x Wgu, RMSNorm row scale from the ss partials (sc1) -> act (sc1) ----
+  if (wid != 0 && !stage_g && tG > 0) load_w(wptr(a.Wgu, d, b), 0, U);
+  WaitFor{ctl + MLP_CNT_O, G, ctl + MLP_ERR}();
+  stamp(2);
+  {
+    Pack8 xa[U][2];
+    const __amdgpu_buffer_rsrc_t xr = mk_rsrc(a.xw, (long long)M * d * 2);
+    const int xo = (mr * d + wid * (d / NW) + 8 * h) * 2;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      xa[j][0].u = mok ? ldbuf16_sc1(xr, xo + j * 128) : make_uint4(0, 0, 0, 0);
+      xa[j][1].u = mok ? ldbuf16_sc1(xr, xo + j * 128 + 64) : make_uint4(0, 0, 0, 0);
+    }
+    if (wid == 0 && !stage_g && tG > 0) load_w(wptr(a.Wgu, d, b), 0, U);
+    float rn = 1.f;  // wave 0: the deferred-RMSNorm scale of row r16 (lanes h = 0..3 sum a quarter each)
+    if (wid == 0) {
+      const __amdgpu_buffer_rsrc_t sr = mk_rsrc(a.ss, (long long)M * (d / 16) * 4);
+      float s = 0.f;
+      if (mok)
+        for (int i = 4 * h; i < d / 16; i += 16) {  // 16-B chunks h, h + 4, ... of row r16's partials
+          const uint4 q = ldbuf16_sc1(sr, (mr * (d / 16) + i) * 4);
+          s += __uint_as_float(q.x) + __uint_as_float(q.y) + __uint_as_float(q.z) + __uint_as_float(q.w);
+        }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      rn = rsqrtf(s / (float)d + a.eps);
+    }
+    for (int i = 0; i < tG; ++i) {
+      const int t = b + i * G;
+      if (i == 0 && stage_g) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA landed (and x, needed next anyway)
+        unstage(U);
+      }
+      const f32x4 acc = mma(xa, U);
+      __builtin_amdgcn_sched_barrier(0);
+      if (i + 1 < tG) load_w(wptr(a.Wgu, d, t + G), 0, U);
+      if (i == 0 && stage_d) {  // the down tile's first round streams in for the rest of this phase
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's pf reads are done
+        stage(wptr(a.Wd, F, b), nb);
+      }
+      f32x4 v = reduce(acc);
+      if (wid == 0) {
+        const float sc = mok ? rn : 1.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] *= sc;
+        epilogue<DECODE_EPI_SWIGLU>(eg, v, t, m, mok, h, 2 * F);
+      }
+    }
+  }
+  stamp(3);
+  if (wid == 0) publish(ctl + MLP_CNT_GU);
+
+  // ---- phase down: act (sc1) x Wd, 16 waves splitting K = F -> resid (sc1 reads), xw, ss for the next launch ----
+  const int j1 = stage_d ? U : 0;  // first k-block not staged
+  if (wid != 0 && tD > 0 && j1 < nb) load_w(wptr(a.Wd, F, b), j1, nb);  // the round after the staged one
+  WaitFor{ctl + MLP_CNT_GU, G, ctl + MLP_ERR}();
+  stamp(4);
+  const __amdgpu_buffer_rsrc_t ar = mk_rsrc(a.act, (long long)M * F * 2);
+  for (int i = 0; i < tD; ++i) {
+    const int t = b + i * G;
+    const bf16* wp = wptr(a.Wd, F, t);
+    const int xo = (mr * F + wid * (F / NW) + 8 * h) * 2;
+    auto ldx = [&](Pack8 (&xa)[U][2], int j0) {
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (j0 + j < nb) {
+          xa[j][0].u = mok ? ldbuf16_sc1(ar, xo + (j0 + j) * 128) : make_uint4(0, 0, 0, 0);
+          xa[j][1].u = mok ? ldbuf16_sc1(ar, xo + (j0 + j) * 128 + 64) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    int j0 = 0;
+    if (i == 0 && stage_d) {  // round 0 from LDS; wave != 0 already has round 1 in flight in wa
+      Pack8 xs[U][2];
+      ldx(xs, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA landed (x is the youngest load anyway)
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (j < nb) {  // one k-block of staged weights in registers at a time (wa holds the next round)
+          Pack8 w0, w1;
+          w0.u = *reinterpret_cast<const uint4*>(&pf[wid][j][0][lane * 16]);
+          w1.u = *reinterpret_cast<const uint4*>(&pf[wid][j][1][lane * 16]);
+          acc = mfma16(w0.v, xs[j][0].v, acc);
+          acc = mfma16(w1.v, xs[j][1].v, acc);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      j0 = U;
+    }
+    for (; j0 < nb; j0 += U) {
+      if (!(i == 0 && j0 == j1 && wid != 0)) load_w(wp, j0, nb);  // (wave != 0: round j1 is in flight)
+      Pack8 xa[U][2];
+      ldx(xa, j0);
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (j0 + j < nb) {
+          acc = mfma16(wa[j][0].v, xa[j][0].v, acc);
+          acc = mfma16(wa[j][1].v, xa[j][1].v, acc);
+        }
+    }
+    const f32x4 v = reduce(acc);
+    if (wid == 0) epilogue<DECODE_EPI_RESID>(ed, v, t, m, mok, h, d);
+  }
+  if (st && threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(5);
+  }
+
+  // last workgroup out (every other one is past both waits): re-arm the counter lines for the next launch
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(ctl + MLP_DONE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
+  __syncthreads();
+  if (s_last) {
+    for (int i = threadIdx.x; i < 2 * MLP_LINES; i += blockDim.x)
+      __hip_atomic_store(ctl + i * MLP_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(ctl + MLP_DONE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// ---------------------------------------------------------------------------------------------------
 // Fused decode attention block: QKV projection (+ RoPE, paged K/V write) -> split-KV attention ->
 // O-projection (+ residual, ln2 prep) of one layer in ONE launch (M <= 16 rows, TP = 1).
 //
@@ -950,8 +1238,35 @@ void go_mlp(const DecodeMlpArgs& a, hipStream_t s) {
   decode_mlp_kernel<NW, U, WPE><<<std::min(total, resident), NW * 64, 0, s>>>(a);
 }
 
+// x-resident persistent MLP: one 16-wave workgroup per CU; false when the shapes or the residency do not fit
+long long* g_mlp_stamps = nullptr;
+
+bool go_mlp_xres(const DecodeMlpArgs& a0, hipStream_t s) {
+  DecodeMlpArgs a = a0;
+  a.stamps = g_mlp_stamps;
+  a.xcfg = g_mlp_xcfg;
+  if (a.M > 16 || a.dq != a.d || a.d % 1024 || a.d > 4096 || a.F % 1024) return false;
+  static int grid = -1;
+  if (grid < 0) {  // every workgroup must be resident at once (they wait on each other)
+    int dev = 0, cus = 0, per_cu = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_mlp_xres_kernel<4>, 1024, 0);
+    grid = per_cu >= 1 ? std::max(1, cus) : 0;
+  }
+  if (grid == 0) return false;
+  switch (a.d / 1024) {
+    case 1: decode_mlp_xres_kernel<1><<<grid, 1024, 0, s>>>(a); return true;
+    case 2: decode_mlp_xres_kernel<2><<<grid, 1024, 0, s>>>(a); return true;
+    case 4: decode_mlp_xres_kernel<4><<<grid, 1024, 0, s>>>(a); return true;
+    default: return false;
+  }
+}
+
 void launch_decode_mlp(const DecodeMlpArgs& a, hipStream_t s) {
-  // (waves per tile, k-blocks in flight per wave, waves per SIMD): A/B by bench/kernels/bench_decode_mlp.py
+  // default: the x-resident persistent kernel where it applies; configurations 0-6 select the gemm_tile
+  // kernel's (waves per tile, k-blocks in flight per wave, waves per SIMD): A/B by bench/kernels/bench_decode_mlp.py
+  if (g_mlp_cfg < 0 && go_mlp_xres(a, s)) return;
   switch (g_mlp_cfg < 0 ? 0 : g_mlp_cfg) {
     case 1: go_mlp<8, 4, 2>(a, s); break;   // 1 WG / CU, deeper
     case 2: go_mlp<4, 2, 4>(a, s); break;   // 4 WGs / CU
@@ -963,9 +1278,16 @@ void launch_decode_mlp(const DecodeMlpArgs& a, hipStream_t s) {
   }
 }
 
+void set_decode_mlp_stamps(long long* stamps) { g_mlp_stamps = stamps; }
+
 void set_decode_ksplit(int on) { g_dg_ksplit = on != 0; }
 
 void set_decode_gemm_variant(int v) {
+  // v >= 2000: A/B knob bits of the x-resident persistent MLP (decode_mlp_xres_kernel)
+  if (v >= 2000) {
+    g_mlp_xcfg = v - 2000;
+    return;
+  }
   // v >= 1000: persistent decode MLP configuration v - 1000 (launch_decode_mlp)
   if (v >= 1000 || v == -1) {
     g_mlp_cfg = v >= 1000 ? v - 1000 : -1;

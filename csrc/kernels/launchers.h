@@ -90,10 +90,13 @@ struct DecodeMlpArgs {
   float* ss = nullptr;         // [M, d / 16]
   bf16* act = nullptr;         // [M, F]
   int* ctl = nullptr;
+  long long* stamps = nullptr;  // optional [grid][8] s_memrealtime phase stamps (x-resident kernel; timing only)
+  int xcfg = 0;                 // x-resident kernel A/B knobs (set by the launcher)
   int M = 0, d = 0, dq = 0, F = 0, wshuf = 0;
   float eps = 0.f;
 };
 void launch_decode_mlp(const DecodeMlpArgs& a, hipStream_t s);
+void set_decode_mlp_stamps(long long* stamps);  // nullptr: off
 // Fused decode attention block (QKV + RoPE + K/V write -> split-KV attention -> O + residual + ln2 prep),
 // M <= 16, D = 128, G = Hq / Hkv <= 8, d % 512 == 0.  ctl: DECODE_BLOCK_CTL_INTS ints, zero-initialised
 // once, re-armed by the kernel (word ctl[(Hkv + 9) * 32] != 0 after a launch: a dependency wait gave up).
