@@ -399,7 +399,8 @@ class TransformerLM:
         ops.embed_prep(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), xw, ss_1, b.src, self.last_ids)
         ss = ss_1
         proj = MG_PROJ if not self._tp_active() else tuple(p for p in MG_PROJ if p in ("qkv", "gu"))
-        mgp = (self._mg_plan(b, proj, need_all=False) or {}) if proj else {}
+        # (SYMMETRY_MG_PROJ picks these per projection, independent of the general path's SYMMETRY_MG_FUSED mode)
+        mgp = (self._mg_plan(b, proj, need_all=False, any_kind=b.kind == "decode") or {}) if proj else {}
         persistent = self._persistent_mlp_ok(T)
         ctl = self.ws.get("mlp_ctl", (ops.DECODE_MLP_CTL,), torch.int32, self.device, zeros=True) if persistent else None
         block = self._attn_block_ok(b)

@@ -142,13 +142,16 @@ def test_wide_decode_batches_native(gpu, monkeypatch, graphs):
 @pytest.mark.parametrize("lens", [(40, 45), (70, 60, 50), (256,)])
 def test_medium_m_prefill_native(gpu, monkeypatch, lens):
     """Prefill steps of 65..256 tokens run their projections on mgemm (split-K slabs summed by rope_cache /
-    add_rms_norm / swiglu) and still generate the oracle's tokens."""
+    add_rms_norm / swiglu, or gate_up as one mgemm launch with the SwiGLU epilogue) and still generate the
+    oracle's tokens."""
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
     from symmetry_amd.engine.sequence import SamplingParams
 
     calls = []
-    orig = ops.mgemm
+    orig, orig_sw = ops.mgemm, ops.dg_swiglu
     monkeypatch.setattr(ops, "mgemm", lambda *a, **k: calls.append(a[0].shape[0]) or orig(*a, **k))
+    monkeypatch.setattr(ops, "dg_swiglu", lambda *a, **k: (k.get("mg") is not None and calls.append(a[0].shape[0]))
+                        or orig_sw(*a, **k))
     eng = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", max_num_seqs=4, max_model_len=1024,
                                  num_kv_blocks=64, use_graphs=True))
     prompts = [list(range(400 + 17 * i, 400 + 17 * i + n)) for i, n in enumerate(lens)]
