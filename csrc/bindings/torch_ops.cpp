@@ -606,6 +606,72 @@ void dg_qkv(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in
   launch_dg(DECODE_EPI_QKV, x, W, sh, e, mg_slab, mg_counters, mg_rw);
 }
 
+// dg_qkv + attn_decode as ONE launch where it applies (decode_gemm.hip, decode_qkv_attn_kernel); returns false
+// (nothing enqueued) otherwise
+bool qkv_attn(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, const Tensor& positions,
+              const Tensor& slots, const Tensor& cos_sin, Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t Hq,
+              int64_t Hkv, bool wshuf, const Tensor& block_tables, const Tensor& ctx_lens, Tensor& out, Tensor& tmp_o,
+              Tensor& tmp_ml, Tensor& counters, double scale, Tensor& ctl) {
+  auto sh = dg_check(x, W);
+  for (auto* t : {&positions, &slots, &block_tables, &ctx_lens}) {
+    check_gpu(*t, "index tensor");
+    check_dtype(*t, at::kInt, "index tensor");
+  }
+  check_gpu(cos_sin, "cos_sin");
+  check_dtype(cos_sin, at::kFloat, "cos_sin");
+  check_cache(k_cache, v_cache);
+  for (auto* t : {&q_out, &out}) {
+    check_gpu(*t, "q_out / out");
+    check_dtype(*t, at::kBFloat16, "q_out / out");
+  }
+  for (auto* t : {&tmp_o, &tmp_ml}) {
+    check_gpu(*t, "tmp_o / tmp_ml");
+    check_dtype(*t, at::kFloat, "tmp_o / tmp_ml");
+  }
+  for (auto* t : {&counters, &ctl}) {
+    check_gpu(*t, "counters / ctl");
+    check_dtype(*t, at::kInt, "counters / ctl");
+  }
+  const int64_t M = sh.M;
+  TORCH_CHECK(sh.N == (Hq + 2 * Hkv) * 128, "qkv_attn: N must be (Hq + 2 Hkv) * 128");
+  TORCH_CHECK(k_cache.size(1) == Hkv && Hq % Hkv == 0, "qkv_attn: head counts");
+  TORCH_CHECK(positions.numel() >= M && slots.numel() >= M && ctx_lens.numel() >= M, "qkv_attn: index tensors");
+  TORCH_CHECK(q_out.numel() >= M * Hq * 128 && out.numel() == M * Hq * 128, "qkv_attn: q_out / out");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == 128, "qkv_attn: cos_sin [max_pos, 128]");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= M, "qkv_attn: block_tables [>=M, max_blocks]");
+  TORCH_CHECK(tmp_o.dim() == 4 && tmp_o.size(0) >= M && tmp_o.size(1) == Hq && tmp_o.size(3) == 128,
+              "qkv_attn: tmp_o [>=M, Hq, max_parts, 128]");
+  const int64_t max_parts = tmp_o.size(2), BS = k_cache.size(2), max_blocks = block_tables.size(1);
+  TORCH_CHECK(tmp_ml.numel() >= M * Hq * max_parts * 2, "qkv_attn: tmp_ml too small");
+  TORCH_CHECK(max_parts * 256 >= max_blocks * BS, "qkv_attn: tmp_o has too few partitions for the block table span");
+  TORCH_CHECK(counters.numel() >= M * Hkv && ctl.numel() >= QKV_ATTN_CTL_INTS, "qkv_attn: counters / ctl");
+  DecodeEpi e;
+  e.wshuf = wshuf ? 1 : 0;
+  dg_norm_in(e, ss_in, M, sh.K, eps);
+  e.positions = ptr<int>(positions);
+  e.slots = ptr<int>(slots);
+  e.cos_sin = ptr<float>(cos_sin);
+  e.q_out = ptr<bf16>(q_out);
+  e.k_cache = ptr<bf16>(k_cache);
+  e.v_cache = ptr<bf16>(v_cache);
+  e.Hq = (int)Hq;
+  e.Hkv = (int)Hkv;
+  e.BS = (int)BS;
+  QkvAttnArgs aa;
+  aa.block_tables = ptr<int>(block_tables);
+  aa.ctx_lens = ptr<int>(ctx_lens);
+  aa.out = ptr<bf16>(out);
+  aa.tmp_o = ptr<float>(tmp_o);
+  aa.tmp_ml = ptr<float>(tmp_ml);
+  aa.counters = ptr<int>(counters);
+  aa.max_blocks = (int)max_blocks;
+  aa.max_parts = (int)max_parts;
+  aa.scale_log2 = (float)scale * 1.4426950408889634f;
+  aa.ctl = ptr<int>(ctl);
+  const at::OptionalDeviceGuard g(x.device());
+  return launch_qkv_attn(ptr<bf16>(x), ptr<bf16>(W), (int)M, (int)sh.N, (int)sh.K, e, aa, cur_stream(x));
+}
+
 void dg_resid(const Tensor& x, const Tensor& W, Tensor& resid, const Tensor& w_next, Tensor& xw_out, Tensor& ss_out, bool wshuf,
               const c10::optional<Tensor>& mg_slab, const c10::optional<Tensor>& mg_counters, int64_t mg_rw) {
   auto sh = dg_check(x, W, is_mg(mg_slab));
@@ -957,6 +1023,9 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) y, int variant=0) -> ()", &skinny_gemm);
   m.def("mgemm(Tensor x, Tensor w, Tensor(a!) y, int rw) -> ()", &mgemm);
   m.def("mgemm_nt(int on) -> ()", [](int64_t on) { set_mgemm_nt((int)on); });
+  m.def("qkv_attn_stamps(Tensor? stamps) -> ()", [](const c10::optional<Tensor>& t) {
+    set_qkv_attn_stamps(t.has_value() ? reinterpret_cast<long long*>(t->data_ptr()) : nullptr);
+  });
   m.def("decode_mlp_stamps(Tensor? stamps) -> ()", [](const c10::optional<Tensor>& t) {
     set_decode_mlp_stamps(t.has_value() ? reinterpret_cast<long long*>(t->data_ptr()) : nullptr);
   });
@@ -973,6 +1042,12 @@ TORCH_LIBRARY(symmetry_amd, m) {
       "Tensor(d!) offsets, Tensor(e!) cursor, Tensor(f!) xs, Tensor(g!) dst) -> ()",
       &moe_route_permute);
   m.def("dg_f32(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor(a!) y, bool wshuf=False) -> ()", &dg_f32);
+  m.def(
+      "qkv_attn(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor positions, Tensor slots, Tensor cos_sin, "
+      "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, bool wshuf, Tensor block_tables, "
+      "Tensor ctx_lens, Tensor(d!) out, Tensor(e!) tmp_o, Tensor(f!) tmp_ml, Tensor(g!) counters, float scale, "
+      "Tensor(h!) ctl) -> bool",
+      &qkv_attn);
   m.def(
       "dg_qkv(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor positions, Tensor slots, Tensor cos_sin, "
       "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, bool wshuf=False, "

@@ -889,6 +889,14 @@ static int g_attn_stream_cfg = [] {
   return knob ? atoi(knob) : 0;
 }();
 
+bool attn_decode_uses_grid(int num_seqs, int Hkv, int BS, int max_blocks, int G) {
+  const int span = max_blocks * BS;
+  const bool wave = g_attn_wave_units > 0 && num_seqs * Hkv >= g_attn_wave_units && span >= g_attn_wave_span &&
+                    G <= 16 && max_blocks <= 64;
+  const bool stream = g_attn_stream_min > 0 && span >= g_attn_stream_min && BS >= 32 && G <= 16;
+  return !wave && !stream;
+}
+
 void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,
                         const int* ctx_lens, bf16* out, float* tmp_o, float* tmp_ml, int* counters, int num_seqs,
                         int Hq, int Hkv, int BS, int max_blocks, int max_parts, float scale, hipStream_t s,

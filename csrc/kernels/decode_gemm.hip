@@ -910,14 +910,13 @@ __global__ __launch_bounds__(512, 4) void decode_block_kernel(DecodeBlockArgs a)
 // handed off after every part with agent fences: the fence writes back / invalidates the XCD's whole L2 and
 // the drain stalls on the next unit's loads, +23 us per QKV launch.)
 template <int U, int KS, int EPI>
-__global__ __launch_bounds__(1024) void decode_gemm_xres_kernel(const bf16* __restrict__ x, const bf16* __restrict__ W,
-                                                                int M, int N, int K, DecodeEpi e, int NF, int P) {
+SYM_DEV void xres_body(const bf16* __restrict__ x, const bf16* __restrict__ W, int M, int N, int K, const DecodeEpi& e,
+                       int NF, int P, int b, int G) {
   constexpr int NW = 16;
   constexpr int WPS = NW / KS;  // waves per k-split
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r16 = lane & 15, h = lane >> 4;
   const int kbeg = wid * (K / NW);
-  const int b = blockIdx.x, G = gridDim.x;
   const int wmul = e.wshuf ? 16 : 1, wsec = e.wshuf ? 512 : 32;
   auto wptr = [&](int t) -> const bf16* {
     return e.wshuf ? W + ((long long)t * (K / 32) + kbeg / 32) * 512 + lane * 8
@@ -1042,6 +1041,12 @@ __global__ __launch_bounds__(1024) void decode_gemm_xres_kernel(const bf16* __re
   }
 }
 
+template <int U, int KS, int EPI>
+__global__ __launch_bounds__(1024) void decode_gemm_xres_kernel(const bf16* __restrict__ x, const bf16* __restrict__ W,
+                                                                int M, int N, int K, DecodeEpi e, int NF, int P) {
+  xres_body<U, KS, EPI>(x, W, M, N, K, e, NF, P, blockIdx.x, gridDim.x);
+}
+
 int g_num_cus = 0;
 
 // Remainder split: OFF by default.  Measured (profiles/r3/ksplit_ab.jsonl, alternating runs): 8B 10 clients
@@ -1101,6 +1106,71 @@ bool go_xres(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi&
     case 32 + 2: go_xres_ks<2, 4, EPI>(x, W, M, N, K, e, grid, NF, P, s); return true;
     case 32 + 4: go_xres_ks<4, 4, EPI>(x, W, M, N, K, e, grid, NF, P, s); return true;
     default: return false;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Fused QKV + decode attention launch (M <= 16, K = 1024 U, G = Hq / Hkv <= 8).
+//
+// The x-resident QKV GEMM walks its 16-row tiles on ceil(ntiles / per) workgroups -- Llama-3-8B: 384 tiles,
+// two per workgroup on 192 of the 256 CUs -- and the decode attention then runs as its own launch: a launch
+// boundary plus a dependent load chain (~6.5 us at 10 sequences) on a chip whose HBM sits idle.  Here the
+// attention units ride in the same launch as extra 16-wave workgroups (two 8-wave units each, attn_decode.h
+// attn_pair_units) after the QKV workgroups, i.e. on the CUs the QKV grid leaves idle: they read their
+// context length, block-table entry and every K/V group not written this step while the QKV tiles stream,
+// then wait for all QKV workgroups, and only the query and the newest token's group remain to be read.
+// Hand-off (MI355X_MICROARCH.md hand-off table, first row): the QKV epilogue (wave 0) stores q / K / V
+// write-through (sc1), drains vmcnt after the workgroup's last tile and ONE lane adds to the workgroup's
+// counter line (b % 64); the attention workgroup's wave 0 polls the 64 lines, a barrier follows, and every
+// load of those bytes is an sc1 load.  Deadlock freedom: the attention workgroups come after every QKV
+// workgroup in the grid (dispatched in order), spins are bounded (error word), and the last workgroup out
+// re-arms the lines (graph-replay safe).  Results equal dg_qkv + attn_decode (same arithmetic, same order).
+// ctl: QKV_ATTN_CTL_INTS ints [64 lines x 32 | exit | error], zero-initialised once.
+// ---------------------------------------------------------------------------------------------------
+constexpr int QA_EXIT = MLP_LINES * MLP_STRIDE, QA_ERR = QA_EXIT + MLP_STRIDE;
+static_assert(QA_ERR + 1 <= QKV_ATTN_CTL_INTS, "qkv_attn ctl block too small");
+
+template <int U, int GMAX>
+__global__ __launch_bounds__(1024) void decode_qkv_attn_kernel(const bf16* __restrict__ x, const bf16* __restrict__ W,
+                                                               int M, int N, int K, DecodeEpi e, int Gq,
+                                                               QkvAttnArgs aa) {
+  int* ctl = aa.ctl;
+  const int b = blockIdx.x;
+  long long* st = aa.stamps ? aa.stamps + 4 * b : nullptr;  // timing only: start, mid, end, role
+  if (st && threadIdx.x == 0) {
+    st[0] = (long long)__builtin_amdgcn_s_memrealtime();
+    st[3] = b < Gq ? 0 : 1;
+  }
+  if (b < Gq) {
+    xres_body<U, 1, DECODE_EPI_QKV>(x, W, M, N, K, e, N / 16, 0, b, Gq);
+    if (threadIdx.x < 64) {  // wave 0 ran every epilogue of this workgroup: its stores acknowledged, one add
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(ctl + (b % MLP_LINES) * MLP_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (st && threadIdx.x == 0) st[1] = (long long)__builtin_amdgcn_s_memrealtime();
+    }
+  } else {
+    WaitFor wf{ctl, Gq, ctl + QA_ERR};
+    attn_pair_units<GMAX>(e.q_out, e.k_cache, e.v_cache, aa.block_tables, aa.ctx_lens, aa.out, aa.tmp_o, aa.tmp_ml,
+                          aa.counters, e.Hq, e.Hkv, e.BS, aa.max_blocks, aa.max_parts, aa.scale_log2, M, b - Gq,
+                          [&]() {
+                            wf();
+                            if (st && threadIdx.x == 0) st[1] = (long long)__builtin_amdgcn_s_memrealtime();
+                          });
+  }
+  if (st && threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st[2] = (long long)__builtin_amdgcn_s_memrealtime();
+  }
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(ctl + QA_EXIT, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (s_last) {  // every other workgroup is past its wait: re-arm for the next launch
+    for (int i = threadIdx.x; i < MLP_LINES; i += blockDim.x)
+      __hip_atomic_store(ctl + i * MLP_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(ctl + QA_EXIT, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1209,6 +1279,41 @@ void launch_epi(const bf16* x, const bf16* W, int M, int N, int K, const DecodeE
 }
 
 }  // namespace
+
+long long* g_qa_stamps = nullptr;
+void set_qkv_attn_stamps(long long* p) { g_qa_stamps = p; }
+
+bool launch_qkv_attn(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e0, const QkvAttnArgs& aa,
+                     hipStream_t s) {
+  const int G = e0.Hq / e0.Hkv;
+  if (M > 16 || K % 1024 || K > 4096 || G > 8 || !e0.wshuf || (e0.BS & (e0.BS - 1)) ||
+      !attn_decode_uses_grid(M, e0.Hkv, e0.BS, aa.max_blocks, G))
+    return false;
+  if (!g_num_cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    g_num_cus = std::max(1, g_num_cus);
+  }
+  const int ntiles = N / 16, per = (ntiles + g_num_cus - 1) / g_num_cus;
+  const int Gq = (ntiles + per - 1) / per;
+  const int Ga = (M * e0.Hkv * aa.max_parts + 1) / 2;
+  DecodeEpi e = e0;
+  e.sc1 = 1;  // q / K / V read by the attention workgroups of this launch
+  e.wnt = g_wnt;
+  QkvAttnArgs a2 = aa;
+  a2.stamps = g_qa_stamps;
+  auto go = [&](auto kern) { kern<<<Gq + Ga, 1024, 0, s>>>(x, W, M, N, K, e, Gq, a2); };
+  switch (K / 1024 * 16 + (G <= 4 ? 4 : 8)) {
+    case 16 + 4: go(decode_qkv_attn_kernel<1, 4>); return true;
+    case 16 + 8: go(decode_qkv_attn_kernel<1, 8>); return true;
+    case 32 + 4: go(decode_qkv_attn_kernel<2, 4>); return true;
+    case 32 + 8: go(decode_qkv_attn_kernel<2, 8>); return true;
+    case 64 + 4: go(decode_qkv_attn_kernel<4, 4>); return true;
+    case 64 + 8: go(decode_qkv_attn_kernel<4, 8>); return true;
+    default: return false;
+  }
+}
 
 void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e,
                         hipStream_t s) {

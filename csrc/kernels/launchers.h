@@ -136,6 +136,27 @@ struct DecodeBlockArgs {
   int M = 0, d = 0, Hq = 0, Hkv = 0, BS = 0, wshuf = 0;
 };
 void launch_decode_block(const DecodeBlockArgs& a, hipStream_t s);
+// Fused QKV projection (+ RoPE, paged K/V write) + split-KV decode attention in ONE launch (decode_gemm.hip,
+// decode_qkv_attn_kernel): the attention units run on the CUs the x-resident QKV grid leaves idle.  Returns
+// false (nothing launched) where it does not apply -- the caller then runs dg_qkv + attn_decode.
+constexpr int QKV_ATTN_CTL_INTS = 2176;
+struct QkvAttnArgs {
+  const int* block_tables = nullptr;
+  const int* ctx_lens = nullptr;
+  bf16* out = nullptr;        // [M, Hq, 128]
+  float* tmp_o = nullptr;     // split-KV partials [M, Hq, max_parts, 128]
+  float* tmp_ml = nullptr;
+  int* counters = nullptr;    // [M * Hkv] split-KV arrivals, self re-arming
+  int max_blocks = 0, max_parts = 0;
+  float scale_log2 = 0.f;
+  int* ctl = nullptr;         // QKV_ATTN_CTL_INTS ints, zero once; word 2080 != 0 after a launch: a wait gave up
+  long long* stamps = nullptr;  // optional [grid][4] s_memrealtime stamps (set by the launcher; timing only)
+};
+void set_qkv_attn_stamps(long long* stamps);
+bool launch_qkv_attn(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, const QkvAttnArgs& aa,
+                     hipStream_t s);
+// attention.hip: true where launch_attn_decode would run its grid kernel (the form the fused launch embeds)
+bool attn_decode_uses_grid(int num_seqs, int Hkv, int BS, int max_blocks, int G);
 void set_decode_gemm_variant(int v);  // -1: default heuristic
 void set_decode_ksplit(int on);       // x-resident decode GEMM remainder split over K (default off)
 void set_decode_gemm_nt(int on);      // non-temporal weight-stream loads (keeps the variant choice)

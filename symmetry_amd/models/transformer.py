@@ -79,6 +79,9 @@ MG_FUSED_GU = MG_FUSED_MODE == "gu"
 # projections of the FUSED decode path (below GENERAL_ROWS rows) that run on mgemm with their epilogue
 # instead of the decode GEMM (comma list of qkv, o, gu, down; A/B knob)
 MG_PROJ = tuple(p for p in os.environ.get("SYMMETRY_MG_PROJ", "").split(",") if p)
+# fused decode path: QKV + decode attention as one launch, the attention units on the CUs the QKV grid leaves
+# idle (csrc/kernels/decode_gemm.hip, decode_qkv_attn_kernel)
+QKV_ATTN = os.environ.get("SYMMETRY_QKV_ATTN", "0") == "1"
 
 
 @dataclass
@@ -294,6 +297,17 @@ class TransformerLM:
         return y
 
     # ------------------------------------------------------------------------------------------
+    def _qkv_attn(self, b: ForwardBatch, kv: KVCache, i: int, xw, wq, ss, eps, q, attn) -> bool:
+        """QKV projection + decode attention of layer i as one launch (ops.qkv_attn); False: not applicable."""
+        span = b.block_tables.shape[1] * kv.block_size
+        max_parts = (span + ops.ATTN_DECODE_PART - 1) // ops.ATTN_DECODE_PART
+        tmp_o = self._buf("tmp_o", (b.num_seqs, self.hq, max_parts, self.D), torch.float32)
+        tmp_ml = self._buf("tmp_ml", (b.num_seqs, self.hq, max_parts, 2), torch.float32)
+        cnt = self.ws.get("attn_counters", (b.num_seqs * self.hkv,), torch.int32, self.device, zeros=True)
+        ctl = self.ws.get("qa_ctl", (ops.QKV_ATTN_CTL,), torch.int32, self.device, zeros=True)
+        return ops.qkv_attn(xw, wq, ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq,
+                            self.hkv, True, b.block_tables, b.ctx_lens, attn, tmp_o, tmp_ml, cnt, self.scale, ctl)
+
     def _attention(self, b: ForwardBatch, kv: KVCache, i: int, q: torch.Tensor, attn: torch.Tensor,
                    prefetch: torch.Tensor | None = None) -> None:
         if b.kind == "decode":
@@ -423,7 +437,8 @@ class TransformerLM:
                                  b.block_tables, b.ctx_lens, attn, tmp_o, tmp_ml, cnt, self.scale, wo, resid,
                                  w.layer(i, "ln2"), xw, ss_t, bctl, wshuf=shq)
                 ss = ss_t
-            else:
+            elif not (QKV_ATTN and b.kind == "decode" and shq and "qkv" not in mgp and ATTN_PREFETCH_WGS == 0
+                      and self._qkv_attn(b, kv, i, xw, wq, ss, eps, q, attn)):
                 ops.dg_qkv(xw, wq, ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq,
                            self.hkv, wshuf=shq, mg=mgp.get("qkv") if shq else None)
                 # spare workgroups of the latency-bound attention launch pull the O weight into the

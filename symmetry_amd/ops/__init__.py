@@ -50,6 +50,7 @@ __all__ = [
     "rownorm",
     "sample_filtered",
     "decode_mlp",
+    "qkv_attn",
     "linear",
     "lib_splits",
     "linear_splitk",
@@ -309,6 +310,20 @@ def moe_combine(y, dst, ids, e_lo, e_hi, w, k, out, accumulate=False):
 
 
 DECODE_MLP_CTL = 4224  # csrc/kernels/launchers.h DECODE_MLP_CTL_INTS
+QKV_ATTN_CTL = 2176  # csrc/kernels/launchers.h QKV_ATTN_CTL_INTS
+
+
+def qkv_attn(x, W, ss_in, eps, positions, slots, cos_sin, q, k_cache, v_cache, Hq, Hkv, wshuf, block_tables,
+             ctx_lens, attn, tmp_o, tmp_ml, counters, scale, ctl) -> bool:
+    """dg_qkv + attn_decode as ONE launch (csrc/kernels/decode_gemm.hip, decode_qkv_attn_kernel): the attention
+    units run on the CUs the x-resident QKV grid leaves idle.  Returns False -- nothing enqueued -- where the
+    fused form does not apply (CPU, shapes, the attention form the standalone launch would pick); the caller
+    then runs the two ops.  ``ctl``: int32[QKV_ATTN_CTL] zero-initialised once (re-armed by the kernel)."""
+    if not _gpu(x):
+        return False
+    return bool(_native.ops().qkv_attn(x, W, ss_in, float(eps), positions, slots, cos_sin, q, k_cache, v_cache,
+                                       int(Hq), int(Hkv), bool(wshuf), block_tables, ctx_lens, attn, tmp_o, tmp_ml,
+                                       counters, float(scale), ctl))
 DECODE_BLOCK_CTL = 1024  # csrc/kernels/launchers.h DECODE_BLOCK_CTL_INTS
 ATTN_BLOCK_PART = 256  # tokens per split-KV partition inside decode_block (csrc/kernels/attn_decode.h PART_F)
 

@@ -556,3 +556,96 @@ def test_dg_resid_swiglu_ksplit_xres(gpu, M):
         _close(resid, r_ref, atol=2e-3, rtol=1e-3)
         _close(xw, xw_ref, atol=2e-2, rtol=1e-2)
         _close(ss, ss_ref, atol=1e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("M", [1, 10, 16])
+@pytest.mark.parametrize("Hq,Hkv,d", [(32, 8, 4096), (16, 2, 2048), (8, 1, 1024)])
+def test_qkv_attn_fused_equals_two_launches(gpu, M, Hq, Hkv, d):
+    """QKV + decode attention in one launch (qkv_attn: the attention units on the CUs the x-resident QKV grid
+    leaves idle) vs dg_qkv + attn_decode: q, the paged K/V cache and the attention output are bitwise equal,
+    including multi-partition contexts (split-KV combine in the launch); the control block and the split-KV
+    counters re-arm themselves, also under graph replay; a block-table span the grid attention kernel does
+    not serve (the streaming kernel's >= 1024 tokens) falls back (False, nothing enqueued)."""
+    import math
+
+    from symmetry_amd.models.layout import preshuffle
+
+    D, BS = 128, 64
+    g = torch.Generator(device=gpu).manual_seed(300 + M + Hq)
+    ctx_lens = [(97 * i * i + 131 * i + 5) % 890 + 1 for i in range(M)]
+    max_blocks = max((c + BS - 1) // BS for c in ctx_lens) + 1  # span < 1024: the grid attention kernel
+    NB = sum((c + BS - 1) // BS for c in ctx_lens) + 3
+    kc0 = torch.randn(NB, Hkv, BS, D, device=gpu, generator=g).bfloat16()
+    vc0 = torch.randn(NB, Hkv, D, BS, device=gpu, generator=g).bfloat16()
+    perm = torch.randperm(NB, generator=torch.Generator().manual_seed(7)).tolist()
+    bt = torch.zeros(M, max_blocks, dtype=torch.int32)
+    i = 0
+    for s, c in enumerate(ctx_lens):
+        for blk in range((c + BS - 1) // BS):
+            bt[s, blk] = perm[i]
+            i += 1
+    pos = torch.tensor([c - 1 for c in ctx_lens], dtype=torch.int32)
+    slots = torch.tensor([int(bt[s, p // BS]) * BS + p % BS for s, p in enumerate(pos.tolist())], dtype=torch.int32)
+    bt, pos, slots = bt.to(gpu), pos.to(gpu), slots.to(gpu)
+    ctx = torch.tensor(ctx_lens, device=gpu, dtype=torch.int32)
+    N = (Hq + 2 * Hkv) * D
+    xw = torch.randn(M, d, device=gpu, generator=g).bfloat16()
+    ss_in = torch.rand(M, d // 16, device=gpu, generator=g) * 16 + 1
+    Wqkv = (torch.randn(N, d, device=gpu, generator=g) / d ** 0.5).bfloat16()[qkv_perm(Hq, Hkv, D).to(gpu)].contiguous()
+    Wqkv = preshuffle(Wqkv)
+    cs = ref.rope_table(4096, D, 500000.0, device=gpu)
+    scale = 1 / math.sqrt(D)
+    max_parts = (max_blocks * BS + ops.ATTN_DECODE_PART - 1) // ops.ATTN_DECODE_PART
+
+    def state():
+        return dict(kc=kc0.clone(), vc=vc0.clone(), q=torch.empty(M, Hq, D, device=gpu, dtype=torch.bfloat16),
+                    attn=torch.full((M, Hq, D), float("nan"), device=gpu, dtype=torch.bfloat16),
+                    tmp_o=torch.empty(M, Hq, max_parts, D, device=gpu), tmp_ml=torch.empty(M, Hq, max_parts, 2, device=gpu),
+                    cnt=torch.zeros(M * Hkv, device=gpu, dtype=torch.int32))
+
+    def fused(st, ctl):
+        return ops.qkv_attn(xw, Wqkv, ss_in, 1e-5, pos, slots, cs, st["q"], st["kc"], st["vc"], Hq, Hkv, True, bt, ctx,
+                            st["attn"], st["tmp_o"], st["tmp_ml"], st["cnt"], scale, ctl)
+
+    a = state()
+    ops.dg_qkv(xw, Wqkv, ss_in, 1e-5, pos, slots, cs, a["q"], a["kc"], a["vc"], Hq, Hkv, wshuf=True)
+    ops.attn_decode(a["q"], a["kc"], a["vc"], bt, ctx, a["attn"], a["tmp_o"], a["tmp_ml"], a["cnt"], scale)
+    bf = state()
+    ctl = torch.zeros(ops.QKV_ATTN_CTL, device=gpu, dtype=torch.int32)
+    assert fused(bf, ctl)
+    torch.cuda.synchronize()
+    assert not ctl.any(), ctl.nonzero().flatten().tolist()
+    assert not bf["cnt"].any()
+    for k in ("q", "kc", "vc", "attn"):
+        assert torch.equal(bf[k], a[k]), k
+    at_r = torch.empty(M, Hq, D, dtype=torch.bfloat16)
+    ref.attn_decode(bf["q"].cpu(), bf["kc"].cpu(), bf["vc"].cpu(), bt.cpu(), ctx.cpu(), at_r, scale=scale)
+    _close(bf["attn"], at_r, atol=2e-2, rtol=2e-2)
+    # graph replays from the same inputs: identical outputs, control words re-armed every time
+    gr = state()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            assert fused(gr, ctl)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        gr["attn"].fill_(float("nan"))
+        gr["kc"].copy_(kc0)
+        gr["vc"].copy_(vc0)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert not ctl.any() and not gr["cnt"].any()
+        for k in ("q", "kc", "vc", "attn"):
+            assert torch.equal(gr[k], bf[k]), k
+    # a 1024-token span: the standalone launch would stream (another kernel): not fused, nothing enqueued
+    bt_long = torch.zeros(M, 16, dtype=torch.int32, device=gpu)
+    bt_long[:, :max_blocks] = bt
+    st = state()
+    st["tmp_o"] = torch.empty(M, Hq, 4, D, device=gpu)
+    st["tmp_ml"] = torch.empty(M, Hq, 4, 2, device=gpu)
+    q_before = st["q"].clone()
+    assert not ops.qkv_attn(xw, Wqkv, ss_in, 1e-5, pos, slots, cs, st["q"], st["kc"], st["vc"], Hq, Hkv, True,
+                            bt_long, ctx, st["attn"], st["tmp_o"], st["tmp_ml"], st["cnt"], scale, ctl)
+    torch.cuda.synchronize()
+    assert torch.equal(st["kc"], kc0) and torch.equal(st["q"].view(-1)[:8], q_before.view(-1)[:8])
