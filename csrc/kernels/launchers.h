@@ -23,7 +23,7 @@ enum {
 constexpr int XG_MAX_WORLD = 8;
 constexpr int XG_MAX_WG = 4096;
 constexpr int XG_KEYS_WG = XG_MAX_WG - 1;  // flag word of the sampling-keys collective (others stay below)
-constexpr long long XG_HDR_BYTES = 256;   // [0] collective counter, [32] arrivals of the current collective
+constexpr long long XG_HDR_BYTES = 256;   // [0] u32 epoch mirror, [64] u64 {epoch, arrivals} of the current collective
 constexpr long long XG_FLAG_BYTES = XG_HDR_BYTES + (long long)XG_MAX_WG * XG_MAX_WORLD * 4;
 // DECODE_EPI_XPUSH target: every rank's mapped buffer; the GEMM reads (never bumps) this rank's counter
 struct XgmiPush {

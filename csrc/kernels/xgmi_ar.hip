@@ -47,13 +47,18 @@ SYM_DEV char* xg_slot(const XgmiArgs& c, int r, int par, int src) {
 SYM_DEV unsigned xg_epoch(const XgmiArgs& c, int nwg) {
   __shared__ unsigned s_epoch;
   if (threadIdx.x == 0) {
-    unsigned* ctr = reinterpret_cast<unsigned*>(c.bufs[c.rank]);
-    const unsigned e = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    // acq_rel: the counter load above is ordered before this workgroup counts itself in
-    const unsigned n = __hip_atomic_fetch_add(ctr + 8, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (n == (unsigned)nwg - 1u) {  // last to arrive: every workgroup has read the counter
-      __hip_atomic_store(ctr + 8, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctr, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    // ONE returning atomic per workgroup on a packed {epoch (high 32), arrivals (low 32)} word: the add
+    // counts this workgroup in and returns the epoch of the previous collective in the same round trip
+    // (round 2 read the counter, waited, then counted in: two dependent round trips to uncached memory on
+    // every collective).  The last arrival folds the arrivals back into an epoch increment -- the next
+    // collective on the stream starts after this launch retired, so it finds {e, 0} -- and mirrors the
+    // epoch into the u32 at byte 0 that the XPUSH GEMM epilogue (decode_epi.h, xp_epoch) reads.
+    unsigned long long* w = reinterpret_cast<unsigned long long*>(c.bufs[c.rank] + 64);
+    const unsigned long long old = __hip_atomic_fetch_add(w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned e = (unsigned)(old >> 32) + 1u;
+    if ((unsigned)old == (unsigned)nwg - 1u) {  // last to arrive: every workgroup has counted itself in
+      __hip_atomic_fetch_add(w, (1ull << 32) - (unsigned long long)nwg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<unsigned*>(c.bufs[c.rank]), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     s_epoch = e;
   }
@@ -72,16 +77,13 @@ SYM_DEV void xg_delay(unsigned long long delay) {
 // buffer (its own included, so the reduce reads all slots from one place), raise flag (wg, rank) in every
 // rank, wait for every rank's flag (wg, src).  `wg` indexes flags only; `nwg` = workgroups of this rank in
 // the launch (epoch accounting).  Returns the epoch parity (the slot set to reduce).
-template <typename V = uint4>
-SYM_DEV int xg_exchange(const XgmiArgs& c, int wg, int nwg, const V* __restrict__ src, long long off, int nvec,
-                        unsigned long long delay = 0) {
+// `push(par)` stores this thread's part of the chunk into slot (par, rank) of every rank.
+template <typename PushFn>
+SYM_DEV int xg_exchange_fn(const XgmiArgs& c, int wg, int nwg, PushFn push, unsigned long long delay = 0) {
   const unsigned epoch = xg_epoch(c, nwg);
   xg_delay(delay);
   const int par = (int)(epoch & 1u);
-  for (int v = threadIdx.x; v < nvec; v += XG_THREADS) {
-    const V x = src[v];
-    for (int r = 0; r < c.world; ++r) reinterpret_cast<V*>(xg_slot(c, r, par, c.rank) + off)[v] = x;
-  }
+  push(par);
   // Every wave waits for its slot stores to be acknowledged before the workgroup signals: the AMDGPU
   // memory model's system-scope release is `buffer_wbl2 sc0 sc1; s_waitcnt vmcnt(0)`, and the L2
   // write-back half has nothing to do here -- the buffers are uncached (MTYPE UC), so the stores never
@@ -105,6 +107,20 @@ SYM_DEV int xg_exchange(const XgmiArgs& c, int wg, int nwg, const V* __restrict_
   }
   __syncthreads();  // the pollers saw every flag: the slot bytes behind them are in memory (uncached)
   return par;
+}
+
+template <typename V = uint4>
+SYM_DEV int xg_exchange(const XgmiArgs& c, int wg, int nwg, const V* __restrict__ src, long long off, int nvec,
+                        unsigned long long delay = 0) {
+  return xg_exchange_fn(
+      c, wg, nwg,
+      [&](int par) {
+        for (int v = threadIdx.x; v < nvec; v += XG_THREADS) {
+          const V x = src[v];
+          for (int r = 0; r < c.world; ++r) reinterpret_cast<V*>(xg_slot(c, r, par, c.rank) + off)[v] = x;
+        }
+      },
+      delay);
 }
 
 // Plain all-reduce (sum) of n elements, in place or out of place; ELEM: 0 = fp32, 1 = bf16.
@@ -155,9 +171,55 @@ SYM_DEV void xg_add_prep_body(const XgmiArgs& c, int row, int part, int T, int P
   const int wg = row * P + part;
   const long long rb = (long long)row * d + (long long)part * dp;
   const long long off = rb * 4;
-  const int par = xg_exchange<uint4>(c, wg, T * P, reinterpret_cast<const uint4*>(y + rb), off, dp / 4, delay);
   const bf16* wp = w + (long long)part * dp;
   float acc = 0.f;
+  if (dp / 8 <= XG_THREADS) {
+    // one 8-column vector per thread (every decode shape: d / P <= 2048): the partial, the residual and the
+    // norm weight are loaded BEFORE the collective's epoch / flag round trips (none depends on a peer), so
+    // their latency hides behind them; the partial is pushed from registers
+    const int vi = threadIdx.x;
+    const bool on = vi < dp / 8;
+    float yv[8], r[8], g[8];
+    if (on) {
+      load8f(y + rb + vi * 8, yv);
+      load8f(resid + rb + vi * 8, r);
+      load8(wp + vi * 8, g);
+    }
+    const int par = xg_exchange_fn(
+        c, wg, T * P,
+        [&](int pr) {
+          if (!on) return;
+          const float4 a = make_float4(yv[0], yv[1], yv[2], yv[3]), b = make_float4(yv[4], yv[5], yv[6], yv[7]);
+          for (int s = 0; s < c.world; ++s) {
+            float4* dst = reinterpret_cast<float4*>(xg_slot(c, s, pr, c.rank) + off) + 2 * vi;
+            dst[0] = a;
+            dst[1] = b;
+          }
+        },
+        delay);
+    if (on) {
+      float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < c.world; ++s) {  // the all-reduced delta first (rank order), then the residual add
+        float dd[8];
+        load8f(reinterpret_cast<const float*>(xg_slot(c, c.rank, par, s) + off) + vi * 8, dd);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sum[i] += dd[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] += sum[i];
+      store8f(resid + rb + vi * 8, r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        acc += r[i] * r[i];
+        g[i] *= r[i];
+      }
+      store8(xw + rb + vi * 8, g);
+    }
+    acc = block_sum<XG_THREADS>(acc, scratch);
+    if (threadIdx.x == 0) ss[row * P + part] = acc;
+    return;
+  }
+  const int par = xg_exchange<uint4>(c, wg, T * P, reinterpret_cast<const uint4*>(y + rb), off, dp / 4, delay);
   for (int vi = threadIdx.x; vi < dp / 8; vi += XG_THREADS) {
     float r[8], g[8];
     float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
