@@ -1023,6 +1023,7 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) y, int variant=0) -> ()", &skinny_gemm);
   m.def("mgemm(Tensor x, Tensor w, Tensor(a!) y, int rw) -> ()", &mgemm);
   m.def("mgemm_nt(int on) -> ()", [](int64_t on) { set_mgemm_nt((int)on); });
+  m.def("decode_halves(int on) -> ()", [](int64_t on) { set_decode_halves((int)on); });
   m.def("qkv_attn_stamps(Tensor? stamps) -> ()", [](const c10::optional<Tensor>& t) {
     set_qkv_attn_stamps(t.has_value() ? reinterpret_cast<long long*>(t->data_ptr()) : nullptr);
   });

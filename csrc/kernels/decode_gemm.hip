@@ -922,21 +922,30 @@ SYM_DEV void xres_body(const bf16* __restrict__ x, const bf16* __restrict__ W, i
     return e.wshuf ? W + ((long long)t * (K / 32) + kbeg / 32) * 512 + lane * 8
                    : W + (long long)(16 * t + r16) * K + kbeg + 8 * h;
   };
-  // this workgroup's units: whole tiles b, b + G, ... < NF, then parts b, b + G, ... < P
+  // this workgroup's units: whole tiles b, b + G, ... < NF, then parts b, b + G, ... < P.  KS > 1: part p is
+  // k-split p % KS of tile NF + p / KS; KS == 1 with P > 0: part p is row half p % 2 of tile NF + p / 2 -- rows
+  // {0-3, 8-11} or {4-7, 12-15}, i.e. the A-operand lanes with ((lane >> 2) & 1) == half and the accumulator
+  // lanes with (h & 1) == half: every RoPE / SwiGLU partner pair (rows r, r + 8) stays in one half, so a half
+  // tile is final in one workgroup (no partial hand-off) and the weight loads of the other half's lanes are
+  // masked off (half the bytes)
+  constexpr int PDIV = KS > 1 ? KS : 2;
   const int nf = NF > b ? (NF - b + G - 1) / G : 0;
-  const int np = (KS > 1 && P > b) ? (P - b + G - 1) / G : 0;
+  const int np = P > b ? (P - b + G - 1) / G : 0;
   const int nu = nf + np;
   if (nu == 0) return;  // uniform over the workgroup
-  auto unit_tile = [&](int i) { return i < nf ? b + i * G : NF + (b + (i - nf) * G) / KS; };
-  auto unit_active = [&](int i) { return i < nf || wid / WPS == (b + (i - nf) * G) % KS; };
+  auto unit_tile = [&](int i) { return i < nf ? b + i * G : NF + (b + (i - nf) * G) / PDIV; };
+  auto unit_active = [&](int i) { return KS == 1 || i < nf || wid / WPS == (b + (i - nf) * G) % KS; };
+  auto unit_half = [&](int i) { return (KS > 1 || i < nf) ? -1 : (b + (i - nf) * G) % 2; };
   Pack8 wa[U][2];
   auto load_w = [&](int i) {
     if (!unit_active(i)) return;
     const bf16* wp = wptr(unit_tile(i));
+    const int hf = unit_half(i);
+    const bool on = hf < 0 || ((lane >> 2) & 1) == hf;
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      wa[j][0].u = *reinterpret_cast<const uint4*>(wp + j * 64 * wmul);
-      wa[j][1].u = *reinterpret_cast<const uint4*>(wp + j * 64 * wmul + wsec);
+      wa[j][0].u = on ? *reinterpret_cast<const uint4*>(wp + j * 64 * wmul) : make_uint4(0, 0, 0, 0);
+      wa[j][1].u = on ? *reinterpret_cast<const uint4*>(wp + j * 64 * wmul + wsec) : make_uint4(0, 0, 0, 0);
     }
   };
   load_w(0);
@@ -962,11 +971,11 @@ SYM_DEV void xres_body(const bf16* __restrict__ x, const bf16* __restrict__ W, i
   if constexpr (EPI == DECODE_EPI_XPUSH) xep = xp_epoch(e.xp);
   const int m = r16;
   const bool mok = m < M;
-  auto finish = [&](f32x4 v, int t) {  // wave 0: row scale + epilogue of a final tile
+  auto finish = [&](f32x4 v, int t, int hf = -1) {  // wave 0: row scale + epilogue of a final tile (or half)
     const float sc = (e.ss_in && mok) ? rn_s[m] : 1.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] *= sc;
-    epilogue<EPI>(e, v, t, m, mok, h, N, xep);
+    epilogue<EPI>(e, v, t, m, mok && (hf < 0 || (h & 1) == hf), h, N, xep);
     if constexpr (EPI == DECODE_EPI_XPUSH) {  // wave 0 stored the whole tile: acknowledged, then flag it
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane < e.xp.world) xp_flag(e.xp, lane, t, xep);
@@ -996,7 +1005,9 @@ SYM_DEV void xres_body(const bf16* __restrict__ x, const bf16* __restrict__ W, i
       }
       if (i < nf) {
         finish(v, unit_tile(i));
-      } else if constexpr (KS > 1) {  // part: publish the partial (write-through), no wait here
+      } else if constexpr (KS == 1) {  // row half of a remainder tile
+        finish(v, unit_tile(i), unit_half(i));
+      } else {  // part: publish the partial (write-through), no wait here
         unsigned long long* slot =
             reinterpret_cast<unsigned long long*>(e.ks_ws + (long long)(b + (i - nf) * G) * 256 + lane * 4);
         const float4 f4 = make_float4(v[0], v[1], v[2], v[3]);
@@ -1058,6 +1069,16 @@ static bool g_dg_ksplit = [] {
   return knob && knob[0] == '1';
 }();
 
+// Remainder tiles as row halves: OFF by default.  Measured (profiles/r3/xres_row_halves_ab.jsonl, alternating
+// runs): 8B 10 clients 3.316 vs 3.261 ms per step, TP = 4 / 8 shards unchanged.  A half tile issues as many
+// load instructions as a whole one (half the lanes masked), and at M <= 16 the launch is bound by the load
+// pipeline's latency per CU, not by its bytes -- the same finding as the k split above.
+// SYMMETRY_DG_HALVES=1 / set_decode_halves(1).
+static bool g_dg_halves = [] {
+  const char* knob = getenv("SYMMETRY_DG_HALVES");
+  return knob && knob[0] == '1';
+}();
+
 template <int U, int KS, int EPI>
 void go_xres_ks(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, int grid, int NF, int P,
                 hipStream_t s) {
@@ -1093,6 +1114,18 @@ bool go_xres(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi&
         NF = f * C;
         P = parts;
       }
+    }
+  }
+  // remainder tiles as row halves (xres_body): epilogues whose partner rows pair r with r + 8 and that reduce
+  // nothing across a tile's rows -- when it lowers the busiest CU's weight bytes (Llama-3-8B QKV: 384 tiles =
+  // 2 per CU on 192 CUs -> 1 whole + 1 half on all 256; TP = 8 QKV: 48 tiles -> 96 halves)
+  constexpr bool kHalvable = EPI == DECODE_EPI_QKV || EPI == DECODE_EPI_SWIGLU || EPI == DECODE_EPI_F32;
+  if (kHalvable && KS == 1 && g_dg_halves && R > 0) {
+    const int parts = 2 * R, g = f > 0 ? C : std::min(C, parts), q = (parts + g - 1) / g;
+    if (2 * f + q < 2 * per) {
+      grid = g;
+      NF = f * C;
+      P = parts;
     }
   }
   switch (KS * 8 + K / 1024) {
@@ -1386,6 +1419,7 @@ void launch_decode_mlp(const DecodeMlpArgs& a, hipStream_t s) {
 void set_decode_mlp_stamps(long long* stamps) { g_mlp_stamps = stamps; }
 
 void set_decode_ksplit(int on) { g_dg_ksplit = on != 0; }
+void set_decode_halves(int on) { g_dg_halves = on != 0; }
 
 void set_decode_gemm_variant(int v) {
   // v >= 2000: A/B knob bits of the x-resident persistent MLP (decode_mlp_xres_kernel)

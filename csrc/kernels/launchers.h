@@ -159,6 +159,7 @@ bool launch_qkv_attn(const bf16* x, const bf16* W, int M, int N, int K, const De
 bool attn_decode_uses_grid(int num_seqs, int Hkv, int BS, int max_blocks, int G);
 void set_decode_gemm_variant(int v);  // -1: default heuristic
 void set_decode_ksplit(int on);       // x-resident decode GEMM remainder split over K (default off)
+void set_decode_halves(int on);       // x-resident decode GEMM remainder tiles as row halves (default off)
 void set_decode_gemm_nt(int on);      // non-temporal weight-stream loads (keeps the variant choice)
 void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e,
                         hipStream_t s);

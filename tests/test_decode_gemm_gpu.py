@@ -649,3 +649,65 @@ def test_qkv_attn_fused_equals_two_launches(gpu, M, Hq, Hkv, d):
                             bt_long, ctx, st["attn"], st["tmp_o"], st["tmp_ml"], st["cnt"], scale, ctl)
     torch.cuda.synchronize()
     assert torch.equal(st["kc"], kc0) and torch.equal(st["q"].view(-1)[:8], q_before.view(-1)[:8])
+
+
+@pytest.mark.parametrize("M", [1, 10, 16])
+# 8B QKV (384 tiles: 256 whole + 256 row halves), its TP=4 / TP=8 shards (96 / 48 tiles: halves only), and
+# gate_up under TP=2 (896 tiles: 3 whole + 1 half per CU)
+@pytest.mark.parametrize("what,Hq,Hkv,N", [("qkv", 32, 8, 0), ("qkv", 8, 2, 0), ("qkv", 4, 1, 0), ("gu", 0, 0, 14336)])
+def test_xres_row_halves_bitwise(gpu, M, what, Hq, Hkv, N):
+    """x-resident decode GEMM with remainder tiles split into row halves (rows {0-3, 8-11} / {4-7, 12-15} of a
+    16-row MFMA tile in two workgroups, the other half's weight lanes masked off): bitwise equal to whole
+    tiles (same sums, same order) for the QKV (RoPE pairs r / r + 8) and SwiGLU (gate / up rows r / r + 8)
+    epilogues, and close to the fp32 reference."""
+    from symmetry_amd.models.layout import preshuffle
+
+    D, BS, NB, K = 128, 64, 8, 4096
+    lib = ops._native.ops()
+    g = torch.Generator(device=gpu).manual_seed(40 + M)
+    if what == "qkv":
+        N = (Hq + 2 * Hkv) * D
+        x, W, s = _inputs(gpu, M, N, K, seed=41)
+        W = W[qkv_perm(Hq, Hkv, D).to(gpu)].contiguous()
+        cs = ref.rope_table(1024, D, 500000.0, device=gpu)
+        pos = torch.randint(0, 1024, (M,), device=gpu, generator=g, dtype=torch.int32)
+        slots = torch.randperm(NB * BS, device=gpu, generator=g)[:M].int()
+
+        def run():
+            q = torch.full((M, Hq, D), float("nan"), device=gpu, dtype=torch.bfloat16)
+            kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=torch.bfloat16)
+            vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=torch.bfloat16)
+            ops.dg_qkv(x, preshuffle(W), s, 1e-5, pos, slots, cs, q, kc, vc, Hq, Hkv, wshuf=True)
+            torch.cuda.synchronize()
+            return q, kc, vc
+    else:
+        x, W, s = _inputs(gpu, M, N, K, seed=42)
+        W = W[gu_perm(N // 2).to(gpu)].contiguous()
+
+        def run():
+            act = torch.full((M, N // 2), float("nan"), device=gpu, dtype=torch.bfloat16)
+            ops.dg_swiglu(x, preshuffle(W), s, 1e-5, act, wshuf=True)
+            torch.cuda.synchronize()
+            return (act,)
+
+    try:
+        lib.decode_halves(1)
+        halves = run()
+        lib.decode_halves(0)
+        whole = run()
+    finally:
+        lib.decode_halves(0)
+    for a, b in zip(halves, whole):
+        assert not torch.isnan(a.float()).any()
+        assert torch.equal(a, b)
+    if what == "qkv":
+        q_r, kc_r, vc_r = (torch.empty(M, Hq, D, dtype=torch.bfloat16), torch.zeros(NB, Hkv, BS, D, dtype=torch.bfloat16),
+                           torch.zeros(NB, Hkv, D, BS, dtype=torch.bfloat16))
+        ref.dg_qkv(x.cpu(), W.cpu(), s.cpu(), 1e-5, pos.cpu(), slots.cpu(), cs.cpu(), q_r, kc_r, vc_r, Hq, Hkv)
+        _close(halves[0], q_r, atol=2e-2, rtol=2e-2)
+        _close(halves[1], kc_r, atol=2e-2, rtol=2e-2)
+        _close(halves[2], vc_r, atol=2e-2, rtol=2e-2)
+    else:
+        act_r = torch.empty(M, N // 2, dtype=torch.bfloat16)
+        ref.dg_swiglu(x.cpu(), W.cpu(), s.cpu(), 1e-5, act_r)
+        _close(halves[0], act_r, atol=3e-2, rtol=2e-2)
