@@ -13,6 +13,7 @@ frees its KV blocks (item 10).
 from __future__ import annotations
 
 import asyncio
+import collections
 import itertools
 import time
 
@@ -33,6 +34,10 @@ class NativeBackend(Backend):
         self._overrides = engine_overrides
         self.aengine: AsyncEngine | None = None
         self.model_name = str(config.get("modelName", "llama3:8b"))
+        # request-path timing of the direct stream (perf_counter = CLOCK_MONOTONIC, comparable with the
+        # clients' clocks on the same host): receive -> submit -> first token on the engine thread -> first
+        # output callback on the event loop -> first SSE event written; keyed by the prompt's first 24 chars
+        self.timings: collections.deque = collections.deque(maxlen=4096)
 
     @property
     def engine(self) -> LLMEngine:
@@ -94,6 +99,10 @@ class NativeBackend(Backend):
         limit = int(backlog or self.aengine.queue_limit)
         done = asyncio.get_running_loop().create_future()
         st = {"first": True, "congested": 0}
+        content = messages[-1].get("content") if messages and isinstance(messages[-1], dict) else None
+        tm = {"key": str(content)[:24] if content is not None else None, "recv": request.get("_t_recv"),
+              "enter": time.perf_counter()}
+        self.timings.append(tm)
 
         def finish(exc: BaseException | None = None) -> None:
             if not done.done():
@@ -105,10 +114,16 @@ class NativeBackend(Backend):
             if out.error:
                 return finish(BackendError(out.error))
             if out.text or st["first"] or out.finished:
+                first = st["first"]
+                if first:
+                    tm["engine_first"] = getattr(out, "t_engine", None)
+                    tm["callback_first"] = time.perf_counter()
                 ev = sse.chunk_event(rid, self.model_name, out.text, role="assistant" if st["first"] else None,
                                      finish_reason=out.finish_reason if out.finished else None, created=created)
                 st["first"] = False
                 ok = write(ev.encode("utf-8"), out.text)
+                if first:
+                    tm["written_first"] = time.perf_counter()
                 if ok is None:  # peer gone
                     self.aengine.abort(rid)
                     return finish()
@@ -121,6 +136,7 @@ class NativeBackend(Backend):
                 finish()
 
         self.aengine.submit(rid, on_output, messages=messages, params=params, cache_scope=scope)
+        tm["submitted"] = time.perf_counter()
         try:
             await done
         finally:

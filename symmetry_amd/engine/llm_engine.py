@@ -12,6 +12,7 @@ item 6).
 from __future__ import annotations
 
 import asyncio
+import collections
 import hashlib
 import os
 import queue
@@ -162,6 +163,8 @@ class LLMEngine:
         self.lock = threading.Lock()
         self._inflight: dict | None = None
         self._last_done = 0.0
+        # (launch, done, kind, seqs, tokens, enqueued) of recent steps, perf_counter clock (TTFT breakdowns, e2e.py)
+        self.step_trace: collections.deque = collections.deque(maxlen=2048)
         # pipelined decode on one GPU and under TP (the workers poll the shared-memory metadata ring and
         # never synchronise: parallel/metaplane.py)
         self.pipeline = cfg.pipeline
@@ -327,7 +330,7 @@ class LLMEngine:
                 if batch.kind == "prefill" and n > 1:
                     # prompt blocks completed by this (enqueued) step become adoptable by later arrivals
                     self.blocks.register(seq)
-        return {"batch": batch, "handle": handle, "t0": t0}
+        return {"batch": batch, "handle": handle, "t0": t0, "t_enq": time.perf_counter()}
 
     def _complete(self, fl: dict, t_launch: float) -> list[RequestOutput]:
         """Wait for a launched step and stream its tokens.  ``t_launch``: host seconds this iteration spent
@@ -339,6 +342,7 @@ class LLMEngine:
         except Exception as exc:
             return self._fail(batch, exc)
         now = time.perf_counter()
+        self.step_trace.append((t0, now, batch.kind, len(batch.seqs), batch.num_tokens, fl.get("t_enq", t0)))
         # step latency: completion-to-completion while the pipeline is full, launch-to-completion otherwise
         dt = now - max(t0, self._last_done)
         self._last_done = now
@@ -528,6 +532,7 @@ class AsyncEngine:
         loop = asyncio.get_running_loop()
 
         def cb(out: RequestOutput) -> None:
+            out.t_engine = time.perf_counter()  # (request-path timing: NativeBackend.timings)
             if self._batch and threading.current_thread() is self._thread:
                 self._pending.append((loop, on_output, out))
             else:
@@ -565,6 +570,7 @@ class AsyncEngine:
             q.put_nowait(out)
 
         def cb(out: RequestOutput) -> None:
+            out.t_engine = time.perf_counter()  # (request-path timing: NativeBackend.timings)
             if self._batch and threading.current_thread() is self._thread:
                 self._pending.append((loop, deliver, out))  # flushed after the engine step
             else:

@@ -31,6 +31,7 @@ from __future__ import annotations
 import asyncio
 import base64
 import signal
+import time
 
 from ..backends.base import Backend, BackendError
 from ..config import ConfigManager
@@ -227,6 +228,8 @@ class SymmetryProvider:
             if key == Keys.NEW_CONVERSATION:
                 self._conversation_index += 1
             elif key == Keys.INFERENCE:
+                if isinstance(data.get("data"), dict):  # request-path timing (NativeBackend.timings)
+                    data["data"]["_t_recv"] = time.perf_counter()
                 logger.info(f"📦 Inference message received from {peer.raw_stream.remote_host}")
                 t = asyncio.ensure_future(self._serialized(lock, data, peer))
                 self._tasks.add(t)

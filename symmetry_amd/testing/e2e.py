@@ -50,7 +50,8 @@ def _client_proc(boot, server_key, model, n, prompt_tokens, max_tokens, out_q, s
                              timeout=600)
             return {"ttft_ms": None if r.ttft_s is None else r.ttft_s * 1e3, "tokens_per_s": r.tokens_per_s,
                     "events": r.content_events, "ended": r.ended, "error": r.error,
-                    "wall_s": r.t_end - r.t_start}
+                    "wall_s": r.t_end - r.t_start, "key": prompt_text(i, prompt_tokens)[:24],
+                    "t_write": r.t_start, "t_first": None if r.ttft_s is None else r.t_start + r.ttft_s}
         finally:
             await c.stop()
 
@@ -121,6 +122,8 @@ async def client_end_run(engine, model: str, clients: int, prompt_tokens: int = 
             p.kill()
         stats = provider.stats()
         saved = len(provider.saved_files)
+        timings = list(getattr(provider.backend, "timings", []))
+        trace = list(getattr(engine, "step_trace", []))
         # the provider's backend stop would shut the engine down: detach it (the caller owns the engine)
         backend = provider.backend
         if getattr(backend, "aengine", None) is not None:
@@ -148,4 +151,47 @@ async def client_end_run(engine, model: str, clients: int, prompt_tokens: int = 
         "content_events": total_events,
         "data_collection_files": saved,
         "engine": {k: stats.get(k) for k in ("mean_decode_batch", "p50_itl_ms", "decode_steps", "step_phase_ms")},
+        "ttft_path_ms": ttft_breakdown(res, timings),
+        "first_steps": first_steps(timings, trace),
     }
+
+
+def first_steps(timings: list, trace: list, n: int = 5) -> list | None:
+    """The engine's first n steps after the first request of the run arrived: (kind, sequences, tokens, launch,
+    end of the host's enqueue and completion in ms after that arrival)."""
+    recvs = [t["recv"] for t in timings if t.get("recv") is not None]
+    if not recvs or not trace:
+        return None
+    t0 = min(recvs)
+    steps = [s for s in trace if s[1] >= t0 - 0.05][:n]
+    return [{"kind": k, "seqs": ns, "tokens": nt, "launch_ms": round((a - t0) * 1e3, 3),
+             "enqueued_ms": round((q - t0) * 1e3, 3), "done_ms": round((b - t0) * 1e3, 3)}
+            for a, b, k, ns, nt, q in steps]
+
+
+def ttft_breakdown(res: list, timings: list) -> dict | None:
+    """Median of each leg of the client-end TTFT (perf_counter is CLOCK_MONOTONIC, one clock for the client
+    and provider processes of one host): client write -> provider receive -> engine submit -> first token on
+    the engine thread -> first output callback on the event loop -> first SSE event written -> first content
+    event read by the client; plus the spread of the receive times (how long the burst took to arrive)."""
+    by_key = {t.get("key"): t for t in timings if t.get("key") is not None}
+    legs = {"write_to_recv": [], "recv_to_submit": [], "submit_to_engine_first": [], "engine_to_callback": [],
+            "callback_to_written": [], "written_to_client": []}
+    recvs = []
+    for r in res:
+        t = by_key.get(r.get("key"))
+        if t is None or r.get("t_first") is None:
+            continue
+        pts = [r["t_write"], t.get("recv"), t.get("submitted"), t.get("engine_first"), t.get("callback_first"),
+               t.get("written_first"), r["t_first"]]
+        if any(p is None for p in pts):
+            continue
+        recvs.append(t["recv"])
+        for (name, vals), a, b in zip(legs.items(), pts[:-1], pts[1:]):
+            vals.append((b - a) * 1e3)
+    if not recvs:
+        return None
+    out = {k: round(statistics.median(v), 3) for k, v in legs.items()}
+    out["receive_spread"] = round((max(recvs) - min(recvs)) * 1e3, 3)
+    out["matched"] = len(recvs)
+    return out
