@@ -1221,7 +1221,16 @@ __global__ __launch_bounds__(1024) void decode_qkv_attn_kernel(const bf16* __res
 }
 
 int g_variant = -1;
-int g_wnt = 0;
+// Non-temporal weight loads (aux nt) in the decode GEMMs: ON by default.  Once-read weights stream faster
+// without allocating in the caches (bench/kernels/read_bw_policy.py: 235 MB at 5.73 -> 6.08 TB/s); decode GEMMs
+// at 10 rows (profiles/r3/nt_weights_xres_kernels.jsonl): gate_up 43.1 -> 39.1 us, qkv 14.6 -> 13.6, o 11.7 ->
+// 10.6; 10-client step 3.281 -> 3.181 ms (profiles/r3/nt_weights_xres_ab.jsonl, 3 alternating runs).  (The round-2
+// A/B that found no gain never reached the x-resident kernels, which ignored the knob.)  SYMMETRY_DG_NT=0 reverts.
+const int g_wnt_default = [] {
+  const char* knob = getenv("SYMMETRY_DG_NT");
+  return knob && knob[0] == '0' ? 0 : 1;
+}();
+int g_wnt = g_wnt_default;
 
 template <int MT, int NW, int U, int RT, int EPI, int WPE = 1>
 void go(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e0, hipStream_t s) {
@@ -1445,8 +1454,9 @@ void set_decode_gemm_variant(int v) {
     g_mlp_cfg = v >= 1000 ? v - 1000 : -1;
     if (v >= 1000) return;
   }
-  // v >= 100: variant v - 100 with non-temporal weight loads (A/B knob of bench_decode_gemm.py)
-  g_wnt = v >= 100;
+  // v >= 100: variant v - 100 with non-temporal weight loads, 0..99: with default-policy loads (A/B knob of
+  // bench_decode_gemm.py); -1: the default heuristic and the default policy
+  g_wnt = v >= 100 ? 1 : (v == -1 ? g_wnt_default : 0);
   g_variant = v >= 100 ? v - 100 : v;
 }
 
