@@ -17,6 +17,7 @@ Per client: TTFT = ``inference`` write -> first content delta on the client's so
 from __future__ import annotations
 
 import asyncio
+import collections
 import multiprocessing as mp
 import os
 import statistics
@@ -174,8 +175,8 @@ def ttft_breakdown(res: list, timings: list) -> dict | None:
     and provider processes of one host): client write -> provider receive -> engine submit -> first token on
     the engine thread -> first output callback on the event loop -> first SSE event written -> first content
     event read by the client; plus the spread of the receive times (how long the burst took to arrive)."""
-    keys = [t.get("key") for t in timings]
-    dup = {k for k in keys if keys.count(k) > 1}  # (prompts repeat with a period of 78 clients: skip those)
+    counts = collections.Counter(t.get("key") for t in timings)
+    dup = {k for k, c in counts.items() if c > 1}  # (prompts repeat with a period of 78 clients: skip those)
     by_key = {t.get("key"): t for t in timings if t.get("key") is not None and t.get("key") not in dup}
     legs = {"write_to_recv": [], "recv_to_submit": [], "submit_to_engine_first": [], "engine_to_callback": [],
             "callback_to_written": [], "written_to_client": []}
