@@ -69,6 +69,46 @@ __global__ __launch_bounds__(256) void read_lds_kernel(const uint4* __restrict__
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// Buffer loads (raw_buffer_load_b128) with an explicit cache-policy operand (gfx950 CPol bits: 1 = sc0,
+// 2 = nt, 16 = sc1): which policy streams once-read weights fastest
+template <int U, int AUX>
+__global__ __launch_bounds__(256) void read_buf_kernel(const uint4* __restrict__ w, long long n16_per_wave,
+                                                       unsigned* __restrict__ sink, long long bytes) {
+  const int lane = threadIdx.x & 63;
+  const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(w), (short)0,
+                                                                       (int)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL),
+                                                                       0x00020000);
+  const long long base = (wave * n16_per_wave + lane) * 16;
+  unsigned acc = 0;
+  for (long long i = 0; i < n16_per_wave; i += 64 * U) {
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    u4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(base + (i + 64 * u) * 16), 0, AUX);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+extern "C" int run_read_buf(const void* w, long long bytes, int waves, int aux, void* sink, hipStream_t s) {
+  const long long per_wave = bytes / 16 / waves;
+  const int blocks = waves / 4;
+  const uint4* wp = (const uint4*)w;
+  switch (aux) {
+    case 0: read_buf_kernel<8, 0><<<blocks, 256, 0, s>>>(wp, per_wave, (unsigned*)sink, bytes); break;
+    case 1: read_buf_kernel<8, 1><<<blocks, 256, 0, s>>>(wp, per_wave, (unsigned*)sink, bytes); break;
+    case 2: read_buf_kernel<8, 2><<<blocks, 256, 0, s>>>(wp, per_wave, (unsigned*)sink, bytes); break;
+    case 3: read_buf_kernel<8, 3><<<blocks, 256, 0, s>>>(wp, per_wave, (unsigned*)sink, bytes); break;
+    case 16: read_buf_kernel<8, 16><<<blocks, 256, 0, s>>>(wp, per_wave, (unsigned*)sink, bytes); break;
+    case 17: read_buf_kernel<8, 17><<<blocks, 256, 0, s>>>(wp, per_wave, (unsigned*)sink, bytes); break;
+    case 18: read_buf_kernel<8, 18><<<blocks, 256, 0, s>>>(wp, per_wave, (unsigned*)sink, bytes); break;
+    default: read_buf_kernel<8, 19><<<blocks, 256, 0, s>>>(wp, per_wave, (unsigned*)sink, bytes); break;
+  }
+  return (int)hipGetLastError();
+}
+
 extern "C" int run_read_variant(const void* w, long long bytes, int waves, int variant, void* sink, hipStream_t s) {
   const long long per_wave = bytes / 16 / waves;
   const int blocks = waves / 4;

@@ -25,7 +25,7 @@ def main():
     lib = ctypes.CDLL(so)
     dev = torch.device("cuda")
     sink = torch.zeros(4, dtype=torch.int32, device=dev)
-    for name, mb in (("o", 33.5), ("down", 117.4), ("gate_up", 234.9)):
+    for name, mb in (("o", 32.0), ("down", 117.4), ("gate_up", 234.9)):
         nbytes = int(mb * 1e6) // (1 << 20) * (1 << 20)
         copies = max(2, (1 << 30) // nbytes + 1)
         ws = [torch.empty(nbytes // 2, dtype=torch.bfloat16, device=dev) for _ in range(copies)]
@@ -53,6 +53,29 @@ def main():
                     ts.append(e0.elapsed_time(e1) * 1e3 / 16)
                 us = sorted(ts)[len(ts) // 2]
                 print(json.dumps({"shape": name, "MB": round(nbytes / 1e6, 1), "waves": waves, "variant": NAMES[v],
+                                  "us": round(us, 2), "TBps": round(nbytes / us / 1e6, 3)}), flush=True)
+            for aux in (0, 1, 2, 3, 16, 17, 18, 19):  # buffer loads by cache policy (CPol: 1 sc0, 2 nt, 16 sc1)
+                if nbytes // 16 // waves % (64 * 8):
+                    continue
+                g = torch.cuda.CUDAGraph()
+                lib.run_read_buf(ctypes.c_void_p(ws[0].data_ptr()), ctypes.c_longlong(nbytes), waves, aux,
+                                 ctypes.c_void_p(sink.data_ptr()), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                torch.cuda.synchronize()
+                with torch.cuda.graph(g):
+                    st = torch.cuda.current_stream().cuda_stream
+                    for c in range(16):
+                        lib.run_read_buf(ctypes.c_void_p(ws[c % copies].data_ptr()), ctypes.c_longlong(nbytes), waves,
+                                         aux, ctypes.c_void_p(sink.data_ptr()), ctypes.c_void_p(st))
+                ts = []
+                for _ in range(6):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    g.replay()
+                    e1.record()
+                    torch.cuda.synchronize()
+                    ts.append(e0.elapsed_time(e1) * 1e3 / 16)
+                us = sorted(ts)[len(ts) // 2]
+                print(json.dumps({"shape": name, "MB": round(nbytes / 1e6, 1), "waves": waves, "variant": f"buf_aux{aux}",
                                   "us": round(us, 2), "TBps": round(nbytes / us / 1e6, 3)}), flush=True)
         del ws
         torch.cuda.empty_cache()
