@@ -32,11 +32,15 @@ def timed(fn, reps=10, rounds=5):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--t", type=int, nargs="+", default=[512, 1280, 2048, 4096])
+    args = ap.parse_args()
     dev = torch.device("cuda")
     lnw = torch.ones(4096, device=dev, dtype=torch.bfloat16)
     for name, N, K in (("o", 4096, 4096), ("down", 4096, 14336), ("qkv", 6144, 4096)):
         w = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
-        for T in (512, 1280, 2048, 4096):
+        for T in args.t:
             x = (torch.rand(T, K, device=dev) * 2 - 1).to(torch.bfloat16)
             resid = torch.zeros(T, 4096, device=dev)
             xo = torch.empty(T, 4096, device=dev, dtype=torch.bfloat16)
