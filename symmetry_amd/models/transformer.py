@@ -82,6 +82,9 @@ MG_PROJ = tuple(p for p in os.environ.get("SYMMETRY_MG_PROJ", "").split(",") if 
 # fused decode path: QKV + decode attention as one launch, the attention units on the CUs the QKV grid leaves
 # idle (csrc/kernels/decode_gemm.hip, decode_qkv_attn_kernel)
 QKV_ATTN = os.environ.get("SYMMETRY_QKV_ATTN", "0") == "1"
+# MFMA-preshuffled copy of the lm_head for the fused decode path's dg_argmax (1 KB per wave load like the layer
+# weights; +1 GB for Llama-3-8B): SYMMETRY_LMHEAD_SHUF=0 keeps the row-major stream
+LMHEAD_SHUF = os.environ.get("SYMMETRY_LMHEAD_SHUF", "1") != "0"
 
 
 @dataclass
@@ -207,6 +210,10 @@ class TransformerLM:
             return {}
         names = ["wqkv", "wo"] + ([] if self.cfg.is_moe else ["w_gu", "w_down"])
         extra = sum(self.w.layer(i, n).numel() * 2 for i in range(self.cfg.num_layers) for n in names)
+        head = self.w["lm_head"] if LMHEAD_SHUF else None
+        if head is not None and (head.shape[0] % 16 or head.shape[1] % 32):
+            head = None
+        extra += head.numel() * 2 if head is not None else 0
         if mode == "auto":
             free, total = torch.cuda.mem_get_info(self.device)
             if extra > 0.4 * free:
@@ -217,6 +224,8 @@ class TransformerLM:
         for i in range(self.cfg.num_layers):
             for n in names:
                 out[(i, n)] = preshuffle(self.w.layer(i, n))
+        if head is not None:
+            out[(-1, "lm_head")] = preshuffle(head)
         return out
 
     def _persistent_mlp_ok(self, T: int) -> bool:
@@ -241,9 +250,11 @@ class TransformerLM:
         return self._dgw(0, "wqkv")[1] == self._dgw(0, "wo")[1]
 
     def _dgw(self, i: int, name: str):
-        """(weight, wshuf) for decode GEMM `name` of layer i."""
+        """(weight, wshuf) for decode GEMM `name` of layer i (i = -1: the lm_head)."""
         t = self.dgw.get((i, name))
-        return (t, True) if t is not None else (self.w.layer(i, name), False)
+        if t is not None:
+            return t, True
+        return (self.w[name] if i < 0 else self.w.layer(i, name)), False
 
     def _shuf(self, i: int, name: str):
         """The MFMA-preshuffled copy of weight `name` of layer i, or None (medium-M prefill GEMMs)."""
@@ -477,8 +488,9 @@ class TransformerLM:
         keys = self._buf("keys", (n,), torch.int64)
         tk = self._buf("tile_keys", (n * (self.vocab_shard // 16),), torch.int64)
         logits = self._buf("logits", (n, self.vocab_shard), torch.float32) if b.need_logits or b.filtered else None
-        ops.dg_argmax(xl, w["lm_head"], sl, eps, b.temps, b.seeds, b.step, tk, keys, ids,
-                      self.tp_rank * self.vocab_shard, logits)
+        head, hsh = self._dgw(-1, "lm_head")
+        ops.dg_argmax(xl, head, sl, eps, b.temps, b.seeds, b.step, tk, keys, ids,
+                      self.tp_rank * self.vocab_shard, logits, wshuf=hsh)
         return self._finish_sampling(b, ids, keys, logits)
 
     def _forward_general_fused(self, b: ForwardBatch, kv: KVCache, mgs: dict) -> torch.Tensor:

@@ -121,6 +121,30 @@ def test_dg_argmax(gpu, M, N):
     assert torch.equal(keys.cpu()[greedy], k_ref[greedy])
 
 
+@pytest.mark.parametrize("M,N", [(1, 128256), (10, 128256), (16, 16032), (33, 128256)])
+def test_dg_argmax_preshuffled(gpu, M, N):
+    """The lm_head as an MFMA-preshuffled copy (fused decode path): same logits / ids as the row-major weight."""
+    from symmetry_amd.models.layout import preshuffle
+
+    K = 4096
+    x, W, s = _inputs(gpu, M, N, K, seed=16)
+    temps = torch.zeros(M, device=gpu)
+    seeds = torch.zeros(M, device=gpu, dtype=torch.int64)
+    step = torch.tensor([1], device=gpu, dtype=torch.int64)
+    outs = []
+    for sh in (False, True):
+        tk = torch.empty(M * (N // 16), device=gpu, dtype=torch.int64)
+        keys = torch.empty(M, device=gpu, dtype=torch.int64)
+        ids = torch.empty(M, device=gpu, dtype=torch.int32)
+        logits = torch.empty(M, N, device=gpu)
+        ops.dg_argmax(x, preshuffle(W) if sh else W, s, 1e-5, temps, seeds, step, tk, keys, ids, 0, logits, wshuf=sh)
+        outs.append((logits, ids))
+    lg_ref = torch.empty(M, N)
+    ref.dg_f32(x.cpu(), W.cpu(), s.cpu(), 1e-5, lg_ref)
+    _close(outs[1][0], lg_ref, atol=2e-3, rtol=1e-2)
+    assert torch.equal(outs[1][1].cpu().long(), outs[1][0].cpu().argmax(1))
+
+
 @pytest.mark.parametrize("T,P", [(33, 4), (64, 4), (3, 2)])
 def test_add_prep_partial_sums_from_slabs(gpu, T, P):
     """add_prep over fp32 k-split slabs with P workgroups per row: ss holds P column-slice partials."""
