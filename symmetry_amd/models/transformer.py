@@ -585,8 +585,12 @@ class TransformerLM:
         if self.fused and n <= SKINNY_MAX_M:
             # the decode lm_head kernel (row-tile variants for wide batches), on already-normalised rows
             tk = self._buf("tile_keys", (n * ntiles,), torch.int64)
-            ops.dg_argmax(xl, self.w["lm_head"], None, self.cfg.rms_eps, b.temps, b.seeds, b.step, tk, keys, ids,
-                          self.tp_rank * self.vocab_shard, logits)
+            # preshuffled copy up to 16 rows; the row-major stream's row-tile variants win at 24-32 rows
+            # (profiles/r3/lmhead_preshuffle_ab.jsonl: 1 row 189.5 -> 175.1 us, 6 rows 192.9 -> 168.8, 24 rows
+            # 222.6 vs 232.3, 64 rows even)
+            head, hsh = self._dgw(-1, "lm_head") if n <= 16 else (self.w["lm_head"], False)
+            ops.dg_argmax(xl, head, None, self.cfg.rms_eps, b.temps, b.seeds, b.step, tk, keys, ids,
+                          self.tp_rank * self.vocab_shard, logits, wshuf=hsh)
             return self._finish_sampling(b, ids, keys, logits)
         if n <= SKINNY_MAX_M:
             tk = self._buf("tile_keys", (n * ntiles,), torch.int64)
