@@ -26,6 +26,10 @@ client) are timed between sync points (every rank's GPU idle + a barrier) on
 both sides; the max over ranks is reported.  Every generated token is
 detokenized and SSE-encoded for its client inside the timed loop.
 
+Headline ``value``: streamed tokens/s PER CLIENT (the metric's own unit), the median over the clients of
+the client-end run below -- measured at the client sockets; the engine-side per-client rate (1000 /
+ms_per_step) and the aggregate over all clients are reported next to it.
+
 Client end (``--client-end``, default on): after the timed steps the same
 engine serves as a real provider -- discovery node, Symmetry server, provider
 node and ``--clients`` swarm clients in a separate process over Noise XX +
@@ -64,8 +68,6 @@ def _args():
     ap.add_argument("--client-end", type=int, default=1, help="1: also measure at the client sockets")
     ap.add_argument("--client-tokens", type=int, default=256, help="tokens per client in the client-end run")
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--persistent-mlp", action="store_true", help="O/gate_up/down as one persistent launch (A/B)")
-    ap.add_argument("--attn-block", type=int, default=None, help="A/B: QKV -> attention -> O as one launch (0/1)")
     ap.add_argument("--nt-weights", type=int, default=None, help="A/B: non-temporal decode weight loads (0/1)")
     ap.add_argument("--max-batched-tokens", type=int, default=None, help="A/B: token budget of a pure-prefill step")
     ap.add_argument("--mixed-prefill-tokens", type=int, default=None, help="A/B: prompt budget of mixed steps")
@@ -102,14 +104,11 @@ def main() -> int:
     blocks = C * ((args.max_model_len + block - 1) // block) + 16
     cfg = EngineConfig(model=args.model, device="auto", seed=1234 + (0 if parallel == "tp" else rank),
                        max_num_seqs=C, max_model_len=args.max_model_len, block_size=block, num_kv_blocks=blocks,
-                       use_graphs=not args.no_graphs, max_num_batched_tokens=max(8192, C * P),
-                       persistent_mlp=args.persistent_mlp)
+                       use_graphs=not args.no_graphs, max_num_batched_tokens=max(8192, C * P))
     if args.max_batched_tokens is not None:
         cfg.max_num_batched_tokens = args.max_batched_tokens
     if args.mixed_prefill_tokens is not None:
         cfg.mixed_prefill_tokens = args.mixed_prefill_tokens
-    if args.attn_block is not None:
-        cfg.fused_attn_block = bool(args.attn_block)
 
     t0 = time.perf_counter()
     if parallel == "tp" and world > 1:
@@ -203,7 +202,7 @@ def main() -> int:
         eng.shutdown()
     elif world > 1:
         dist.barrier(group=group)
-    elapsed, ttfts = _reduce(group, elapsed, ttfts, world, gather_ttft=parallel == "dp")
+    elapsed, ttfts, rank_elapsed = _reduce(group, elapsed, ttfts, world, gather_ttft=parallel == "dp")
 
     p50_ttft = ttfts[len(ttfts) // 2] * 1e3
     mean_ttft, max_ttft = sum(ttfts) / len(ttfts) * 1e3, ttfts[-1] * 1e3
@@ -211,11 +210,15 @@ def main() -> int:
     n_clients = C * (world if parallel == "dp" else 1)
     total_tps = n_clients * K / elapsed
     per_client = 1e3 / ms_step
+    ce_ok = client_end is not None and client_end.get("per_client_tokens_per_s_median") is not None
+    # the headline IS the metric's "per client" rate: measured at the client sockets (SSE over Noise XX +
+    # secretstream, clients in another process) when the client-end run worked, else the engine-side rate
+    value = client_end["per_client_tokens_per_s_median"] if ce_ok else round(per_client, 2)
     if rank == 0:
         line = {
             "metric": METRIC,
-            "value": round(total_tps, 2),
-            "unit": "tokens/s",
+            "value": value,
+            "unit": "tokens/s per client",
             "n_gpus": world,
             "steps": K,
             "warmup": W,
@@ -232,7 +235,10 @@ def main() -> int:
                        "tp_comm": type(eng.model.tp).__name__ if eng.model.tp is not None else None,
                        "ops": ("torch-eager (baseline B1)" if ops.torch_mode() else
                                "native gfx950 HIP" if gpu else "torch reference (CPU)")},
-            "per_client_tokens_per_s": round(per_client, 2),
+            "value_source": "client_end (socket-measured median over clients)" if ce_ok else "engine timed steps",
+            "aggregate_tokens_per_s": round(total_tps, 2),
+            "engine_per_client_tokens_per_s": round(per_client, 2),
+            "per_rank_ms_per_step": [round(e / K * 1e3, 4) for e in rank_elapsed],
             "engine_p50_ttft_ms": round(p50_ttft, 2),
             "engine_mean_ttft_ms": round(mean_ttft, 2),
             "engine_max_ttft_ms": round(max_ttft, 2),
@@ -258,20 +264,22 @@ def main() -> int:
 
 
 def _reduce(group, elapsed, ttfts, world, gather_ttft):
-    """Max elapsed over ranks; all ranks' TTFTs (dp: every rank has its own clients)."""
+    """Max elapsed over ranks (+ every rank's own); all ranks' TTFTs (dp: every rank has its own clients)."""
     import torch
     import torch.distributed as dist
 
     if world == 1:
-        return elapsed, ttfts
+        return elapsed, ttfts, [elapsed]
     tt = torch.tensor([elapsed], dtype=torch.float64)
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=group)
+    every = [torch.zeros_like(tt) for _ in range(world)]
+    dist.all_gather(every, tt, group=group)
+    per_rank = [float(t.item()) for t in every]
     if gather_ttft:
         tf = torch.tensor(ttfts, dtype=torch.float64)
         allt = [torch.zeros_like(tf) for _ in range(world)]
         dist.all_gather(allt, tf, group=group)
         ttfts = sorted(torch.cat(allt).tolist())
-    return float(tt.item()), ttfts
+    return max(per_rank), ttfts, per_rank
 
 
 def _reduce_and_exit(group, elapsed, ttfts, world):

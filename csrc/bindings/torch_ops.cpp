@@ -168,8 +168,7 @@ void check_cache(const Tensor& k_cache, const Tensor& v_cache) {
 }
 
 void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
-                 const Tensor& ctx_lens, Tensor& out, Tensor& tmp_o, Tensor& tmp_ml, Tensor& counters, double scale,
-                 const c10::optional<Tensor>& prefetch, int64_t prefetch_wgs) {
+                 const Tensor& ctx_lens, Tensor& out, Tensor& tmp_o, Tensor& tmp_ml, Tensor& counters, double scale) {
   check_gpu(q, "q");
   check_dtype(q, at::kBFloat16, "q");
   check_cache(k_cache, v_cache);
@@ -196,19 +195,10 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, 
   check_gpu(counters, "counters");
   check_dtype(counters, at::kInt, "counters");
   TORCH_CHECK(counters.numel() >= S * Hkv, "counters must hold num_seqs * Hkv zero-initialised ints");
-  const void* pf = nullptr;
-  long long pf_bytes = 0;
-  if (prefetch.has_value() && prefetch_wgs > 0) {  // Infinity-Cache prefetch of the next launch's weight
-    check_gpu(*prefetch, "prefetch");
-    TORCH_CHECK(prefetch->get_device() == q.get_device(), "prefetch must live on q's GPU");
-    pf = prefetch->data_ptr();
-    pf_bytes = prefetch->numel() * prefetch->element_size() / 16 * 16;  // whole 16-byte vectors only
-  }
   const at::OptionalDeviceGuard g(q.device());
   launch_attn_decode(ptr<bf16>(q), ptr<bf16>(k_cache), ptr<bf16>(v_cache), ptr<int>(block_tables), ptr<int>(ctx_lens),
                      ptr<bf16>(out), ptr<float>(tmp_o), ptr<float>(tmp_ml), ptr<int>(counters), (int)S, (int)Hq,
-                     (int)Hkv, (int)BS, (int)max_blocks, (int)max_parts, (float)scale, cur_stream(q), pf, pf_bytes,
-                     (int)prefetch_wgs);
+                     (int)Hkv, (int)BS, (int)max_blocks, (int)max_parts, (float)scale, cur_stream(q));
 }
 
 void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
@@ -606,72 +596,6 @@ void dg_qkv(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in
   launch_dg(DECODE_EPI_QKV, x, W, sh, e, mg_slab, mg_counters, mg_rw);
 }
 
-// dg_qkv + attn_decode as ONE launch where it applies (decode_gemm.hip, decode_qkv_attn_kernel); returns false
-// (nothing enqueued) otherwise
-bool qkv_attn(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, const Tensor& positions,
-              const Tensor& slots, const Tensor& cos_sin, Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t Hq,
-              int64_t Hkv, bool wshuf, const Tensor& block_tables, const Tensor& ctx_lens, Tensor& out, Tensor& tmp_o,
-              Tensor& tmp_ml, Tensor& counters, double scale, Tensor& ctl) {
-  auto sh = dg_check(x, W);
-  for (auto* t : {&positions, &slots, &block_tables, &ctx_lens}) {
-    check_gpu(*t, "index tensor");
-    check_dtype(*t, at::kInt, "index tensor");
-  }
-  check_gpu(cos_sin, "cos_sin");
-  check_dtype(cos_sin, at::kFloat, "cos_sin");
-  check_cache(k_cache, v_cache);
-  for (auto* t : {&q_out, &out}) {
-    check_gpu(*t, "q_out / out");
-    check_dtype(*t, at::kBFloat16, "q_out / out");
-  }
-  for (auto* t : {&tmp_o, &tmp_ml}) {
-    check_gpu(*t, "tmp_o / tmp_ml");
-    check_dtype(*t, at::kFloat, "tmp_o / tmp_ml");
-  }
-  for (auto* t : {&counters, &ctl}) {
-    check_gpu(*t, "counters / ctl");
-    check_dtype(*t, at::kInt, "counters / ctl");
-  }
-  const int64_t M = sh.M;
-  TORCH_CHECK(sh.N == (Hq + 2 * Hkv) * 128, "qkv_attn: N must be (Hq + 2 Hkv) * 128");
-  TORCH_CHECK(k_cache.size(1) == Hkv && Hq % Hkv == 0, "qkv_attn: head counts");
-  TORCH_CHECK(positions.numel() >= M && slots.numel() >= M && ctx_lens.numel() >= M, "qkv_attn: index tensors");
-  TORCH_CHECK(q_out.numel() >= M * Hq * 128 && out.numel() == M * Hq * 128, "qkv_attn: q_out / out");
-  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == 128, "qkv_attn: cos_sin [max_pos, 128]");
-  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= M, "qkv_attn: block_tables [>=M, max_blocks]");
-  TORCH_CHECK(tmp_o.dim() == 4 && tmp_o.size(0) >= M && tmp_o.size(1) == Hq && tmp_o.size(3) == 128,
-              "qkv_attn: tmp_o [>=M, Hq, max_parts, 128]");
-  const int64_t max_parts = tmp_o.size(2), BS = k_cache.size(2), max_blocks = block_tables.size(1);
-  TORCH_CHECK(tmp_ml.numel() >= M * Hq * max_parts * 2, "qkv_attn: tmp_ml too small");
-  TORCH_CHECK(max_parts * 256 >= max_blocks * BS, "qkv_attn: tmp_o has too few partitions for the block table span");
-  TORCH_CHECK(counters.numel() >= M * Hkv && ctl.numel() >= QKV_ATTN_CTL_INTS, "qkv_attn: counters / ctl");
-  DecodeEpi e;
-  e.wshuf = wshuf ? 1 : 0;
-  dg_norm_in(e, ss_in, M, sh.K, eps);
-  e.positions = ptr<int>(positions);
-  e.slots = ptr<int>(slots);
-  e.cos_sin = ptr<float>(cos_sin);
-  e.q_out = ptr<bf16>(q_out);
-  e.k_cache = ptr<bf16>(k_cache);
-  e.v_cache = ptr<bf16>(v_cache);
-  e.Hq = (int)Hq;
-  e.Hkv = (int)Hkv;
-  e.BS = (int)BS;
-  QkvAttnArgs aa;
-  aa.block_tables = ptr<int>(block_tables);
-  aa.ctx_lens = ptr<int>(ctx_lens);
-  aa.out = ptr<bf16>(out);
-  aa.tmp_o = ptr<float>(tmp_o);
-  aa.tmp_ml = ptr<float>(tmp_ml);
-  aa.counters = ptr<int>(counters);
-  aa.max_blocks = (int)max_blocks;
-  aa.max_parts = (int)max_parts;
-  aa.scale_log2 = (float)scale * 1.4426950408889634f;
-  aa.ctl = ptr<int>(ctl);
-  const at::OptionalDeviceGuard g(x.device());
-  return launch_qkv_attn(ptr<bf16>(x), ptr<bf16>(W), (int)M, (int)sh.N, (int)sh.K, e, aa, cur_stream(x));
-}
-
 void dg_resid(const Tensor& x, const Tensor& W, Tensor& resid, const Tensor& w_next, Tensor& xw_out, Tensor& ss_out, bool wshuf,
               const c10::optional<Tensor>& mg_slab, const c10::optional<Tensor>& mg_counters, int64_t mg_rw) {
   auto sh = dg_check(x, W, is_mg(mg_slab));
@@ -849,142 +773,6 @@ void logits_argmax(const Tensor& logits, const Tensor& temps, const Tensor& seed
                        reinterpret_cast<unsigned long long*>(out_keys.data_ptr()), ptr<int>(out_ids), cur_stream(logits));
 }
 
-void decode_mlp(const Tensor& attn, const Tensor& Wo, const Tensor& Wgu, const Tensor& Wd, Tensor& resid,
-                const Tensor& ln2, const Tensor& w_next, Tensor& xw, Tensor& ss, Tensor& act, Tensor& ctl, double eps,
-                bool wshuf) {
-  for (const Tensor* t : {&attn, &Wo, &Wgu, &Wd, &ln2, &w_next, static_cast<const Tensor*>(&xw),
-                          static_cast<const Tensor*>(&act)}) {
-    check_gpu(*t, "decode_mlp tensor");
-    check_dtype(*t, at::kBFloat16, "decode_mlp tensor");
-  }
-  check_gpu(resid, "resid");
-  check_dtype(resid, at::kFloat, "resid");
-  check_gpu(ss, "ss");
-  check_dtype(ss, at::kFloat, "ss");
-  check_gpu(ctl, "ctl");
-  check_dtype(ctl, at::kInt, "ctl");
-  const int64_t M = attn.size(0), dq = attn.size(1), d = Wo.size(0), F = Wd.size(1);
-  TORCH_CHECK(M >= 1 && M <= 16, "decode_mlp: M must be in [1, 16]");
-  TORCH_CHECK(Wo.size(1) == dq && Wgu.size(0) == 2 * F && Wgu.size(1) == d && Wd.size(0) == d,
-              "decode_mlp: weight shapes");
-  TORCH_CHECK(dq % 512 == 0 && d % 512 == 0 && F % 512 == 0, "decode_mlp: every K must be a multiple of 512");
-  TORCH_CHECK(resid.numel() == M * d && xw.numel() == M * d && act.numel() == M * F, "decode_mlp: activations");
-  TORCH_CHECK(ss.dim() == 2 && ss.size(0) >= M && ss.size(1) == d / 16, "decode_mlp: ss [M, d/16]");
-  TORCH_CHECK(ln2.numel() == d && w_next.numel() == d && ctl.numel() >= DECODE_MLP_CTL_INTS, "decode_mlp: norms / ctl");
-  DecodeMlpArgs a;
-  a.attn = ptr<bf16>(attn);
-  a.Wo = ptr<bf16>(Wo);
-  a.Wgu = ptr<bf16>(Wgu);
-  a.Wd = ptr<bf16>(Wd);
-  a.resid = ptr<float>(resid);
-  a.ln2 = ptr<bf16>(ln2);
-  a.w_next = ptr<bf16>(w_next);
-  a.xw = ptr<bf16>(xw);
-  a.ss = ptr<float>(ss);
-  a.act = ptr<bf16>(act);
-  a.ctl = ptr<int>(ctl);
-  a.M = (int)M;
-  a.d = (int)d;
-  a.dq = (int)dq;
-  a.F = (int)F;
-  a.wshuf = wshuf ? 1 : 0;
-  a.eps = (float)eps;
-  const at::OptionalDeviceGuard g(attn.device());
-  launch_decode_mlp(a, cur_stream(attn));
-}
-
-void decode_block(const Tensor& xw, const Tensor& Wqkv, const c10::optional<Tensor>& ss_in, double eps,
-                  const Tensor& positions, const Tensor& slots, const Tensor& cos_sin, Tensor& q, Tensor& k_cache,
-                  Tensor& v_cache, const Tensor& block_tables, const Tensor& ctx_lens, Tensor& attn, Tensor& tmp_o,
-                  Tensor& tmp_ml, Tensor& counters, double scale, const Tensor& Wo, Tensor& resid, const Tensor& ln2,
-                  Tensor& xw_out, Tensor& ss_out, Tensor& ctl, bool wshuf, const c10::optional<Tensor>& stamps, int64_t cfg) {
-  auto sh = dg_check(xw, Wqkv);
-  const int64_t M = sh.M, d = sh.K, Hkv = k_cache.size(1), Hq = sh.N / 128 - 2 * Hkv;
-  TORCH_CHECK(M <= 16, "decode_block: M must be in [1, 16]");
-  TORCH_CHECK(sh.N % 128 == 0 && Hq > 0 && Hq % Hkv == 0 && Hq / Hkv <= 8, "decode_block: heads (G <= 8)");
-  TORCH_CHECK(d % 512 == 0 && (Hq * 128) % 512 == 0, "decode_block: d and Hq * 128 must be multiples of 512");
-  for (auto* t : {&positions, &slots, &block_tables, &ctx_lens}) {
-    check_gpu(*t, "index tensor");
-    check_dtype(*t, at::kInt, "index tensor");
-  }
-  check_gpu(cos_sin, "cos_sin");
-  check_dtype(cos_sin, at::kFloat, "cos_sin");
-  check_cache(k_cache, v_cache);
-  for (const Tensor* t : {static_cast<const Tensor*>(&q), static_cast<const Tensor*>(&attn), &Wo, &ln2,
-                          static_cast<const Tensor*>(&xw_out)}) {
-    check_gpu(*t, "decode_block tensor");
-    check_dtype(*t, at::kBFloat16, "decode_block tensor");
-  }
-  for (const Tensor* t : {static_cast<const Tensor*>(&resid), static_cast<const Tensor*>(&ss_out),
-                          static_cast<const Tensor*>(&tmp_o), static_cast<const Tensor*>(&tmp_ml)}) {
-    check_gpu(*t, "decode_block tensor");
-    check_dtype(*t, at::kFloat, "decode_block tensor");
-  }
-  check_gpu(counters, "counters");
-  check_dtype(counters, at::kInt, "counters");
-  check_gpu(ctl, "ctl");
-  check_dtype(ctl, at::kInt, "ctl");
-  TORCH_CHECK(positions.numel() >= M && slots.numel() >= M && ctx_lens.numel() >= M, "decode_block: index tensors");
-  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == 128, "decode_block: cos_sin [max_pos, 128]");
-  TORCH_CHECK(q.numel() >= M * Hq * 128 && attn.numel() == M * Hq * 128, "decode_block: q / attn");
-  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= M, "decode_block: block_tables [>=M, max_blocks]");
-  const int64_t BS = k_cache.size(2), max_blocks = block_tables.size(1);
-  TORCH_CHECK(tmp_o.dim() == 4 && tmp_o.size(0) >= M && tmp_o.size(1) == Hq && tmp_o.size(3) == 128,
-              "decode_block: tmp_o [>=M, Hq, max_parts, 128]");
-  const int64_t max_parts = tmp_o.size(2);
-  TORCH_CHECK(max_parts * 256 >= max_blocks * BS, "decode_block: tmp_o has too few 256-token partitions");
-  TORCH_CHECK(tmp_ml.numel() >= M * Hq * max_parts * 2 && counters.numel() >= M * Hkv, "decode_block: tmp_ml / counters");
-  TORCH_CHECK(Wo.dim() == 2 && Wo.size(0) == d && Wo.size(1) == Hq * 128, "decode_block: Wo [d, Hq * 128]");
-  TORCH_CHECK(resid.numel() == M * d && xw_out.numel() == M * d && ln2.numel() == d, "decode_block: residual");
-  TORCH_CHECK(ss_out.dim() == 2 && ss_out.size(0) >= M && ss_out.size(1) == d / 16, "decode_block: ss_out [M, d/16]");
-  TORCH_CHECK(ctl.numel() >= DECODE_BLOCK_CTL_INTS && (Hkv + 10) * 32 <= DECODE_BLOCK_CTL_INTS, "decode_block: ctl");
-  DecodeBlockArgs a;
-  DecodeEpi e;
-  dg_norm_in(e, ss_in, M, d, eps);
-  a.xw = ptr<bf16>(xw);
-  a.Wqkv = ptr<bf16>(Wqkv);
-  a.ss_in = e.ss_in;
-  a.ss_tiles = e.ss_tiles;
-  a.inv_d = e.inv_d;
-  a.eps = e.eps;
-  a.positions = ptr<int>(positions);
-  a.slots = ptr<int>(slots);
-  a.cos_sin = ptr<float>(cos_sin);
-  a.q = ptr<bf16>(q);
-  a.k_cache = ptr<bf16>(k_cache);
-  a.v_cache = ptr<bf16>(v_cache);
-  a.block_tables = ptr<int>(block_tables);
-  a.ctx_lens = ptr<int>(ctx_lens);
-  a.attn = ptr<bf16>(attn);
-  a.tmp_o = ptr<float>(tmp_o);
-  a.tmp_ml = ptr<float>(tmp_ml);
-  a.part_counters = ptr<int>(counters);
-  a.max_blocks = (int)max_blocks;
-  a.max_parts = (int)max_parts;
-  a.scale_log2 = (float)scale * 1.4426950408889634f;
-  a.Wo = ptr<bf16>(Wo);
-  a.resid = ptr<float>(resid);
-  a.ln2 = ptr<bf16>(ln2);
-  a.xw_out = ptr<bf16>(xw_out);
-  a.ss_out = ptr<float>(ss_out);
-  a.ctl = ptr<int>(ctl);
-  a.M = (int)M;
-  a.d = (int)d;
-  a.Hq = (int)Hq;
-  a.Hkv = (int)Hkv;
-  a.BS = (int)BS;
-  a.wshuf = wshuf ? 1 : 0;
-  a.cfg = (int)cfg;
-  if (stamps.has_value()) {
-    check_gpu(*stamps, "stamps");
-    TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->numel() >= 4 * ((Hq + 2 * Hkv) * 8 + M * Hkv * max_parts + d / 16),
-                "decode_block: stamps int64 [grid, 4]");
-    a.stamps = reinterpret_cast<long long*>(stamps->data_ptr<int64_t>());
-  }
-  const at::OptionalDeviceGuard g(xw.device());
-  launch_decode_block(a, cur_stream(xw));
-}
-
 void rownorm(const Tensor& xw, const Tensor& ss, double eps, Tensor& out) {
   check_gpu(xw, "xw");
   check_dtype(xw, at::kBFloat16, "xw");
@@ -1013,8 +801,7 @@ TORCH_LIBRARY(symmetry_amd, m) {
       &rope_cache);
   m.def(
       "attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, Tensor(a!) out, "
-      "Tensor(b!) tmp_o, Tensor(c!) tmp_ml, Tensor(d!) counters, float scale, Tensor? prefetch=None, "
-      "int prefetch_wgs=0) -> ()",
+      "Tensor(b!) tmp_o, Tensor(c!) tmp_ml, Tensor(d!) counters, float scale) -> ()",
       &attn_decode);
   m.def(
       "attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, Tensor cu_q, "
@@ -1024,12 +811,6 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("mgemm(Tensor x, Tensor w, Tensor(a!) y, int rw) -> ()", &mgemm);
   m.def("mgemm_nt(int on) -> ()", [](int64_t on) { set_mgemm_nt((int)on); });
   m.def("decode_halves(int on) -> ()", [](int64_t on) { set_decode_halves((int)on); });
-  m.def("qkv_attn_stamps(Tensor? stamps) -> ()", [](const c10::optional<Tensor>& t) {
-    set_qkv_attn_stamps(t.has_value() ? reinterpret_cast<long long*>(t->data_ptr()) : nullptr);
-  });
-  m.def("decode_mlp_stamps(Tensor? stamps) -> ()", [](const c10::optional<Tensor>& t) {
-    set_decode_mlp_stamps(t.has_value() ? reinterpret_cast<long long*>(t->data_ptr()) : nullptr);
-  });
   m.def("attn_stream_min(int tokens) -> ()", [](int64_t t) { set_attn_stream_min((int)t); });
   m.def("attn_wave(int min_units, int min_span) -> ()",
         [](int64_t u, int64_t span) { set_attn_wave((int)u, (int)span); });
@@ -1043,12 +824,6 @@ TORCH_LIBRARY(symmetry_amd, m) {
       "Tensor(d!) offsets, Tensor(e!) cursor, Tensor(f!) xs, Tensor(g!) dst) -> ()",
       &moe_route_permute);
   m.def("dg_f32(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor(a!) y, bool wshuf=False) -> ()", &dg_f32);
-  m.def(
-      "qkv_attn(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor positions, Tensor slots, Tensor cos_sin, "
-      "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, bool wshuf, Tensor block_tables, "
-      "Tensor ctx_lens, Tensor(d!) out, Tensor(e!) tmp_o, Tensor(f!) tmp_ml, Tensor(g!) counters, float scale, "
-      "Tensor(h!) ctl) -> bool",
-      &qkv_attn);
   m.def(
       "dg_qkv(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor positions, Tensor slots, Tensor cos_sin, "
       "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, bool wshuf=False, "
@@ -1072,10 +847,6 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("add_prep(Tensor delta, Tensor(a!) resid, Tensor w, Tensor(b!) xw, Tensor(c!) ss) -> ()", &add_prep);
   m.def("rownorm(Tensor xw, Tensor ss, float eps, Tensor(a!) out) -> ()", &rownorm);
   m.def(
-      "decode_mlp(Tensor attn, Tensor Wo, Tensor Wgu, Tensor Wd, Tensor(a!) resid, Tensor ln2, Tensor w_next, "
-      "Tensor(b!) xw, Tensor(c!) ss, Tensor(d!) act, Tensor(e!) ctl, float eps, bool wshuf=False) -> ()",
-      &decode_mlp);
-  m.def(
       "sample_filtered(Tensor logits, Tensor temps, Tensor top_k, Tensor top_p, Tensor seeds, Tensor step, "
       "Tensor(a!) out_ids) -> ()",
       &sample_filtered);
@@ -1083,12 +854,6 @@ TORCH_LIBRARY(symmetry_amd, m) {
       "logits_argmax(Tensor logits, Tensor temps, Tensor seeds, Tensor step, int n_offset, Tensor(a!) out_keys, "
       "Tensor(b!) out_ids) -> ()",
       &logits_argmax);
-  m.def(
-      "decode_block(Tensor xw, Tensor Wqkv, Tensor? ss_in, float eps, Tensor positions, Tensor slots, Tensor cos_sin, "
-      "Tensor(a!) q, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor block_tables, Tensor ctx_lens, Tensor(d!) attn, "
-      "Tensor(e!) tmp_o, Tensor(f!) tmp_ml, Tensor(g!) counters, float scale, Tensor Wo, Tensor(h!) resid, Tensor ln2, "
-      "Tensor(i!) xw_out, Tensor(j!) ss_out, Tensor(k!) ctl, bool wshuf=False, Tensor(l!)? stamps=None, int cfg=0) -> ()",
-      &decode_block);
   m.def("decode_gemm_variant(int v) -> ()", [](int64_t v) { set_decode_gemm_variant((int)v); });
   m.def("decode_ksplit(int on) -> ()", [](int64_t on) { set_decode_ksplit((int)on); });
   m.def("decode_gemm_nt(int on) -> ()", [](int64_t on) { set_decode_gemm_nt((int)on); });

@@ -11,6 +11,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -359,13 +360,18 @@ void xgmi_keys_max_multi(std::vector<Tensor> keys, std::vector<Tensor> ids, std:
   launch_xgmi_keys_max_multi(m, world, (int)B, stream_of(keys[0]));
 }
 
-// reads (and clears) the error word: 1 + the source rank that never signalled within the wait limit
-// (host-mapped memory: no device synchronisation; a kernel still running may set it later)
-int64_t xgmi_error(int64_t h) {
+// reads the error word: 1 + the source rank that never signalled within the wait limit, or the code the host
+// declared (xgmi_set_error).  Sticky: a communicator that lost a peer stays failed (every later collective
+// skips its waits), the provider exits and a supervisor starts fresh ranks.  Host-mapped memory: no device
+// synchronisation; a kernel still running may set it later.
+int64_t xgmi_error(int64_t h) { return *get(h)->err_host; }
+
+// the host's health monitor declares a fault (e.g. 1 + the rank whose process died): spinning collectives
+// stop waiting within a few polls; code 0 clears the word (tests)
+void xgmi_set_error(int64_t h, int64_t code) {
   Xgmi* x = get(h);
-  const int v = *x->err_host;
-  if (v) *x->err_host = 0;
-  return v;
+  *x->err_host = (int)code;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
 }
 
 int64_t xgmi_slot_bytes(int64_t h) { return get(h)->args.slot_bytes; }
@@ -418,6 +424,7 @@ TORCH_LIBRARY_FRAGMENT(symmetry_amd, m) {
   m.def("xgmi_keys_max_multi(Tensor[] keys, Tensor(a!)[] ids, int[] comms, int delay_rank=-1, int delay_us=0) -> ()",
         &xgmi_keys_max_multi);
   m.def("xgmi_error(int comm) -> int", &xgmi_error);
+  m.def("xgmi_set_error(int comm, int code) -> ()", &xgmi_set_error);
   m.def("xgmi_slot_bytes(int comm) -> int", &xgmi_slot_bytes);
   m.def("xgmi_destroy(int comm) -> ()", &xgmi_destroy);
 }

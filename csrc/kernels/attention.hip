@@ -39,36 +39,16 @@
 namespace {
 
 // ---------------------------------------------------------------------------------------------
-// Decode (body: attn_decode.h, shared with the fused decode block launch)
+// Decode (body: attn_decode.h)
 // ---------------------------------------------------------------------------------------------
 // GMAX >= G query heads per kv head: the cross-wave merge stages GMAX columns in LDS (GMAX = 4 for
 // Llama-3 GQA: 17 KB instead of 68 KB, so LDS no longer caps the resident workgroups per CU)
-// Infinity-Cache prefetch role (optional extra workgroups of the launch, blockIdx.x >= num_seqs): a
-// decode-sized attention launch is latency-bound and leaves HBM idle, so spare workgroups stream the
-// NEXT launch's weight (the O projection) through L2 into the 256 MB Infinity Cache, from which the O
-// GEMM then reads (profiles/mall_prefetch_probe_r2.jsonl: a 33 MB weight streams ~2.3 us faster from it).
-// Loads are made live with an empty asm (no stores); 4 KB per wave per round trip, 16 KB chunks.
-SYM_DEV void mall_prefetch(const uint4* __restrict__ w, long long n16, long long wave, long long nwaves) {
-  const int lane = threadIdx.x & 63;
-  for (long long c = wave; (c + 1) * 256 <= n16; c += nwaves) {
-    const uint4* p = w + c * 256 + lane;
-    const uint4 v0 = p[0], v1 = p[64], v2 = p[128], v3 = p[192];
-    asm volatile("" ::"v"(v0.x), "v"(v1.x), "v"(v2.x), "v"(v3.x));
-  }
-}
-
 template <int GMAX>
 __global__ __launch_bounds__(DWAVES * 64, 4) void attn_decode_kernel(
     const bf16* __restrict__ q, const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
     const int* __restrict__ block_tables, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
     float* __restrict__ tmp_o, float* __restrict__ tmp_ml, int* __restrict__ counters, int Hq, int Hkv, int BS,
-    int max_blocks, int max_parts, float scale_log2, int num_seqs, const uint4* __restrict__ pf, long long pf_n16) {
-  if ((int)blockIdx.x >= num_seqs) {  // prefetch workgroups: (gridDim.x - num_seqs) x Hkv x max_parts
-    const long long wg = ((long long)(blockIdx.x - num_seqs) * gridDim.y + blockIdx.y) * gridDim.z + blockIdx.z;
-    const long long nwg = (long long)(gridDim.x - num_seqs) * gridDim.y * gridDim.z;
-    mall_prefetch(pf, pf_n16, wg * DWAVES + (threadIdx.x >> 6), nwg * DWAVES);
-    return;
-  }
+    int max_blocks, int max_parts, float scale_log2) {
   attn_decode_unit<GMAX>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters, Hq, Hkv, BS,
                        max_blocks, max_parts, scale_log2, blockIdx.x, blockIdx.y, blockIdx.z);
 }
@@ -889,18 +869,9 @@ static int g_attn_stream_cfg = [] {
   return knob ? atoi(knob) : 0;
 }();
 
-bool attn_decode_uses_grid(int num_seqs, int Hkv, int BS, int max_blocks, int G) {
-  const int span = max_blocks * BS;
-  const bool wave = g_attn_wave_units > 0 && num_seqs * Hkv >= g_attn_wave_units && span >= g_attn_wave_span &&
-                    G <= 16 && max_blocks <= 64;
-  const bool stream = g_attn_stream_min > 0 && span >= g_attn_stream_min && BS >= 32 && G <= 16;
-  return !wave && !stream;
-}
-
 void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,
                         const int* ctx_lens, bf16* out, float* tmp_o, float* tmp_ml, int* counters, int num_seqs,
-                        int Hq, int Hkv, int BS, int max_blocks, int max_parts, float scale, hipStream_t s,
-                        const void* prefetch, long long prefetch_bytes, int prefetch_wgs) {
+                        int Hq, int Hkv, int BS, int max_blocks, int max_parts, float scale, hipStream_t s) {
   if (num_seqs == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
   const int G = Hq / Hkv;
@@ -931,24 +902,16 @@ void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache,
     }
     return;
   }
-  // optional prefetch workgroups: ~prefetch_wgs extra, as whole (Hkv x max_parts) columns of the grid
-  const int pfx = (prefetch != nullptr && prefetch_bytes >= 4096 && prefetch_wgs > 0)
-                      ? std::max(1, prefetch_wgs / (Hkv * max_parts)) : 0;
-  const uint4* pf = reinterpret_cast<const uint4*>(prefetch);
-  const long long pf_n16 = pfx ? prefetch_bytes / 16 : 0;
-  dim3 grid(num_seqs + pfx, Hkv, max_parts);
+  dim3 grid(num_seqs, Hkv, max_parts);
   if (G <= 4)
     attn_decode_kernel<4><<<grid, DWAVES * 64, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml,
-                                                       counters, Hq, Hkv, BS, max_blocks, max_parts, scale_log2,
-                                                       num_seqs, pf, pf_n16);
+                                                       counters, Hq, Hkv, BS, max_blocks, max_parts, scale_log2);
   else if (G <= 8)
     attn_decode_kernel<8><<<grid, DWAVES * 64, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml,
-                                                       counters, Hq, Hkv, BS, max_blocks, max_parts, scale_log2,
-                                                       num_seqs, pf, pf_n16);
+                                                       counters, Hq, Hkv, BS, max_blocks, max_parts, scale_log2);
   else
     attn_decode_kernel<16><<<grid, DWAVES * 64, 0, s>>>(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml,
-                                                        counters, Hq, Hkv, BS, max_blocks, max_parts, scale_log2,
-                                                        num_seqs, pf, pf_n16);
+                                                        counters, Hq, Hkv, BS, max_blocks, max_parts, scale_log2);
 }
 
 void launch_attn_prefill(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,

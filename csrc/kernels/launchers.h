@@ -75,88 +75,6 @@ struct DecodeEpi {
   long long ks_cap = 0;  // floats in ks_ws
   int ks_ncnt = 0;       // ints in ks_cnt
 };
-// Persistent decode MLP block (O-proj + residual + ln2 prep -> gate_up + SwiGLU -> down + residual + next
-// norm prep), M <= 16, every K % 512 == 0.  ctl: DECODE_MLP_CTL_INTS ints, zero-initialised once, re-armed by the kernel.
-constexpr int DECODE_MLP_CTL_INTS = 4224;
-struct DecodeMlpArgs {
-  const bf16* attn = nullptr;  // [M, dq] attention output
-  const bf16* Wo = nullptr;    // [d, dq]
-  const bf16* Wgu = nullptr;   // [2F, d] gate/up interleaved per 16 rows
-  const bf16* Wd = nullptr;    // [d, F]
-  float* resid = nullptr;      // [M, d] fp32 residual stream
-  const bf16* ln2 = nullptr;   // post-attention norm weight
-  const bf16* w_next = nullptr;  // next layer's input norm (or the final norm)
-  bf16* xw = nullptr;          // [M, d]
-  float* ss = nullptr;         // [M, d / 16]
-  bf16* act = nullptr;         // [M, F]
-  int* ctl = nullptr;
-  long long* stamps = nullptr;  // optional [grid][8] s_memrealtime phase stamps (x-resident kernel; timing only)
-  int xcfg = 0;                 // x-resident kernel A/B knobs (set by the launcher)
-  int M = 0, d = 0, dq = 0, F = 0, wshuf = 0;
-  float eps = 0.f;
-};
-void launch_decode_mlp(const DecodeMlpArgs& a, hipStream_t s);
-void set_decode_mlp_stamps(long long* stamps);  // nullptr: off
-// Fused decode attention block (QKV + RoPE + K/V write -> split-KV attention -> O + residual + ln2 prep),
-// M <= 16, D = 128, G = Hq / Hkv <= 8, d % 512 == 0.  ctl: DECODE_BLOCK_CTL_INTS ints, zero-initialised
-// once, re-armed by the kernel (word ctl[(Hkv + 9) * 32] != 0 after a launch: a dependency wait gave up).
-constexpr int DECODE_BLOCK_CTL_INTS = 1024;
-struct DecodeBlockArgs {
-  // QKV
-  const bf16* xw = nullptr;      // [M, d] normalised-input prep (deferred RMSNorm)
-  const bf16* Wqkv = nullptr;    // [(Hq + 2 Hkv) * 128, d]
-  const float* ss_in = nullptr;  // row sum-of-squares partials [M, ss_tiles]
-  int ss_tiles = 0;
-  float inv_d = 0.f, eps = 0.f;
-  const int* positions = nullptr;
-  const int* slots = nullptr;
-  const float* cos_sin = nullptr;
-  bf16* q = nullptr;             // [M, Hq, 128]
-  bf16* k_cache = nullptr;
-  bf16* v_cache = nullptr;
-  // attention
-  const int* block_tables = nullptr;
-  const int* ctx_lens = nullptr;
-  bf16* attn = nullptr;          // [M, Hq * 128]
-  float* tmp_o = nullptr;
-  float* tmp_ml = nullptr;
-  int* part_counters = nullptr;  // split-KV arrival counters [M * Hkv], self re-arming
-  int max_blocks = 0, max_parts = 0;
-  float scale_log2 = 0.f;
-  // O projection + residual
-  const bf16* Wo = nullptr;      // [d, Hq * 128]
-  float* resid = nullptr;
-  const bf16* ln2 = nullptr;
-  bf16* xw_out = nullptr;        // may alias xw: written only after every QKV tile has read it
-  float* ss_out = nullptr;       // [M, d / 16]; may alias ss_in (same argument)
-  int* ctl = nullptr;
-  long long* stamps = nullptr;   // optional [grid][4] s_memrealtime stamps (start, wait done, end, role)
-  int cfg = 0;                   // A/B knobs (bench_decode_block.py): 1 = O waits before its weight loads,
-                                 // 2 = no acquire after the polls (timing only: NOT a valid hand-off)
-  int M = 0, d = 0, Hq = 0, Hkv = 0, BS = 0, wshuf = 0;
-};
-void launch_decode_block(const DecodeBlockArgs& a, hipStream_t s);
-// Fused QKV projection (+ RoPE, paged K/V write) + split-KV decode attention in ONE launch (decode_gemm.hip,
-// decode_qkv_attn_kernel): the attention units run on the CUs the x-resident QKV grid leaves idle.  Returns
-// false (nothing launched) where it does not apply -- the caller then runs dg_qkv + attn_decode.
-constexpr int QKV_ATTN_CTL_INTS = 2176;
-struct QkvAttnArgs {
-  const int* block_tables = nullptr;
-  const int* ctx_lens = nullptr;
-  bf16* out = nullptr;        // [M, Hq, 128]
-  float* tmp_o = nullptr;     // split-KV partials [M, Hq, max_parts, 128]
-  float* tmp_ml = nullptr;
-  int* counters = nullptr;    // [M * Hkv] split-KV arrivals, self re-arming
-  int max_blocks = 0, max_parts = 0;
-  float scale_log2 = 0.f;
-  int* ctl = nullptr;         // QKV_ATTN_CTL_INTS ints, zero once; word 2080 != 0 after a launch: a wait gave up
-  long long* stamps = nullptr;  // optional [grid][4] s_memrealtime stamps (set by the launcher; timing only)
-};
-void set_qkv_attn_stamps(long long* stamps);
-bool launch_qkv_attn(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, const QkvAttnArgs& aa,
-                     hipStream_t s);
-// attention.hip: true where launch_attn_decode would run its grid kernel (the form the fused launch embeds)
-bool attn_decode_uses_grid(int num_seqs, int Hkv, int BS, int max_blocks, int G);
 void set_decode_gemm_variant(int v);  // -1: default heuristic
 void set_decode_ksplit(int on);       // x-resident decode GEMM remainder split over K (default off)
 void set_decode_halves(int on);       // x-resident decode GEMM remainder tiles as row halves (default off)
@@ -196,8 +114,7 @@ void launch_rope_cache(LinOut qkv, const int* positions, const int* slots, const
 // attention.hip
 void launch_attn_decode(const bf16* q, const bf16* k_cache, const bf16* v_cache, const int* block_tables,
                         const int* ctx_lens, bf16* out, float* tmp_o, float* tmp_ml, int* counters, int num_seqs,
-                        int Hq, int Hkv, int BS, int max_blocks, int max_parts, float scale, hipStream_t s,
-                        const void* prefetch = nullptr, long long prefetch_bytes = 0, int prefetch_wgs = 0);
+                        int Hq, int Hkv, int BS, int max_blocks, int max_parts, float scale, hipStream_t s);
 // decode attention switches to the streaming long-context kernel from this block-table span (0: never)
 void set_attn_stream_min(int tokens);
 // wide batches: one wave per (seq, kv head) from min_units units for spans of >= min_span tokens

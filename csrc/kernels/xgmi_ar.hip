@@ -24,7 +24,8 @@
 // collectives split their bytes over workgroups (add_prep parts, all-reduce chunks and the keys
 // collective all address the same slot bytes differently).  Flags are compared with a signed
 // difference (a fast peer may already have raised a later epoch in the same flag word).
-// Spins are bounded: a missing peer sets the error word and the kernel exits instead of hanging.
+// Spins are bounded: a missing peer sets the error word and the kernel exits instead of hanging; every later
+// spin sees that word and exits at once (xg_fault_declared).
 #include "common.h"
 #include "launchers.h"
 
@@ -35,6 +36,15 @@ constexpr int XG_THREADS = 256;
 // first collectives of a provider start-up, where ranks can drift by the time each one spends loading
 // library GEMM code objects before its first prefill.
 constexpr unsigned long long XG_WAIT_TICKS = 3000000000ull;
+
+// Fault containment: once the error word is set -- by an earlier collective that gave up on a peer, or by the
+// host's health monitor that saw a rank die (parallel/health.py) -- no collective waits any more: the step
+// finishes with garbage that the host discards, so a dead peer costs at most ONE wait limit per provider, not
+// one per collective (a captured 70B TP=8 step holds 161).  The word is host-mapped (a PCIe round trip), so a
+// spin reads it only after 16 polls and then every 256: a collective whose peers are on time never pays it.
+SYM_DEV bool xg_fault_declared(const XgmiArgs& c, int it) {
+  return (it & 255) == 16 && __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
 
 SYM_DEV char* xg_slot(const XgmiArgs& c, int r, int par, int src) {
   return c.bufs[r] + XG_FLAG_BYTES + ((long long)par * c.world + src) * c.slot_bytes;
@@ -97,7 +107,9 @@ SYM_DEV int xg_exchange_fn(const XgmiArgs& c, int wg, int nwg, PushFn push, unsi
     const unsigned* mine =
         reinterpret_cast<const unsigned*>(c.bufs[c.rank] + XG_HDR_BYTES) + wg * XG_MAX_WORLD + threadIdx.x;
     const unsigned long long t0 = wall_clock64();
+    int it = 0;
     while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      if (xg_fault_declared(c, ++it)) break;
       if (wall_clock64() - t0 > XG_WAIT_TICKS) {  // error word: 1 + the source rank that never arrived
         __hip_atomic_store(c.err, 1 + (int)threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
@@ -264,7 +276,9 @@ SYM_DEV void xg_reduce_add_prep_body(const XgmiArgs& c, int row, int part, int T
     const int tile = t0 + i / c.world, src = i % c.world;
     const unsigned* f = flags + tile * XG_MAX_WORLD + src;
     const unsigned long long w0 = wall_clock64();
+    int it = 0;
     while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      if (xg_fault_declared(c, ++it)) break;
       if (wall_clock64() - w0 > XG_WAIT_TICKS) {
         __hip_atomic_store(c.err, 1 + src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;

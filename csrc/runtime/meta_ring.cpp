@@ -13,11 +13,19 @@
 // Layout of the mapping:  Header | slot[nslots] where slot = {u64 seq, u32 bytes, u32 pad, payload}.
 // A slot is published by storing its seq (release) after the payload; a reader owns message k when
 // slot[k % nslots].seq == k + 1 (acquire), and releases it by advancing its cursor (release).
+//
+// Back-channel (fault containment): every process registers its pid in the header; a worker that fails
+// stores a nonzero error code in its own word before it exits.  Rank 0's health monitor reads
+// `faults()` -- reported codes, plus readers whose process is gone (killed: no chance to report) -- so a
+// dead peer is noticed on the host within one poll instead of by the device collectives' wait limit, and a
+// worker notices a dead rank 0 the same way (pop returns None).
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 
 #include <atomic>
 #include <cerrno>
+#include <csignal>
+#include <cstdio>
 #include <chrono>
 #include <cstdint>
 #include <cstring>
@@ -57,6 +65,9 @@ struct Header {
   alignas(64) std::atomic<uint64_t> written;  // messages published
   alignas(64) std::atomic<uint32_t> closed;   // the producer shut the ring down
   Cursor read[kMaxReaders];                   // messages consumed, per reader
+  alignas(64) std::atomic<int32_t> rerr[kMaxReaders];  // worker -> rank 0 error codes (0 = healthy)
+  std::atomic<int32_t> rpid[kMaxReaders];              // reader pids (0 = not registered)
+  std::atomic<int32_t> wpid;                           // producer pid
 };
 
 struct SlotHdr {
@@ -66,6 +77,22 @@ struct SlotHdr {
 };
 
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory atomics must be lock-free");
+
+// false once `pid` has exited (gone, or a zombie its parent has not reaped yet)
+bool pid_alive(int pid) {
+  if (pid <= 0) return true;
+  if (kill(pid, 0) != 0 && errno == ESRCH) return false;
+  char path[64];
+  std::snprintf(path, sizeof(path), "/proc/%d/stat", pid);
+  FILE* f = std::fopen(path, "r");
+  if (f == nullptr) return true;  // no procfs: trust kill()
+  char buf[512];
+  const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+  std::fclose(f);
+  buf[n] = 0;
+  const char* rp = std::strrchr(buf, ')');  // "pid (comm) S ...": the state follows the last ')'
+  return !(rp != nullptr && rp[1] == ' ' && (rp[2] == 'Z' || rp[2] == 'X'));
+}
 
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -159,10 +186,13 @@ class MetaRing {
     {
       py::gil_scoped_release nogil;
       Backoff bo(0.002);
+      int it = 0;
       while (k - min_read() >= h_->nslots) {
         if (bo.wait() > timeout_s && timeout_s >= 0)
           throw std::runtime_error("MetaRing.push: a reader is " + std::to_string(h_->nslots) +
                                    " messages behind and made no progress");
+        if ((++it & 1023) == 0 && first_fault() >= 0)
+          throw std::runtime_error("MetaRing.push: a reader failed (see faults())");
       }
     }
     SlotHdr* s = slot(k % h_->nslots);
@@ -172,8 +202,8 @@ class MetaRing {
     h_->written.store(k + 1, std::memory_order_release);
   }
 
-  // Reader `r`: the next message as int32 (None if the producer closed the ring).  Waits with the GIL
-  // released; raises TimeoutError after `timeout_s` (< 0: wait forever).
+  // Reader `r`: the next message as int32 (None once the producer closed the ring AND it is drained).
+  // Waits with the GIL released; raises TimeoutError after `timeout_s` (< 0: wait forever).
   py::object pop(int64_t r, double timeout_s) {
     check_open();
     if (r < 0 || (uint64_t)r >= h_->readers) throw std::invalid_argument("MetaRing.pop: bad reader index");
@@ -183,9 +213,13 @@ class MetaRing {
     {
       py::gil_scoped_release nogil;
       Backoff bo(0.005);
+      int it = 0;
       while (s->seq.load(std::memory_order_acquire) != k + 1) {
-        if (h_->closed.load(std::memory_order_acquire)) {
-          closed = true;
+        const bool gone = (++it & 1023) == 0 && !pid_alive(h_->wpid.load(std::memory_order_relaxed));
+        if (gone || h_->closed.load(std::memory_order_acquire)) {
+          // the producer may have published message k between our seq load and its shut(): the closed
+          // flag was stored after that seq (release), so this acquire re-load sees it if it exists
+          closed = s->seq.load(std::memory_order_acquire) != k + 1;
           break;
         }
         if (bo.wait() > timeout_s && timeout_s >= 0) {
@@ -194,7 +228,10 @@ class MetaRing {
         }
       }
     }
-    if (timed_out) throw py::value_error("MetaRing.pop: timed out");
+    if (timed_out) {
+      PyErr_SetString(PyExc_TimeoutError, "MetaRing.pop: timed out");
+      throw py::error_already_set();
+    }
     if (closed) return py::none();
     const uint32_t n = s->bytes;
     py::array_t<int32_t> out((py::ssize_t)(n / 4));
@@ -207,6 +244,35 @@ class MetaRing {
   void shut() {
     check_open();
     h_->closed.store(1, std::memory_order_release);
+  }
+
+  // Register this process as reader r (r < 0: the producer) for the liveness checks.
+  void register_pid(int64_t r, int64_t pid) {
+    check_open();
+    if (r < 0) {
+      h_->wpid.store((int32_t)pid, std::memory_order_release);
+      return;
+    }
+    if ((uint64_t)r >= h_->readers) throw std::invalid_argument("MetaRing.register_pid: bad reader index");
+    h_->rpid[r].store((int32_t)pid, std::memory_order_release);
+  }
+
+  // Reader r reports a failure (code != 0) to the producer before it exits.
+  void report(int64_t r, int64_t code) {
+    check_open();
+    if (r < 0 || (uint64_t)r >= h_->readers) throw std::invalid_argument("MetaRing.report: bad reader index");
+    h_->rerr[r].store(code ? (int32_t)code : 1, std::memory_order_release);
+  }
+
+  // Producer: [(reader, code)] of every faulted reader: its reported code, or -1 if its process is gone.
+  py::list faults() const {
+    check_open();
+    py::list out;
+    for (uint64_t r = 0; r < h_->readers; ++r) {
+      const int code = fault_of(r);
+      if (code != 0) out.append(py::make_tuple((int64_t)r, (int64_t)code));
+    }
+    return out;
   }
 
   void unlink() {
@@ -224,6 +290,16 @@ class MetaRing {
  private:
   SlotHdr* slot(uint64_t i) const {
     return reinterpret_cast<SlotHdr*>(base_ + sizeof(Header) + i * slot_stride_);
+  }
+  int fault_of(uint64_t r) const {
+    const int code = h_->rerr[r].load(std::memory_order_acquire);
+    if (code != 0) return code;
+    return pid_alive(h_->rpid[r].load(std::memory_order_acquire)) ? 0 : -1;
+  }
+  int first_fault() const {
+    for (uint64_t r = 0; r < h_->readers; ++r)
+      if (fault_of(r) != 0) return (int)r;
+    return -1;
   }
   uint64_t min_read() const {
     uint64_t m = UINT64_MAX;
@@ -255,6 +331,9 @@ PYBIND11_MODULE(_runtime, m) {
       .def("push", &MetaRing::push, py::arg("buf"), py::arg("timeout_s") = 60.0)
       .def("pop", &MetaRing::pop, py::arg("reader"), py::arg("timeout_s") = -1.0)
       .def("shut", &MetaRing::shut)
+      .def("register_pid", &MetaRing::register_pid, py::arg("reader"), py::arg("pid"))
+      .def("report", &MetaRing::report, py::arg("reader"), py::arg("code"))
+      .def("faults", &MetaRing::faults)
       .def("unlink", &MetaRing::unlink)
       .def("release", &MetaRing::release)
       .def_property_readonly("slot_bytes", &MetaRing::slot_bytes)

@@ -55,7 +55,7 @@ def _init_config(path: str, native: bool) -> int:
     return 0
 
 
-async def _run_provider(cfg: ConfigManager, bootstrap, engine=None) -> None:
+async def _run_provider(cfg: ConfigManager, bootstrap, engine=None) -> int:
     from .backends.native import NativeBackend
     from .provider.node import SymmetryProvider
 
@@ -63,6 +63,7 @@ async def _run_provider(cfg: ConfigManager, bootstrap, engine=None) -> None:
     prov = SymmetryProvider(cfg, backend=backend, bootstrap=bootstrap, install_signal_handlers=True)
     await prov.init()
     await prov.wait_closed()
+    return prov.exit_code
 
 
 def _distributed_engine(cfg: ConfigManager):
@@ -78,9 +79,23 @@ def _distributed_engine(cfg: ConfigManager):
     engine, rank = init_tp_engine(ecfg)
     _exit_when_orphaned()
     if rank != 0:
-        engine.runner.worker_loop()
+        try:
+            engine.runner.worker_loop()  # reports a failure to rank 0 over the metadata ring before raising
+        except BaseException:
+            import traceback
+
+            traceback.print_exc()
+            _hard_exit(1)
         sys.exit(0)
     return engine
+
+
+def _hard_exit(code: int) -> None:
+    """Leave without interpreter teardown: the process-group / communicator destructors can block forever on a
+    peer that is gone (fault containment: the supervisor restarts the ranks)."""
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(code)
 
 
 def _exit_when_orphaned(period_s: float = 1.0) -> None:
@@ -247,11 +262,14 @@ def main(argv=None) -> int:
         return _launch_tp(cfg, args.config, args.bootstrap)
     if world > 1 and cfg.is_native:
         engine = _distributed_engine(cfg)
+    code = 0
     try:
-        asyncio.run(_run_provider(cfg, args.bootstrap, engine))
+        code = asyncio.run(_run_provider(cfg, args.bootstrap, engine)) or 0
     except KeyboardInterrupt:
         pass
-    return 0
+    if engine is not None and (code or engine.fatal is not None):
+        _hard_exit(code or 1)  # a TP peer is gone: do not wait on its collectives / process group at teardown
+    return code
 
 
 def server_main(argv=None) -> int:

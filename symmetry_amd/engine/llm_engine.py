@@ -57,8 +57,6 @@ class EngineConfig:
     pipeline: bool = True                # enqueue decode step N+1 before step N's tokens reach the host
     mixed_prefill_tokens: int = 512      # prompt-chunk budget of steps that also carry decodes
     decode_weights: str = "auto"         # "preshuffled" | "shared" | "auto": extra MFMA-ordered decode copies
-    persistent_mlp: bool = False         # O -> gate_up -> down as one persistent launch (measured slower: profiles/)
-    fused_attn_block: bool = False       # QKV -> attention -> O as one launch per layer (decode_block)
     enable_prefix_caching: bool = True   # adopt cached KV blocks of a known prompt prefix (multi-turn chats)
     # a burst of >= 4 prompts totalling >= this many tokens, arriving while nothing decodes, prefills its
     # first n // 2 + 1 prompts in one step and the rest in the next (0 = one step for the whole burst)
@@ -84,7 +82,6 @@ class EngineConfig:
              "device": "device",
              "useGraphs": "use_graphs", "numKvBlocks": "num_kv_blocks", "decodeWeights": "decode_weights",
              "prefillChunk": "mixed_prefill_tokens",
-             "persistentMlp": "persistent_mlp", "fusedAttnBlock": "fused_attn_block",
              "enablePrefixCaching": "enable_prefix_caching", "burstSplitTokens": "burst_split_tokens",
              "arrivalQuietUs": "arrival_quiet_us", "arrivalWindowUs": "arrival_window_us"}
         for k, attr in m.items():
@@ -141,8 +138,7 @@ class LLMEngine:
         self.weights: ModelWeights = weights
         self.load_time = time.perf_counter() - t0
         self.model = TransformerLM(weights, self.device, tp_comm=tp_comm, ep_comm=ep_comm,
-                                   max_decode_ctx=max_model_len, decode_weights=cfg.decode_weights,
-                                   persistent_mlp=cfg.persistent_mlp, fused_attn_block=cfg.fused_attn_block)
+                                   max_decode_ctx=max_model_len, decode_weights=cfg.decode_weights)
         self.tokenizer = load_tokenizer(mcfg, cfg.tokenizer or (cfg.weights if cfg.weights != "random" else None))
         nb = cfg.num_kv_blocks or self._auto_blocks(max_model_len)
         self.kv = KVCache(mcfg.num_layers, nb, mcfg.num_kv_heads // cfg.tp_size, mcfg.head_dim, cfg.block_size,
@@ -171,6 +167,12 @@ class LLMEngine:
         self._profiler = None
         self._profile_left = int(os.environ.get("SYMMETRY_PROFILE_STEPS", "20"))
         self.profile_trace: str | None = None
+        # fault containment (tensor parallel): once a peer rank is lost the engine cannot compute any step; it
+        # fails every request and refuses new ones, and its listeners (the backend -> the provider) take the
+        # provider offline (parallel/health.py)
+        self.fatal: str | None = None
+        self.health = None  # rank 0's TPHealthMonitor (parallel/launch.py), if any
+        self._fatal_listeners: list = []
 
     # ------------------------------------------------------------------------------------------
     @staticmethod
@@ -217,10 +219,53 @@ class LLMEngine:
         budget = max(0, int((free - reserve) * self.cfg.kv_cache_fraction))
         return max(16, budget // per_block)
 
+    # ---- fault containment ----------------------------------------------------------------------
+    def add_fatal_listener(self, fn) -> None:
+        """``fn(message)`` once, when the engine becomes unusable (a TP peer was lost)."""
+        if self.fatal is not None:
+            fn(self.fatal)
+        else:
+            self._fatal_listeners.append(fn)
+
+    def declare_fatal(self, message: str) -> None:
+        """Any thread: the engine can no longer compute steps.  The engine thread fails every request at its next
+        step; the listeners run here, once."""
+        with self.lock:
+            if self.fatal is not None:
+                return
+            self.fatal = message
+            listeners, self._fatal_listeners = self._fatal_listeners, []
+        if self.health is not None:
+            self.health.declare(message)  # stops the device collectives if the monitor has not yet
+        for fn in listeners:
+            try:
+                fn(message)
+            except Exception:  # noqa: BLE001
+                traceback.print_exc()
+
+    def _fail_all(self, message: str) -> list[RequestOutput]:
+        """Fail every known request (running, waiting, in flight) with an error output."""
+        outs = []
+        with self.lock:
+            self._inflight = None
+            for rid, (seq, _, cb) in list(self.requests.items()):
+                if not seq.status.finished:
+                    self.metrics.on_abort(error=True)
+                    self.scheduler.finish(seq, SeqStatus.FINISHED_ERROR)
+                out = RequestOutput(rid, [], "", True, "error", error=message, seq=seq)
+                outs.append(out)
+                self._emit(cb, out)
+            self.requests.clear()
+            for seq in list(self.scheduler.running) + list(self.scheduler.waiting):
+                self.scheduler.finish(seq, SeqStatus.FINISHED_ERROR)
+        return outs
+
     def add_request(self, request_id: str, prompt_ids: list, params: SamplingParams | None = None,
                     callback=None, cache_scope: bytes = b"") -> Sequence:
         """``cache_scope``: prefix-cache namespace (the provider passes the client's public key, so one
         client's conversation reuses only its own cached KV blocks)."""
+        if self.fatal is not None:
+            raise RuntimeError(f"engine unavailable: {self.fatal}")
         params = params or SamplingParams(max_tokens=self.cfg.default_max_tokens)
         seq = Sequence(request_id, list(prompt_ids), params, eos_ids=tuple(self.model_cfg.eos_token_ids),
                        cache_scope=bytes(cache_scope))
@@ -268,6 +313,8 @@ class LLMEngine:
         step N.  Host scheduling, detokenization and the provider's socket writes thus overlap the GPU,
         which never idles between decode steps.  A sequence that stops at step N has already been
         given one extra step; that token is discarded (its KV blocks are released in stream order)."""
+        if self.fatal is not None:
+            return self._fail_all(self.fatal) if self.requests or self.scheduler.has_work() else []
         t_sched = time.perf_counter()
         prev = self._inflight
         if prev is not None:
@@ -295,9 +342,17 @@ class LLMEngine:
         return self._inflight is not None
 
     def _fail(self, batch, exc) -> list[RequestOutput]:
-        """Engine watchdog: fail the requests of a step that raised, keep serving the others."""
+        """Engine watchdog: fail the requests of a step that raised, keep serving the others -- unless the step
+        lost a tensor-parallel peer: then no later step can succeed either (fault containment)."""
+        from ..parallel.health import TPFaultError
+
         msg = f"{type(exc).__name__}: {exc}"
         traceback.print_exc()
+        if self.health is not None and self.fatal is None:
+            self.health.check()  # a collective that raised (gloo: peer socket closed) -- is a peer gone?
+        if isinstance(exc, TPFaultError) or self.fatal is not None:
+            self.declare_fatal(self.fatal or str(exc))
+            return self._fail_all(self.fatal)
         outs = []
         with self.lock:
             for seq in batch.seqs:
@@ -479,6 +534,12 @@ class AsyncEngine:
     def _loop(self) -> None:
         idle = True
         while not self._stop:
+            if self.engine.fatal is not None:  # fault containment: fail whatever is left, then serve nothing
+                self.engine.step()
+                self._flush()
+                self._wake.wait(0.05)
+                self._wake.clear()
+                continue
             if not self.engine.has_unfinished():
                 idle = True
                 self._wake.wait(0.05)

@@ -319,7 +319,9 @@ class ModelRunner:
             ids = handle["pin"].tolist()
             check = getattr(self.model.tp, "error", None)  # xGMI collectives: host-mapped word, no sync
             if check is not None and check():
-                raise RuntimeError("xGMI all-reduce: a peer rank never signalled within the wait limit; "
+                from ..parallel.health import TPFaultError
+
+                raise TPFaultError("xGMI collective: a tensor-parallel peer never signalled (or was declared lost); "
                                    "this step's outputs are invalid")
         else:
             ids = handle["ids"]
@@ -447,6 +449,18 @@ class ModelRunner:
         collectives keep the ranks in step on the device).  A collective that gave up waiting for a peer
         (the communicator's host-mapped error word) ends the worker with an error: its partial sums would
         be garbage."""
+        try:
+            self._worker_loop()
+        except BaseException as exc:
+            # tell rank 0 at once over the ring's back-channel (its health monitor fails the provider), then die
+            code = 2 if isinstance(exc, KeyboardInterrupt) else 3
+            try:
+                self.meta.report(code)
+            except Exception:  # noqa: BLE001
+                pass
+            raise
+
+    def _worker_loop(self) -> None:
         check = getattr(self.model.tp, "error", None)
         while True:
             msg = self.meta.recv()
@@ -474,4 +488,6 @@ class ModelRunner:
                 continue
             err = check() if check is not None else 0
             if err:
-                raise RuntimeError(f"TP rank {self.tp_rank}: xGMI collective timed out waiting for rank {err - 1}")
+                from ..parallel.health import TPFaultError
+
+                raise TPFaultError(f"TP rank {self.tp_rank}: xGMI collective gave up waiting for rank {err - 1}")

@@ -101,8 +101,11 @@ class BlockManager:
         """Adopt the cached blocks of the longest matching full-block prefix of a sequence that has no
         KV yet; returns the number of tokens whose prefill is skipped.  At least one prompt token is
         always left to compute (its logits give the first output token)."""
-        if not self.prefix_caching or seq.block_table or seq.num_computed:
+        if not self.prefix_caching or seq.block_table or seq.num_computed or seq.prefix_checked:
             return 0
+        # once per fresh KV state (again after a preemption): a miss is not re-queried on every schedule(),
+        # which kept the hit-rate denominator growing while a prompt waited
+        seq.prefix_checked = True
         tokens = seq.token_ids
         target = seq.prefill_target
         nfull = max(0, target - 1) // self.block_size  # >= 1 token left to prefill
@@ -347,6 +350,7 @@ class Scheduler:
     def _preempt(self, seq: Sequence) -> None:
         self.blocks.release(seq)
         seq.num_computed = 0
+        seq.prefix_checked = False
         seq.num_preemptions += 1
         seq.status = SeqStatus.WAITING
         if seq in self.running:

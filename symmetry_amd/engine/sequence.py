@@ -83,6 +83,7 @@ class Sequence:
     sampling_seed: int = 0
     output_text: str = ""
     cache_scope: bytes = b""       # prefix-cache namespace (client identity)
+    prefix_checked: bool = False   # the prefix cache was consulted for the current (fresh) KV state
 
     @property
     def token_ids(self) -> list:

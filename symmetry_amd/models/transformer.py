@@ -61,9 +61,6 @@ SPLITK_RESID_ROWS = int(os.environ.get("SYMMETRY_SPLITK_RESID_ROWS", "24"))
 # Decode batches are padded to buckets (.., 16, 24, ..), so 17..24-row steps run as 24.  0 disables.
 GENERAL_ROWS = int(os.environ.get("SYMMETRY_GENERAL_ROWS", "20"))  # profiles/general_rows_ab_r2.jsonl
 MAX_STEP_SEQS = 4096  # sequences per step (rows of last_ids)
-# extra workgroups of the decode attention launch that stream the O weight into the Infinity Cache
-# (0 = off; csrc/kernels/attention.hip, mall_prefetch)
-ATTN_PREFETCH_WGS = int(os.environ.get("SYMMETRY_ATTN_PREFETCH", "0"))
 # decode steps on the general path run rope_cache's per-row form (A/B knob)
 ROPE_DECODE_ROWS = os.environ.get("SYMMETRY_ROPE_DECODE_ROWS", "1") != "0"
 # general path (20-256 rows): which projections run on mgemm with the fused decode epilogue (in-launch split-K
@@ -76,12 +73,6 @@ ROPE_DECODE_ROWS = os.environ.get("SYMMETRY_ROPE_DECODE_ROWS", "1") != "0"
 MG_FUSED_MODE = os.environ.get("SYMMETRY_MG_FUSED", "gu")
 MG_FUSED = MG_FUSED_MODE in ("1", "all")
 MG_FUSED_GU = MG_FUSED_MODE == "gu"
-# projections of the FUSED decode path (below GENERAL_ROWS rows) that run on mgemm with their epilogue
-# instead of the decode GEMM (comma list of qkv, o, gu, down; A/B knob)
-MG_PROJ = tuple(p for p in os.environ.get("SYMMETRY_MG_PROJ", "").split(",") if p)
-# fused decode path: QKV + decode attention as one launch, the attention units on the CUs the QKV grid leaves
-# idle (csrc/kernels/decode_gemm.hip, decode_qkv_attn_kernel)
-QKV_ATTN = os.environ.get("SYMMETRY_QKV_ATTN", "0") == "1"
 # MFMA-preshuffled copy of the lm_head for the fused decode path's dg_argmax (1 KB per wave load like the layer
 # weights; +1 GB for Llama-3-8B): SYMMETRY_LMHEAD_SHUF=0 keeps the row-major stream
 LMHEAD_SHUF = os.environ.get("SYMMETRY_LMHEAD_SHUF", "1") != "0"
@@ -165,7 +156,7 @@ class Workspace:
 
 class TransformerLM:
     def __init__(self, weights: ModelWeights, device, tp_comm=None, ep_comm=None, max_decode_ctx: int | None = None,
-                 decode_weights: str = "auto", persistent_mlp: bool = False, fused_attn_block: bool = False):
+                 decode_weights: str = "auto"):
         self.cfg: ModelConfig = weights.cfg
         self.w = weights
         self.device = torch.device(device)
@@ -197,8 +188,6 @@ class TransformerLM:
         if self.device.type != "cpu":
             ops.decode_ks_ws(self.device)  # allocated before any graph capture (stable address)
         self.dgw = self._decode_copies(decode_weights)
-        self.persistent_mlp = persistent_mlp
-        self.fused_attn_block = fused_attn_block
         self.tp_reduced_bytes: dict[str, int] = {}  # bytes per rank of the last general-path all-reduce
 
     def _decode_copies(self, mode: str) -> dict:
@@ -213,11 +202,14 @@ class TransformerLM:
         head = self.w["lm_head"] if LMHEAD_SHUF else None
         if head is not None and (head.shape[0] % 16 or head.shape[1] % 32):
             head = None
-        extra += head.numel() * 2 if head is not None else 0
         if mode == "auto":
-            free, total = torch.cuda.mem_get_info(self.device)
-            if extra > 0.4 * free:
+            # the layer copies first (-9 % per layer); the head copy (~1 GB for Llama-3-8B, -12 % of one lm_head
+            # launch) only from what the same budget has left, so it never costs a model its layer copies
+            budget = 0.4 * torch.cuda.mem_get_info(self.device)[0]
+            if extra > budget:
                 return {}
+            if head is not None and extra + head.numel() * 2 > budget:
+                head = None
         from .layout import preshuffle
 
         out = {}
@@ -228,26 +220,11 @@ class TransformerLM:
             out[(-1, "lm_head")] = preshuffle(head)
         return out
 
-    def _persistent_mlp_ok(self, T: int) -> bool:
-        """decode_mlp preconditions: single GPU dense model, <= 16 rows, K dims % 512, one weight layout."""
-        if not self.persistent_mlp or self.cfg.is_moe or self._tp_active() or T > 16:
-            return False
-        d, dq = self.cfg.hidden_size, self.hq * self.D
-        F = self.w.layer(0, "w_gu").shape[0] // 2
-        if d % 512 or dq % 512 or F % 512:
-            return False
-        shs = {self._dgw(0, n)[1] for n in ("wo", "w_gu", "w_down")}
-        return len(shs) == 1
-
-    def _attn_block_ok(self, b: ForwardBatch) -> bool:
-        """decode_block preconditions: a pure decode step on one GPU, <= 16 rows, GQA group <= 8, K dims
-        % 512, QKV and O in one weight layout."""
-        if not self.fused_attn_block or b.kind != "decode" or self._tp_active() or b.num_tokens > 16:
-            return False
-        d, dq = self.cfg.hidden_size, self.hq * self.D
-        if d % 512 or dq % 512 or self.hq // self.hkv > 8:
-            return False
-        return self._dgw(0, "wqkv")[1] == self._dgw(0, "wo")[1]
+    def _lm_head(self, rows: int):
+        """(weight, wshuf) of the decode lm_head for a ``rows``-row sampling launch: the MFMA-preshuffled copy up
+        to 16 rows, the row-major stream's row-tile variants above (profiles/r3/lmhead_preshuffle_ab.jsonl: 1 row
+        189.5 -> 175.1 us, 6 rows 192.9 -> 168.8; 24 rows 222.6 vs 232.3, 32 rows 220 vs 228; 64 rows even)."""
+        return self._dgw(-1, "lm_head") if rows <= 16 else (self.w["lm_head"], False)
 
     def _dgw(self, i: int, name: str):
         """(weight, wshuf) for decode GEMM `name` of layer i (i = -1: the lm_head)."""
@@ -308,27 +285,14 @@ class TransformerLM:
         return y
 
     # ------------------------------------------------------------------------------------------
-    def _qkv_attn(self, b: ForwardBatch, kv: KVCache, i: int, xw, wq, ss, eps, q, attn) -> bool:
-        """QKV projection + decode attention of layer i as one launch (ops.qkv_attn); False: not applicable."""
-        span = b.block_tables.shape[1] * kv.block_size
-        max_parts = (span + ops.ATTN_DECODE_PART - 1) // ops.ATTN_DECODE_PART
-        tmp_o = self._buf("tmp_o", (b.num_seqs, self.hq, max_parts, self.D), torch.float32)
-        tmp_ml = self._buf("tmp_ml", (b.num_seqs, self.hq, max_parts, 2), torch.float32)
-        cnt = self.ws.get("attn_counters", (b.num_seqs * self.hkv,), torch.int32, self.device, zeros=True)
-        ctl = self.ws.get("qa_ctl", (ops.QKV_ATTN_CTL,), torch.int32, self.device, zeros=True)
-        return ops.qkv_attn(xw, wq, ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq,
-                            self.hkv, True, b.block_tables, b.ctx_lens, attn, tmp_o, tmp_ml, cnt, self.scale, ctl)
-
-    def _attention(self, b: ForwardBatch, kv: KVCache, i: int, q: torch.Tensor, attn: torch.Tensor,
-                   prefetch: torch.Tensor | None = None) -> None:
+    def _attention(self, b: ForwardBatch, kv: KVCache, i: int, q: torch.Tensor, attn: torch.Tensor) -> None:
         if b.kind == "decode":
             span = b.block_tables.shape[1] * kv.block_size
             max_parts = (span + ops.ATTN_DECODE_PART - 1) // ops.ATTN_DECODE_PART
             tmp_o = self._buf("tmp_o", (b.num_seqs, self.hq, max_parts, self.D), torch.float32)
             tmp_ml = self._buf("tmp_ml", (b.num_seqs, self.hq, max_parts, 2), torch.float32)
             cnt = self.ws.get("attn_counters", (b.num_seqs * self.hkv,), torch.int32, self.device, zeros=True)
-            ops.attn_decode(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, attn, tmp_o, tmp_ml, cnt, self.scale,
-                            prefetch, ATTN_PREFETCH_WGS if prefetch is not None else 0)
+            ops.attn_decode(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, attn, tmp_o, tmp_ml, cnt, self.scale)
         else:
             ops.attn_prefill(q, kv.k[i], kv.v[i], b.block_tables, b.ctx_lens, b.cu_q, b.tiles, attn, self.scale)
 
@@ -378,13 +342,10 @@ class TransformerLM:
     def _tp_active(self) -> bool:
         return self.tp is not None and self.tp_size > 1
 
-    def _resid_proj(self, name, x, Wsh, resid, w_next, xw, ss_t, ss_1, w_row=None, mg=None) -> torch.Tensor:
+    def _resid_proj(self, name, x, Wsh, resid, w_next, xw, ss_t, ss_1, w_row=None) -> torch.Tensor:
         """Row-parallel projection + residual add + next-norm prep; returns the ss partials to use."""
         W, sh = Wsh
         M = x.shape[0]
-        if mg is not None and sh and not self._tp_active():
-            ops.dg_resid(x, W, resid, w_next, xw, ss_t, wshuf=True, mg=mg)
-            return ss_t
         if w_row is not None and not self._tp_active() and 0 < SPLITK_RESID_ROWS <= M:
             N, K = w_row.shape
             y = self._buf(name + ".slab", (ops.choose_splits(N, K), M, N), torch.float32)
@@ -423,50 +384,15 @@ class TransformerLM:
         attn = self._buf("attn", (T, self.hq, self.D), torch.bfloat16)
         ops.embed_prep(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), xw, ss_1, b.src, self.last_ids)
         ss = ss_1
-        proj = MG_PROJ if not self._tp_active() else tuple(p for p in MG_PROJ if p in ("qkv", "gu"))
-        # (SYMMETRY_MG_PROJ picks these per projection, independent of the general path's SYMMETRY_MG_FUSED mode)
-        mgp = (self._mg_plan(b, proj, need_all=False, any_kind=b.kind == "decode") or {}) if proj else {}
-        persistent = self._persistent_mlp_ok(T)
-        ctl = self.ws.get("mlp_ctl", (ops.DECODE_MLP_CTL,), torch.int32, self.device, zeros=True) if persistent else None
-        block = self._attn_block_ok(b)
-        if block:
-            span = b.block_tables.shape[1] * kv.block_size
-            max_parts = (span + ops.ATTN_BLOCK_PART - 1) // ops.ATTN_BLOCK_PART
-            tmp_o = self._buf("tmp_o_blk", (b.num_seqs, self.hq, max_parts, self.D), torch.float32)
-            tmp_ml = self._buf("tmp_ml_blk", (b.num_seqs, self.hq, max_parts, 2), torch.float32)
-            cnt = self.ws.get("attn_counters", (b.num_seqs * self.hkv,), torch.int32, self.device, zeros=True)
-            bctl = self.ws.get("block_ctl", (ops.DECODE_BLOCK_CTL,), torch.int32, self.device, zeros=True)
         for i in range(cfg.num_layers):
             wq, shq = self._dgw(i, "wqkv")
             attn2d = attn.view(T, self.hq * self.D)
             nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
-            if block:
-                # QKV -> attention -> O + residual in one launch (csrc/kernels/decode_gemm.hip,
-                # decode_block_kernel): the O weight stream overlaps the attention phase
-                wo, _ = self._dgw(i, "wo")
-                ops.decode_block(xw, wq, ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i],
-                                 b.block_tables, b.ctx_lens, attn, tmp_o, tmp_ml, cnt, self.scale, wo, resid,
-                                 w.layer(i, "ln2"), xw, ss_t, bctl, wshuf=shq)
-                ss = ss_t
-            elif not (QKV_ATTN and b.kind == "decode" and shq and "qkv" not in mgp and ATTN_PREFETCH_WGS == 0
-                      and self._qkv_attn(b, kv, i, xw, wq, ss, eps, q, attn)):
-                ops.dg_qkv(xw, wq, ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq,
-                           self.hkv, wshuf=shq, mg=mgp.get("qkv") if shq else None)
-                # spare workgroups of the latency-bound attention launch pull the O weight into the
-                # Infinity Cache for the next launch
-                self._attention(b, kv, i, q, attn, self._dgw(i, "wo")[0] if ATTN_PREFETCH_WGS > 0 else None)
-            if persistent and not block:
-                # O -> gate_up/SwiGLU -> down in one persistent launch: each phase's weight stream starts
-                # while the previous phase finishes (csrc/kernels/decode_gemm.hip, decode_mlp_kernel)
-                (wo, sh), (w_gu, _), (w_dn, _) = self._dgw(i, "wo"), self._dgw(i, "w_gu"), self._dgw(i, "w_down")
-                act = self._buf("act", (T, w_gu.shape[0] // 2), torch.bfloat16)
-                ops.decode_mlp(attn2d, wo, w_gu, w_dn, resid, w.layer(i, "ln2"), nxt, xw, ss_t, act, ctl, eps,
-                               wshuf=sh)
-                ss = ss_t
-                continue
-            if not block:
-                ss = self._resid_proj("o", attn2d, self._dgw(i, "wo"), resid, w.layer(i, "ln2"), xw, ss_t, ss_1,
-                                     w.layer(i, "wo"), mg=mgp.get("o"))
+            ops.dg_qkv(xw, wq, ss, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq,
+                       self.hkv, wshuf=shq)
+            self._attention(b, kv, i, q, attn)
+            ss = self._resid_proj("o", attn2d, self._dgw(i, "wo"), resid, w.layer(i, "ln2"), xw, ss_t, ss_1,
+                                  w.layer(i, "wo"))
             if cfg.is_moe:
                 # router + experts are not decode GEMMs: materialise RMSNorm(resid) (one bf16 rounding)
                 xn = self._buf("x", (T, d), torch.bfloat16)
@@ -476,9 +402,9 @@ class TransformerLM:
             else:
                 w_gu, shg = self._dgw(i, "w_gu")
                 act = self._buf("act", (T, w_gu.shape[0] // 2), torch.bfloat16)
-                ops.dg_swiglu(xw, w_gu, ss, eps, act, wshuf=shg, mg=mgp.get("gu") if shg else None)
+                ops.dg_swiglu(xw, w_gu, ss, eps, act, wshuf=shg)
                 ss = self._resid_proj("down", act, self._dgw(i, "w_down"), resid, nxt, xw, ss_t, ss_1,
-                                     w.layer(i, "w_down"), mg=mgp.get("down"))
+                                      w.layer(i, "w_down"))
         n = b.num_seqs
         if b.kind == "decode":
             xl, sl = xw, ss
@@ -488,7 +414,7 @@ class TransformerLM:
         keys = self._buf("keys", (n,), torch.int64)
         tk = self._buf("tile_keys", (n * (self.vocab_shard // 16),), torch.int64)
         logits = self._buf("logits", (n, self.vocab_shard), torch.float32) if b.need_logits or b.filtered else None
-        head, hsh = self._dgw(-1, "lm_head")
+        head, hsh = self._lm_head(n)
         ops.dg_argmax(xl, head, sl, eps, b.temps, b.seeds, b.step, tk, keys, ids,
                       self.tp_rank * self.vocab_shard, logits, wshuf=hsh)
         return self._finish_sampling(b, ids, keys, logits)
@@ -585,10 +511,7 @@ class TransformerLM:
         if self.fused and n <= SKINNY_MAX_M:
             # the decode lm_head kernel (row-tile variants for wide batches), on already-normalised rows
             tk = self._buf("tile_keys", (n * ntiles,), torch.int64)
-            # preshuffled copy up to 16 rows; the row-major stream's row-tile variants win at 24-32 rows
-            # (profiles/r3/lmhead_preshuffle_ab.jsonl: 1 row 189.5 -> 175.1 us, 6 rows 192.9 -> 168.8, 24 rows
-            # 222.6 vs 232.3, 64 rows even)
-            head, hsh = self._dgw(-1, "lm_head") if n <= 16 else (self.w["lm_head"], False)
+            head, hsh = self._lm_head(n)
             ops.dg_argmax(xl, head, None, self.cfg.rms_eps, b.temps, b.seeds, b.step, tk, keys, ids,
                           self.tp_rank * self.vocab_shard, logits, wshuf=hsh)
             return self._finish_sampling(b, ids, keys, logits)

@@ -49,8 +49,6 @@ __all__ = [
     "add_prep",
     "rownorm",
     "sample_filtered",
-    "decode_mlp",
-    "qkv_attn",
     "linear",
     "lib_splits",
     "linear_splitk",
@@ -97,14 +95,12 @@ def rope_cache(qkv, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv,
 ATTN_DECODE_PART = 256  # context tokens per split-KV partition of attn_decode (csrc/kernels/attn_decode.h PART)
 
 
-def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters, scale,
-                prefetch=None, prefetch_wgs=0):
+def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters, scale):
     """Split-KV paged decode attention.  ``counters``: int32 [>= num_seqs * Hkv], zero-initialised once;
-    the kernel re-arms it (graph-replay safe).  ``prefetch``: a tensor (the next launch's weight) that
-    ~``prefetch_wgs`` extra workgroups of the launch stream into the Infinity Cache (GPU only)."""
+    the kernel re-arms it (graph-replay safe)."""
     if _gpu(q):
         return _native.ops().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, counters,
-                                         float(scale), prefetch, int(prefetch_wgs))
+                                         float(scale))
     return reference.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, out, tmp_o, tmp_ml, scale)
 
 
@@ -307,53 +303,6 @@ def moe_combine(y, dst, ids, e_lo, e_hi, w, k, out, accumulate=False):
     if _gpu(out):
         return _native.ops().moe_combine(y, dst, ids, int(e_lo), int(e_hi), w, int(k), out, bool(accumulate))
     return reference.moe_combine(y, dst, ids, e_lo, e_hi, w, k, out, accumulate)
-
-
-DECODE_MLP_CTL = 4224  # csrc/kernels/launchers.h DECODE_MLP_CTL_INTS
-QKV_ATTN_CTL = 2176  # csrc/kernels/launchers.h QKV_ATTN_CTL_INTS
-
-
-def qkv_attn(x, W, ss_in, eps, positions, slots, cos_sin, q, k_cache, v_cache, Hq, Hkv, wshuf, block_tables,
-             ctx_lens, attn, tmp_o, tmp_ml, counters, scale, ctl) -> bool:
-    """dg_qkv + attn_decode as ONE launch (csrc/kernels/decode_gemm.hip, decode_qkv_attn_kernel): the attention
-    units run on the CUs the x-resident QKV grid leaves idle.  Returns False -- nothing enqueued -- where the
-    fused form does not apply (CPU, shapes, the attention form the standalone launch would pick); the caller
-    then runs the two ops.  ``ctl``: int32[QKV_ATTN_CTL] zero-initialised once (re-armed by the kernel)."""
-    if not _gpu(x):
-        return False
-    return bool(_native.ops().qkv_attn(x, W, ss_in, float(eps), positions, slots, cos_sin, q, k_cache, v_cache,
-                                       int(Hq), int(Hkv), bool(wshuf), block_tables, ctx_lens, attn, tmp_o, tmp_ml,
-                                       counters, float(scale), ctl))
-DECODE_BLOCK_CTL = 1024  # csrc/kernels/launchers.h DECODE_BLOCK_CTL_INTS
-ATTN_BLOCK_PART = 256  # tokens per split-KV partition inside decode_block (csrc/kernels/attn_decode.h PART_F)
-
-
-def decode_mlp(attn, Wo, Wgu, Wd, resid, ln2, w_next, xw, ss, act, ctl, eps, wshuf=False):
-    """Persistent O-proj -> gate_up/SwiGLU -> down block (one launch, M <= 16): the same result as
-    dg_resid(O) + dg_swiglu + dg_resid(down).  ``ctl``: int32[DECODE_MLP_CTL] zero-initialised once
-    (re-armed by the kernel; a non-zero word after a launch flags a dependency wait that gave up)."""
-    if _gpu(attn):
-        return _native.ops().decode_mlp(attn, Wo, Wgu, Wd, resid, ln2, w_next, xw, ss, act, ctl, float(eps),
-                                        bool(wshuf))
-    return reference.decode_mlp(attn, reference.unshuffled(Wo, wshuf), reference.unshuffled(Wgu, wshuf),
-                                reference.unshuffled(Wd, wshuf), resid, ln2, w_next, xw, ss, act, eps)
-
-
-def decode_block(xw, Wqkv, ss_in, eps, positions, slots, cos_sin, q, k_cache, v_cache, block_tables, ctx_lens,
-                 attn, tmp_o, tmp_ml, counters, scale, Wo, resid, ln2, xw_out, ss_out, ctl, wshuf=False):
-    """Fused decode attention block (one launch, M <= 16): the same result as dg_qkv + attn_decode +
-    dg_resid(O).  ``ctl``: int32[DECODE_BLOCK_CTL] zero-initialised once (re-armed by the kernel; word
-    ``(Hkv + 9) * 32`` non-zero after a launch flags a dependency wait that gave up)."""
-    if _gpu(xw):
-        return _native.ops().decode_block(xw, Wqkv, ss_in, float(eps), positions, slots, cos_sin, q, k_cache, v_cache,
-                                          block_tables, ctx_lens, attn, tmp_o, tmp_ml, counters, float(scale), Wo,
-                                          resid, ln2, xw_out, ss_out, ctl, bool(wshuf))
-    Hkv = k_cache.shape[1]
-    Hq = Wqkv.shape[0] // 128 - 2 * Hkv
-    reference.dg_qkv(xw, reference.unshuffled(Wqkv, wshuf), ss_in, eps, positions, slots, cos_sin, q, k_cache,
-                     v_cache, Hq, Hkv)
-    reference.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, attn, tmp_o, tmp_ml, scale)
-    reference.dg_resid(attn.view(attn.shape[0], -1), reference.unshuffled(Wo, wshuf), resid, ln2, xw_out, ss_out)
 
 
 def sample_filtered(logits, temps, top_k, top_p, seeds, step, out_ids):

@@ -484,10 +484,3 @@ def sample_filtered(logits, temps, top_k, top_p, seeds, step, out_ids) -> None:
         v = l / t - torch.log(-torch.log(u.to(l.device)))
         v = torch.where(l >= thr, v, torch.full_like(v, -float("inf")))
         out_ids[r] = int(torch.argmax(v))
-
-
-def decode_mlp(attn, Wo, Wgu, Wd, resid, ln2, w_next, xw, ss, act, eps) -> None:
-    """O-proj + residual + ln2 prep -> gate_up + SwiGLU -> down + residual + next-norm prep."""
-    dg_resid(attn, Wo, resid, ln2, xw, ss)
-    dg_swiglu(xw, Wgu, ss, eps, act)
-    dg_resid(act, Wd, resid, w_next, xw, ss)

@@ -249,9 +249,14 @@ class XgmiComm(Comm):
         self.inner.broadcast(t, src)
 
     def error(self) -> int:
-        """1 + the source rank a collective gave up waiting for since the last call, else 0 (cleared on read;
-        host-mapped, so it costs no device synchronisation: the model runner polls it after every step)."""
+        """1 + the source rank a collective gave up waiting for (or the code the host declared), else 0.  Sticky
+        (the communicator stays failed); host-mapped, so it costs no device synchronisation: the model runner
+        polls it after every step."""
         return int(self.ops.xgmi_error(self.handle))
+
+    def set_error(self, code: int) -> None:
+        """Declare a fault from the host (rank 0's health monitor): every spinning collective stops waiting."""
+        self.ops.xgmi_set_error(self.handle, int(code))
 
     def destroy(self, inner_too: bool = True):
         if self.handle is not None:

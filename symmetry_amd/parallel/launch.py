@@ -109,4 +109,12 @@ def init_tp_engine(ecfg):
     if on_gpu:
         ecfg.device = f"cuda:{local}"
     engine = LLMEngine(ecfg, tp_comm=comm, ep_comm=ep_comm, cpu_group=cpu_group)
+    if rank == 0 and world > 1:
+        # fault containment: a lost worker takes the provider offline within ~0.1 s (parallel/health.py)
+        from .health import TPHealthMonitor
+
+        engine.health = TPHealthMonitor(engine.runner.meta, comm,
+                                        period_s=float(os.environ.get("SYMMETRY_HEALTH_PERIOD_S", "0.1")))
+        engine.health.add_listener(engine.declare_fatal)
+        engine.health.start()
     return engine, rank

@@ -33,6 +33,14 @@ class MetaPlane:
     def close(self) -> None:
         pass
 
+    def faults(self) -> list:
+        """Rank 0: [(worker rank, code)] of workers that reported a failure (code > 0) or whose process is
+        gone (code -1).  The gloo plane has no back-channel: its broadcasts raise on a dead peer instead."""
+        return []
+
+    def report(self, code: int) -> None:
+        """Worker: tell rank 0 this rank failed (before it exits)."""
+
 
 class GlooMetaPlane(MetaPlane):
     def __init__(self, group, header_len: int):
@@ -72,6 +80,9 @@ class ShmMetaPlane(MetaPlane):
         dist.barrier(group=group)
         if rank == 0:
             self.ring.unlink()  # every rank has it mapped: no name left behind in /dev/shm
+        # liveness back-channel: rank 0 polls the workers' pids / error words (faults()), workers rank 0's pid
+        self.ring.register_pid(rank - 1, os.getpid())
+        dist.barrier(group=group)
         self._buf = np.zeros(1024, dtype=np.int32)
 
     def send(self, header, payload):
@@ -94,6 +105,13 @@ class ShmMetaPlane(MetaPlane):
     def close(self):
         if self.rank == 0:
             self.ring.shut()
+
+    def faults(self):
+        return [(int(r) + 1, int(c)) for r, c in self.ring.faults()]
+
+    def report(self, code: int) -> None:
+        if self.rank > 0:
+            self.ring.report(self.rank - 1, int(code) or 1)
 
 
 def make_metaplane(group, rank: int, world: int, header_len: int, slot_bytes: int) -> MetaPlane:

@@ -96,6 +96,11 @@ class SymmetryProvider:
         self.completed = 0
         self.saved_files: list[str] = []
         self._stopped = asyncio.Event()
+        # fault containment: 0 = healthy / orderly shutdown; 1 = the backend lost its engine (e.g. a tensor-
+        # parallel rank died): the provider left the server and the CLI exits with this code
+        self.exit_code = 0
+        self.fatal: str | None = None
+        self._closing = False
 
     # ------------------------------------------------------------------------------------------
     @property
@@ -138,11 +143,14 @@ class SymmetryProvider:
             self.stats, interval_s=float(cfg.get("metricsInterval", 60) or 0),
             path=cfg.get("metricsFile"), log=lambda line: logger.info(f"📊 {line}"))
         self.metrics_reporter.start()
+        add_fatal = getattr(self.backend, "add_fatal_listener", None)
+        if add_fatal is not None:
+            add_fatal(self._on_backend_fatal)
         if self.install_signal_handlers:
             loop = asyncio.get_running_loop()
             for sig in (signal.SIGINT, signal.SIGTERM):
                 try:
-                    loop.add_signal_handler(sig, lambda: asyncio.ensure_future(self.destroy()))
+                    loop.add_signal_handler(sig, lambda: asyncio.ensure_future(self.shutdown("provider shutting down")))
                 except (NotImplementedError, RuntimeError):
                     pass
 
@@ -304,6 +312,45 @@ class SymmetryProvider:
                 await gen.aclose()
 
     # ------------------------------------------------------------------------------------------
+    def _on_backend_fatal(self, message: str) -> None:
+        """The backend can no longer serve (a tensor-parallel peer died): every open stream has already been
+        ended with the error event + ``inferenceEnded`` (deviation 9); leave the server so no client is assigned
+        here any more, and stop with a non-zero exit code for the supervisor (the reference would keep answering
+        pings, ``src/provider.ts:124-126``, while every request failed)."""
+        logger.error(f"🚨 {message}")
+        self.fatal = message
+        self.exit_code = 1
+        asyncio.ensure_future(self.shutdown(None))
+
+    def _send_leave(self) -> None:
+        peer = self._server_peer
+        if peer is not None and getattr(peer, "writable", False):
+            peer.write(create_message(Keys.LEAVE, {"discoveryKey": self._discovery_key.hex()
+                                                   if self._discovery_key else None, "reason": self.fatal}))
+
+    async def shutdown(self, message: str | None) -> None:
+        """Orderly stop (signal or fault): end open streams with an error event + ``inferenceEnded`` (``message``;
+        None: already ended by the backend), send ``leave`` to the server, let those writes drain, destroy."""
+        if self._closing:
+            return
+        self._closing = True
+        probe = getattr(self.backend, "health_fault", None)
+        fault = probe() if (probe is not None and self.fatal is None) else None
+        if fault:  # e.g. SIGTERM from torchrun after a worker rank died: that is a fault, not a clean stop
+            logger.error(f"🚨 {fault}")
+            self.fatal, self.exit_code = fault, 1
+            message = f"provider unavailable: {fault}"
+        fail = getattr(self.backend, "fail_active", None)
+        n = fail(message) if (fail is not None and message) else 0
+        self._send_leave()
+        if n or self._tasks or self.fatal:
+            # the streams' error events + inferenceEnded are written by their own tasks: give them the loop
+            deadline = asyncio.get_running_loop().time() + 2.0
+            while self._tasks and asyncio.get_running_loop().time() < deadline:
+                await asyncio.sleep(0.02)
+            await asyncio.sleep(0.1)  # the encrypted writes (and leave) leave the socket buffers
+        await self.destroy()
+
     def stats(self) -> dict:
         """Backend (engine) metrics merged with the provider's own counters."""
         d = dict(self.backend.stats())

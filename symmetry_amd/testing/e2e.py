@@ -51,7 +51,7 @@ def _client_proc(boot, server_key, model, n, prompt_tokens, max_tokens, out_q, s
                              timeout=600)
             return {"ttft_ms": None if r.ttft_s is None else r.ttft_s * 1e3, "tokens_per_s": r.tokens_per_s,
                     "events": r.content_events, "ended": r.ended, "error": r.error,
-                    "wall_s": r.t_end - r.t_start, "key": prompt_text(i, prompt_tokens)[:24],
+                    "wall_s": r.t_end - r.t_start, "client": i,
                     "t_write": r.t_start, "t_first": None if r.ttft_s is None else r.t_start + r.ttft_s}
         finally:
             await c.stop()
@@ -80,7 +80,7 @@ async def client_end_run(engine, model: str, clients: int, prompt_tokens: int = 
     """Serve ``engine`` as a provider and measure ``clients`` concurrent streamed chats at the client end."""
     import yaml
 
-    from ..backends.native import NativeBackend
+    from ..backends.native import NativeBackend, timing_key
     from ..net import DiscoveryServer
     from ..provider.node import SymmetryProvider
     from .mock_server import SymmetryServer
@@ -99,7 +99,7 @@ async def client_end_run(engine, model: str, clients: int, prompt_tokens: int = 
     path = os.path.join(tmp, "provider.yaml")
     with open(path, "w") as f:
         yaml.safe_dump(cfg, f)
-    provider = SymmetryProvider(path, backend=NativeBackend(cfg, engine=engine), bootstrap=boot)
+    provider = SymmetryProvider(path, backend=NativeBackend(cfg, engine=engine, record_timings=True), bootstrap=boot)
     await provider.init()
     for _ in range(200):
         if server.providers(model):
@@ -138,6 +138,8 @@ async def client_end_run(engine, model: str, clients: int, prompt_tokens: int = 
         await ds.stop()
     if isinstance(res, str):
         raise RuntimeError(res)
+    for r in res:  # the provider's timing key of each client's prompt (salted per process: computed here)
+        r["key"] = timing_key(prompt_text(r["client"], prompt_tokens))
     ttfts = sorted(r["ttft_ms"] for r in res if r["ttft_ms"] is not None)
     tps = [r["tokens_per_s"] for r in res]
     total_events = sum(r["events"] for r in res)

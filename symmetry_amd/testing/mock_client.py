@@ -86,7 +86,8 @@ class SymmetryClient:
 
     async def chat(self, conn, messages, emitter_key: str = "inference", timeout: float = 120.0,
                    extra: dict | None = None, new_conversation: bool = True, disconnect_after: int | None = None,
-                   slow_reader_s: float = 0.0) -> ChatResult:
+                   slow_reader_s: float = 0.0, on_chunk=None) -> ChatResult:
+        """``on_chunk(result)``: called after every streamed message (fault-injection tests act mid-stream)."""
         res = ChatResult()
         q: asyncio.Queue = asyncio.Queue()
         handler = q.put_nowait
@@ -121,6 +122,8 @@ class SymmetryClient:
                             res.ttft_s = time.perf_counter() - res.t_start
                         res.content_events += 1
                         res.text += d
+                if on_chunk is not None:
+                    on_chunk(res)
                 if disconnect_after is not None and len(res.chunks) >= disconnect_after:
                     conn.destroy()
                     break

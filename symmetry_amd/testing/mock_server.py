@@ -44,6 +44,7 @@ class SymmetryServer:
         self.swarm: Swarm | None = None
         self.provider_peers: dict[str, object] = {}
         self.joins: list[dict] = []
+        self.leaves: list[dict] = []
         self.challenges_signed = 0
         self.pongs = 0
         self._ping_task: asyncio.Task | None = None
@@ -111,6 +112,7 @@ class SymmetryServer:
                 pid = (data or {}).get("providerId")
                 self.db.execute("UPDATE providers SET completions = completions + 1 WHERE peer_key = ?", (pid,))
             elif k == Keys.LEAVE:
+                self.leaves.append({"peer_key": key, "data": data})
                 self._unregister(key)
 
         peer.on("data", on_data)

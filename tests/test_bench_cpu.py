@@ -1,4 +1,4 @@
-"""bench.py contract (driver-facing): one JSON line from rank 0 with the BASELINE metric, whole-job value,
+"""bench.py contract (driver-facing): one JSON line from rank 0 with the BASELINE metric, the per-client value,
 max-over-ranks timing; single process, a 2-rank torchrun in the default tensor-parallel mode (one provider
 over both ranks, strong scaling) and in data-parallel mode (gloo on CPU, tiny model)."""
 import json
@@ -37,12 +37,17 @@ def _check(r, n, mode):
     assert r["value"] > 0 and r["ms_per_step"] > 0
     assert 0 < r["engine_mean_ttft_ms"] <= r["engine_max_ttft_ms"]
     assert r["engine_p50_ttft_ms"] <= r["engine_max_ttft_ms"]
-    # whole-job aggregate = clients * (1000 / ms_per_step)
-    assert abs(r["value"] - clients * 1e3 / r["ms_per_step"]) / r["value"] < 0.01
-    # the client-end run: every client streamed over the swarm and got its inferenceEnded
+    # engine-side whole-job aggregate = clients * (1000 / ms_per_step); per client = 1000 / ms_per_step
+    assert abs(r["aggregate_tokens_per_s"] - clients * 1e3 / r["ms_per_step"]) / r["aggregate_tokens_per_s"] < 0.01
+    assert abs(r["engine_per_client_tokens_per_s"] - 1e3 / r["ms_per_step"]) < 0.01 * r["engine_per_client_tokens_per_s"]
+    assert len(r["per_rank_ms_per_step"]) == n and max(r["per_rank_ms_per_step"]) == r["ms_per_step"]
+    # the client-end run: every client streamed over the swarm and got its inferenceEnded; its per-client
+    # socket-measured median is the headline value (the metric's unit)
     ce = r["client_end"]
     assert ce["all_ended"] and ce["clients"] == 2 and ce["p50_ttft_ms"] > 0, ce
     assert r["p50_ttft_ms"] == ce["p50_ttft_ms"] and r["client_end_per_client_tokens_per_s"] > 0
+    assert r["unit"] == "tokens/s per client" and r["value"] == ce["per_client_tokens_per_s_median"]
+    assert r["value_source"].startswith("client_end")
 
 
 def test_bench_single_process():

@@ -266,43 +266,6 @@ def test_decodes_keep_streaming_while_a_long_prompt_prefills():
             assert float(row.max() - row[t]) <= 0.05
 
 
-def test_persistent_mlp_path_matches_three_launch_path():
-    """persistentMlp: decode steps of a dense model run O -> gate_up -> down through ops.decode_mlp;
-    greedy outputs equal the default fused path (small-llama: every K % 512 == 0)."""
-    prompts = _prompts(3, seed=5, lo=4, hi=20)
-    outs = []
-    for persistent in (False, True):
-        eng = _engine("small-llama", max_num_seqs=4, use_graphs=False, persistent_mlp=persistent)
-        assert eng.runner.model._persistent_mlp_ok(3) == persistent
-        seqs = [eng.add_request(f"r{i}", p, SamplingParams(max_tokens=6, ignore_eos=True))
-                for i, p in enumerate(prompts)]
-        while eng.has_unfinished():
-            eng.step()
-        outs.append([s.output_ids for s in seqs])
-    assert outs[0] == outs[1]
-
-
-def test_fused_attn_block_path_matches_default_path(monkeypatch):
-    """fusedAttnBlock: decode steps run QKV -> attention -> O through ops.decode_block (one launch per layer
-    on the GPU); greedy outputs equal the default path, and prefill steps keep the general path."""
-    from symmetry_amd import ops
-
-    calls = []
-    orig = ops.decode_block
-    monkeypatch.setattr(ops, "decode_block", lambda *a, **k: calls.append(1) or orig(*a, **k))
-    prompts = _prompts(3, seed=7, lo=4, hi=20)
-    outs = []
-    for block in (False, True):
-        eng = _engine("small-llama", max_num_seqs=4, use_graphs=False, fused_attn_block=block)
-        seqs = [eng.add_request(f"r{i}", p, SamplingParams(max_tokens=6, ignore_eos=True))
-                for i, p in enumerate(prompts)]
-        while eng.has_unfinished():
-            eng.step()
-        outs.append([s.output_ids for s in seqs])
-        assert bool(calls) == block
-    assert outs[0] == outs[1]
-
-
 def test_splitk_resid_path_for_wide_decode_batches(monkeypatch):
     """Decode steps with >= SPLITK_RESID_ROWS rows run O / down as k-split skinny GEMMs + add_prep; the
     outputs follow the naive fp32 forward (teacher forcing) like the fused dg_resid path."""

@@ -435,27 +435,3 @@ def test_mixtral_prefill_grouped_path_matches_oracle(gpu):
         assert len(s.output_ids) == 6
         _agree(eng.weights, p, s.output_ids, tol=0.08)
 
-
-@pytest.mark.parametrize("proj", [("qkv",), ("qkv", "o", "gu", "down")])
-def test_fused_decode_with_mgemm_projections(gpu, monkeypatch, proj):
-    """The fused decode path (below GENERAL_ROWS rows) with chosen projections on mgemm + fused epilogue
-    (SYMMETRY_MG_PROJ), graphs on, against the fp32 oracle."""
-    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
-    from symmetry_amd.engine.sequence import SamplingParams
-    from symmetry_amd.models import transformer
-
-    monkeypatch.setattr(transformer, "MG_PROJ", proj)
-    calls = []
-    orig = ops.dg_qkv
-    monkeypatch.setattr(ops, "dg_qkv", lambda *a, **k: (calls.append(1) if k.get("mg") else None) or orig(*a, **k))
-    eng = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", max_num_seqs=6, max_model_len=1024,
-                                 num_kv_blocks=64, use_graphs=True))
-    prompts = [list(range(500 + 13 * i, 530 + 7 * i)) for i in range(5)]
-    seqs = [eng.add_request(f"mp{i}", p, SamplingParams(max_tokens=8, ignore_eos=True))
-            for i, p in enumerate(prompts)]
-    while eng.has_unfinished():
-        eng.step()
-    assert calls, "decode steps must have run the qkv projection on mgemm"
-    for p, s in zip(prompts, seqs):
-        assert len(s.output_ids) == 8
-        _agree(eng.weights, p, s.output_ids, tol=0.08)

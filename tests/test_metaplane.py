@@ -1,6 +1,6 @@
 """R4 metadata plane: the native shared-memory ring (csrc/runtime/meta_ring.cpp) that carries rank 0's
 step metadata to the TP workers -- order, wrap-around, several readers in other processes, back-pressure
-when a reader lags a whole ring, close, oversized messages."""
+when a reader lags a whole ring, close, oversized messages, and the worker -> rank 0 fault back-channel."""
 import multiprocessing as mp
 import os
 import uuid
@@ -33,7 +33,7 @@ def test_ring_refuses_oversized_and_times_out():
     w.unlink()
     with pytest.raises(ValueError):
         w.push(np.zeros(17, dtype=np.int32))  # 68 B > 64 B slot
-    with pytest.raises(ValueError):
+    with pytest.raises(TimeoutError):
         w.pop(0, 0.01)  # nothing published
     w.push(np.zeros(2, dtype=np.int32))
     w.push(np.zeros(2, dtype=np.int32))
@@ -76,3 +76,55 @@ def test_ring_three_reader_processes_backpressure_and_close():
     w.unlink()
     assert [r[1] for r in res] == [500] * 3
     assert all(r[2] == expect for r in res)
+
+
+def test_ring_message_published_before_close_is_delivered():
+    """A message pushed right before shut() is still delivered (pop re-checks the slot after seeing closed)."""
+    name = _name()
+    w = _runtime.MetaRing(name, 64, 4, 1, True)
+    r = _runtime.MetaRing(name, 0, 0, 1, False)
+    w.unlink()
+    w.push(np.array([7, 8], dtype=np.int32))
+    w.shut()
+    assert r.pop(0, 1.0).tolist() == [7, 8]
+    assert r.pop(0, 1.0) is None
+
+
+def _failing_worker(name):
+    r = _runtime.MetaRing(name, 0, 0, 2, False)
+    r.register_pid(1, os.getpid())
+    r.report(1, 5)
+
+
+def _sleeper(name, ev):
+    r = _runtime.MetaRing(name, 0, 0, 2, False)
+    r.register_pid(0, os.getpid())
+    ev.set()
+    import time
+    time.sleep(60)
+
+
+def test_ring_faults_report_and_dead_reader():
+    """faults(): a worker's reported code, and -1 for a registered reader whose process is gone."""
+    name = _name()
+    w = _runtime.MetaRing(name, 64, 2, 2, True)
+    w.register_pid(-1, os.getpid())
+    assert w.faults() == []
+    ctx = mp.get_context("fork")
+    ev = ctx.Event()
+    sl = ctx.Process(target=_sleeper, args=(name, ev))
+    sl.start()
+    assert ev.wait(30)
+    fw = ctx.Process(target=_failing_worker, args=(name,))
+    fw.start()
+    fw.join(30)
+    assert w.faults() == [(1, 5)]
+    sl.kill()  # SIGKILL: no chance to report
+    sl.join(30)
+    assert sorted(w.faults()) == [(0, -1), (1, 5)]
+    # a push blocked on the dead reader fails fast instead of waiting out its timeout
+    w.push(np.zeros(1, dtype=np.int32))
+    w.push(np.zeros(1, dtype=np.int32))
+    with pytest.raises(RuntimeError, match="failed"):
+        w.push(np.zeros(1, dtype=np.int32), 30.0)
+    w.unlink()

@@ -256,3 +256,38 @@ def test_xgmi_gemm_push_then_reduce(gpu, world, M, shuf):
     finally:
         for h in hs:
             ops.xgmi_destroy(h)
+
+
+def test_xgmi_declared_fault_stops_every_wait(gpu):
+    """Fault containment: rank 1 of a world-2 communicator never runs.  (a) A collective already spinning on it
+    ends promptly once the host declares the fault (``xgmi_set_error``, what rank 0's health monitor does), not
+    after the 30 s wait limit; (b) with the word set, 200 further collectives -- a captured 70B TP=8 step holds
+    161 -- finish at once instead of waiting 30 s EACH.  The word is sticky (the communicator stays failed)."""
+    import time
+
+    from symmetry_amd.ops import _native
+
+    ops = _native.ops()
+    hs = _comms(ops, 2)
+    x = torch.randn(8192, device=gpu)
+    try:
+        t0 = time.perf_counter()
+        ops.xgmi_all_reduce(x, x, hs[0])  # waits for rank 1's flag
+        time.sleep(0.3)
+        ops.xgmi_set_error(hs[0], 2)
+        torch.cuda.synchronize()
+        first = time.perf_counter() - t0
+        assert first < 5.0, first
+        t1 = time.perf_counter()
+        for _ in range(100):
+            ops.xgmi_all_reduce(x, x, hs[0])
+            ops.xgmi_keys_max(torch.zeros(4, dtype=torch.int64, device=gpu),
+                              torch.zeros(4, dtype=torch.int32, device=gpu), hs[0])
+        torch.cuda.synchronize()
+        rest = time.perf_counter() - t1
+        assert rest < 5.0, rest
+        assert ops.xgmi_error(hs[0]) == 2 and ops.xgmi_error(hs[0]) == 2  # sticky
+    finally:
+        ops.xgmi_set_error(hs[0], 0)
+        for h in hs:
+            ops.xgmi_destroy(h)
