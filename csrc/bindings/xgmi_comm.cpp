@@ -360,6 +360,76 @@ void xgmi_keys_max_multi(std::vector<Tensor> keys, std::vector<Tensor> ids, std:
   launch_xgmi_keys_max_multi(m, world, (int)B, stream_of(keys[0]));
 }
 
+// ---- R3: unpadded expert all-to-all (xgmi_a2a_kernel) ------------------------------------------------------
+XgmiA2AArgs a2a_args(Xgmi* x, const Tensor& src, const Tensor& counts, const c10::optional<Tensor>& side, Tensor& dst,
+                     const c10::optional<Tensor>& dst_side, const c10::optional<Tensor>& dst_counts, int64_t cap) {
+  const int world = x->args.world;
+  check_ready(x, src);
+  check_ready(x, dst);
+  check_ready(x, counts);
+  TORCH_CHECK(counts.scalar_type() == at::kInt && counts.numel() == world, "xgmi_a2a: counts int32 [world]");
+  TORCH_CHECK(cap >= 1 && src.size(0) == world * cap && dst.size(0) == world * cap,
+              "xgmi_a2a: src / dst must be [world * cap, ...]");
+  TORCH_CHECK(src.scalar_type() == dst.scalar_type() && src.numel() == dst.numel(), "xgmi_a2a: src / dst mismatch");
+  const int64_t rb = src.numel() / src.size(0) * src.element_size();
+  TORCH_CHECK(rb % 16 == 0, "xgmi_a2a: row bytes must be a multiple of 16");
+  TORCH_CHECK(xgmi_a2a_slot_bytes((int)cap, (int)rb) <= x->args.slot_bytes, "xgmi_a2a: ", cap, " rows of ", rb,
+              " B exceed the communicator's ", x->args.slot_bytes, " B slot");
+  XgmiA2AArgs a;
+  a.c = x->args;
+  a.src = reinterpret_cast<const char*>(src.data_ptr());
+  a.counts = counts.data_ptr<int>();
+  a.dst = reinterpret_cast<char*>(dst.data_ptr());
+  a.cap = (int)cap;
+  a.row_bytes = (int)rb;
+  if (side.has_value()) {
+    check_ready(x, *side);
+    TORCH_CHECK(side->scalar_type() == at::kInt && side->numel() == world * cap, "xgmi_a2a: side int32 [world * cap]");
+    a.side = side->data_ptr<int>();
+  }
+  if (dst_side.has_value()) {
+    check_ready(x, *dst_side);
+    TORCH_CHECK(dst_side->scalar_type() == at::kInt && dst_side->numel() == world * cap,
+                "xgmi_a2a: dst_side int32 [world * cap]");
+    a.dst_side = dst_side->data_ptr<int>();
+  }
+  if (dst_counts.has_value()) {
+    check_ready(x, *dst_counts);
+    TORCH_CHECK(dst_counts->scalar_type() == at::kInt && dst_counts->numel() == world, "xgmi_a2a: dst_counts int32 [world]");
+    a.dst_counts = dst_counts->data_ptr<int>();
+  }
+  return a;
+}
+
+// rows [q cap, q cap + counts[q]) of src -> rows [rank cap, ...) of rank q's dst (+ side ints, received counts)
+void xgmi_a2a(const Tensor& src, const Tensor& counts, const c10::optional<Tensor>& side, Tensor& dst,
+              const c10::optional<Tensor>& dst_side, const c10::optional<Tensor>& dst_counts, int64_t cap, int64_t h) {
+  Xgmi* x = get(h);
+  launch_xgmi_a2a(a2a_args(x, src, counts, side, dst, dst_side, dst_counts, cap), stream_of(src));
+}
+
+// test-only: every rank of this process in one launch (grid slice per rank)
+void xgmi_a2a_multi(std::vector<Tensor> srcs, std::vector<Tensor> counts, std::vector<Tensor> sides,
+                    std::vector<Tensor> dsts, std::vector<Tensor> dst_sides, std::vector<Tensor> dst_counts,
+                    int64_t cap, std::vector<int64_t> comms, int64_t delay_rank, int64_t delay_us) {
+  const int world = (int)comms.size();
+  TORCH_CHECK(world >= 1 && world <= XG_MULTI_MAX && (int)srcs.size() == world && (int)counts.size() == world &&
+                  (int)sides.size() == world && (int)dsts.size() == world && (int)dst_sides.size() == world &&
+                  (int)dst_counts.size() == world, "xgmi_a2a_multi: one set of tensors per rank");
+  TORCH_CHECK(world * XA_WG <= XG_MULTI_MAX_GROUPS, "xgmi_a2a_multi: slices would not be co-resident");
+  XgmiA2AMulti m{};
+  m.delay_rank = (int)delay_rank;
+  m.delay_ticks = (unsigned long long)std::max<int64_t>(delay_us, 0) * 100ull;
+  for (int r = 0; r < world; ++r) {
+    Xgmi* x = get(comms[r]);
+    TORCH_CHECK(x->args.rank == r && x->args.world == world, "xgmi_a2a_multi: communicator order");
+    m.a[r] = a2a_args(x, srcs[r], counts[r], sides[r], dsts[r], dst_sides[r], dst_counts[r], cap);
+  }
+  launch_xgmi_a2a_multi(m, world, stream_of(srcs[0]));
+}
+
+int64_t xgmi_a2a_slot(int64_t cap, int64_t row_bytes) { return xgmi_a2a_slot_bytes((int)cap, (int)row_bytes); }
+
 // reads the error word: 1 + the source rank that never signalled within the wait limit, or the code the host
 // declared (xgmi_set_error).  Sticky: a communicator that lost a peer stays failed (every later collective
 // skips its waits), the provider exits and a supervisor starts fresh ranks.  Host-mapped memory: no device
@@ -423,6 +493,15 @@ TORCH_LIBRARY_FRAGMENT(symmetry_amd, m) {
       &xgmi_reduce_add_prep_multi);
   m.def("xgmi_keys_max_multi(Tensor[] keys, Tensor(a!)[] ids, int[] comms, int delay_rank=-1, int delay_us=0) -> ()",
         &xgmi_keys_max_multi);
+  m.def(
+      "xgmi_a2a(Tensor src, Tensor counts, Tensor? side, Tensor(a!) dst, Tensor(b!)? dst_side, Tensor(c!)? dst_counts, "
+      "int cap, int comm) -> ()",
+      &xgmi_a2a);
+  m.def(
+      "xgmi_a2a_multi(Tensor[] srcs, Tensor[] counts, Tensor[] sides, Tensor(a!)[] dsts, Tensor(b!)[] dst_sides, "
+      "Tensor(c!)[] dst_counts, int cap, int[] comms, int delay_rank=-1, int delay_us=0) -> ()",
+      &xgmi_a2a_multi);
+  m.def("xgmi_a2a_slot(int cap, int row_bytes) -> int", &xgmi_a2a_slot);
   m.def("xgmi_error(int comm) -> int", &xgmi_error);
   m.def("xgmi_set_error(int comm, int code) -> ()", &xgmi_set_error);
   m.def("xgmi_slot_bytes(int comm) -> int", &xgmi_slot_bytes);

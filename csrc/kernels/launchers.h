@@ -194,3 +194,27 @@ void launch_xgmi_keys_max_multi(const XgmiMulti& m, int world, int B, hipStream_
 void launch_xgmi_reduce_add_prep(const XgmiArgs& c, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d,
                                  int parts, hipStream_t s);
 void launch_xgmi_reduce_add_prep_multi(const XgmiMulti& m, int world, int T, int d, int parts, hipStream_t s);
+// R3: unpadded expert all-to-all over xGMI peer memory (xgmi_ar.hip, xgmi_a2a_kernel).  Block q of `src` (rows
+// [q cap, q cap + counts[q]), counts read on the DEVICE) lands as block `rank` of rank q's `dst`; only routed rows
+// cross the links (no worst-case capacity padding on the wire).  Slot (parity, source) of the communicator's
+// buffer: [0, 64) row count | side ints [cap] | rows [cap][row_bytes] (16-B aligned).
+constexpr int XA_WG = 128;  // workgroups per rank in one all-to-all launch (flag words wg x source)
+struct XgmiA2AArgs {
+  XgmiArgs c;
+  const char* src = nullptr;    // [world * cap][row_bytes]
+  const int* counts = nullptr;  // [world] rows of block q for rank q
+  const int* side = nullptr;    // optional [world * cap] int travelling with each row
+  char* dst = nullptr;          // [world * cap][row_bytes]: block s <- rank s (rows past its count untouched)
+  int* dst_side = nullptr;      // optional [world * cap]: received side ints, -1 past each block's count
+  int* dst_counts = nullptr;    // optional [world]: rows received from each rank
+  int cap = 0, row_bytes = 0;
+};
+long long xgmi_a2a_slot_bytes(int cap, int row_bytes);
+void launch_xgmi_a2a(const XgmiA2AArgs& a, hipStream_t s);
+// test-only: every rank of this process in one launch (grid y = rank), rank `delay_rank` held back delay_ticks
+struct XgmiA2AMulti {
+  XgmiA2AArgs a[XG_MULTI_MAX];
+  int delay_rank;
+  unsigned long long delay_ticks;
+};
+void launch_xgmi_a2a_multi(const XgmiA2AMulti& m, int world, hipStream_t s);

@@ -391,7 +391,94 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_keys_max_multi_kernel(XgmiMul
                    xg_multi_delay(m, r));
 }
 
+// ---- R3: expert all-to-all, unpadded -----------------------------------------------------------------------
+// Mixtral prefill under expert parallelism: rank r routes its token slice and groups the routed rows by owner
+// rank into blocks of capacity `cap` (worst case: every row to one owner).  RCCL's all-to-all moves whole
+// blocks -- N x the routed rows.  Here the counts stay on the device and each workgroup pushes only ITS share of
+// the real rows of every block straight into the owner's slot for this rank (one hop over the owner's link),
+// with the count and the rows' side ints (expert ids) beside them, raises flag (wg, rank) in the owner, waits
+// for flag (wg, s) of every source s, and copies its share of every source's rows out of its own slot into the
+// caller's buffer -- the same share rule on both ends (rows [wg n / G, (wg + 1) n / G) of an n-row block), so
+// the flag a workgroup waits for covers exactly the rows it copies.  Epochs, parities, bounded spins and the
+// declared-fault exit are the all-reduce's (xg_epoch, xg_fault_declared).
+SYM_DEV long long xa_rows_off(int cap) { return (64 + 4LL * cap + 15) / 16 * 16; }
+
+SYM_DEV void xg_a2a_body(const XgmiA2AArgs& a, int wg, int G, unsigned long long delay = 0) {
+  const XgmiArgs& c = a.c;
+  const unsigned epoch = xg_epoch(c, G);
+  xg_delay(delay);
+  const int par = (int)(epoch & 1u);
+  const int tid = threadIdx.x, rb = a.row_bytes, cap = a.cap;
+  const long long roff = xa_rows_off(cap);
+  // push my share of every block to its owner
+  for (int q = 0; q < c.world; ++q) {
+    const int n = a.counts[q];
+    const long long r0 = (long long)wg * n / G, r1 = (long long)(wg + 1) * n / G;
+    char* slot = xg_slot(c, q, par, c.rank);
+    const uint4* sp = reinterpret_cast<const uint4*>(a.src + ((long long)q * cap + r0) * rb);
+    uint4* dp = reinterpret_cast<uint4*>(slot + roff + r0 * rb);
+    const long long nv = (r1 - r0) * rb / 16;
+    for (long long v = tid; v < nv; v += XG_THREADS) dp[v] = sp[v];
+    if (a.side != nullptr)
+      for (long long j = r0 + tid; j < r1; j += XG_THREADS)
+        reinterpret_cast<int*>(slot + 64)[j] = a.side[(long long)q * cap + j];
+    if (tid == 0) *reinterpret_cast<unsigned*>(slot) = (unsigned)n;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store acknowledged (uncached buffers: no L2 write-back)
+  __syncthreads();
+  if (tid < c.world) {
+    unsigned* f = reinterpret_cast<unsigned*>(c.bufs[tid] + XG_HDR_BYTES) + wg * XG_MAX_WORLD + c.rank;
+    __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned* mine = reinterpret_cast<const unsigned*>(c.bufs[c.rank] + XG_HDR_BYTES) + wg * XG_MAX_WORLD + tid;
+    const unsigned long long t0 = wall_clock64();
+    int it = 0;
+    while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      if (xg_fault_declared(c, ++it)) break;
+      if (wall_clock64() - t0 > XG_WAIT_TICKS) {
+        __hip_atomic_store(c.err, 1 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  // copy my share of every source's rows out of my slot
+  for (int s = 0; s < c.world; ++s) {
+    const char* slot = xg_slot(c, c.rank, par, s);
+    const int n = (int)min(*reinterpret_cast<const unsigned*>(slot), (unsigned)cap);
+    const long long r0 = (long long)wg * n / G, r1 = (long long)(wg + 1) * n / G;
+    const uint4* sp = reinterpret_cast<const uint4*>(slot + roff + r0 * rb);
+    uint4* dp = reinterpret_cast<uint4*>(a.dst + ((long long)s * cap + r0) * rb);
+    const long long nv = (r1 - r0) * rb / 16;
+    for (long long v = tid; v < nv; v += XG_THREADS) dp[v] = sp[v];
+    if (a.dst_side != nullptr) {
+      int* ds = a.dst_side + (long long)s * cap;
+      for (long long j = r0 + tid; j < r1; j += XG_THREADS) ds[j] = reinterpret_cast<const int*>(slot + 64)[j];
+      const long long e0 = n + (long long)wg * (cap - n) / G, e1 = n + (long long)(wg + 1) * (cap - n) / G;
+      for (long long j = e0 + tid; j < e1; j += XG_THREADS) ds[j] = -1;
+    }
+    if (a.dst_counts != nullptr && wg == 0 && tid == 0) a.dst_counts[s] = n;
+  }
+}
+
+__global__ __launch_bounds__(XG_THREADS) void xgmi_a2a_kernel(XgmiA2AArgs a) { xg_a2a_body(a, blockIdx.x, gridDim.x); }
+
+__global__ __launch_bounds__(XG_THREADS) void xgmi_a2a_multi_kernel(XgmiA2AMulti m) {
+  const int r = blockIdx.y;
+  xg_a2a_body(m.a[r], blockIdx.x, gridDim.x, r == m.delay_rank ? m.delay_ticks : 0ull);
+}
+
 }  // namespace
+
+long long xgmi_a2a_slot_bytes(int cap, int row_bytes) {
+  return (64 + 4LL * cap + 15) / 16 * 16 + (long long)cap * row_bytes;
+}
+
+void launch_xgmi_a2a(const XgmiA2AArgs& a, hipStream_t s) { xgmi_a2a_kernel<<<XA_WG, XG_THREADS, 0, s>>>(a); }
+
+void launch_xgmi_a2a_multi(const XgmiA2AMulti& m, int world, hipStream_t s) {
+  xgmi_a2a_multi_kernel<<<dim3(XA_WG, world), XG_THREADS, 0, s>>>(m);
+}
 
 long long xgmi_buffer_bytes(int world, long long slot_bytes) { return XG_FLAG_BYTES + 2LL * world * slot_bytes; }
 

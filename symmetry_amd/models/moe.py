@@ -13,13 +13,14 @@ every rank holds the same T tokens when the block starts):
   rank applies its own experts to all routed rows and one all-reduce sums the partial outputs (on the
   one-shot xGMI kernel at decode sizes);
 * expert all-to-all (``mode="a2a"``, and ``"auto"`` from ``A2A_ROWS`` rows -- prefill): rank r takes token
-  slice r (ceil(T / N) rows), routes it, DISPATCHES each routed row to the rank owning its expert, the
+  slice r (S = ceil(T / N) rows), routes it, DISPATCHES each routed row to the rank owning its expert, the
   owners run their grouped GEMMs, the results RETURN to the slice owners, who combine their slice; an
-  all-gather rebuilds the [T, d] output on every rank.  Exchanges use fixed capacity blocks (a rank sends
-  at most ceil(T / N) * k rows to any one owner) with the expert id travelling beside each row (-1 marks
-  an empty slot), so no counts are ever read on the host: the dispatch and return are graph-capturable
-  collectives of host-known size (RCCL send/recv groups on GPUs).  Per rank the exchange moves
-  ~T k d / N rows each way + the gathered output, instead of the all-reduce's full [T, d] fp32 partials.
+  all-gather rebuilds the [T, d] output on every rank.  Rows are grouped by owner into blocks of capacity
+  S * k with the expert id beside each row, and no count is ever read on the host.  On an xGMI node
+  (``XgmiComm.a2a_rows``, ``csrc/kernels/xgmi_ar.hip`` xgmi_a2a_kernel) each rank pushes ONLY its routed
+  rows straight into the owners' peer buffers -- S k d x 2 B dispatched (bf16) and S k d x 4 B returned
+  (fp32) per rank, i.e. T k d x 2 / N each way -- with the device-side counts travelling beside them.
+  Elsewhere (RCCL / gloo) the blocks move whole: N x the routed rows, empty slots marked -1.
 * :meth:`MoEBlock.forward_tokens` is the same exchange for ranks that hold DIFFERENT tokens (data-parallel
   attention in front of expert-parallel MoE): dispatch, expert GEMMs, return, combine, no gather.
 """
@@ -35,6 +36,8 @@ SKINNY_ROWS = 64
 # "auto": expert all-to-all from this many tokens (prefill); decode steps (<= 64 rows under MoE) all-reduce
 A2A_ROWS = int(os.environ.get("SYMMETRY_MOE_A2A_ROWS", "128"))
 GROUPED = os.environ.get("SYMMETRY_MOE_GROUPED", "1") != "0"  # A/B: 0 = per-expert library GEMMs (host sync)
+# count the all-to-all bytes this rank pushes (reads the device counts: a host sync per layer -- tests / benches)
+A2A_STATS = os.environ.get("SYMMETRY_MOE_A2A_STATS", "0") == "1"
 
 
 class MoEBlock:
@@ -51,6 +54,7 @@ class MoEBlock:
         self.mode = mode or os.environ.get("SYMMETRY_MOE_MODE", "auto")
         self.F = cfg.intermediate_size
         self.calls = {"allreduce": 0, "a2a": 0}
+        self.a2a_bytes = {"dispatch": 0, "return": 0, "routed_rows": 0, "padded_dispatch": 0}
         # router rows padded to a multiple of 16 for the skinny GEMM (padded logits are never read)
         self.router = {}
         Ep = (self.E + 15) // 16 * 16
@@ -172,21 +176,32 @@ class MoEBlock:
         dst = self._buf("a2a.dst", (max(R, 1),), torch.int32)
         send = self._buf("a2a.send", (N * cap, d), torch.bfloat16)
         send_e = self._buf("a2a.send_e", (N * cap, 1), torch.int32)
-        send_e.fill_(-1)
+        cursor = self._buf("a2a.cursor", (N,), torch.int32)  # after moe_scatter: routed rows per owner
+        cursor.zero_()
+        # xGMI path: only the routed rows cross the links (counts stay on the device); else RCCL moves whole
+        # capacity blocks with -1 marking the empty slots
+        xg = getattr(self.comm, "a2a_fits", None)
+        xg = xg is not None and xg(cap, d * 4)
+        if not xg:
+            send_e.fill_(-1)
         if Tr > 0:
             logits = self.m._linear("router", x, self.router[i])
             ops.moe_route(logits, Tr, k, E, ids, w)
             owner = self._buf("a2a.owner", (R,), torch.int32)
             torch.floor_divide(ids[:R], El, out=owner)
             blocks = self._blocks(N, cap, dev)
-            cursor = self._buf("a2a.cursor", (N,), torch.int32)
-            cursor.zero_()
             ops.moe_scatter(x, owner, k, N, blocks, cursor, send, dst)
             send_e.view(-1).index_copy_(0, dst[:R].long(), ids[:R])
         # ---- dispatch: block q of every rank's send buffer goes to rank q
         splits = [cap] * N
-        recv = self.comm.all_to_all_rows(send, splits, splits)            # [N * cap, d]  (src-major)
-        recv_e = self.comm.all_to_all_rows(send_e, splits, splits).view(-1)  # expert id per slot, -1 = empty
+        if xg:
+            recv = self._buf("a2a.recv", (N * cap, d), torch.bfloat16)
+            recv_e = self._buf("a2a.recv_e", (N * cap,), torch.int32)
+            rcnt = self._buf("a2a.rcnt", (N,), torch.int32)
+            self.comm.a2a_rows(send, cursor, send_e.view(-1), recv, recv_e, rcnt)
+        else:
+            recv = self.comm.all_to_all_rows(send, splits, splits)            # [N * cap, d]  (src-major)
+            recv_e = self.comm.all_to_all_rows(send_e, splits, splits).view(-1)  # expert id per slot, -1 = empty
         # ---- group the received rows by local expert, run the grouped GEMMs
         counts = self._buf("a2a.counts", (E,), torch.int32)
         offsets = self._buf("a2a.offsets", (E + 1,), torch.int32)
@@ -205,7 +220,17 @@ class MoEBlock:
         # ---- return: every received slot's result goes back to the slot it came from
         back = self._buf("a2a.back", (N * cap, d), torch.float32)
         torch.index_select(yl, 0, ldst.long(), out=back)
-        ret = self.comm.all_to_all_rows(back, splits, splits)             # [N * cap, d]: my slots' results
+        if xg:  # the return is the transpose: block s of `back` holds rcnt[s] real rows for rank s
+            ret = self._buf("a2a.ret", (N * cap, d), torch.float32)
+            self.comm.a2a_rows(back, rcnt, None, ret)
+            if A2A_STATS:
+                sent, got = int(cursor.sum()), int(rcnt.sum())
+                self.a2a_bytes["dispatch"] += sent * d * 2
+                self.a2a_bytes["return"] += got * d * 4
+                self.a2a_bytes["routed_rows"] += R
+                self.a2a_bytes["padded_dispatch"] += N * cap * d * 2
+        else:
+            ret = self.comm.all_to_all_rows(back, splits, splits)             # [N * cap, d]: my slots' results
         out = self._buf("a2a.out", (max(Tr, 1), d), torch.float32)[:Tr]
         if Tr > 0:
             ops.moe_combine(ret, dst, ids, 0, E, w, k, out)

@@ -232,6 +232,26 @@ class XgmiComm(Comm):
         self.calls["gemm_add_prep"] = self.calls.get("gemm_add_prep", 0) + 1
         return True
 
+    # ---- R3: unpadded expert all-to-all on a second peer-memory communicator ------------------------------
+    def attach_a2a(self, group, cap: int, row_bytes: int) -> None:
+        """Collective (every rank): a second xGMI communicator whose slots hold ``cap`` rows of up to
+        ``row_bytes`` each (+ counts and side ints) for :meth:`a2a_rows`.  Mixtral prefill: cap = ceil(max
+        tokens / N) * top_k rows, row_bytes = d * 4 (the fp32 return) -- ~0.5 GB of uncached HBM per rank."""
+        slot = (int(self.ops.xgmi_a2a_slot(int(cap), int(row_bytes))) + 255) // 256 * 256
+        self.a2a = XgmiComm(self.inner, group, torch.device("cuda", torch.cuda.current_device()), slot_bytes=slot)
+        self.a2a_cap, self.a2a_row_bytes = int(cap), int(row_bytes)
+        self.calls["a2a"] = 0
+
+    def a2a_fits(self, cap: int, row_bytes: int) -> bool:
+        return getattr(self, "a2a", None) is not None and cap <= self.a2a_cap and row_bytes <= self.a2a_row_bytes
+
+    def a2a_rows(self, src, counts, side, dst, dst_side=None, dst_counts=None) -> None:
+        """Block q of ``src`` ([world * cap, ...] rows; its first ``counts[q]`` -- a DEVICE int32 [world] -- are
+        real) becomes block ``rank`` of rank q's ``dst``; only real rows cross the links, no host sync."""
+        cap = src.shape[0] // self.world
+        self.ops.xgmi_a2a(src, counts, side, dst, dst_side, dst_counts, cap, self.a2a.handle)
+        self.calls["a2a"] += 1
+
     def argmax_keys(self, keys, ids):
         if keys.is_cuda and keys.is_contiguous() and keys.numel() <= 4096:
             self.ops.xgmi_keys_max(keys, ids, self.handle)
@@ -251,14 +271,22 @@ class XgmiComm(Comm):
     def error(self) -> int:
         """1 + the source rank a collective gave up waiting for (or the code the host declared), else 0.  Sticky
         (the communicator stays failed); host-mapped, so it costs no device synchronisation: the model runner
-        polls it after every step."""
-        return int(self.ops.xgmi_error(self.handle))
+        polls it after every step.  Covers the all-to-all communicator too."""
+        e = int(self.ops.xgmi_error(self.handle))
+        if not e and getattr(self, "a2a", None) is not None:
+            e = int(self.ops.xgmi_error(self.a2a.handle))
+        return e
 
     def set_error(self, code: int) -> None:
         """Declare a fault from the host (rank 0's health monitor): every spinning collective stops waiting."""
         self.ops.xgmi_set_error(self.handle, int(code))
+        if getattr(self, "a2a", None) is not None:
+            self.ops.xgmi_set_error(self.a2a.handle, int(code))
 
     def destroy(self, inner_too: bool = True):
+        if getattr(self, "a2a", None) is not None:
+            self.a2a.destroy(inner_too=False)
+            self.a2a = None
         if self.handle is not None:
             self.ops.xgmi_destroy(self.handle)
         if inner_too and hasattr(self.inner, "destroy"):

@@ -108,6 +108,10 @@ def init_tp_engine(ecfg):
         ep_comm = comm
     if on_gpu:
         ecfg.device = f"cuda:{local}"
+    if ep_comm is not None and isinstance(comm, XgmiComm) and os.environ.get("SYMMETRY_MOE_XGMI_A2A", "1") != "0":
+        # the unpadded expert all-to-all (prefill dispatch / return of routed rows) on its own peer buffers
+        tokens = max(ecfg.max_num_batched_tokens, 8192)
+        comm.attach_a2a(cpu_group, -(-tokens // world) * mcfg.top_k, mcfg.hidden_size * 4)
     engine = LLMEngine(ecfg, tp_comm=comm, ep_comm=ep_comm, cpu_group=cpu_group)
     if rank == 0 and world > 1:
         # fault containment: a lost worker takes the provider offline within ~0.1 s (parallel/health.py)

@@ -291,3 +291,47 @@ def test_xgmi_declared_fault_stops_every_wait(gpu):
         ops.xgmi_set_error(hs[0], 0)
         for h in hs:
             ops.xgmi_destroy(h)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_xgmi_a2a_unpadded_exchange(gpu, world, dtype):
+    """R3 expert all-to-all (xgmi_a2a): every rank sends block q (rows [q cap, q cap + counts[q]), counts only on
+    the device) to rank q, which receives it as block `source`; side ints (expert ids) travel with the rows and
+    read -1 past each block's count; rows past the count are never written (only routed rows cross the links).
+    Four rounds (both slot parities, twice), a rotating rank held back 30 us."""
+    from symmetry_amd.ops import _native
+
+    ops = _native.ops()
+    cap, d = 40, 256
+    esz = torch.finfo(dtype).bits // 8
+    slot = (int(ops.xgmi_a2a_slot(cap, d * esz)) + 255) // 256 * 256
+    hs = _comms(ops, world, slot_bytes=slot)
+    g = torch.Generator(device="cpu").manual_seed(world * 10 + esz)
+    try:
+        for it in range(4):
+            cnt = torch.randint(0, cap + 1, (world, world), generator=g, dtype=torch.int32)
+            cnt[0, world - 1] = cap  # a full block
+            cnt[world - 1, 0] = 0    # an empty one
+            srcs = [torch.randn(world * cap, d, generator=g).to(gpu, dtype) for _ in range(world)]
+            sides = [torch.randint(0, 1 << 20, (world * cap,), generator=g, dtype=torch.int32).to(gpu)
+                     for _ in range(world)]
+            counts = [cnt[r].to(gpu) for r in range(world)]
+            dsts = [torch.full((world * cap, d), float("nan"), device=gpu, dtype=dtype) for _ in range(world)]
+            dsides = [torch.full((world * cap,), -7, dtype=torch.int32, device=gpu) for _ in range(world)]
+            dcnts = [torch.full((world,), -7, dtype=torch.int32, device=gpu) for _ in range(world)]
+            ops.xgmi_a2a_multi(srcs, counts, sides, dsts, dsides, dcnts, cap, hs, it % world, 30)
+            torch.cuda.synchronize()
+            for r in range(world):
+                assert ops.xgmi_error(hs[r]) == 0
+                assert dcnts[r].tolist() == cnt[:, r].tolist()
+                for s in range(world):
+                    n = int(cnt[s, r])
+                    got, want = dsts[r][s * cap:(s + 1) * cap], srcs[s][r * cap:r * cap + n]
+                    assert torch.equal(got[:n], want), (r, s, n)
+                    assert torch.isnan(got[n:].float()).all(), (r, s, n)  # nothing past the count was written
+                    gs = dsides[r][s * cap:(s + 1) * cap]
+                    assert torch.equal(gs[:n], sides[s][r * cap:r * cap + n]) and (gs[n:] == -1).all()
+    finally:
+        for h in hs:
+            ops.xgmi_destroy(h)
