@@ -5,7 +5,8 @@ An N-GPU node is not available to this repo's development runs, so this measures
 on one MI355X: rank 0's shard of Llama-3-8B (or 70B) at TP=N -- the same sharded weights, the same fused
 decode kernels at the shard shapes (e.g. QKV N = 768, O K = 512 at TP=8), the same hipGraph-captured
 pipelined step -- with every collective running the real one-shot xGMI kernel on a world-1 communicator
-(its push, flag and reduce on local HBM, no peer latency).  The step time is therefore a lower bound of
+(its push, flag and reduce on local HBM, no peer latency; the fused row-parallel GEMM + all-reduce launches
+have no other rank's granules to wait for).  The step time is therefore a lower bound of
 the TP=N step: real xGMI adds the peers' flag latency to each of the 2 per-layer collectives + the
 sampling-keys one.  The model math is one shard's (outputs are not the full model's): timing only.
 
@@ -24,9 +25,6 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
-PUSH = os.environ.get("SYMMETRY_XGMI_PUSH", "0") == "1"
-
-
 class LocalXgmi:
     """The XgmiComm interface over a world-1 xGMI communicator (every collective a real kernel launch)."""
 
@@ -41,6 +39,10 @@ class LocalXgmi:
         self.handle = int(self.ops.xgmi_create(slot_bytes, 1, 0, device.index or 0))
         self.ops.xgmi_connect_local(self.handle, [self.handle])
         self.calls = {"all_reduce": 0, "add_prep": 0, "keys": 0}
+        # the fused GEMM + all-reduce communicator (own slots of epoch-tagged granules, world 1: no peer granule
+        # to wait for -- the launch is the GEMM + residual epilogue)
+        self.xar = int(self.ops.xgmi_create(slot_bytes, 1, 0, device.index or 0))
+        self.ops.xgmi_connect_local(self.xar, [self.xar])
 
     def all_reduce(self, t, op="sum"):
         # prefill-sized messages go to RCCL on a real node; a world-1 sum is the identity (not timed here)
@@ -56,12 +58,15 @@ class LocalXgmi:
         self.ops.xgmi_keys_max(keys, ids, self.handle)
         self.calls["keys"] += 1
 
-    def gemm_add_prep(self, x, W, wshuf, resid, w_next, xw, ss) -> bool:
-        if not PUSH or x.shape[0] * resid.shape[1] * 4 > self.slot_bytes:
+    def gemm_ar_resid(self, x, W, wshuf, resid, w_next, xw, ss) -> bool:
+        from symmetry_amd.parallel.comm import XAR
+
+        if not XAR or x.shape[0] > 64 or x.shape[0] * resid.shape[1] * 8 > self.slot_bytes:
             return False
-        self.ops.xgmi_gemm_add_prep(x, W, bool(wshuf), resid, w_next, xw, ss, self.handle)
-        self.calls["gemm_add_prep"] = self.calls.get("gemm_add_prep", 0) + 1
-        return True
+        ok = bool(self.ops.xgmi_gemm_ar_resid(x, W, bool(wshuf), resid, w_next, xw, ss, self.xar))
+        if ok:
+            self.calls["gemm_ar"] = self.calls.get("gemm_ar", 0) + 1
+        return ok
 
     def all_gather(self, t):
         import torch
@@ -69,7 +74,7 @@ class LocalXgmi:
         return torch.cat([t] * self.world, 0)
 
     def error(self) -> int:
-        return int(self.ops.xgmi_error(self.handle))
+        return int(self.ops.xgmi_error(self.handle)) or int(self.ops.xgmi_error(self.xar))
 
 
 def main():

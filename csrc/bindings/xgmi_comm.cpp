@@ -192,81 +192,58 @@ void xgmi_keys_max(const Tensor& keys, Tensor& ids, int64_t h) {
                        (int)B, stream_of(keys));
 }
 
-// ---- row-parallel projection + all-reduce + residual add + next-norm prep as GEMM-push + reduce ------------
-// The decode GEMM (DECODE_EPI_XPUSH) stores its fp32 output tiles straight into every rank's slot and raises
-// a flag per 16-column tile; the reduce kernel waits for the flags of its columns and finishes like
-// xgmi_add_prep.  The all-reduce's push rides the GEMM's own epilogue (no y round trip through local HBM,
-// no separate push phase on the critical path).
-void dg_push(Xgmi* x, const Tensor& a, const Tensor& W, bool wshuf) {
+// ---- row-parallel projection + all-reduce + residual + next-norm prep in ONE launch (DECODE_EPI_XAR) -------
+DecodeEpi xar_epi(Xgmi* x, const Tensor& a, const Tensor& W, bool wshuf, Tensor& resid, const Tensor& w_next,
+                  Tensor& xw, Tensor& ss) {
   check_ready(x, a);
   check_ready(x, W);
-  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && W.scalar_type() == at::kBFloat16, "xgmi gemm: bf16 x and W");
-  TORCH_CHECK(a.dim() == 2 && W.dim() == 2 && a.size(1) == W.size(1), "xgmi gemm: x [M, K], W [N, K]");
-  const int64_t M = a.size(0), K = a.size(1), N = W.size(0);
-  TORCH_CHECK(M >= 1 && M <= 64 && N % 16 == 0 && K % 256 == 0, "xgmi gemm: M <= 64, N % 16, K % 256");
-  TORCH_CHECK(N / 16 < XG_KEYS_WG, "xgmi gemm: too many column tiles");
-  TORCH_CHECK(M * N * 4 <= x->args.slot_bytes, "xgmi gemm: output exceeds the slot");
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&resid, &w_next, &xw, &ss}) check_ready(x, *t);
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && W.scalar_type() == at::kBFloat16 && w_next.scalar_type() == at::kBFloat16 &&
+                  xw.scalar_type() == at::kBFloat16, "xgmi_gemm_ar_resid: x, W, w_next, xw bf16");
+  TORCH_CHECK(resid.scalar_type() == at::kFloat && ss.scalar_type() == at::kFloat, "xgmi_gemm_ar_resid: resid, ss fp32");
+  TORCH_CHECK(a.dim() == 2 && W.dim() == 2 && a.size(1) == W.size(1), "xgmi_gemm_ar_resid: x [M, K], W [N, K]");
+  const int64_t M = a.size(0), N = W.size(0);
+  TORCH_CHECK(resid.dim() == 2 && resid.size(0) == M && resid.size(1) == N && xw.numel() == M * N &&
+                  w_next.numel() == N, "xgmi_gemm_ar_resid: resid / xw [M, N], w_next [N]");
+  TORCH_CHECK(ss.dim() == 2 && ss.size(0) >= M && ss.size(1) == N / 16, "xgmi_gemm_ar_resid: ss [M, N / 16]");
+  TORCH_CHECK(M * N * 8 <= x->args.slot_bytes, "xgmi_gemm_ar_resid: output granules exceed the slot");
   DecodeEpi e;
   e.wshuf = wshuf ? 1 : 0;
-  for (int r = 0; r < XG_MAX_WORLD; ++r) e.xp.bufs[r] = x->args.bufs[r];
-  e.xp.rank = x->args.rank;
-  e.xp.world = x->args.world;
-  e.xp.slot_bytes = x->args.slot_bytes;
-  launch_decode_gemm(DECODE_EPI_XPUSH, reinterpret_cast<const bf16*>(a.data_ptr()),
-                     reinterpret_cast<const bf16*>(W.data_ptr()), (int)M, (int)N, (int)K, e, stream_of(a));
+  e.xp = x->args;
+  e.resid = resid.data_ptr<float>();
+  e.w_next = reinterpret_cast<const bf16*>(w_next.data_ptr());
+  e.xw_out = reinterpret_cast<bf16*>(xw.data_ptr());
+  e.ss_out = ss.data_ptr<float>();
+  return e;
 }
 
-void check_prep(Xgmi* x, const Tensor& resid, const Tensor& w, const Tensor& xw, const Tensor& ss, int64_t* P) {
-  for (const Tensor* t : std::initializer_list<const Tensor*>{&resid, &w, &xw, &ss}) check_ready(x, *t);
-  TORCH_CHECK(resid.scalar_type() == at::kFloat && ss.scalar_type() == at::kFloat && w.scalar_type() == at::kBFloat16 &&
-                  xw.scalar_type() == at::kBFloat16 && resid.dim() == 2, "xgmi reduce: resid / ss fp32, w / xw bf16");
-  const int64_t T = resid.size(0), d = resid.size(1);
-  *P = ss.dim() == 2 ? ss.size(1) : 1;
-  TORCH_CHECK(xw.numel() == T * d && w.numel() == d && ss.numel() >= T * *P, "xgmi reduce: shapes");
-  TORCH_CHECK(*P >= 1 && *P <= 16 && d % (16 * *P) == 0 && T * *P < XG_KEYS_WG,
-              "xgmi reduce: parts must split d into 16-column tiles");
-}
-
-// resid += all_reduce(x @ W^T); xw = bf16(resid * w_next); ss[row][part] = sum(resid^2)
-void xgmi_gemm_add_prep(const Tensor& a, const Tensor& W, bool wshuf, Tensor& resid, const Tensor& w_next, Tensor& xw,
+// resid += all_reduce(x @ W^T); xw = bf16(resid * w_next); ss[m][tile] = sum(resid^2) over each 16 columns.
+// Returns false (nothing launched) where no co-resident decomposition exists: run GEMM + add_prep instead.
+bool xgmi_gemm_ar_resid(const Tensor& a, const Tensor& W, bool wshuf, Tensor& resid, const Tensor& w_next, Tensor& xw,
                         Tensor& ss, int64_t h) {
   Xgmi* x = get(h);
-  int64_t P = 1;
-  check_prep(x, resid, w_next, xw, ss, &P);
-  TORCH_CHECK(resid.size(0) == a.size(0) && resid.size(1) == W.size(0), "xgmi_gemm_add_prep: resid [M, N]");
-  dg_push(x, a, W, wshuf);
-  launch_xgmi_reduce_add_prep(x->args, resid.data_ptr<float>(), reinterpret_cast<const bf16*>(w_next.data_ptr()),
-                              reinterpret_cast<bf16*>(xw.data_ptr()), ss.data_ptr<float>(), (int)resid.size(0),
-                              (int)resid.size(1), (int)P, stream_of(resid));
+  const DecodeEpi e = xar_epi(x, a, W, wshuf, resid, w_next, xw, ss);
+  TORCH_CHECK(a.size(1) % 256 == 0 && W.size(0) % 16 == 0, "xgmi_gemm_ar_resid: K % 256, N % 16");
+  return launch_decode_gemm_xar(reinterpret_cast<const bf16*>(a.data_ptr()), reinterpret_cast<const bf16*>(W.data_ptr()),
+                                (int)a.size(0), (int)W.size(0), (int)a.size(1), e, stream_of(a));
 }
 
-// test-only: the GEMM-push half for one rank (push launches never wait, so ranks may run one by one)
-void xgmi_gemm_push(const Tensor& a, const Tensor& W, bool wshuf, int64_t h) { dg_push(get(h), a, W, wshuf); }
-
-// test-only: the reduce half for every rank of this process in one launch (they wait on each other's flags)
-void xgmi_reduce_add_prep_multi(std::vector<Tensor> resids, const Tensor& w, std::vector<Tensor> xws,
-                                std::vector<Tensor> sss, std::vector<int64_t> comms, int64_t delay_rank,
-                                int64_t delay_us) {
+// test-only: every rank of this process in one launch (grid z = rank); xres: the x-resident walk
+bool xgmi_gemm_ar_resid_multi(std::vector<Tensor> xs, const Tensor& W, bool wshuf, std::vector<Tensor> resids,
+                              const Tensor& w_next, std::vector<Tensor> xws, std::vector<Tensor> sss,
+                              std::vector<int64_t> comms, bool xres) {
   const int world = (int)comms.size();
-  TORCH_CHECK(world >= 1 && world <= XG_MULTI_MAX && (int)resids.size() == world && (int)xws.size() == world &&
-                  (int)sss.size() == world, "xgmi_reduce_add_prep_multi: one set of tensors per rank");
-  XgmiMulti m{};
-  m.delay_rank = (int)delay_rank;
-  m.delay_ticks = (unsigned long long)std::max<int64_t>(delay_us, 0) * 100ull;
-  int64_t P = 1;
+  TORCH_CHECK(world >= 1 && world <= XAR_MULTI_MAX && (int)xs.size() == world && (int)resids.size() == world &&
+                  (int)xws.size() == world && (int)sss.size() == world, "xgmi_gemm_ar_resid_multi: one set per rank");
+  XarMulti m{};
   for (int r = 0; r < world; ++r) {
     Xgmi* x = get(comms[r]);
-    TORCH_CHECK(x->args.rank == r && x->args.world == world, "xgmi_reduce_add_prep_multi: communicator order");
-    check_prep(x, resids[r], w, xws[r], sss[r], &P);
-    m.c[r] = x->args;
-    m.out[r] = resids[r].data_ptr();
-    m.xw[r] = xws[r].data_ptr();
-    m.ss[r] = sss[r].data_ptr<float>();
+    TORCH_CHECK(x->args.rank == r && x->args.world == world, "xgmi_gemm_ar_resid_multi: communicator order");
+    m.e[r] = xar_epi(x, xs[r], W, wshuf, resids[r], w_next, xws[r], sss[r]);
+    m.x[r] = reinterpret_cast<const bf16*>(xs[r].data_ptr());
   }
-  const int64_t T = resids[0].size(0), d = resids[0].size(1);
-  TORCH_CHECK(world * T * P <= XG_MULTI_MAX_GROUPS, "xgmi_reduce_add_prep_multi: not co-resident");
-  m.w = reinterpret_cast<const bf16*>(w.data_ptr());
-  launch_xgmi_reduce_add_prep_multi(m, world, (int)T, (int)d, (int)P, stream_of(resids[0]));
+  return launch_decode_gemm_xar_multi(m, world, reinterpret_cast<const bf16*>(W.data_ptr()), (int)xs[0].size(0),
+                                      (int)W.size(0), (int)xs[0].size(1), xres ? 1 : 0, stream_of(xs[0]));
 }
 
 // test-only: every rank of this process in one launch (grid slice per rank; see xgmi_ar.hip)
@@ -483,14 +460,13 @@ TORCH_LIBRARY_FRAGMENT(symmetry_amd, m) {
       &xgmi_add_prep_multi);
   m.def("xgmi_keys_max(Tensor keys, Tensor(a!) ids, int comm) -> ()", &xgmi_keys_max);
   m.def(
-      "xgmi_gemm_add_prep(Tensor x, Tensor W, bool wshuf, Tensor(a!) resid, Tensor w_next, Tensor(b!) xw, "
-      "Tensor(c!) ss, int comm) -> ()",
-      &xgmi_gemm_add_prep);
-  m.def("xgmi_gemm_push(Tensor x, Tensor W, bool wshuf, int comm) -> ()", &xgmi_gemm_push);
+      "xgmi_gemm_ar_resid(Tensor x, Tensor W, bool wshuf, Tensor(a!) resid, Tensor w_next, Tensor(b!) xw, "
+      "Tensor(c!) ss, int comm) -> bool",
+      &xgmi_gemm_ar_resid);
   m.def(
-      "xgmi_reduce_add_prep_multi(Tensor(a!)[] resids, Tensor w, Tensor(b!)[] xws, Tensor(c!)[] sss, int[] comms, "
-      "int delay_rank=-1, int delay_us=0) -> ()",
-      &xgmi_reduce_add_prep_multi);
+      "xgmi_gemm_ar_resid_multi(Tensor[] xs, Tensor W, bool wshuf, Tensor(a!)[] resids, Tensor w_next, "
+      "Tensor(b!)[] xws, Tensor(c!)[] sss, int[] comms, bool xres) -> bool",
+      &xgmi_gemm_ar_resid_multi);
   m.def("xgmi_keys_max_multi(Tensor[] keys, Tensor(a!)[] ids, int[] comms, int delay_rank=-1, int delay_us=0) -> ()",
         &xgmi_keys_max_multi);
   m.def(

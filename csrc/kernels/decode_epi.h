@@ -7,6 +7,7 @@
 
 #include "common.h"
 #include "launchers.h"
+#include "xgmi_proto.h"
 
 namespace {
 
@@ -42,18 +43,59 @@ SYM_DEV void store4bf_sc1(bf16* p, float a, float b, float c, float d) {
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ---- XPUSH (row-parallel projection under TP, xgmi_ar.hip protocol): the collective's epoch is this
-// rank's counter + 1 (read here, bumped by the reduce kernel that follows on the stream); tiles are stored
-// into slot (epoch parity, this rank) of every rank's buffer, then flag (tile, this rank) is raised in
-// every rank once the storing wave's stores are acknowledged (uncached buffers: no cache maintenance).
-SYM_DEV unsigned xp_epoch(const XgmiPush& xp) {
-  return __hip_atomic_load(reinterpret_cast<const unsigned*>(xp.bufs[xp.rank]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT) + 1u;
+// ---- XAR (row-parallel projection under TP, all-reduced inside the GEMM launch) ----------------------------
+// Granules of 8 B {fp32 value, u32 tag = collective epoch} in the XAR communicator's slot (parity, source):
+// granule (m, n) at byte (m N + n) * 8.  A lane pushes its 4 values to every OTHER rank with 8-B stores (one
+// single-copy-atomic write each, no flag, no ack wait), then polls the other ranks' granules of the same
+// columns until their tags equal this epoch, and sums all ranks' values in rank order (its own from
+// registers: the same fp32 bits the peers receive), so every rank gets bit-identical sums.  A stale granule
+// (an older epoch of the same parity) never matches; the communicator carries nothing but XAR granules.
+SYM_DEV long long xar_goff(int m, int N, int n) { return ((long long)m * N + n) * 8; }
+
+SYM_DEV void xar_push(const XgmiArgs& c, const f32x4& v, long long goff, unsigned ep) {
+  const int par = (int)(ep & 1u);
+  for (int r = 0; r < c.world; ++r) {
+    if (r == c.rank) continue;
+    unsigned long long* d = reinterpret_cast<unsigned long long*>(c.bufs[r] + XG_FLAG_BYTES +
+                                                                 ((long long)par * c.world + c.rank) * c.slot_bytes + goff);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __hip_atomic_store(d + i, ((unsigned long long)ep << 32) | __float_as_uint(v[i]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
-SYM_DEV void xp_flag(const XgmiPush& xp, int r, int tile, unsigned epoch) {
-  unsigned* f = reinterpret_cast<unsigned*>(xp.bufs[r] + XG_HDR_BYTES) + tile * XG_MAX_WORLD + xp.rank;
-  __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+SYM_DEV f32x4 xar_collect(const XgmiArgs& c, const f32x4& own, long long goff, unsigned ep) {
+  const int par = (int)(ep & 1u);
+  f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < c.world; ++s) {
+    if (s == c.rank) {
+      sum += own;
+      continue;
+    }
+    const unsigned long long* g = reinterpret_cast<const unsigned long long*>(
+        c.bufs[c.rank] + XG_FLAG_BYTES + ((long long)par * c.world + s) * c.slot_bytes + goff);
+    unsigned long long q[4];
+    const unsigned long long t0 = wall_clock64();
+    int it = 0;
+    for (;;) {
+      bool ok = true;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        q[i] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = ok && (unsigned)(q[i] >> 32) == ep;
+      }
+      if (ok || xg_fault_declared(c, ++it)) break;
+      if (wall_clock64() - t0 > XG_WAIT_TICKS) {
+        __hip_atomic_store(c.err, 1 + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    sum += f32x4{__uint_as_float((unsigned)q[0]), __uint_as_float((unsigned)q[1]), __uint_as_float((unsigned)q[2]),
+                 __uint_as_float((unsigned)q[3])};
+  }
+  return sum;
 }
 
 template <int EPI>
@@ -61,13 +103,31 @@ SYM_DEV void epilogue(const DecodeEpi& e, f32x4 v, int tile, int m, bool mok, in
   const int n0 = tile * 16;
   if constexpr (EPI == DECODE_EPI_F32) {
     if (mok) *reinterpret_cast<float4*>(e.y + (long long)m * N + n0 + 4 * h) = make_float4(v[0], v[1], v[2], v[3]);
-  } else if constexpr (EPI == DECODE_EPI_XPUSH) {
+  } else if constexpr (EPI == DECODE_EPI_XAR) {
+    // the residual epilogue's own operands first (no peer involved), then push, collect, finish
+    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint2 wraw = make_uint2(0, 0);
+    const long long goff = xar_goff(m, N, n0 + 4 * h);
     if (mok) {
-      const long long off = XG_FLAG_BYTES + ((long long)(xep & 1u) * e.xp.world + e.xp.rank) * e.xp.slot_bytes +
-                            ((long long)m * N + n0 + 4 * h) * 4;
-      const float4 val = make_float4(v[0], v[1], v[2], v[3]);
-      for (int r = 0; r < e.xp.world; ++r) *reinterpret_cast<float4*>(e.xp.bufs[r] + off) = val;
+      r = *reinterpret_cast<const float4*>(e.resid + (long long)m * N + n0 + 4 * h);
+      wraw = *reinterpret_cast<const uint2*>(e.w_next + n0 + 4 * h);
+      xar_push(e.xp, v, goff, xep);
     }
+    const f32x4 t = mok ? xar_collect(e.xp, v, goff, xep) : f32x4{0.f, 0.f, 0.f, 0.f};
+    float sq = 0.f;
+    if (mok) {
+      const float rr[4] = {r.x + t[0], r.y + t[1], r.z + t[2], r.w + t[3]};
+      Pack8 wp;
+      wp.u = make_uint4(wraw.x, wraw.y, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sq += rr[i] * rr[i];
+      *reinterpret_cast<float4*>(e.resid + (long long)m * N + n0 + 4 * h) = make_float4(rr[0], rr[1], rr[2], rr[3]);
+      store4bf(e.xw_out + (long long)m * N + n0 + 4 * h, rr[0] * (float)wp.h[0], rr[1] * (float)wp.h[1],
+               rr[2] * (float)wp.h[2], rr[3] * (float)wp.h[3]);
+    }
+    sq += __shfl_xor(sq, 16, 64);
+    sq += __shfl_xor(sq, 32, 64);
+    if (mok && h == 0) e.ss_out[(long long)m * (N / 16) + tile] = sq;
   } else if constexpr (EPI == DECODE_EPI_QKV) {
     const int D = 128;
     const int head = n0 / D, jj = (n0 % D) / 16;

@@ -29,9 +29,26 @@
 #include "common.h"
 #include "decode_epi.h"
 #include "launchers.h"
+#include "xgmi_proto.h"
 
 namespace {
 
+
+// This lane's share of one row's sum-of-squares partials (deferred RMSNorm prologue): 16-B loads when the row
+// holds a multiple of 4 (the d / 16 per-tile partials of the fused epilogues: 256 for d = 4096 = ONE load per
+// lane instead of four dependent 4-B ones)
+SYM_DEV float ss_row_share(const float* __restrict__ row, int n, int lane) {
+  float s = 0.f;
+  if ((n & 3) == 0) {
+    for (int i = 4 * lane; i < n; i += 256) {
+      const float4 q = *reinterpret_cast<const float4*>(row + i);
+      s += (q.x + q.y) + (q.z + q.w);
+    }
+  } else {
+    for (int i = lane; i < n; i += 64) s += row[i];
+  }
+  return s;
+}
 
 // One workgroup-tile of the decode GEMM (RT consecutive 16-row weight tiles starting at 16 * RT * blk).
 // (The persistent MLP / attention-block launches that once reused this body with device-side phase waits
@@ -69,7 +86,8 @@ SYM_DEV void gemm_tile(const bf16* __restrict__ x, const bf16* __restrict__ W, i
   __shared__ f32x4 red[NW][RT * MT][64];
   __shared__ float rn_s[64];
   unsigned xep = 0;
-  if constexpr (EPI == DECODE_EPI_XPUSH) xep = xp_epoch(e.xp);
+  unsigned long long xold = 0;
+  if constexpr (EPI == DECODE_EPI_XAR) xold = xg_epoch_arrive(e.xp);  // resolved after the weight stream
 
   f32x4 acc[RT][MT];
 #pragma unroll
@@ -87,9 +105,7 @@ SYM_DEV void gemm_tile(const bf16* __restrict__ x, const bf16* __restrict__ W, i
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int m = m0 + j * NW;
-          s[j] = 0.f;
-          if (m < M)
-            for (int i = lane; i < e.ss_tiles; i += 64) s[j] += e.ss_in[(long long)m * e.ss_tiles + i];
+          s[j] = m < M ? ss_row_share(e.ss_in + (long long)m * e.ss_tiles, e.ss_tiles, lane) : 0.f;
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -186,6 +202,7 @@ SYM_DEV void gemm_tile(const bf16* __restrict__ x, const bf16* __restrict__ W, i
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) red[wid][rt * MT + mt][lane] = acc[rt][mt];
   __syncthreads();
+  if constexpr (EPI == DECODE_EPI_XAR) xep = xg_epoch_resolve(e.xp, xold, gridDim.x);
   // parallel epilogue: wave `wid` finishes accumulator tiles job = wid, wid + NW, ...
   for (int job = wid; job < RT * MT; job += NW) {
     const int rt = job / MT, mt = job % MT;
@@ -198,12 +215,6 @@ SYM_DEV void gemm_tile(const bf16* __restrict__ x, const bf16* __restrict__ W, i
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] *= sc;
     epilogue<EPI>(e, v, tile0 + rt, m, mok, h, N, xep);
-  }
-  if constexpr (EPI == DECODE_EPI_XPUSH) {  // every wave's slot stores acknowledged, then the tile flags
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const int tid = threadIdx.x;
-    if (tid < RT * e.xp.world) xp_flag(e.xp, tid % e.xp.world, tile0 + tid / e.xp.world, xep);
   }
 }
 
@@ -317,6 +328,14 @@ SYM_DEV void xres_body(const bf16* __restrict__ x, const bf16* __restrict__ W, i
   const int nf = NF > b ? (NF - b + G - 1) / G : 0;
   const int np = P > b ? (P - b + G - 1) / G : 0;
   const int nu = nf + np;
+  unsigned long long xold = 0;
+  if constexpr (EPI == DECODE_EPI_XAR) {
+    xold = xg_epoch_arrive(e.xp);  // every workgroup counts in (resolved once the weight stream is in flight)
+    if (nu == 0) {
+      xg_epoch_resolve(e.xp, xold, G);
+      return;
+    }
+  }
   if (nu == 0) return;  // uniform over the workgroup
   auto unit_tile = [&](int i) { return i < nf ? b + i * G : NF + (b + (i - nf) * G) / PDIV; };
   auto unit_active = [&](int i) { return KS == 1 || i < nf || wid / WPS == (b + (i - nf) * G) % KS; };
@@ -358,15 +377,13 @@ SYM_DEV void xres_body(const bf16* __restrict__ x, const bf16* __restrict__ W, i
   __shared__ float rn_s[16];
   if (e.ss_in) {  // deferred-RMSNorm row scales, once per workgroup
     for (int m = wid; m < M; m += NW) {
-      float sacc = 0.f;
-      for (int i = lane; i < e.ss_tiles; i += 64) sacc += e.ss_in[(long long)m * e.ss_tiles + i];
-      sacc = wave_sum(sacc);
+      const float sacc = wave_sum(ss_row_share(e.ss_in + (long long)m * e.ss_tiles, e.ss_tiles, lane));
       if (lane == 0) rn_s[m] = rsqrtf(sacc * e.inv_d + e.eps);
     }
   }
   __shared__ f32x4 red[2][NW][64];
   unsigned xep = 0;
-  if constexpr (EPI == DECODE_EPI_XPUSH) xep = xp_epoch(e.xp);
+  if constexpr (EPI == DECODE_EPI_XAR) xep = xg_epoch_resolve(e.xp, xold, G);
   const int m = r16;
   const bool mok = m < M;
   auto finish = [&](f32x4 v, int t, int hf = -1) {  // wave 0: row scale + epilogue of a final tile (or half)
@@ -374,10 +391,6 @@ SYM_DEV void xres_body(const bf16* __restrict__ x, const bf16* __restrict__ W, i
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] *= sc;
     epilogue<EPI>(e, v, t, m, mok && (hf < 0 || (h & 1) == hf), h, N, xep);
-    if constexpr (EPI == DECODE_EPI_XPUSH) {  // wave 0 stored the whole tile: acknowledged, then flag it
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane < e.xp.world) xp_flag(e.xp, lane, t, xep);
-    }
   };
   int buf = 0;
   for (int i = 0; i < nu; ++i) {
@@ -499,7 +512,8 @@ bool go_xres(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi&
   // remainder split: weight bytes on the busiest CU, f K + q K / KS, must drop >= 10 % (<= 4 parts per
   // workgroup, >= 4 waves per part)
   const int f = ntiles / C, R = ntiles - f * C;
-  if (g_dg_ksplit && R > 0 && e.ks_ws && e.ks_cnt && e.ks_ncnt >= R && EPI != DECODE_EPI_ARGMAX) {
+  if (g_dg_ksplit && R > 0 && e.ks_ws && e.ks_cnt && e.ks_ncnt >= R && EPI != DECODE_EPI_ARGMAX &&
+      EPI != DECODE_EPI_XAR) {
     long long best = (long long)per * K * 9 / 10;
     for (int ks = 2; ks <= 4; ks *= 2) {
       const int parts = R * ks, g = f > 0 ? C : std::min(C, parts), q = (parts + g - 1) / g;
@@ -656,6 +670,55 @@ void launch_epi(const bf16* x, const bf16* W, int M, int N, int K, const DecodeE
 }  // namespace
 
 
+// ---- DECODE_EPI_XAR: row-parallel projection + xGMI all-reduce + residual epilogue in ONE launch ----------
+// Every workgroup pushes its tiles to every rank, then WAITS for the other ranks' copies of the same tiles: the
+// whole grid must be resident at once (a waiting workgroup holds its CU), so only one-tile-per-workgroup
+// decompositions whose grid fits the occupancy are used -- the x-resident walk (one workgroup per CU) or
+// gemm_tile with 8 / 4 waves -- and the caller falls back to GEMM + add_prep launches otherwise.
+template <typename Kern>
+bool xar_resident(Kern kern, int threads, long long grid) {
+  int dev = 0, cus = 0, per_cu = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0);
+  return per_cu > 0 && grid <= (long long)cus * per_cu;
+}
+
+template <int MT>
+bool xar_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e0, hipStream_t s) {
+  constexpr int U0 = MT == 1 ? 4 : (MT == 2 ? 2 : 1);
+  DecodeEpi e = e0;
+  e.wnt = g_wnt;
+  if constexpr (MT == 1) {
+    if (e.wshuf && K % 1024 == 0 && K <= 4096 && go_xres<DECODE_EPI_XAR>(x, W, M, N, K, e, s)) return true;
+  }
+  // 8 waves per tile where the plain launch would use them (else, or when 8-wave workgroups do not all fit at
+  // once -- e.g. Llama-3-70B down at TP = 8: 512 tiles -- 4 waves)
+  const int grid = N / 16;
+  if (K % 512 == 0 && !(N <= 4096 && K >= 4096) &&
+      xar_resident(decode_gemm_kernel<MT, 8, U0, 1, DECODE_EPI_XAR>, 512, grid)) {
+    decode_gemm_kernel<MT, 8, U0, 1, DECODE_EPI_XAR><<<grid, 512, 0, s>>>(x, W, M, N, K, e);
+    return true;
+  }
+  if (K % 256 || !xar_resident(decode_gemm_kernel<MT, 4, U0, 1, DECODE_EPI_XAR>, 256, grid)) return false;
+  decode_gemm_kernel<MT, 4, U0, 1, DECODE_EPI_XAR><<<grid, 256, 0, s>>>(x, W, M, N, K, e);
+  return true;
+}
+
+template <int MT, int NW, int U>
+__global__ __launch_bounds__(NW * 64) void decode_gemm_xar_multi_kernel(XarMulti m, const bf16* __restrict__ W,
+                                                                       int M, int N, int K) {
+  const int r = blockIdx.z;
+  gemm_tile<MT, NW, U, 1, DECODE_EPI_XAR>(m.x[r], W, M, N, K, m.e[r], blockIdx.x);
+}
+
+template <int U>
+__global__ __launch_bounds__(1024) void decode_gemm_xar_multi_xres_kernel(XarMulti m, const bf16* __restrict__ W,
+                                                                          int M, int N, int K) {
+  const int r = blockIdx.z;
+  xres_body<U, 1, DECODE_EPI_XAR>(m.x[r], W, M, N, K, m.e[r], N / 16, 0, blockIdx.x, gridDim.x);
+}
+
 void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e,
                         hipStream_t s) {
   switch (epi) {
@@ -663,11 +726,60 @@ void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int
     case DECODE_EPI_QKV: launch_epi<DECODE_EPI_QKV>(x, W, M, N, K, e, s); break;
     case DECODE_EPI_RESID: launch_epi<DECODE_EPI_RESID>(x, W, M, N, K, e, s); break;
     case DECODE_EPI_SWIGLU: launch_epi<DECODE_EPI_SWIGLU>(x, W, M, N, K, e, s); break;
-    case DECODE_EPI_XPUSH: launch_epi<DECODE_EPI_XPUSH>(x, W, M, N, K, e, s); break;
     default: launch_epi<DECODE_EPI_ARGMAX>(x, W, M, N, K, e, s); break;
   }
 }
 
+
+bool launch_decode_gemm_xar(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, hipStream_t s) {
+  if (M < 1 || M > 64 || N % 16 || N / 16 >= XG_KEYS_WG) return false;
+  switch ((M + 15) / 16) {
+    case 1: return xar_mt<1>(x, W, M, N, K, e, s);
+    case 2: return xar_mt<2>(x, W, M, N, K, e, s);
+    case 3: return xar_mt<3>(x, W, M, N, K, e, s);
+    default: return xar_mt<4>(x, W, M, N, K, e, s);
+  }
+}
+
+static_assert(sizeof(XarMulti) <= 4000, "XarMulti must fit the kernel argument space");
+
+bool launch_decode_gemm_xar_multi(const XarMulti& m, int world, const bf16* W, int M, int N, int K, int xres,
+                                  hipStream_t s) {
+  if (M < 1 || M > 16 || N % 16 || world < 1 || world > XAR_MULTI_MAX) return false;
+  int dev = 0, cus = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (xres) {  // x-resident walk, ~cus / world workgroups per rank (one per CU, all ranks resident)
+    if (K % 1024 || K > 4096 || !m.e[0].wshuf) return false;
+    const int G = std::max(1, std::min(N / 16, cus / world));
+    const dim3 grid(G, 1, world);
+    switch (K / 1024) {
+      case 1:
+        if (!xar_resident(decode_gemm_xar_multi_xres_kernel<1>, 1024, (long long)G * world)) return false;
+        decode_gemm_xar_multi_xres_kernel<1><<<grid, 1024, 0, s>>>(m, W, M, N, K);
+        return true;
+      case 2:
+        if (!xar_resident(decode_gemm_xar_multi_xres_kernel<2>, 1024, (long long)G * world)) return false;
+        decode_gemm_xar_multi_xres_kernel<2><<<grid, 1024, 0, s>>>(m, W, M, N, K);
+        return true;
+      case 4:
+        if (!xar_resident(decode_gemm_xar_multi_xres_kernel<4>, 1024, (long long)G * world)) return false;
+        decode_gemm_xar_multi_xres_kernel<4><<<grid, 1024, 0, s>>>(m, W, M, N, K);
+        return true;
+      default: return false;
+    }
+  }
+  if (K % 256) return false;
+  const dim3 grid(N / 16, 1, world);
+  if (K % 512 == 0) {
+    if (!xar_resident(decode_gemm_xar_multi_kernel<1, 8, 4>, 512, (long long)(N / 16) * world)) return false;
+    decode_gemm_xar_multi_kernel<1, 8, 4><<<grid, 512, 0, s>>>(m, W, M, N, K);
+  } else {
+    if (!xar_resident(decode_gemm_xar_multi_kernel<1, 4, 4>, 256, (long long)(N / 16) * world)) return false;
+    decode_gemm_xar_multi_kernel<1, 4, 4><<<grid, 256, 0, s>>>(m, W, M, N, K);
+  }
+  return true;
+}
 
 void set_decode_ksplit(int on) { g_dg_ksplit = on != 0; }
 void set_decode_halves(int on) { g_dg_halves = on != 0; }

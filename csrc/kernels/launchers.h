@@ -15,7 +15,10 @@ enum {
   DECODE_EPI_RESID = 2,
   DECODE_EPI_SWIGLU = 3,
   DECODE_EPI_ARGMAX = 4,
-  DECODE_EPI_XPUSH = 5,  // fp32 tile straight into every TP rank's xGMI slot + a per-tile flag (row-parallel)
+  // row-parallel projection under TP, all-reduced in the launch: every tile's values go to every other rank as
+  // epoch-tagged granules, the tile's workgroup sums every rank's copy in rank order and runs the RESID
+  // epilogue (residual add + next-norm prep, ss per 16-column tile) -- decode_epi.h, xar_push / xar_collect
+  DECODE_EPI_XAR = 6,
 };
 
 // xGMI communicator buffer layout (xgmi_ar.hip): header (collective counter) | flags [XG_MAX_WG][XG_MAX_WORLD]
@@ -25,11 +28,13 @@ constexpr int XG_MAX_WG = 4096;
 constexpr int XG_KEYS_WG = XG_MAX_WG - 1;  // flag word of the sampling-keys collective (others stay below)
 constexpr long long XG_HDR_BYTES = 256;   // [0] u32 epoch mirror, [64] u64 {epoch, arrivals} of the current collective
 constexpr long long XG_FLAG_BYTES = XG_HDR_BYTES + (long long)XG_MAX_WG * XG_MAX_WORLD * 4;
-// DECODE_EPI_XPUSH target: every rank's mapped buffer; the GEMM reads (never bumps) this rank's counter
-struct XgmiPush {
-  char* bufs[XG_MAX_WORLD] = {};
+// One xGMI communicator as seen by a kernel (xgmi_ar.hip protocol; also the DECODE_EPI_XAR target)
+struct XgmiArgs {
+  char* bufs[XG_MAX_WORLD] = {};  // every rank's comm buffer as mapped in this process (own one included; its
+                                  // header holds this rank's collective counter)
+  int* err = nullptr;             // local error word (a peer never arrived / a fault was declared; host-mapped)
   int rank = 0, world = 0;
-  long long slot_bytes = 0;
+  long long slot_bytes = 0;       // bytes of one (parity, source rank) data slot
 };
 struct DecodeEpi {
   // weight layout: 0 = row-major [N][K]; 1 = MFMA-preshuffled (models/layout.py::preshuffle): each
@@ -65,8 +70,8 @@ struct DecodeEpi {
   const long long* step = nullptr;
   unsigned long long* keys = nullptr;
   int n_offset = 0;
-  // XPUSH (row-parallel projection under TP): y tiles go to slot (parity, rank) of every rank's buffer
-  XgmiPush xp;
+  // XAR (row-parallel projection under TP): the all-reduce communicator (granule slots, decode_epi.h)
+  XgmiArgs xp;
   // split-K workspace of the x-resident decode GEMM (decode_gemm.hip, go_xres): ks_ws fp32 partial tiles
   // (256 floats per (tile, split)), ks_cnt one arrival counter per 16-row tile (zero, re-armed in-launch);
   // nullptr -> whole-K tiles only
@@ -81,6 +86,18 @@ void set_decode_halves(int on);       // x-resident decode GEMM remainder tiles 
 void set_decode_gemm_nt(int on);      // non-temporal weight-stream loads (keeps the variant choice)
 void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e,
                         hipStream_t s);
+// Row-parallel decode projection + xGMI all-reduce + residual add + next-norm prep in ONE launch
+// (DECODE_EPI_XAR).  false (nothing launched): no variant whose whole grid is co-resident on this GPU (the
+// workgroups wait on their peers' tiles) -- the caller runs the two-launch form.
+bool launch_decode_gemm_xar(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, hipStream_t s);
+// test-only: every rank of this process in ONE launch (grid z = rank; co-residency checked)
+constexpr int XAR_MULTI_MAX = 8;
+struct XarMulti {
+  const bf16* x[XAR_MULTI_MAX];
+  DecodeEpi e[XAR_MULTI_MAX];
+};
+bool launch_decode_gemm_xar_multi(const XarMulti& m, int world, const bf16* W, int M, int N, int K, int xres,
+                                  hipStream_t s);
 // ss: [T][parts] partial sums of squares, as launch_add_prep
 void launch_embed_prep(const int* ids, const int* src, const int* prev, const bf16* table, float* resid, const bf16* w,
                        bf16* xw, float* ss, int T, int d, int parts, hipStream_t s);
@@ -159,13 +176,6 @@ void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_l
 
 // xgmi_ar.hip: one-shot all-reduce over xGMI peer memory (IPC-mapped buffers of every TP rank); the
 // constants and the push descriptor live at the top of this header (the decode GEMMs push into the slots)
-struct XgmiArgs {
-  char* bufs[XG_MAX_WORLD];  // every rank's comm buffer as mapped in this process (own one included; its
-                             // header holds this rank's collective counter)
-  int* err;                  // local error word (a peer never arrived)
-  int rank, world;
-  long long slot_bytes;      // bytes of one (parity, source rank) data slot
-};
 long long xgmi_buffer_bytes(int world, long long slot_bytes);
 int xgmi_chunk(long long n, long long max_wg);
 void launch_xgmi_all_reduce(const XgmiArgs& c, const void* in, void* out, long long n, int elem, hipStream_t s);
@@ -189,11 +199,6 @@ struct XgmiMulti {
 void launch_xgmi_all_reduce_multi(const XgmiMulti& m, int world, long long n, int elem, hipStream_t s);
 void launch_xgmi_add_prep_multi(const XgmiMulti& m, int world, int T, int d, int parts, hipStream_t s);
 void launch_xgmi_keys_max_multi(const XgmiMulti& m, int world, int B, hipStream_t s);
-// the reduce half of a GEMM-pushed row-parallel all-reduce (DECODE_EPI_XPUSH): wait for every rank's tile
-// flags of this part's columns, sum the slots in rank order + residual add + next-norm prep (add_prep)
-void launch_xgmi_reduce_add_prep(const XgmiArgs& c, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d,
-                                 int parts, hipStream_t s);
-void launch_xgmi_reduce_add_prep_multi(const XgmiMulti& m, int world, int T, int d, int parts, hipStream_t s);
 // R3: unpadded expert all-to-all over xGMI peer memory (xgmi_ar.hip, xgmi_a2a_kernel).  Block q of `src` (rows
 // [q cap, q cap + counts[q]), counts read on the DEVICE) lands as block `rank` of rank q's `dst`; only routed rows
 // cross the links (no worst-case capacity padding on the wire).  Slot (parity, source) of the communicator's

@@ -28,61 +28,11 @@
 // spin sees that word and exits at once (xg_fault_declared).
 #include "common.h"
 #include "launchers.h"
+#include "xgmi_proto.h"
 
 namespace {
 
 constexpr int XG_THREADS = 256;
-// 30 s of the 100 MHz wall clock: a peer that never arrives is an error, not a hang.  Long enough for the
-// first collectives of a provider start-up, where ranks can drift by the time each one spends loading
-// library GEMM code objects before its first prefill.
-constexpr unsigned long long XG_WAIT_TICKS = 3000000000ull;
-
-// Fault containment: once the error word is set -- by an earlier collective that gave up on a peer, or by the
-// host's health monitor that saw a rank die (parallel/health.py) -- no collective waits any more: the step
-// finishes with garbage that the host discards, so a dead peer costs at most ONE wait limit per provider, not
-// one per collective (a captured 70B TP=8 step holds 161).  The word is host-mapped (a PCIe round trip), so a
-// spin reads it only after 16 polls and then every 256: a collective whose peers are on time never pays it.
-SYM_DEV bool xg_fault_declared(const XgmiArgs& c, int it) {
-  return (it & 255) == 16 && __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
-}
-
-SYM_DEV char* xg_slot(const XgmiArgs& c, int r, int par, int src) {
-  return c.bufs[r] + XG_FLAG_BYTES + ((long long)par * c.world + src) * c.slot_bytes;
-}
-
-// Push this workgroup's chunk (nvec 16-byte vectors at byte offset `off`) into slot (parity, rank) of
-// every rank's buffer (its own included, so the reduce reads all slots from one place), signal, wait for
-// every rank's signal of the same chunk.  Returns the epoch parity (the slot set to reduce).
-// This workgroup's epoch of the current collective (nwg workgroups per rank in the launch).
-SYM_DEV unsigned xg_epoch(const XgmiArgs& c, int nwg) {
-  __shared__ unsigned s_epoch;
-  if (threadIdx.x == 0) {
-    // ONE returning atomic per workgroup on a packed {epoch (high 32), arrivals (low 32)} word: the add
-    // counts this workgroup in and returns the epoch of the previous collective in the same round trip
-    // (round 2 read the counter, waited, then counted in: two dependent round trips to uncached memory on
-    // every collective).  The last arrival folds the arrivals back into an epoch increment -- the next
-    // collective on the stream starts after this launch retired, so it finds {e, 0} -- and mirrors the
-    // epoch into the u32 at byte 0 that the XPUSH GEMM epilogue (decode_epi.h, xp_epoch) reads.
-    unsigned long long* w = reinterpret_cast<unsigned long long*>(c.bufs[c.rank] + 64);
-    const unsigned long long old = __hip_atomic_fetch_add(w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned e = (unsigned)(old >> 32) + 1u;
-    if ((unsigned)old == (unsigned)nwg - 1u) {  // last to arrive: every workgroup has counted itself in
-      __hip_atomic_fetch_add(w, (1ull << 32) - (unsigned long long)nwg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(reinterpret_cast<unsigned*>(c.bufs[c.rank]), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_epoch = e;
-  }
-  __syncthreads();
-  return s_epoch;
-}
-
-// Test hook: hold this rank's workgroups back before they push (a slow peer), `delay` wall-clock ticks.
-SYM_DEV void xg_delay(unsigned long long delay) {
-  if (delay == 0) return;
-  const unsigned long long t0 = wall_clock64();
-  while (wall_clock64() - t0 < delay) __builtin_amdgcn_s_sleep(8);
-}
-
 // Push this workgroup's chunk (nvec vectors at byte offset `off`) into slot (parity, rank) of every rank's
 // buffer (its own included, so the reduce reads all slots from one place), raise flag (wg, rank) in every
 // rank, wait for every rank's flag (wg, src).  `wg` indexes flags only; `nwg` = workgroups of this rank in
@@ -257,72 +207,6 @@ SYM_DEV void xg_add_prep_body(const XgmiArgs& c, int row, int part, int T, int P
   if (threadIdx.x == 0) ss[row * P + part] = acc;
 }
 
-// Reduce half of a GEMM-pushed row-parallel all-reduce: the decode GEMM (DECODE_EPI_XPUSH, same epoch:
-// it reads the counter this kernel bumps) already stored its fp32 [T][d] tile columns into slot (parity,
-// rank) of every rank and raised flag (tile, rank) per 16-column tile.  Workgroup (row, part) waits for
-// every source's flags of the tiles covering its columns, then sums the slots in rank order and applies
-// the residual add + next-norm prep exactly like xg_add_prep_body (bit-identical results on every rank).
-SYM_DEV void xg_reduce_add_prep_body(const XgmiArgs& c, int row, int part, int T, int P, float* __restrict__ resid,
-                                     const bf16* __restrict__ w, bf16* __restrict__ xw, float* __restrict__ ss,
-                                     int d, unsigned long long delay = 0) {
-  __shared__ float scratch[XG_THREADS / 64];
-  const unsigned epoch = xg_epoch(c, T * P);
-  xg_delay(delay);
-  const int par = (int)(epoch & 1u);
-  const int dp = d / P;
-  const int t0 = part * dp / 16, nt = dp / 16;
-  const unsigned* flags = reinterpret_cast<const unsigned*>(c.bufs[c.rank] + XG_HDR_BYTES);
-  for (int i = threadIdx.x; i < nt * c.world; i += XG_THREADS) {
-    const int tile = t0 + i / c.world, src = i % c.world;
-    const unsigned* f = flags + tile * XG_MAX_WORLD + src;
-    const unsigned long long w0 = wall_clock64();
-    int it = 0;
-    while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-      if (xg_fault_declared(c, ++it)) break;
-      if (wall_clock64() - w0 > XG_WAIT_TICKS) {
-        __hip_atomic_store(c.err, 1 + src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-  const long long rb = (long long)row * d + (long long)part * dp;
-  const long long off = rb * 4;
-  const bf16* wp = w + (long long)part * dp;
-  float acc = 0.f;
-  for (int vi = threadIdx.x; vi < dp / 8; vi += XG_THREADS) {
-    float r[8], g[8];
-    float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < c.world; ++s) {
-      float dd[8];
-      load8f(reinterpret_cast<const float*>(xg_slot(c, c.rank, par, s) + off) + vi * 8, dd);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) sum[i] += dd[i];
-    }
-    load8f(resid + rb + vi * 8, r);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r[i] += sum[i];
-    store8f(resid + rb + vi * 8, r);
-    load8(wp + vi * 8, g);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      acc += r[i] * r[i];
-      g[i] *= r[i];
-    }
-    store8(xw + rb + vi * 8, g);
-  }
-  acc = block_sum<XG_THREADS>(acc, scratch);
-  if (threadIdx.x == 0) ss[row * P + part] = acc;
-}
-
-__global__ __launch_bounds__(XG_THREADS) void xgmi_reduce_add_prep_kernel(XgmiArgs c, float* __restrict__ resid,
-                                                                         const bf16* __restrict__ w,
-                                                                         bf16* __restrict__ xw,
-                                                                         float* __restrict__ ss, int d) {
-  xg_reduce_add_prep_body(c, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, resid, w, xw, ss, d);
-}
-
 // Vocab-parallel greedy / Gumbel sampling combine: every rank holds per-row packed u64 keys (order-
 // preserving value bits | inverted vocabulary index) of its vocabulary shard; the max over ranks is the
 // global argmax, and ids = 0xFFFFFFFF - low 32 bits.  One workgroup (rows <= 4096) on flag word XG_KEYS_WG.
@@ -379,11 +263,6 @@ __global__ __launch_bounds__(XG_THREADS) void xgmi_add_prep_multi_kernel(XgmiMul
                    xg_multi_delay(m, r));
 }
 
-__global__ __launch_bounds__(XG_THREADS) void xgmi_reduce_add_prep_multi_kernel(XgmiMulti m, int d) {
-  const int r = blockIdx.z;
-  xg_reduce_add_prep_body(m.c[r], blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, reinterpret_cast<float*>(m.out[r]),
-                          m.w, reinterpret_cast<bf16*>(m.xw[r]), m.ss[r], d, xg_multi_delay(m, r));
-}
 
 __global__ __launch_bounds__(XG_THREADS) void xgmi_keys_max_multi_kernel(XgmiMulti m, int B) {
   const int r = blockIdx.z;
@@ -525,17 +404,6 @@ void launch_xgmi_all_reduce_multi(const XgmiMulti& m, int world, long long n, in
 void launch_xgmi_add_prep_multi(const XgmiMulti& m, int world, int T, int d, int parts, hipStream_t s) {
   if (T == 0) return;
   xgmi_add_prep_multi_kernel<<<dim3(T, parts, world), XG_THREADS, 0, s>>>(m, d);
-}
-
-void launch_xgmi_reduce_add_prep(const XgmiArgs& c, float* resid, const bf16* w, bf16* xw, float* ss, int T, int d,
-                                 int parts, hipStream_t s) {
-  if (T == 0) return;
-  xgmi_reduce_add_prep_kernel<<<dim3(T, parts), XG_THREADS, 0, s>>>(c, resid, w, xw, ss, d);
-}
-
-void launch_xgmi_reduce_add_prep_multi(const XgmiMulti& m, int world, int T, int d, int parts, hipStream_t s) {
-  if (T == 0) return;
-  xgmi_reduce_add_prep_multi_kernel<<<dim3(T, parts, world), XG_THREADS, 0, s>>>(m, d);
 }
 
 void launch_xgmi_keys_max_multi(const XgmiMulti& m, int world, int B, hipStream_t s) {

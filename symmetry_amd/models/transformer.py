@@ -356,16 +356,16 @@ class TransformerLM:
             ops.add_prep(y, resid, w_next, xw, ss_p)
             return ss_p
         if self._tp_active():
+            fused = getattr(self.tp, "gemm_ar_resid", None)
+            if fused is not None and fused(x, W, sh, resid, w_next, xw, ss_t):
+                # GEMM + all-reduce + residual + next-norm prep in ONE launch (DECODE_EPI_XAR): ss per 16 columns
+                return ss_t
             # all-reduce + residual add + next-norm prep (one launch on the xGMI communicator); P column
             # parts per row = P workgroups per row (8 up to 16 rows, 4 beyond:
             # profiles/xgmi_allreduce_local_r2.jsonl, add_prep_P*), P sum-of-squares partials per row
             d = resid.shape[1]
             P = next((p for p in ((8, 4, 2) if M <= 16 else (4, 2)) if d % (16 * p) == 0), 1)
             ss_p = self._buf(f"ss_tp{P}", (M, P), torch.float32)
-            push = getattr(self.tp, "gemm_add_prep", None)
-            if push is not None and push(x, W, sh, resid, w_next, xw, ss_p):
-                # the GEMM epilogue pushes its tiles into every rank's slot; one reduce launch follows
-                return ss_p
             y = self._buf(name + ".f32", (x.shape[0], W.shape[0]), torch.float32)
             ops.dg_f32(x, W, None, 0.0, y, wshuf=sh)
             self.tp.all_reduce_add_prep(y, resid, w_next, xw, ss_p)

@@ -31,6 +31,11 @@ import torch
 import torch.distributed as dist
 
 
+# Row-parallel decode projections under TP run GEMM + all-reduce + residual epilogue as ONE launch
+# (XgmiComm.gemm_ar_resid); SYMMETRY_XGMI_FUSED=0 restores GEMM + the fused all-reduce / add_prep launch (A/B)
+XAR = os.environ.get("SYMMETRY_XGMI_FUSED", "1") != "0"
+
+
 class Comm:
     rank: int = 0
     world: int = 1
@@ -178,12 +183,8 @@ class XgmiComm(Comm):
         dev = torch.device(device)
         self.slot_bytes = int(slot_bytes)
         self.calls = {"all_reduce": 0, "add_prep": 0}  # collectives issued on the xGMI kernels (host count)
-        # SYMMETRY_XGMI_PUSH=1: row-parallel decode projections push their tiles into the peers' slots from the
-        # GEMM epilogue (+ one reduce launch) instead of GEMM into a local fp32 buffer + the fused all-reduce /
-        # add_prep launch.  Off by default: on one GPU (world-1 communicator, no link latency) it measured
-        # 1.535 vs 1.522 ms per TP=8-shard step (profiles/r3/tp_shard_push_ab.jsonl); its point -- the remote
-        # stores overlapping the GEMM -- needs real xGMI links to show
-        self.push = os.environ.get("SYMMETRY_XGMI_PUSH", "0") == "1"
+        self.xar = None  # the fused row-parallel GEMM + all-reduce communicator (attach_xar)
+        self.a2a = None  # the expert all-to-all communicator (attach_a2a)
         try:
             self.handle = int(self.ops.xgmi_create(int(slot_bytes), self.world, self.rank, dev.index or 0))
             mine = self.ops.xgmi_ipc_handle(self.handle)
@@ -218,20 +219,6 @@ class XgmiComm(Comm):
         else:
             super().all_reduce_add_prep(y, resid, w_next, xw, ss)
 
-    def gemm_add_prep(self, x, W, wshuf, resid, w_next, xw, ss) -> bool:
-        """Row-parallel decode projection + all-reduce + residual add + next-norm prep as ONE GEMM launch
-        whose epilogue pushes its fp32 tiles into every rank's slot, then one reduce launch
-        (``xgmi_gemm_add_prep``).  Returns False when the shapes do not fit (the caller runs GEMM + add_prep)."""
-        if not self.push or not x.is_cuda or x.shape[0] > 64 or W.shape[0] % 16 or x.shape[1] % 256:
-            return False
-        P = ss.shape[1] if ss.dim() == 2 else 1
-        d = resid.shape[1]
-        if x.shape[0] * d * 4 > self.slot_bytes or d % (16 * P) or W.shape[0] != d:
-            return False
-        self.ops.xgmi_gemm_add_prep(x, W, bool(wshuf), resid, w_next, xw, ss, self.handle)
-        self.calls["gemm_add_prep"] = self.calls.get("gemm_add_prep", 0) + 1
-        return True
-
     # ---- R3: unpadded expert all-to-all on a second peer-memory communicator ------------------------------
     def attach_a2a(self, group, cap: int, row_bytes: int) -> None:
         """Collective (every rank): a second xGMI communicator whose slots hold ``cap`` rows of up to
@@ -243,7 +230,7 @@ class XgmiComm(Comm):
         self.calls["a2a"] = 0
 
     def a2a_fits(self, cap: int, row_bytes: int) -> bool:
-        return getattr(self, "a2a", None) is not None and cap <= self.a2a_cap and row_bytes <= self.a2a_row_bytes
+        return self.a2a is not None and cap <= self.a2a_cap and row_bytes <= self.a2a_row_bytes
 
     def a2a_rows(self, src, counts, side, dst, dst_side=None, dst_counts=None) -> None:
         """Block q of ``src`` ([world * cap, ...] rows; its first ``counts[q]`` -- a DEVICE int32 [world] -- are
@@ -251,6 +238,26 @@ class XgmiComm(Comm):
         cap = src.shape[0] // self.world
         self.ops.xgmi_a2a(src, counts, side, dst, dst_side, dst_counts, cap, self.a2a.handle)
         self.calls["a2a"] += 1
+
+    def attach_xar(self, group, rows: int, d: int) -> None:
+        """Collective (every rank): the communicator of the fused row-parallel decode projections -- slots of
+        ``rows`` x ``d`` epoch-tagged 8-B granules (csrc/kernels/decode_epi.h, xar_push / xar_collect)."""
+        self.xar = XgmiComm(self.inner, group, torch.device("cuda", torch.cuda.current_device()),
+                            slot_bytes=(int(rows) * int(d) * 8 + 255) // 256 * 256)
+
+    def gemm_ar_resid(self, x, W, wshuf, resid, w_next, xw, ss) -> bool:
+        """Row-parallel decode projection + all-reduce + residual add + next-norm prep as ONE launch
+        (``DECODE_EPI_XAR``): ``ss`` gets one sum-of-squares partial per 16 columns ([M, d / 16], the layout
+        the single-GPU dg_resid writes).  False: shapes or occupancy do not fit (the caller runs GEMM +
+        ``all_reduce_add_prep``)."""
+        if not XAR or self.xar is None or not x.is_cuda or x.shape[0] > 64 or W.shape[0] % 16 or x.shape[1] % 256:
+            return False
+        if x.shape[0] * resid.shape[1] * 8 > self.xar.slot_bytes or ss.shape[1] != W.shape[0] // 16:
+            return False
+        ok = bool(self.ops.xgmi_gemm_ar_resid(x, W, bool(wshuf), resid, w_next, xw, ss, self.xar.handle))
+        if ok:
+            self.calls["gemm_ar"] = self.calls.get("gemm_ar", 0) + 1
+        return ok
 
     def argmax_keys(self, keys, ids):
         if keys.is_cuda and keys.is_contiguous() and keys.numel() <= 4096:
@@ -273,20 +280,24 @@ class XgmiComm(Comm):
         (the communicator stays failed); host-mapped, so it costs no device synchronisation: the model runner
         polls it after every step.  Covers the all-to-all communicator too."""
         e = int(self.ops.xgmi_error(self.handle))
-        if not e and getattr(self, "a2a", None) is not None:
-            e = int(self.ops.xgmi_error(self.a2a.handle))
+        for sub in (self.xar, self.a2a):
+            if not e and sub is not None:
+                e = int(self.ops.xgmi_error(sub.handle))
         return e
 
     def set_error(self, code: int) -> None:
         """Declare a fault from the host (rank 0's health monitor): every spinning collective stops waiting."""
         self.ops.xgmi_set_error(self.handle, int(code))
-        if getattr(self, "a2a", None) is not None:
-            self.ops.xgmi_set_error(self.a2a.handle, int(code))
+        for sub in (self.xar, self.a2a):
+            if sub is not None:
+                self.ops.xgmi_set_error(sub.handle, int(code))
 
     def destroy(self, inner_too: bool = True):
-        if getattr(self, "a2a", None) is not None:
-            self.a2a.destroy(inner_too=False)
-            self.a2a = None
+        for name in ("xar", "a2a"):
+            sub = getattr(self, name, None)
+            if sub is not None:
+                sub.destroy(inner_too=False)
+                setattr(self, name, None)
         if self.handle is not None:
             self.ops.xgmi_destroy(self.handle)
         if inner_too and hasattr(self.inner, "destroy"):

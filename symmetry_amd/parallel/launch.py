@@ -108,6 +108,9 @@ def init_tp_engine(ecfg):
         ep_comm = comm
     if on_gpu:
         ecfg.device = f"cuda:{local}"
+    if isinstance(comm, XgmiComm):
+        # the fused row-parallel decode projections (GEMM + all-reduce + residual in one launch): <= 64 rows
+        comm.attach_xar(cpu_group, 64, mcfg.hidden_size)
     if ep_comm is not None and isinstance(comm, XgmiComm) and os.environ.get("SYMMETRY_MOE_XGMI_A2A", "1") != "0":
         # the unpadded expert all-to-all (prefill dispatch / return of routed rows) on its own peer buffers
         tokens = max(ecfg.max_num_batched_tokens, 8192)

@@ -58,9 +58,9 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None):
             eng.shutdown()  # the worker leaves its loop whatever happened here
         if xgmi == "1":
             calls = eng.runner.model.tp.calls
-            # decode steps ran the peer-memory all-reduce: fused into the row-parallel GEMMs (XPUSH epilogue
-            # + reduce launch) for the dense model, the fused add_prep kernel around the MoE block
-            assert calls.get("gemm_add_prep", 0) + calls["add_prep"] > 0, calls
+            # decode steps ran the peer-memory all-reduce: fused into the row-parallel GEMMs (one XAR launch each:
+            # GEMM + all-reduce + residual) for the dense model, the fused add_prep kernel around the MoE block
+            assert calls.get("gemm_ar", 0) + calls["add_prep"] > 0, calls
             assert calls.get("keys", 0) > 0, calls  # and the vocab-parallel sampling combine
             assert eng.runner.model.tp.error() == 0
         extra = {}

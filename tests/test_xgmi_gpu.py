@@ -204,60 +204,6 @@ def test_xgmi_mixed_geometry_with_slow_rank(gpu, world):
             ops.xgmi_destroy(h)
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-@pytest.mark.parametrize("M,shuf", [(1, True), (10, True), (10, False), (33, True)])
-def test_xgmi_gemm_push_then_reduce(gpu, world, M, shuf):
-    """Row-parallel projection under TP as GEMM-push + reduce: every rank's decode GEMM (XPUSH epilogue)
-    stores its fp32 tiles into slot (parity, rank) of every rank and flags each 16-column tile; the reduce
-    kernels (one launch, ranks as slices, one held back) wait for the flags of their columns, then add the
-    rank-ordered sum to the residual and prep the next norm.  Interleaved with plain add_prep collectives
-    so the two kinds share the counter / parity sequence; bit-identical on every rank, fp32-reference close."""
-    from symmetry_amd.models.layout import preshuffle
-    from symmetry_amd.ops import _native, reference
-
-    ops = _native.ops()
-    d, K = 4096, 1024
-    P = 8 if M <= 16 else 4
-    if world * M * P > 1024:
-        pytest.skip("the reduce slices of one launch would not all be co-resident")
-    hs = _comms(ops, world, slot_bytes=M * d * 4 + 256)
-    g = torch.Generator(device="cpu").manual_seed(world * 100 + M)
-    w = (torch.rand(d, generator=g) + 0.5).to(gpu, torch.bfloat16)
-    try:
-        r0 = torch.randn(M, d, generator=g).to(gpu)
-        for it in range(3):
-            xs = [torch.randn(M, K, generator=g).to(gpu, torch.bfloat16) for _ in range(world)]
-            Ws = [(torch.randn(d, K, generator=g) / K ** 0.5).to(gpu, torch.bfloat16) for _ in range(world)]
-            Wk = [preshuffle(W) if shuf else W for W in Ws]
-            resids = [r0.clone() for _ in range(world)]
-            xws = [torch.empty(M, d, dtype=torch.bfloat16, device=gpu) for _ in range(world)]
-            sss = [torch.empty(M, P, dtype=torch.float32, device=gpu) for _ in range(world)]
-            for r in range(world):
-                ops.xgmi_gemm_push(xs[r], Wk[r], shuf, hs[r])
-            ops.xgmi_reduce_add_prep_multi(resids, w, xws, sss, hs, it % world, 30)
-            torch.cuda.synchronize()
-            ysum = torch.zeros(M, d)
-            for x, W in zip(xs, Ws):
-                ysum += x.float().cpu() @ W.float().cpu().t()
-            r_ref, xw_ref, ss_ref = r0.cpu().clone(), torch.empty(M, d, dtype=torch.bfloat16), torch.empty(M, P)
-            reference.add_prep(ysum, r_ref, w.cpu(), xw_ref, ss_ref)
-            for r in range(world):
-                assert ops.xgmi_error(hs[r]) == 0
-                assert torch.equal(resids[r], resids[0]) and torch.equal(sss[r], sss[0])
-                torch.testing.assert_close(resids[r].cpu(), r_ref, rtol=1e-3, atol=1e-3)
-                torch.testing.assert_close(sss[r].cpu(), ss_ref, rtol=1e-3, atol=1e-1)
-            # a plain fused add_prep collective in between (shares the counter and the slot parities)
-            ys = [torch.randn(M, d, generator=g).to(gpu) for _ in range(world)]
-            ops.xgmi_add_prep_multi(ys, resids, w, xws, sss, hs)
-            torch.cuda.synchronize()
-            r0 = resids[0].clone()
-            for r in range(world):
-                assert torch.equal(resids[r], r0)
-    finally:
-        for h in hs:
-            ops.xgmi_destroy(h)
-
-
 def test_xgmi_declared_fault_stops_every_wait(gpu):
     """Fault containment: rank 1 of a world-2 communicator never runs.  (a) A collective already spinning on it
     ends promptly once the host declares the fault (``xgmi_set_error``, what rank 0's health monitor does), not
@@ -332,6 +278,49 @@ def test_xgmi_a2a_unpadded_exchange(gpu, world, dtype):
                     assert torch.isnan(got[n:].float()).all(), (r, s, n)  # nothing past the count was written
                     gs = dsides[r][s * cap:(s + 1) * cap]
                     assert torch.equal(gs[:n], sides[s][r * cap:r * cap + n]) and (gs[n:] == -1).all()
+    finally:
+        for h in hs:
+            ops.xgmi_destroy(h)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+@pytest.mark.parametrize("M", [1, 10, 16])
+@pytest.mark.parametrize("form", ["gemm8", "gemm4", "xres", "gemm8_shuf"])
+def test_xgmi_gemm_all_reduce_resid_one_launch(gpu, world, M, form):
+    """Row-parallel decode projection + xGMI all-reduce + residual add + next-norm prep as ONE launch
+    (DECODE_EPI_XAR): every workgroup pushes its fp32 tiles into every rank's slot, waits for the other ranks'
+    copies of the same tiles, sums them in rank order and runs the residual epilogue.  All ranks in one launch
+    (grid z = rank).  fp32 torch reference; every rank bit-identical; twice (both slot parities)."""
+    from symmetry_amd.models.layout import preshuffle
+    from symmetry_amd.ops import _native
+
+    ops = _native.ops()
+    N, K = {"gemm8": (1024, 512), "gemm4": (1024, 1792), "xres": (2048, 1024), "gemm8_shuf": (1024, 512)}[form]
+    shuf = form in ("xres", "gemm8_shuf")
+    hs = _comms(ops, world, slot_bytes=16 * N * 8 + 256)
+    g = torch.Generator(device="cpu").manual_seed(M * 31 + world)
+    try:
+        for it in range(2):
+            W = (torch.randn(N, K, generator=g) * K ** -0.5).to(gpu, torch.bfloat16)
+            Wk = preshuffle(W) if shuf else W
+            wn = (torch.rand(N, generator=g) + 0.5).to(gpu, torch.bfloat16)
+            xs = [torch.randn(M, K, generator=g).to(gpu, torch.bfloat16) for _ in range(world)]
+            r0 = torch.randn(M, N, generator=g).to(gpu)
+            resids = [r0.clone() for _ in range(world)]
+            xws = [torch.empty(M, N, dtype=torch.bfloat16, device=gpu) for _ in range(world)]
+            sss = [torch.empty(M, N // 16, device=gpu) for _ in range(world)]
+            ok = ops.xgmi_gemm_ar_resid_multi(xs, Wk, shuf, resids, wn, xws, sss, hs, form == "xres")
+            if not ok:
+                pytest.skip("grid not co-resident for this world size")
+            torch.cuda.synchronize()
+            ysum = sum(x.float() @ W.float().t() for x in xs)
+            r_ref = r0 + ysum
+            for r in range(world):
+                assert ops.xgmi_error(hs[r]) == 0
+                torch.testing.assert_close(resids[r], r_ref, rtol=2e-3, atol=2e-3)
+                assert torch.equal(resids[r], resids[0]) and torch.equal(sss[r], sss[0])
+                torch.testing.assert_close(xws[r].float(), (resids[r] * wn.float()).bfloat16().float(), rtol=0, atol=0)
+                torch.testing.assert_close(sss[r], (resids[r] ** 2).view(M, N // 16, 16).sum(-1), rtol=1e-5, atol=1e-4)
     finally:
         for h in hs:
             ops.xgmi_destroy(h)
