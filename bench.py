@@ -178,9 +178,11 @@ def main() -> int:
     for _ in range(W):
         eng.step()
     t1 = sync()
+    tm0 = dict(runner.timing)
     for _ in range(K):
         eng.step()
     elapsed = sync() - t1
+    host_ms = {k: round((runner.timing[k] - tm0[k]) / K * 1e3, 4) for k in ("fill", "send", "run", "d2h")}
     for _ in range(args.profile_steps):
         eng.step()
     for s in seqs:
@@ -239,6 +241,9 @@ def main() -> int:
             "aggregate_tokens_per_s": round(total_tps, 2),
             "engine_per_client_tokens_per_s": round(per_client, 2),
             "per_rank_ms_per_step": [round(e / K * 1e3, 4) for e in rank_elapsed],
+            # rank 0's host time per timed step inside ModelRunner.launch: metadata packing, the TP metadata-plane
+            # push, H2D copy + graph replay enqueue, D2H copy + event enqueue
+            "host_ms_per_step": host_ms,
             "engine_p50_ttft_ms": round(p50_ttft, 2),
             "engine_mean_ttft_ms": round(mean_ttft, 2),
             "engine_max_ttft_ms": round(max_ttft, 2),

@@ -31,6 +31,7 @@ using at::Tensor;
 struct Xgmi {
   XgmiArgs args{};
   volatile int* err_host = nullptr;  // host-mapped error word: polled after every step without a sync
+  unsigned* xar_ctr = nullptr;       // per-output-tile epoch counters of the fused GEMM + all-reduce (XAR_CTR)
   char* own = nullptr;
   std::vector<char*> opened;  // IPC mappings to close
   int device = 0;
@@ -38,6 +39,7 @@ struct Xgmi {
   bool connected = false;
 };
 
+constexpr int XAR_CTR = XG_MAX_WG;  // output tiles (N / 16) a communicator's XAR launches may cover
 std::mutex g_mu;
 std::vector<Xgmi*> g_x;
 // Uncached buffers are never returned to the runtime: memory freed from a hipDeviceMallocUncached
@@ -81,6 +83,9 @@ int64_t xgmi_create(int64_t slot_bytes, int64_t world, int64_t rank, int64_t dev
   HIP_OK(hipHostGetDevicePointer(&ed, eh, 0));
   HIP_OK(hipDeviceSynchronize());
   x->err_host = (volatile int*)eh;
+  HIP_OK(hipMalloc(&x->xar_ctr, XAR_CTR * sizeof(unsigned)));
+  HIP_OK(hipMemset(x->xar_ctr, 0, XAR_CTR * sizeof(unsigned)));
+  HIP_OK(hipDeviceSynchronize());
   x->args.err = (int*)ed;
   x->args.rank = (int)rank;
   x->args.world = (int)world;
@@ -207,9 +212,11 @@ DecodeEpi xar_epi(Xgmi* x, const Tensor& a, const Tensor& W, bool wshuf, Tensor&
                   w_next.numel() == N, "xgmi_gemm_ar_resid: resid / xw [M, N], w_next [N]");
   TORCH_CHECK(ss.dim() == 2 && ss.size(0) >= M && ss.size(1) == N / 16, "xgmi_gemm_ar_resid: ss [M, N / 16]");
   TORCH_CHECK(M * N * 8 <= x->args.slot_bytes, "xgmi_gemm_ar_resid: output granules exceed the slot");
+  TORCH_CHECK(N / 16 <= XAR_CTR, "xgmi_gemm_ar_resid: too many output tiles");
   DecodeEpi e;
   e.wshuf = wshuf ? 1 : 0;
   e.xp = x->args;
+  e.xar_ctr = x->xar_ctr;
   e.resid = resid.data_ptr<float>();
   e.w_next = reinterpret_cast<const bf16*>(w_next.data_ptr());
   e.xw_out = reinterpret_cast<bf16*>(xw.data_ptr());
@@ -435,6 +442,7 @@ void xgmi_destroy(int64_t h) {
   (void)hipDeviceSynchronize();
   for (char* p : x->opened) (void)hipIpcCloseMemHandle(p);
   (void)hipHostFree((void*)x->err_host);
+  (void)hipFree(x->xar_ctr);
   {
     std::lock_guard<std::mutex> g(g_mu);
     g_uc_pool.emplace_back(x->bytes, x->own);

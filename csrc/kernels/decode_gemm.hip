@@ -85,9 +85,12 @@ SYM_DEV void gemm_tile(const bf16* __restrict__ x, const bf16* __restrict__ W, i
 
   __shared__ f32x4 red[NW][RT * MT][64];
   __shared__ float rn_s[64];
-  unsigned xep = 0;
-  unsigned long long xold = 0;
-  if constexpr (EPI == DECODE_EPI_XAR) xold = xg_epoch_arrive(e.xp);  // resolved after the weight stream
+  unsigned xep = 0, xctr = 0;
+  __shared__ unsigned s_xep;
+  if constexpr (EPI == DECODE_EPI_XAR) {  // this tile's epoch counter (read now, used after the weight stream)
+    static_assert(RT == 1, "XAR: one output tile per workgroup");
+    if (threadIdx.x == 0) xctr = e.xar_ctr[tile0];
+  }
 
   f32x4 acc[RT][MT];
 #pragma unroll
@@ -202,7 +205,14 @@ SYM_DEV void gemm_tile(const bf16* __restrict__ x, const bf16* __restrict__ W, i
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) red[wid][rt * MT + mt][lane] = acc[rt][mt];
   __syncthreads();
-  if constexpr (EPI == DECODE_EPI_XAR) xep = xg_epoch_resolve(e.xp, xold, gridDim.x);
+  if constexpr (EPI == DECODE_EPI_XAR) {
+    if (threadIdx.x == 0) {
+      s_xep = xctr + 1u;
+      e.xar_ctr[tile0] = xctr + 1u;
+    }
+    __syncthreads();
+    xep = s_xep;
+  }
   // parallel epilogue: wave `wid` finishes accumulator tiles job = wid, wid + NW, ...
   for (int job = wid; job < RT * MT; job += NW) {
     const int rt = job / MT, mt = job % MT;
@@ -328,15 +338,12 @@ SYM_DEV void xres_body(const bf16* __restrict__ x, const bf16* __restrict__ W, i
   const int nf = NF > b ? (NF - b + G - 1) / G : 0;
   const int np = P > b ? (P - b + G - 1) / G : 0;
   const int nu = nf + np;
-  unsigned long long xold = 0;
-  if constexpr (EPI == DECODE_EPI_XAR) {
-    xold = xg_epoch_arrive(e.xp);  // every workgroup counts in (resolved once the weight stream is in flight)
-    if (nu == 0) {
-      xg_epoch_resolve(e.xp, xold, G);
-      return;
-    }
-  }
   if (nu == 0) return;  // uniform over the workgroup
+  // XAR: per-tile epoch counters of this workgroup's tiles (read now, bumped after the first barrier below)
+  __shared__ unsigned s_xep[XAR_MAX_TILES];
+  unsigned xctr = 0;
+  if constexpr (EPI == DECODE_EPI_XAR)
+    if (threadIdx.x < nf) xctr = e.xar_ctr[b + threadIdx.x * G];
   auto unit_tile = [&](int i) { return i < nf ? b + i * G : NF + (b + (i - nf) * G) / PDIV; };
   auto unit_active = [&](int i) { return KS == 1 || i < nf || wid / WPS == (b + (i - nf) * G) % KS; };
   auto unit_half = [&](int i) { return (KS > 1 || i < nf) ? -1 : (b + (i - nf) * G) % 2; };
@@ -382,14 +389,21 @@ SYM_DEV void xres_body(const bf16* __restrict__ x, const bf16* __restrict__ W, i
     }
   }
   __shared__ f32x4 red[2][NW][64];
-  unsigned xep = 0;
-  if constexpr (EPI == DECODE_EPI_XAR) xep = xg_epoch_resolve(e.xp, xold, G);
+  if constexpr (EPI == DECODE_EPI_XAR) {
+    if (threadIdx.x < nf) {
+      s_xep[threadIdx.x] = xctr + 1u;
+      e.xar_ctr[b + threadIdx.x * G] = xctr + 1u;
+    }
+    __syncthreads();
+  }
   const int m = r16;
   const bool mok = m < M;
   auto finish = [&](f32x4 v, int t, int hf = -1) {  // wave 0: row scale + epilogue of a final tile (or half)
     const float sc = (e.ss_in && mok) ? rn_s[m] : 1.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] *= sc;
+    unsigned xep = 0;
+    if constexpr (EPI == DECODE_EPI_XAR) xep = s_xep[(t - b) / G];  // XAR: whole tiles only (t = b + i G)
     epilogue<EPI>(e, v, t, m, mok && (hf < 0 || (h & 1) == hf), h, N, xep);
   };
   int buf = 0;
@@ -499,6 +513,7 @@ void go_xres_ks(const bf16* x, const bf16* W, int M, int N, int K, const DecodeE
 template <int EPI>
 bool go_xres(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, hipStream_t s) {
   if (M > 16 || K % 1024 || K > 4096) return false;
+  if (EPI == DECODE_EPI_XAR && N / 16 > XAR_MAX_TILES * 64) return false;  // (per-workgroup epoch slots)
   if (!g_num_cus) {
     int dev = 0;
     hipGetDevice(&dev);
@@ -752,6 +767,7 @@ bool launch_decode_gemm_xar_multi(const XarMulti& m, int world, const bf16* W, i
   if (xres) {  // x-resident walk, ~cus / world workgroups per rank (one per CU, all ranks resident)
     if (K % 1024 || K > 4096 || !m.e[0].wshuf) return false;
     const int G = std::max(1, std::min(N / 16, cus / world));
+    if ((N / 16 + G - 1) / G > XAR_MAX_TILES) return false;
     const dim3 grid(G, 1, world);
     switch (K / 1024) {
       case 1:

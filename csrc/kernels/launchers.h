@@ -19,6 +19,7 @@ enum {
   // epoch-tagged granules, the tile's workgroup sums every rank's copy in rank order and runs the RESID
   // epilogue (residual add + next-norm prep, ss per 16-column tile) -- decode_epi.h, xar_push / xar_collect
   DECODE_EPI_XAR = 6,
+  XAR_MAX_TILES = 32,  // output tiles per workgroup of an x-resident XAR launch (epoch slots in LDS)
 };
 
 // xGMI communicator buffer layout (xgmi_ar.hip): header (collective counter) | flags [XG_MAX_WG][XG_MAX_WORLD]
@@ -70,8 +71,12 @@ struct DecodeEpi {
   const long long* step = nullptr;
   unsigned long long* keys = nullptr;
   int n_offset = 0;
-  // XAR (row-parallel projection under TP): the all-reduce communicator (granule slots, decode_epi.h)
+  // XAR (row-parallel projection under TP): the all-reduce communicator (granule slots, decode_epi.h) and its
+  // per-output-tile epoch counters (device memory, zero at creation): every XAR launch on a communicator covers
+  // all N / 16 tiles, so tile t's counter is the same on every rank; the tile's workgroup bumps it with a plain
+  // store (no atomics, no cross-workgroup fan-in), and kernel boundaries make it visible to the next launch
   XgmiArgs xp;
+  unsigned* xar_ctr = nullptr;
   // split-K workspace of the x-resident decode GEMM (decode_gemm.hip, go_xres): ks_ws fp32 partial tiles
   // (256 floats per (tile, split)), ks_cnt one arrival counter per 16-row tile (zero, re-armed in-launch);
   // nullptr -> whole-K tiles only

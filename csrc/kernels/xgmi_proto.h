@@ -76,28 +76,4 @@ SYM_DEV void xg_raise_flag(const XgmiArgs& c, int r, int word, unsigned epoch) {
   __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Split form of xg_epoch for a kernel that must not stall its first loads on the counter round trip: thread 0
-// issues the counting add first thing (xg_epoch_arrive), the workgroup reads the epoch where it needs it
-// (xg_epoch_resolve: the last arrival's fold-in + mirror, an LDS broadcast and a barrier).
-SYM_DEV unsigned long long xg_epoch_arrive(const XgmiArgs& c) {
-  if (threadIdx.x != 0) return 0;
-  unsigned long long* w = reinterpret_cast<unsigned long long*>(c.bufs[c.rank] + 64);
-  return __hip_atomic_fetch_add(w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-SYM_DEV unsigned xg_epoch_resolve(const XgmiArgs& c, unsigned long long old, int nwg) {
-  __shared__ unsigned s_ep;
-  if (threadIdx.x == 0) {
-    const unsigned e = (unsigned)(old >> 32) + 1u;
-    if ((unsigned)old == (unsigned)nwg - 1u) {
-      unsigned long long* w = reinterpret_cast<unsigned long long*>(c.bufs[c.rank] + 64);
-      __hip_atomic_fetch_add(w, (1ull << 32) - (unsigned long long)nwg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(reinterpret_cast<unsigned*>(c.bufs[c.rank]), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_ep = e;
-  }
-  __syncthreads();
-  return s_ep;
-}
-
 }  // namespace

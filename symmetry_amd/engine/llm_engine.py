@@ -170,6 +170,7 @@ class LLMEngine:
         # fault containment (tensor parallel): once a peer rank is lost the engine cannot compute any step; it
         # fails every request and refuses new ones, and its listeners (the backend -> the provider) take the
         # provider offline (parallel/health.py)
+        self.host_phase = {"schedule": 0.0}  # host seconds in scheduling (pipelined decode; bench breakdowns)
         self.fatal: str | None = None
         self.health = None  # rank 0's TPHealthMonitor (parallel/launch.py), if any
         self._fatal_listeners: list = []
@@ -320,6 +321,7 @@ class LLMEngine:
         if prev is not None:
             with self.lock:
                 nxt = self.scheduler.schedule_lookahead()
+            self.host_phase["schedule"] += time.perf_counter() - t_sched
             self._inflight = None
             if nxt is not None:
                 fl = self._launch(nxt, prev)

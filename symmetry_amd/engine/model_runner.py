@@ -124,7 +124,10 @@ class ModelRunner:
         self._pinned = {}
         self.step_counter = 0
         self._parity = 0
-        self.timing = {"h2d": 0.0, "forward": 0.0, "d2h": 0.0, "steps": 0}
+        # host seconds per phase of launch() (TP host-phase breakdown, bench.py "host_ms_per_step"): packing the
+        # metadata, the metadata plane push (TP), the H2D copy + graph replay / eager forward enqueue, the D2H
+        # copy + event; "forward": launch-to-completion as seen by wait()
+        self.timing = {"fill": 0.0, "send": 0.0, "run": 0.0, "d2h": 0.0, "forward": 0.0, "steps": 0}
         self.meta = None
         # (tp_size > 1 without a bootstrap group: ONE rank's shard alone, no workers -- the TP shard timing
         # simulation of bench/tp_shard.py)
@@ -298,9 +301,12 @@ class ModelRunner:
         self._fill(lay, host, seqs, counts, prev_rows)
         header = np.array([0 if batch.kind == "decode" else 1, lay.T, lay.nseq, lay.max_blocks, lay.ntiles, nseq,
                            int(self._filtered(seqs))], dtype=np.int32)
+        t1 = time.perf_counter()
         if self.meta is not None:
             self._broadcast(header, host_t)
+        t2 = time.perf_counter()
         ids = self._run(header, host_t)
+        t3 = time.perf_counter()
         handle = {"nseq": nseq, "t0": t0}
         if self.is_gpu:
             pin = self._host(max(ids.numel(), 1), f"ids_out{self._parity}")[:ids.numel()]
@@ -310,7 +316,12 @@ class ModelRunner:
             handle.update(pin=pin, event=ev)
         else:
             handle["ids"] = ids.tolist()
-        self.timing["steps"] += 1
+        tm = self.timing
+        tm["fill"] += t1 - t0
+        tm["send"] += t2 - t1
+        tm["run"] += t3 - t2
+        tm["d2h"] += time.perf_counter() - t3
+        tm["steps"] += 1
         return handle
 
     def wait(self, handle: dict) -> list[int]:

@@ -113,6 +113,7 @@ async def client_end_run(engine, model: str, clients: int, prompt_tokens: int = 
     try:
         await asyncio.sleep(0.5)
         engine.metrics = type(engine.metrics)()
+        tm0 = dict(engine.runner.timing, schedule=engine.host_phase["schedule"])
         t1 = time.perf_counter()
         start_evt.set()
         res = await asyncio.wait_for(asyncio.to_thread(q.get), timeout)
@@ -122,6 +123,7 @@ async def client_end_run(engine, model: str, clients: int, prompt_tokens: int = 
         if p.is_alive():
             p.kill()
         stats = provider.stats()
+        tm1 = dict(engine.runner.timing, schedule=engine.host_phase["schedule"])
         saved = len(provider.saved_files)
         timings = list(getattr(provider.backend, "timings", []))
         trace = list(getattr(engine, "step_trace", []))
@@ -154,6 +156,10 @@ async def client_end_run(engine, model: str, clients: int, prompt_tokens: int = 
         "content_events": total_events,
         "data_collection_files": saved,
         "engine": {k: stats.get(k) for k in ("mean_decode_batch", "p50_itl_ms", "decode_steps", "step_phase_ms")},
+        # host ms per engine step inside ModelRunner.launch during this run (pack / TP metadata push / H2D +
+        # replay enqueue / D2H enqueue): what the engine thread spends outside scheduling and streaming
+        "runner_host_ms_per_step": {k: round((tm1[k] - tm0[k]) / max(1, tm1["steps"] - tm0["steps"]) * 1e3, 4)
+                                    for k in ("schedule", "fill", "send", "run", "d2h")},
         "ttft_path_ms": ttft_breakdown(res, timings),
         "first_steps": first_steps(timings, trace),
     }
