@@ -182,7 +182,8 @@ def main() -> int:
     for _ in range(K):
         eng.step()
     elapsed = sync() - t1
-    host_ms = {k: round((runner.timing[k] - tm0[k]) / K * 1e3, 4) for k in ("fill", "send", "run", "d2h")}
+    host_ms = {k: round((runner.timing[k] - tm0[k]) / K * 1e3, 4)
+               for k in ("fill", "send", "run", "graph_launch", "d2h")}
     for _ in range(args.profile_steps):
         eng.step()
     for s in seqs:

@@ -773,6 +773,31 @@ void logits_argmax(const Tensor& logits, const Tensor& temps, const Tensor& seed
                        reinterpret_cast<unsigned long long*>(out_keys.data_ptr()), ptr<int>(out_ids), cur_stream(logits));
 }
 
+// Replay a captured decode hipGraph (torch.cuda.CUDAGraph.raw_cuda_graph_exec()) on the current stream WITHOUT
+// releasing the GIL: torch's CUDAGraph.replay() drops it, and on a provider whose event-loop thread is busy with
+// the clients' sockets the engine thread then waits out the interpreter's switch interval to get it back (TP=2
+// client-end run: 2.06 ms of "launch" per step).  Our graphs hold no torch RNG state, so replay() would do
+// nothing else.
+void graph_launch(int64_t exec, int64_t device) {
+  TORCH_CHECK(exec != 0, "graph_launch: null graph exec");
+  const hipStream_t s = c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream();
+  const hipError_t e = hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(exec), s);
+  TORCH_CHECK(e == hipSuccess, "hipGraphLaunch: ", hipGetErrorString(e));
+}
+
+// Async copy of n bytes between a pinned host buffer and device memory on the current stream of `device`, with the
+// GIL held (the per-step metadata H2D and sampled-ids D2H of the engine loop; torch's copy_ releases the GIL --
+// see graph_launch).
+void copy_async(Tensor& dst, const Tensor& src, int64_t nbytes, int64_t device) {
+  TORCH_CHECK(nbytes >= 0 && nbytes <= dst.numel() * dst.element_size() && nbytes <= src.numel() * src.element_size(),
+              "copy_async: byte count exceeds a tensor");
+  TORCH_CHECK(dst.is_contiguous() && src.is_contiguous(), "copy_async: contiguous tensors only");
+  if (nbytes == 0) return;
+  const hipStream_t s = c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream();
+  const hipError_t e = hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), (size_t)nbytes, hipMemcpyDefault, s);
+  TORCH_CHECK(e == hipSuccess, "hipMemcpyAsync: ", hipGetErrorString(e));
+}
+
 void rownorm(const Tensor& xw, const Tensor& ss, double eps, Tensor& out) {
   check_gpu(xw, "xw");
   check_dtype(xw, at::kBFloat16, "xw");
@@ -790,6 +815,8 @@ void rownorm(const Tensor& xw, const Tensor& ss, double eps, Tensor& out) {
 }  // namespace
 
 TORCH_LIBRARY(symmetry_amd, m) {
+  m.def("graph_launch(int exec, int device) -> ()", &graph_launch);
+  m.def("copy_async(Tensor(a!) dst, Tensor src, int nbytes, int device) -> ()", &copy_async);
   m.def("rms_norm(Tensor x, Tensor w, float eps, Tensor(a!) out) -> ()", &rms_norm);
   m.def("add_rms_norm(Tensor delta, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out) -> ()", &add_rms_norm);
   m.def("embed_rms_norm(Tensor ids, Tensor table, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out, "

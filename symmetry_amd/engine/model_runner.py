@@ -21,12 +21,14 @@ from __future__ import annotations
 
 import itertools
 import math
+import os
 import time
 
 import numpy as np
 import torch
 
 from ..models.transformer import ForwardBatch, KVCache, TransformerLM
+from ..ops import _native
 from .scheduler import ScheduledBatch
 
 DECODE_BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256)
@@ -127,7 +129,8 @@ class ModelRunner:
         # host seconds per phase of launch() (TP host-phase breakdown, bench.py "host_ms_per_step"): packing the
         # metadata, the metadata plane push (TP), the H2D copy + graph replay / eager forward enqueue, the D2H
         # copy + event; "forward": launch-to-completion as seen by wait()
-        self.timing = {"fill": 0.0, "send": 0.0, "run": 0.0, "d2h": 0.0, "forward": 0.0, "steps": 0}
+        self.timing = {"fill": 0.0, "send": 0.0, "run": 0.0, "graph_launch": 0.0, "d2h": 0.0, "forward": 0.0,
+                       "steps": 0}
         self.meta = None
         # (tp_size > 1 without a bootstrap group: ONE rank's shard alone, no workers -- the TP shard timing
         # simulation of bench/tp_shard.py)
@@ -310,7 +313,10 @@ class ModelRunner:
         handle = {"nseq": nseq, "t0": t0}
         if self.is_gpu:
             pin = self._host(max(ids.numel(), 1), f"ids_out{self._parity}")[:ids.numel()]
-            pin.copy_(ids, non_blocking=True)
+            if _native.available() and ids.is_contiguous():
+                _native.ops().copy_async(pin, ids, ids.numel() * 4, self.device.index or 0)
+            else:
+                pin.copy_(ids, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
             handle.update(pin=pin, event=ev)
@@ -361,9 +367,18 @@ class ModelRunner:
             if g is None:
                 self._capture(T, max_blocks, bool(filt))
                 g = self.graphs[key]
-            graph, dev, out = g
-            dev.copy_(host_t[:lay.size], non_blocking=True)
-            graph.replay()
+            graph, dev, out, exec_ = g
+            if exec_:
+                # H2D + hipGraphLaunch with the GIL held (torch's copy_ / replay() release it and the engine
+                # thread then waits for the event-loop thread: csrc/bindings/torch_ops.cpp, graph_launch)
+                nat = _native.ops()
+                nat.copy_async(dev, host_t, lay.size * 4, self.device.index or 0)
+                t_h2d = time.perf_counter()
+                nat.graph_launch(exec_, self.device.index or 0)
+                self.timing["graph_launch"] += time.perf_counter() - t_h2d
+            else:
+                dev.copy_(host_t[:lay.size], non_blocking=True)
+                graph.replay()
             ids = out
         else:
             dev = self.model.ws.get("meta." + kind, (lay.size,), torch.int32, self.device)
@@ -397,7 +412,13 @@ class ModelRunner:
         with torch.cuda.graph(g, pool=self._graph_pool):
             out = self.model.forward(fb, self.kv)
         torch.cuda.synchronize()
-        self.graphs[(bucket, max_blocks, filtered)] = (g, dev, out)
+        exec_ = 0
+        if _native.available() and os.environ.get("SYMMETRY_GRAPH_LAUNCH", "native") == "native":
+            try:
+                exec_ = int(g.raw_cuda_graph_exec())
+            except Exception:  # noqa: BLE001 -- older torch: replay() it is
+                exec_ = 0
+        self.graphs[(bucket, max_blocks, filtered)] = (g, dev, out, exec_)
 
     def capture_all(self) -> float:
         """Rank 0: capture every (batch, context) decode graph; under TP each capture is mirrored by the

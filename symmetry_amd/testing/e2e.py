@@ -159,7 +159,7 @@ async def client_end_run(engine, model: str, clients: int, prompt_tokens: int = 
         # host ms per engine step inside ModelRunner.launch during this run (pack / TP metadata push / H2D +
         # replay enqueue / D2H enqueue): what the engine thread spends outside scheduling and streaming
         "runner_host_ms_per_step": {k: round((tm1[k] - tm0[k]) / max(1, tm1["steps"] - tm0["steps"]) * 1e3, 4)
-                                    for k in ("schedule", "fill", "send", "run", "d2h")},
+                                    for k in ("schedule", "fill", "send", "run", "graph_launch", "d2h")},
         "ttft_path_ms": ttft_breakdown(res, timings),
         "first_steps": first_steps(timings, trace),
     }
