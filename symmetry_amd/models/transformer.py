@@ -41,6 +41,8 @@ from .layout import apply_decode_layout
 from .weights import ModelWeights
 
 SKINNY_MAX_M = 64
+# TP prefill: row-parallel partials all-reduced in bf16 (SYMMETRY_TP_REDUCE_BF16=0: fp32, the A/B reference)
+TP_REDUCE_BF16 = os.environ.get("SYMMETRY_TP_REDUCE_BF16", "1") != "0"
 # Decode steps with at least this many rows run the O and down projections as k-split skinny GEMMs into
 # fp32 slabs (summed by add_prep) instead of one fused dg_resid launch: those projections have only
 # N / 16 = 256 row tiles, so every workgroup re-reads all M rows of x over the full K range and the x
@@ -280,6 +282,13 @@ class TransformerLM:
                 ys = self._buf(name + ".red", (1, T, N), torch.float32)
                 torch.sum(y, dim=0, keepdim=True, out=ys)
                 y = ys
+            if TP_REDUCE_BF16 and T > SKINNY_MAX_M and y.dtype == torch.float32:
+                # prefill-sized: all-reduce the partial in bf16 -- half the bytes of every row-parallel collective
+                # (the TP=1 library GEMM of these shapes writes bf16 too); decode-sized ones stay fp32 (one-shot
+                # xGMI kernels, fused with the residual epilogue)
+                yb = self._buf(name + ".redbf", (T, N), torch.bfloat16)
+                yb.copy_(y.view(T, N))
+                y = yb
             self.tp_reduced_bytes[name] = y.numel() * y.element_size()
             self.tp.all_reduce(y)
         return y

@@ -367,3 +367,70 @@ def test_tp_prefill_reduce_moves_one_summed_partial():
     assert seen == [(1, T, N)] and m.tp_reduced_bytes["o"] == T * N * 4
     # the reduced partial equals the plain product (slab order only changes fp32 rounding)
     torch.testing.assert_close(y[0], x.float() @ wo.float().t(), rtol=2e-2, atol=2e-2)
+
+
+def test_tp_prefill_reduce_is_bf16_past_decode_sizes():
+    """Prefill-sized steps (> 64 rows) all-reduce the row-parallel partial in bf16: half the bytes of the fp32
+    [T, N] partial per collective; the result is the fp32 product rounded once."""
+    from symmetry_amd.models.config import resolve
+    from symmetry_amd.models.transformer import TransformerLM
+    from symmetry_amd.models.weights import ShardSpec, random_weights
+
+    seen = []
+
+    class RecComm:
+        rank, world, capturable = 0, 2, False
+
+        def all_reduce(self, t, op="sum"):
+            seen.append((tuple(t.shape), t.dtype))
+
+    cfg = resolve("tiny-llama-kv8")
+    w = random_weights(cfg, ShardSpec(0, 2), seed=1)
+    m = TransformerLM(w, "cpu", tp_comm=RecComm())
+    T = 96
+    x = torch.randn(T, m.hq * m.D).bfloat16()
+    wo = w.layer(0, "wo")
+    N, K = wo.shape
+    y = m._linear("o", x, wo, reduce=True)
+    assert seen == [((T, N), torch.bfloat16)] and m.tp_reduced_bytes["o"] == T * N * 2
+    torch.testing.assert_close(y.float(), x.float() @ wo.float().t(), rtol=2e-2, atol=2e-2)
+
+
+def _tp_long_worker(rank, world):
+    from symmetry_amd.engine.llm_engine import EngineConfig
+    from symmetry_amd.engine.sequence import SamplingParams
+    from symmetry_amd.parallel.launch import init_tp_engine
+
+    ecfg = EngineConfig(model="tiny-llama-kv8", device="cpu", max_num_seqs=4, max_model_len=512, block_size=32,
+                        weight_init="full")
+    eng, r = init_tp_engine(ecfg)
+    if r != 0:
+        eng.runner.worker_loop()
+        return None
+    seqs = [eng.add_request(f"l{i}", p, SamplingParams(max_tokens=8, ignore_eos=True))
+            for i, p in enumerate(LONG_PROMPTS)]
+    while eng.has_unfinished():
+        eng.step()
+    eng.shutdown()
+    return [s.output_ids for s in seqs], dict(eng.model.tp_reduced_bytes)
+
+
+LONG_PROMPTS = [list(range(5, 95)), list(range(100, 170)), list(range(300, 310))]  # one 170-token prefill step
+
+
+def test_tp2_bf16_prefill_reduce_matches_oracle():
+    """TP=2 over gloo with a 170-token prefill step: the row-parallel all-reduces of that step move bf16
+    partials (2 B per element) and every generated token still agrees with the fp32 oracle."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.models import reference_model as rm
+
+    res = _run(_tp_long_worker)
+    outs, red = res[0][1]
+    eng = LLMEngine(EngineConfig(model="tiny-llama-kv8", device="cpu", max_num_seqs=4, max_model_len=512,
+                                 block_size=32, weight_init="full"))
+    for p, out in zip(LONG_PROMPTS, outs):
+        assert len(out) == 8
+        lg = rm.forward_logits(eng.weights, p + out[:-1])
+        for j, t in enumerate(out):
+            row = lg[len(p) - 1 + j]
+            assert float(row.max() - row[t]) <= 0.06, (j, t, float(row.max() - row[t]))
