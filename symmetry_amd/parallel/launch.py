@@ -108,10 +108,12 @@ def init_tp_engine(ecfg):
         ep_comm = comm
     if on_gpu:
         ecfg.device = f"cuda:{local}"
-    if isinstance(comm, XgmiComm) and torch.cuda.device_count() >= world:
+    xar = os.environ.get("SYMMETRY_XGMI_FUSED", "1")
+    if isinstance(comm, XgmiComm) and xar != "0" and (torch.cuda.device_count() >= world or xar == "force"):
         # the fused row-parallel decode projections (GEMM + all-reduce + residual in one launch): <= 64 rows.  Not
         # when ranks share a GPU (the one-GPU rehearsal): a fused launch's workgroups wait for the other ranks'
         # tiles while holding their CUs, and one rank's grid can fill the whole device before the other's starts
+        # (SYMMETRY_XGMI_FUSED=force: a test whose grids are small enough to be co-resident anyway)
         comm.attach_xar(cpu_group, 64, mcfg.hidden_size)
     if ep_comm is not None and isinstance(comm, XgmiComm) and os.environ.get("SYMMETRY_MOE_XGMI_A2A", "1") != "0":
         # the unpadded expert all-to-all (prefill dispatch / return of routed rows) on its own peer buffers

@@ -32,7 +32,10 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None):
 
     prompts = prompts or PROMPTS
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK="0", SYMMETRY_TP_COMM="gloo", SYMMETRY_XGMI=xgmi, SYMMETRY_MOE_A2A_STATS="1")
+                      LOCAL_RANK="0", SYMMETRY_TP_COMM="gloo", SYMMETRY_XGMI=xgmi, SYMMETRY_MOE_A2A_STATS="1",
+                      # the fused GEMM + all-reduce launches between the two processes: the small test models' grids
+                      # (<= 64 workgroups per rank) are co-resident on the one GPU
+                      SYMMETRY_XGMI_FUSED="force")
     try:
         from symmetry_amd.engine.llm_engine import EngineConfig
         from symmetry_amd.engine.sequence import SamplingParams
@@ -61,6 +64,8 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None):
             # decode steps ran the peer-memory all-reduce: fused into the row-parallel GEMMs (one XAR launch each:
             # GEMM + all-reduce + residual) for the dense model, the fused add_prep kernel around the MoE block
             assert calls.get("gemm_ar", 0) + calls["add_prep"] > 0, calls
+            if model == "small-llama":  # dense: every row-parallel decode projection ran as ONE fused XAR launch
+                assert calls.get("gemm_ar", 0) > 0 and calls["add_prep"] == 0, calls
             assert calls.get("keys", 0) > 0, calls  # and the vocab-parallel sampling combine
             assert eng.runner.model.tp.error() == 0
         extra = {}
