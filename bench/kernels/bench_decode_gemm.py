@@ -27,6 +27,9 @@ SHAPES = {
     # Llama-3-70B at TP=1 (config 4 on one GPU)
     "qkv_70b": ("qkv", 10240, 8192), "o_70b": ("resid", 8192, 8192), "gate_up_70b": ("swiglu", 57344, 8192),
     "down_70b": ("resid", 8192, 28672),
+    # Llama-3-70B TP=8 shards (config 4: one rank's projections)
+    "qkv_70b_tp8": ("qkv", 1280, 8192), "o_70b_tp8": ("f32", 8192, 1024), "gate_up_70b_tp8": ("swiglu", 7168, 8192),
+    "down_70b_tp8": ("f32", 8192, 3584),
     # plain fp32-output twins: the difference to the fused shapes is the epilogue's cost
     "qkv_f32": ("f32", 6144, 4096), "o_f32": ("f32", 4096, 4096), "gate_up_f32": ("f32", 28672, 4096),
 }
@@ -47,7 +50,7 @@ def make_call(epi, x, W, M, N, K, dev, sh=False):
         act = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
         return lambda w: ops.dg_swiglu(x, w, ss, 1e-5, act, wshuf=sh)
     if epi == "qkv":
-        g = 8 if N == 10240 else 4  # Llama-3-70B: 64 q / 8 kv heads; 8B (and shards): 32 / 8
+        g = 8 if N in (10240, 1280) else 4  # Llama-3-70B (and its TP=8 shard): 64 q / 8 kv heads; 8B: 32 / 8
         hkv = N // 128 // (g + 2)
         hq = g * hkv
         cs = torch.rand(4096, 128, device=dev)

@@ -54,14 +54,23 @@ SYM_DEV float ss_row_share(const float* __restrict__ row, int n, int lane) {
 // (The persistent MLP / attention-block launches that once reused this body with device-side phase waits
 // measured slower than the launches and were removed: profiles/r3/mlp_xres_persistent.jsonl,
 // profiles/r3/qkv_attn_fused.jsonl, profiles/decode_block_r1.jsonl.)
-template <int MT, int NW, int U, int RT, int EPI>
+//
+// KS > 1 (few output tiles, long K: the Llama-3-70B TP = 8 QKV shard has 80 tiles x K = 8192, i.e. 80 of 256 CUs
+// streaming 262 KB each): workgroup blk computes tile blk / KS over the k range of split blk % KS, stores its
+// reduced 16 x 16 fp32 partial write-through into the split-K workspace, drains, and bumps the tile's counter;
+// the workgroup whose add completes the set sums the KS partials in split order (bitwise reproducible), applies
+// the row scale and runs the epilogue, then re-arms the counter (graph-replay safe).  MI355X_MICROARCH.md
+// hand-off: sc1 payload stores + agent-scope add, agent-scope (L2-bypassing) loads by the last arriver.
+template <int MT, int NW, int U, int RT, int EPI, int KS = 1>
 SYM_DEV void gemm_tile(const bf16* __restrict__ x, const bf16* __restrict__ W, int M, int N, int K,
                        const DecodeEpi& e, int blk) {
-  const int tile0 = blk * RT;
+  static_assert(KS == 1 || (RT == 1 && EPI != DECODE_EPI_XAR && EPI != DECODE_EPI_ARGMAX), "split-K: one tile");
+  const int split = KS > 1 ? blk % KS : 0;
+  const int tile0 = (KS > 1 ? blk / KS : blk) * RT;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r16 = lane & 15, h = lane >> 4;
-  const int wk = K / NW;
-  const int kbeg = wid * wk;
+  const int wk = K / KS / NW;
+  const int kbeg = split * (K / KS) + wid * wk;
   const int nblk = wk / 64;
 
   // weight stream: row-major (16 rows x 64 B per load) or preshuffled (1 KB contiguous per load)
@@ -213,6 +222,51 @@ SYM_DEV void gemm_tile(const bf16* __restrict__ x, const bf16* __restrict__ W, i
     __syncthreads();
     xep = s_xep;
   }
+  if constexpr (KS > 1) {  // publish this split's partial, the last arriver finishes the tile
+    float* slot = e.ks_ws + ((long long)tile0 * KS + split) * (MT * 256);
+    for (int job = wid; job < MT; job += NW) {
+      f32x4 v = red[0][job][lane];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) v += red[w][job][lane];
+      unsigned long long* q = reinterpret_cast<unsigned long long*>(slot + job * 256 + lane * 4);
+      const float4 f4 = make_float4(v[0], v[1], v[2], v[3]);
+      const unsigned long long* w64 = reinterpret_cast<const unsigned long long*>(&f4);
+      __hip_atomic_store(q, w64[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(q + 1, w64[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ int s_last;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add(e.ks_cnt + tile0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
+    __syncthreads();
+    if (!s_last) return;
+    const float* base = e.ks_ws + (long long)tile0 * KS * (MT * 256);
+    for (int job = wid; job < MT; job += NW) {
+      unsigned long long r[KS][2];
+#pragma unroll
+      for (int sp = 0; sp < KS; ++sp) {
+        const unsigned long long* q =
+            reinterpret_cast<const unsigned long long*>(base + sp * (MT * 256) + job * 256 + lane * 4);
+        r[sp][0] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r[sp][1] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sp = 0; sp < KS; ++sp) {  // split order
+        const float* qq = reinterpret_cast<const float*>(r[sp]);
+        v += f32x4{qq[0], qq[1], qq[2], qq[3]};
+      }
+      const int m = 16 * job + r16;
+      const bool mok = m < M;
+      const float sc = (e.ss_in && mok) ? rn_s[m] : 1.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] *= sc;
+      epilogue<EPI>(e, v, tile0, m, mok, h, N, xep);
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(e.ks_cnt + tile0, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   // parallel epilogue: wave `wid` finishes accumulator tiles job = wid, wid + NW, ...
   for (int job = wid; job < RT * MT; job += NW) {
     const int rt = job / MT, mt = job % MT;
@@ -233,6 +287,13 @@ __global__ __launch_bounds__(NW * 64, WPE) void decode_gemm_kernel(const bf16* _
                                                               const bf16* __restrict__ W, int M, int N, int K,
                                                               DecodeEpi e) {
   gemm_tile<MT, NW, U, RT, EPI>(x, W, M, N, K, e, blockIdx.x);
+}
+
+template <int MT, int NW, int U, int EPI, int KS>
+__global__ __launch_bounds__(NW * 64) void decode_gemm_ks_kernel(const bf16* __restrict__ x,
+                                                                const bf16* __restrict__ W, int M, int N, int K,
+                                                                DecodeEpi e) {
+  gemm_tile<MT, NW, U, 1, EPI, KS>(x, W, M, N, K, e, blockIdx.x);
 }
 
 // ---- residual producers without a GEMM ----------------------------------------------------------
@@ -494,6 +555,14 @@ static bool g_dg_ksplit = [] {
   return knob && knob[0] == '1';
 }();
 
+// Split K of few-tile long-K launches across whole gemm_tile workgroups (launch_mt, variants 21..24): ON by
+// default (a different regime from the remainder split above: there most CUs would otherwise sit idle).
+// SYMMETRY_DG_TILE_KSPLIT=0 reverts.
+static bool g_dg_tile_ksplit = [] {
+  const char* knob = getenv("SYMMETRY_DG_TILE_KSPLIT");
+  return !(knob && knob[0] == '0');
+}();
+
 // Remainder tiles as row halves: OFF by default.  Measured (profiles/r3/xres_row_halves_ab.jsonl, alternating
 // runs): 8B 10 clients 3.316 vs 3.261 ms per step, TP = 4 / 8 shards unchanged.  A half tile issues as many
 // load instructions as a whole one (half the lanes masked), and at M <= 16 the launch is bound by the load
@@ -588,11 +657,53 @@ void go(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e0, 
   decode_gemm_kernel<MT, NW, U, RT, EPI, WPE><<<N / (16 * RT), NW * 64, 0, s>>>(x, W, M, N, K, e);
 }
 
+template <int MT, int NW, int U, int EPI, int KS>
+void go_ks(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e0, hipStream_t s) {
+  DecodeEpi e = e0;
+  e.wnt = g_wnt;
+  decode_gemm_ks_kernel<MT, NW, U, EPI, KS><<<(N / 16) * KS, NW * 64, 0, s>>>(x, W, M, N, K, e);
+}
+
+// split-K of gemm_tile (variants 21..24): usable when every (tile, split) partial fits the workspace and each
+// wave's k range is whole 64-blocks
+template <int MT, int EPI>
+bool ks_fits(int N, int K, int ks, int nw, const DecodeEpi& e) {
+  if constexpr (EPI == DECODE_EPI_ARGMAX || EPI == DECODE_EPI_XAR) return false;
+  const long long tiles = N / 16;
+  return e.ks_ws && e.ks_cnt && tiles <= e.ks_ncnt && tiles * ks * MT * 256 <= e.ks_cap && K % (ks * nw * 64) == 0;
+}
+
 template <int MT, int EPI>
 void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, hipStream_t s) {
   constexpr int U0 = MT == 1 ? 4 : (MT == 2 ? 2 : 1);
   constexpr int U1 = MT == 1 ? 8 : (MT == 2 ? 4 : 2);
   int v = g_variant;
+  if (v < 0 && g_dg_tile_ksplit && M <= 16 && K > 4096) {
+    // few 16-row tiles over a long K, past the x-resident walk's K <= 4096 (Llama-3-70B TP = 8 QKV: 80 tiles x
+    // K = 8192): whole-tile workgroups would leave 176 of 256 CUs idle, so split K in two across 8-wave
+    // workgroups (profiles/r4/dg_tile_ksplit.jsonl: 12.93 -> 9.31 us at M = 1, 13.45 -> 9.88 at 4, 14.11 -> 11.39
+    // at 10; 4 splits or 4 waves lose to it)
+    if (g_num_cus == 0) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+      g_num_cus = std::max(1, g_num_cus);
+    }
+    const int tiles = N / 16;
+    if (2 * tiles <= g_num_cus) v = ks_fits<MT, EPI>(N, K, 2, 8, e) ? 23 : (ks_fits<MT, EPI>(N, K, 2, 4, e) ? 21 : v);
+  }
+  if ((v == 21 || v == 23) && !ks_fits<MT, EPI>(N, K, 2, v == 21 ? 4 : 8, e)) v = -2;
+  if ((v == 22 || v == 24) && !ks_fits<MT, EPI>(N, K, 4, v == 22 ? 4 : 8, e)) v = -2;
+  if constexpr (EPI != DECODE_EPI_ARGMAX && EPI != DECODE_EPI_XAR) {
+    switch (v) {
+      case 21: go_ks<MT, 4, U0, EPI, 2>(x, W, M, N, K, e, s); return;
+      case 22: go_ks<MT, 4, U0, EPI, 4>(x, W, M, N, K, e, s); return;
+      case 23: go_ks<MT, 8, U0, EPI, 2>(x, W, M, N, K, e, s); return;
+      case 24: go_ks<MT, 8, U0, EPI, 4>(x, W, M, N, K, e, s); return;
+      default: break;
+    }
+  }
+  if (v == -2 || v >= 21) v = -1;  // split-K does not fit: the whole-tile heuristic
   if (v < 0) {
     // Measured on MI355X (profiles/decode_gemm_variants_r1.jsonl): the x fragments (re-read from L2 by
     // every workgroup) dominate the L1/TA traffic once M > 4, so wide-N projections share them over
@@ -614,6 +725,9 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
       else if (M > 16 && N > 4096) v = 3;
       else if (N <= 4096 && K % 1024 == 0) v = K > 4096 ? 4 : 2;  // few row tiles: split K (down_proj: 4 waves,
                                                                   // 24.2 vs 25.7 us at M = 10)
+      // Llama-3-70B TP = 8 gate_up (7168 x 8192) and down (8192 x 3584) at 2..16 rows: 4 waves per tile
+      // (profiles/r4/dg_tile_ksplit.jsonl, variant 4 vs -1: 27.6 vs 29.4 us and 15.2 vs 16.5 at M = 10)
+      else if (M > 1 && N <= 8192 && K >= 3072 && K % 256 == 0) v = 4;
       else v = 0;
     } else if (M <= 4) {
       v = 0;

@@ -258,6 +258,68 @@ def test_preshuffled_weight_stream(gpu, M):
         lib.decode_gemm_variant(-1)
 
 
+@pytest.mark.parametrize("M", [1, 10, 33])
+def test_gemm_tile_split_k(gpu, M):
+    """gemm_tile split across workgroups in k (variants 21..24: 2 / 4 splits at 4 / 8 waves; the default for
+    few-tile long-K shards such as Llama-3-70B's TP=8 QKV): every fused epilogue matches the fp32 reference,
+    repeat launches are bitwise equal (fixed split order) and every tile's arrival counter is re-armed."""
+    from symmetry_amd.ops import _native
+
+    lib = _native.ops()
+    D, BS, NB, Hq, Hkv, K = 128, 32, 8, 8, 1, 8192
+    try:
+        for v in (21, 22, 23, 24):
+            lib.decode_gemm_variant(v)
+            x, W, s = _inputs(gpu, M, 1280, K, seed=40 + v)
+            y0, y1 = torch.empty(M, 1280, device=gpu), torch.empty(M, 1280, device=gpu)
+            ops.dg_f32(x, W, s, 1e-5, y0)
+            ops.dg_f32(x, W, s, 1e-5, y1)
+            assert torch.equal(y0, y1), v
+            y_ref = torch.empty(M, 1280)
+            ref.dg_f32(x.cpu(), W.cpu(), s.cpu(), 1e-5, y_ref)
+            _close(y0, y_ref, atol=2e-3, rtol=1e-2)
+
+            Wq = W[qkv_perm(Hq, Hkv, D).to(gpu)].contiguous()
+            cs = ref.rope_table(1024, D, 500000.0, device=gpu)
+            pos = torch.arange(M, device=gpu, dtype=torch.int32) * 7
+            slots = torch.randperm(NB * BS, device=gpu)[:M].int()
+            q = torch.empty(M, Hq, D, device=gpu, dtype=torch.bfloat16)
+            kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=torch.bfloat16)
+            vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=torch.bfloat16)
+            ops.dg_qkv(x, Wq, s, 1e-5, pos, slots, cs, q, kc, vc, Hq, Hkv)
+            q_r, kc_r, vc_r = torch.empty(M, Hq, D, dtype=torch.bfloat16), torch.zeros_like(kc.cpu()), \
+                torch.zeros_like(vc.cpu())
+            ref.dg_qkv(x.cpu(), Wq.cpu(), s.cpu(), 1e-5, pos.cpu(), slots.cpu(), cs.cpu(), q_r, kc_r, vc_r, Hq, Hkv)
+            _close(q, q_r, atol=2e-2, rtol=2e-2)
+            _close(kc, kc_r, atol=2e-2, rtol=2e-2)
+            _close(vc, vc_r, atol=2e-2, rtol=2e-2)
+
+            xr, Wr, _ = _inputs(gpu, M, 1024, 4096, seed=50 + v)
+            g = torch.Generator(device=gpu).manual_seed(v)
+            resid = torch.randn(M, 1024, device=gpu, generator=g)
+            wn = (torch.randn(1024, device=gpu, generator=g) * 0.1 + 1).bfloat16()
+            xw = torch.empty(M, 1024, device=gpu, dtype=torch.bfloat16)
+            ss = torch.empty(M, 64, device=gpu)
+            r_ref, xw_ref, ss_ref = resid.cpu().clone(), torch.empty(M, 1024, dtype=torch.bfloat16), torch.empty(M, 64)
+            ops.dg_resid(xr, Wr, resid, wn, xw, ss)
+            ref.dg_resid(xr.cpu(), Wr.cpu(), r_ref, wn.cpu(), xw_ref, ss_ref)
+            _close(resid, r_ref, atol=2e-3, rtol=1e-3)
+            _close(xw, xw_ref, atol=2e-2, rtol=1e-2)
+            _close(ss, ss_ref, atol=1e-2, rtol=1e-3)
+
+            F = 640
+            Wg = W[gu_perm(F).to(gpu)].contiguous()
+            act = torch.empty(M, F, device=gpu, dtype=torch.bfloat16)
+            ops.dg_swiglu(x, Wg, s, 1e-5, act)
+            act_ref = torch.empty(M, F, dtype=torch.bfloat16)
+            ref.dg_swiglu(x.cpu(), Wg.cpu(), s.cpu(), 1e-5, act_ref)
+            _close(act, act_ref, atol=1e-2, rtol=2e-2)
+        torch.cuda.synchronize()
+        assert int(ops.decode_ks_ws(gpu)[1].abs().sum()) == 0
+    finally:
+        lib.decode_gemm_variant(-1)
+
+
 def _mg(gpu, M, N, K):
     """(slab, counters, rw) for the mgemm-with-epilogue form of a projection (ops.choose_mgemm's pick, or a
     forced 4-way split when the chooser declines: the in-launch reduction is what is under test)."""
