@@ -201,6 +201,36 @@ class XgmiComm(Comm):
         if barrier:
             dist.barrier(group=group)  # every rank mapped every buffer before the first collective
 
+    def self_test(self) -> bool:
+        """One all-reduce of known values through the peer buffers (every rank, collectively): True when it
+        summed correctly and no rank gave up waiting.  Run once at startup, so a node whose links or IPC
+        mappings misbehave falls back to RCCL instead of failing its first decode step."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        t = torch.full((4096,), float(self.rank + 1), device=dev)
+        self.ops.xgmi_all_reduce(t, t, self.handle)
+        torch.cuda.synchronize(dev)
+        want = self.world * (self.world + 1) / 2
+        return int(self.ops.xgmi_error(self.handle)) == 0 and bool((t == want).all())
+
+    def xar_self_test(self, d: int) -> bool:
+        """The fused row-parallel projection + all-reduce + residual launch on exactly representable data
+        (x = 1, W = (rank + 1) / 256, K = 256, residual 0.5): True when every row came back as 0.5 + sum of
+        (rank + 1), the launch fit (co-resident grid) and no rank gave up waiting."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        M, K = 4, 256
+        x = torch.ones(M, K, device=dev, dtype=torch.bfloat16)
+        W = torch.full((d, K), (self.rank + 1) / 256, device=dev, dtype=torch.bfloat16)
+        resid = torch.full((M, d), 0.5, device=dev)
+        w_next = torch.ones(d, device=dev, dtype=torch.bfloat16)
+        xw = torch.empty(M, d, device=dev, dtype=torch.bfloat16)
+        ss = torch.empty(M, d // 16, device=dev)
+        if not self.gemm_ar_resid(x, W, False, resid, w_next, xw, ss):
+            return False
+        torch.cuda.synchronize(dev)
+        self.calls["gemm_ar"] -= 1
+        want = 0.5 + self.world * (self.world + 1) / 2
+        return int(self.ops.xgmi_error(self.xar.handle)) == 0 and bool((resid == want).all())
+
     def _fits(self, t) -> bool:
         return (t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous()
                 and t.numel() % 8 == 0 and t.numel() * t.element_size() <= self.slot_bytes)

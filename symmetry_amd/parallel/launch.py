@@ -71,17 +71,51 @@ def _try_xgmi(inner, group, dev):
         xg = XgmiComm(inner, group, dev, int(os.environ.get("SYMMETRY_XGMI_SLOT", 4 << 20)), barrier=False)
     except Exception as exc:  # noqa: BLE001 -- any failure means: no one-shot kernels on this node
         err = exc
-    ok = torch.tensor([0 if xg is None else 1], dtype=torch.int32)
-    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
-    if int(ok[0]) == 1:
+    if _vote(xg is not None, group):
         dist.barrier(group=group)  # every rank mapped every buffer before the first collective
-        return xg
+        # a startup all-reduce of known values: links / mappings that misbehave cost one wait limit here and a
+        # fallback to RCCL, not the first decode step
+        passed = False
+        try:
+            passed = xg.self_test()
+        except Exception as exc:  # noqa: BLE001
+            err = exc
+        if _vote(passed, group):
+            return xg
+        err = err or RuntimeError("startup all-reduce self-test failed")
     if err is not None:
         print(f"symmetry: xGMI one-shot collectives unavailable ({type(err).__name__}: {err}); using RCCL",
               file=sys.stderr, flush=True)
     if xg is not None:
         xg.destroy(inner_too=False)
     return None
+
+
+def _vote(ok: bool, group) -> bool:
+    """True on every rank iff ``ok`` on every rank (gloo)."""
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return int(t[0]) == 1
+
+
+def _attach_xar_checked(comm, group, d: int) -> None:
+    """attach_xar + its startup self-test on every rank; on any failure every rank drops the fused path (the
+    decode step then runs GEMM + the one-shot all-reduce)."""
+    import sys
+
+    passed, err = False, None
+    try:
+        comm.attach_xar(group, 64, d)
+        passed = comm.xar_self_test(d)
+    except Exception as exc:  # noqa: BLE001
+        err = exc
+    if _vote(passed, group):
+        return
+    print(f"symmetry: fused GEMM + all-reduce launches disabled ({err or 'startup self-test failed'})",
+          file=sys.stderr, flush=True)
+    if comm.xar is not None:
+        comm.xar.destroy(inner_too=False)
+        comm.xar = None
 
 
 def init_tp_engine(ecfg):
@@ -114,7 +148,7 @@ def init_tp_engine(ecfg):
         # when ranks share a GPU (the one-GPU rehearsal): a fused launch's workgroups wait for the other ranks'
         # tiles while holding their CUs, and one rank's grid can fill the whole device before the other's starts
         # (SYMMETRY_XGMI_FUSED=force: a test whose grids are small enough to be co-resident anyway)
-        comm.attach_xar(cpu_group, 64, mcfg.hidden_size)
+        _attach_xar_checked(comm, cpu_group, mcfg.hidden_size)
     if ep_comm is not None and isinstance(comm, XgmiComm) and os.environ.get("SYMMETRY_MOE_XGMI_A2A", "1") != "0":
         # the unpadded expert all-to-all (prefill dispatch / return of routed rows) on its own peer buffers
         tokens = max(ecfg.max_num_batched_tokens, 8192)

@@ -116,6 +116,45 @@ def test_comm_primitives():
     assert b[3] == [[2.0, 3.0], [4.0, 5.0], [104.0, 105.0]]
 
 
+def _xar_vote_worker(rank, world):
+    """The fused-path startup check drops the fused launches on EVERY rank when one rank's attach or self-test
+    fails (a rank-local fallback would leave the others waiting in a collective that never comes)."""
+    from symmetry_amd.parallel import launch
+
+    class FakeSub:
+        destroyed = False
+
+        def destroy(self, inner_too=True):
+            FakeSub.destroyed = True
+
+    class FakeComm:
+        xar = None
+
+        def __init__(self, fail_attach=False, fail_test=False):
+            self.fail_attach, self.fail_test = fail_attach, fail_test
+
+        def attach_xar(self, group, rows, d):
+            if self.fail_attach:
+                raise RuntimeError("ipc mapping refused")
+            self.xar = FakeSub()
+
+        def xar_self_test(self, d):
+            return not self.fail_test
+
+    group = dist.new_group(backend="gloo")
+    out = []
+    for fail in ((False, False), (rank == 1, False), (False, rank == 0)):
+        c = FakeComm(*fail)
+        launch._attach_xar_checked(c, group, 64)
+        out.append(c.xar is not None)
+    return out
+
+
+def test_fused_path_startup_check_is_all_ranks_or_none():
+    res = _run(_xar_vote_worker, world=2)
+    assert [r[1] for r in res] == [[True, False, False], [True, False, False]]
+
+
 def _tp_worker(rank, world, model="tiny-llama"):
     from symmetry_amd.engine.llm_engine import EngineConfig
     from symmetry_amd.engine.sequence import SamplingParams
