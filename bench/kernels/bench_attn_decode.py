@@ -45,10 +45,12 @@ def main():
                     "bucket; 0: just the context)")
     ap.add_argument("--wave", type=int, nargs="+", default=[-1],
                     help="attn_wave min-units settings to compare (-1: leave the default; 0: never; 1: always)")
+    ap.add_argument("--heads", type=int, nargs=2, default=[32, 8], metavar=("HQ", "HKV"),
+                    help="query / kv heads (one TP rank's shard: 4 1 for Llama-3-8B at TP=8, 8 1 for 70B)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     ops._native.ops()  # load the extension (registers torch.ops.symmetry_amd)
-    Hq, Hkv, D, BS = 32, 8, 128, 64
+    (Hq, Hkv), D, BS = args.heads, 128, 64
     S, L = args.seqs, args.layers
     tiny = torch.zeros(64, device=dev)
     print(json.dumps({"kernel": "trivial launch (graph chain floor)", "us": round(timed(lambda i: tiny.add_(1.0), 64), 2)}))
@@ -75,7 +77,7 @@ def main():
             us = timed(lambda i: ops.attn_decode(q, kc[i % L], vc[i % L], bt, ctxs, out, tmp_o, tmp_ml, cnt,
                                                  1 / math.sqrt(D)), L)
             kv_bytes = 2 * S * ctx * Hkv * D * 2
-            print(json.dumps({"kernel": "attn_decode", "seqs": S, "ctx": ctx, "span": nb * BS, "wave": wv,
+            print(json.dumps({"kernel": "attn_decode", "heads": [Hq, Hkv], "seqs": S, "ctx": ctx, "span": nb * BS, "wave": wv,
                               "us": round(us, 2), "TBps": round(kv_bytes / us / 1e6, 3)}), flush=True)
         torch.ops.symmetry_amd.attn_wave(1024, 513)
         del kc, vc
