@@ -182,6 +182,12 @@ class XgmiComm(Comm):
         self.capturable = inner.capturable  # the xGMI kernels are; the fallbacks are the inner ones
         dev = torch.device(device)
         self.slot_bytes = int(slot_bytes)
+        # largest message on the one-shot kernels; ranks sharing one GPU (rehearsals) keep it to decode sizes: a
+        # prefill-sized collective's grid (up to 4096 spinning workgroups) can fill the device before the other
+        # rank's kernel starts, so neither makes progress until the wait limit
+        self.oneshot_bytes = self.slot_bytes
+        if torch.cuda.device_count() < self.world:
+            self.oneshot_bytes = min(self.slot_bytes, 256 << 10)
         self.calls = {"all_reduce": 0, "add_prep": 0}  # collectives issued on the xGMI kernels (host count)
         self.xar = None  # the fused row-parallel GEMM + all-reduce communicator (attach_xar)
         self.a2a = None  # the expert all-to-all communicator (attach_a2a)
@@ -233,7 +239,7 @@ class XgmiComm(Comm):
 
     def _fits(self, t) -> bool:
         return (t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous()
-                and t.numel() % 8 == 0 and t.numel() * t.element_size() <= self.slot_bytes)
+                and t.numel() % 8 == 0 and t.numel() * t.element_size() <= self.oneshot_bytes)
 
     def all_reduce(self, t, op="sum"):
         if op == "sum" and self._fits(t):
