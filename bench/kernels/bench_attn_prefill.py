@@ -66,6 +66,6 @@ def run(lens, Hq=32, Hkv=8, BS=64, reps=20):
 
 
 if __name__ == "__main__":
-    shapes = {"10x128": [128] * 10, "10x1024": [1024] * 10, "1x4096": [4096], "4x2048": [2048] * 4, "1x8192": [8192]}
+    shapes = {"1x128": [128], "6x128": [128] * 6, "10x128": [128] * 10, "4x256": [256] * 4, "10x1024": [1024] * 10, "1x4096": [4096], "4x2048": [2048] * 4, "1x8192": [8192]}
     for name in (sys.argv[1:] or list(shapes)):
         print(json.dumps(run(shapes[name])), flush=True)
