@@ -477,6 +477,71 @@ void moe_combine(const Tensor& y, const Tensor& dst, const Tensor& ids, int64_t 
                      (int)k, (int)d, ptr<float>(out), accumulate ? 1 : 0, cur_stream(out));
 }
 
+// Decode MoE routing in one launch: resid fp32 [T, d] (T <= 16) -> ids / w [T*k], counts / offsets / cursor,
+// xs [T*k, d] (the normalised rows, expert segments in token order), dst [T*k]
+void moe_decode_route(const Tensor& resid, const Tensor& lnw, double eps, const Tensor& Wr, int64_t k, Tensor& ids,
+                      Tensor& w, Tensor& counts, Tensor& offsets, Tensor& cursor, Tensor& xs, Tensor& dst) {
+  check_gpu(resid, "resid");
+  check_dtype(resid, at::kFloat, "resid");
+  check_gpu(lnw, "lnw");
+  check_dtype(lnw, at::kBFloat16, "lnw");
+  check_gpu(Wr, "Wr");
+  check_dtype(Wr, at::kBFloat16, "Wr");
+  TORCH_CHECK(resid.dim() == 2 && resid.is_contiguous() && Wr.dim() == 2 && Wr.is_contiguous() &&
+                  Wr.size(1) == resid.size(1) && lnw.numel() == resid.size(1),
+              "moe_decode_route: resid [T, d], Wr [E, d], lnw [d]");
+  const int64_t T = resid.size(0), d = resid.size(1), E = Wr.size(0);
+  TORCH_CHECK(T <= 8 && E >= 1 && E <= 64 && k >= 1 && k <= 8 && k <= E && d % 8 == 0 && d <= 4096,
+              "moe_decode_route: T <= 8, k <= E <= 64, k <= 8, d <= 4096, d % 8 == 0");
+  for (auto* t : {&ids, &counts, &offsets, &cursor, &dst}) {
+    check_gpu(*t, "index tensor");
+    check_dtype(*t, at::kInt, "index tensor");
+  }
+  check_gpu(w, "w");
+  check_dtype(w, at::kFloat, "w");
+  check_gpu(xs, "xs");
+  check_dtype(xs, at::kBFloat16, "xs");
+  TORCH_CHECK(ids.numel() >= T * k && w.numel() >= T * k && dst.numel() >= T * k && counts.numel() >= E &&
+                  offsets.numel() >= E + 1 && cursor.numel() >= E && xs.numel() >= T * k * d,
+              "moe_decode_route: outputs too small");
+  const at::OptionalDeviceGuard g(resid.device());
+  launch_moe_decode_route(ptr<float>(resid), ptr<bf16>(lnw), (float)eps, ptr<bf16>(Wr), (int)T, (int)d, (int)E, (int)k,
+                          ptr<int>(ids), ptr<float>(w), ptr<int>(counts), ptr<int>(offsets), ptr<int>(cursor),
+                          ptr<bf16>(xs), ptr<int>(dst), cur_stream(resid));
+}
+
+// moe_combine over every expert + add_prep (resid += combined; xw = bf16(resid * w_next); ss[t] = sum resid^2)
+void moe_combine_prep(const Tensor& y, const Tensor& dst, const Tensor& ids, int64_t E, const Tensor& w, int64_t k,
+                      Tensor& resid, const Tensor& w_next, Tensor& xw, Tensor& ss) {
+  check_gpu(resid, "resid");
+  check_dtype(resid, at::kFloat, "resid");
+  check_gpu(xw, "xw");
+  check_dtype(xw, at::kBFloat16, "xw");
+  check_gpu(w_next, "w_next");
+  check_dtype(w_next, at::kBFloat16, "w_next");
+  check_gpu(ss, "ss");
+  check_dtype(ss, at::kFloat, "ss");
+  check_gpu(dst, "dst");
+  check_dtype(dst, at::kInt, "dst");
+  check_gpu(ids, "ids");
+  check_dtype(ids, at::kInt, "ids");
+  check_gpu(w, "w");
+  check_dtype(w, at::kFloat, "w");
+  TORCH_CHECK(resid.dim() == 2 && resid.is_contiguous(), "resid must be [T, d]");
+  const int64_t T = resid.size(0), d = resid.size(1);
+  const int64_t R = y.dim() == 3 ? y.size(1) : y.size(0);
+  // ss [T, P]: one sum-of-squares partial per column part (P divides d / 8)
+  TORCH_CHECK(ss.dim() == 2 && ss.size(0) >= T && ss.is_contiguous(), "moe_combine_prep: ss must be [T, P]");
+  const int64_t P = ss.size(1);
+  TORCH_CHECK(xw.numel() >= T * d && w_next.numel() == d && d % 8 == 0 && P >= 1 && (d / 8) % P == 0,
+              "moe_combine_prep: shape mismatch");
+  TORCH_CHECK(dst.numel() >= T * k && w.numel() >= T * k && ids.numel() >= T * k, "moe_combine_prep: dst/w too small");
+  const at::OptionalDeviceGuard g(resid.device());
+  launch_moe_combine_prep(linout(y, R, d, "y"), (int)R, ptr<int>(dst), ptr<int>(ids), (int)E, ptr<float>(w), (int)T,
+                          (int)k, (int)d, ptr<float>(resid), ptr<bf16>(w_next), ptr<bf16>(xw), ptr<float>(ss), (int)P,
+                          cur_stream(resid));
+}
+
 // ---- fused decode projections (decode_gemm.hip) ----------------------------------------------------
 struct DGShape {
   int64_t M, N, K;
@@ -817,6 +882,14 @@ void rownorm(const Tensor& xw, const Tensor& ss, double eps, Tensor& out) {
 TORCH_LIBRARY(symmetry_amd, m) {
   m.def("graph_launch(int exec, int device) -> ()", &graph_launch);
   m.def("copy_async(Tensor(a!) dst, Tensor src, int nbytes, int device) -> ()", &copy_async);
+  m.def(
+      "moe_decode_route(Tensor resid, Tensor lnw, float eps, Tensor Wr, int k, Tensor(a!) ids, Tensor(b!) w, "
+      "Tensor(c!) counts, Tensor(d!) offsets, Tensor(e!) cursor, Tensor(f!) xs, Tensor(g!) dst) -> ()",
+      &moe_decode_route);
+  m.def(
+      "moe_combine_prep(Tensor y, Tensor dst, Tensor ids, int E, Tensor w, int k, Tensor(a!) resid, Tensor w_next, "
+      "Tensor(b!) xw, Tensor(c!) ss) -> ()",
+      &moe_combine_prep);
   m.def("rms_norm(Tensor x, Tensor w, float eps, Tensor(a!) out) -> ()", &rms_norm);
   m.def("add_rms_norm(Tensor delta, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out) -> ()", &add_rms_norm);
   m.def("embed_rms_norm(Tensor ids, Tensor table, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out, "

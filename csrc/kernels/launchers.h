@@ -178,6 +178,13 @@ void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, fl
                            int K, int S, hipStream_t s);
 void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_lo, int e_hi, const float* w, int T, int k,
                         int d, float* out, int accumulate, hipStream_t s);
+// decode (T <= 8, E <= 64, k <= 8, d <= 4096, d % 8 == 0): rms_norm + router + route + align + scatter as one launch
+void launch_moe_decode_route(const float* resid, const bf16* lnw, float eps, const bf16* Wr, int T, int d, int E, int k,
+                             int* ids, float* w, int* counts, int* offsets, int* cursor, bf16* xs, int* dst,
+                             hipStream_t s);
+// decode, every expert local: moe_combine + add_prep as one launch (ss [T, parts]: partials over column parts)
+void launch_moe_combine_prep(LinOut y, int R, const int* dst, const int* ids, int E, const float* w, int T, int k, int d,
+                             float* resid, const bf16* w_next, bf16* xw, float* ss, int parts, hipStream_t s);
 
 // xgmi_ar.hip: one-shot all-reduce over xGMI peer memory (IPC-mapped buffers of every TP rank); the
 // constants and the push descriptor live at the top of this header (the decode GEMMs push into the slots)

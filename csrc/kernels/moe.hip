@@ -28,36 +28,46 @@ __global__ __launch_bounds__(256) void moe_route_kernel(LinOut logits, int ld, i
   if (t >= T) return;
   float v = lane < E ? linout_load1(logits, (long long)t * ld + lane) : -INFINITY;
   if (v != v) v = -INFINITY;  // a NaN logit never wins (and never selects a lane >= E)
+  // unrolled over the 8-slot maximum with guards: a runtime-indexed private array would live in scratch memory
   float sel[8];
   int seli[8];
-  for (int j = 0; j < k; ++j) {
-    float m = v;
-    int mi = lane;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float om = __shfl_xor(m, o, 64);
-      const int oi = __shfl_xor(mi, o, 64);
-      if (om > m || (om == m && oi < mi)) {
-        m = om;
-        mi = oi;
+  for (int j = 0; j < 8; ++j) {
+    sel[j] = 0.f;
+    seli[j] = j;
+    if (j < k) {
+      float m = v;
+      int mi = lane;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float om = __shfl_xor(m, o, 64);
+        const int oi = __shfl_xor(mi, o, 64);
+        if (om > m || (om == m && oi < mi)) {
+          m = om;
+          mi = oi;
+        }
       }
+      if (mi >= E) mi = j;  // degenerate rows (all -inf): fall back to experts 0..k-1
+      sel[j] = m;
+      seli[j] = mi;
+      if (lane == mi) v = -INFINITY;
     }
-    if (mi >= E) mi = j;  // degenerate rows (all -inf): fall back to experts 0..k-1
-    sel[j] = m;
-    seli[j] = mi;
-    if (lane == mi) v = -INFINITY;
   }
   if (lane == 0) {
     float mx = sel[0], s = 0.f;
-    if (mx == -INFINITY) {
-      for (int j = 0; j < k; ++j) sel[j] = 0.f;
-      mx = 0.f;
+    const bool deg = mx == -INFINITY;
+    if (deg) mx = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (deg) sel[j] = 0.f;
+      if (j < k) s += __expf(sel[j] - mx);
     }
-    for (int j = 0; j < k; ++j) s += __expf(sel[j] - mx);
-    for (int j = 0; j < k; ++j) {
-      ids[t * k + j] = seli[j];
-      w[t * k + j] = __expf(sel[j] - mx) / s;
-    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < k) {
+        ids[t * k + j] = seli[j];
+        w[t * k + j] = __expf(sel[j] - mx) / s;
+      }
   }
 }
 
@@ -364,7 +374,259 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(LinOut y, int R, const
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Decode-sized MoE routing in ONE launch (T <= 16 token rows, E <= 64 experts, k <= 8; one 16-wave
+// workgroup): RMSNorm of the fp32 residual rows, router logits, top-k + renormalised softmax, expert
+// histogram / offsets, segment rows in token order, and the permuted normalised rows xs -- what rms_norm,
+// the router GEMM, moe_route, moe_align and moe_scatter do as five launches on the general path (4.5-5.2 us
+// each at 4 rows: launch-floor-sized, profiles/r4/prof_mixtral_4clients_decode.csv).  xs rows equal the
+// rms_norm kernel's bf16 output (bf16(w * (x * rsqrt(mean(x^2) + eps)))); the router reads the same values.
+// ---------------------------------------------------------------------------------------------------
+constexpr int MDR_T = 8, MDR_K = 8, MDR_D = 4096, MDR_U = MDR_D / 512;  // rows, top-k, max d, 16-B loads per lane
+constexpr int MDR_WR = 8 * 4096;  // router elements staged in LDS (E * d up to this; else read from global)
+constexpr int MDR_NT = 512;       // 8 waves: 256 VGPRs per lane, so the staged router and a residual row fit
+
+// Latency shape (one workgroup: every step is at most one dependent memory round trip): the router weights
+// are loaded by all threads at entry and parked in LDS (they depend on nothing; parking them keeps registers
+// free -- held in registers across the norm phase they spilled to scratch); wave t < T loads residual row t
+// with the norm weights, reduces its sum of squares and writes the bf16 normalised row into LDS; the logits
+// are LDS x LDS dot products; top-k per token; the segment bookkeeping in parallel; the permuted rows go out
+// from LDS.
+__global__ __launch_bounds__(MDR_NT) void moe_decode_route_kernel(const float* __restrict__ resid,
+                                                                const bf16* __restrict__ lnw, float eps,
+                                                                const bf16* __restrict__ Wr, int T, int d, int E, int k,
+                                                                int* __restrict__ ids, float* __restrict__ w,
+                                                                int* __restrict__ counts, int* __restrict__ offsets,
+                                                                int* __restrict__ cursor, bf16* __restrict__ xs,
+                                                                int* __restrict__ dst) {
+  __shared__ uint4 s_xn[MDR_T * MDR_D / 8];  // bf16 normalised rows, 8 per uint4
+  __shared__ uint4 s_wr[MDR_WR / 8];         // bf16 router rows
+  __shared__ float s_lg[MDR_T][64];
+  __shared__ int s_ids[MDR_T * MDR_K];
+  __shared__ int s_dst[MDR_T * MDR_K];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nv = d / 8;  // 16-B vectors per row
+  const bool wr_lds = E * d <= MDR_WR;
+  uint4 wst[MDR_WR / 8 / MDR_NT];
+  if (wr_lds) {
+#pragma unroll
+    for (int u = 0; u < MDR_WR / 8 / MDR_NT; ++u) {
+      const int v = threadIdx.x + MDR_NT * u;
+      wst[u] = v < E * nv ? reinterpret_cast<const uint4*>(Wr)[v] : make_uint4(0, 0, 0, 0);
+    }
+  }
+  if (wid < T) {
+    float rv[MDR_U][8];
+    Pack8 gw[MDR_U];  // the norm weights, loaded with the row (one memory round trip)
+    float ss = 0.f;
+#pragma unroll
+    for (int u = 0; u < MDR_U; ++u) {
+      const int v = lane + 64 * u;
+      if (v < nv) {
+        load8f(resid + (long long)wid * d + 8 * v, rv[u]);
+        gw[u].u = *reinterpret_cast<const uint4*>(lnw + 8 * v);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < MDR_U; ++u)
+      if (lane + 64 * u < nv)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) ss += rv[u][q] * rv[u][q];
+    ss = wave_sum(ss);
+    const float rn = rsqrtf(ss / (float)d + eps);
+#pragma unroll
+    for (int u = 0; u < MDR_U; ++u) {
+      const int v = lane + 64 * u;
+      if (v < nv) {
+        Pack8 pk;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) pk.h[q] = (bf16)((float)gw[u].h[q] * (rv[u][q] * rn));
+        s_xn[wid * (MDR_D / 8) + v] = pk.u;
+      }
+    }
+  }
+  if (wr_lds) {
+#pragma unroll
+    for (int u = 0; u < MDR_WR / 8 / MDR_NT; ++u) s_wr[threadIdx.x + MDR_NT * u] = wst[u];
+  }
+  __syncthreads();
+  // logits: wave e against every row
+  for (int e = wid; e < E; e += MDR_NT / 64) {
+    float acc[MDR_T];
+#pragma unroll
+    for (int t = 0; t < MDR_T; ++t) acc[t] = 0.f;
+#pragma unroll
+    for (int u = 0; u < MDR_U; ++u) {
+      const int v = lane + 64 * u;
+      if (v < nv) {
+        Pack8 wv;
+        wv.u = wr_lds ? s_wr[e * nv + v] : *reinterpret_cast<const uint4*>(Wr + (long long)e * d + 8 * v);
+#pragma unroll
+        for (int t = 0; t < MDR_T; ++t)
+          if (t < T) {
+            Pack8 xv;
+            xv.u = s_xn[t * (MDR_D / 8) + v];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[t] += (float)xv.h[q] * (float)wv.h[q];
+          }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < MDR_T; ++t)
+      if (t < T) {
+        const float sum = wave_sum(acc[t]);
+        if (lane == 0) s_lg[t][e] = sum;
+      }
+  }
+  __syncthreads();
+  // top-k per token (wave t): the moe_route_kernel selection, ties to the lower expert
+  if (wid < T) {
+    float v = lane < E ? s_lg[wid][lane] : -INFINITY;
+    if (v != v) v = -INFINITY;
+    // (fully unrolled over MDR_K with guards: a runtime-indexed private array would live in scratch memory,
+    // one global round trip per access)
+    float sel[MDR_K];
+    int seli[MDR_K];
+#pragma unroll
+    for (int j = 0; j < MDR_K; ++j) {
+      sel[j] = 0.f;
+      seli[j] = j;
+      if (j < k) {
+        float m = v;
+        int mi = lane;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const float om = __shfl_xor(m, o, 64);
+          const int oi = __shfl_xor(mi, o, 64);
+          if (om > m || (om == m && oi < mi)) {
+            m = om;
+            mi = oi;
+          }
+        }
+        if (mi >= E) mi = j;
+        sel[j] = m;
+        seli[j] = mi;
+        if (lane == mi) v = -INFINITY;
+      }
+    }
+    if (lane == 0) {
+      float mx = sel[0], sum = 0.f;
+      const bool deg = mx == -INFINITY;
+      if (deg) mx = 0.f;
+#pragma unroll
+      for (int j = 0; j < MDR_K; ++j) {
+        if (deg) sel[j] = 0.f;
+        if (j < k) sum += __expf(sel[j] - mx);
+      }
+#pragma unroll
+      for (int j = 0; j < MDR_K; ++j)
+        if (j < k) {
+          ids[wid * k + j] = seli[j];
+          s_ids[wid * k + j] = seli[j];
+          w[wid * k + j] = __expf(sel[j] - mx) / sum;
+        }
+    }
+  }
+  __syncthreads();
+  const int R = T * k;
+  // histogram, offsets and segment rows in token order, in parallel (R <= 64, E <= 64): lane e of wave 0 counts
+  // expert e, a wave scan gives the offsets, and thread a < R places assignment a after the earlier ones of
+  // its expert
+  __shared__ int s_off[65];
+  if (wid == 0) {
+    int c = 0;
+    if (lane < E)
+      for (int a = 0; a < R; ++a) c += s_ids[a] == lane;
+    int incl = c;  // inclusive scan over the 64 lanes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane < E) {
+      s_off[lane] = incl - c;
+      counts[lane] = c;
+      cursor[lane] = 0;
+      offsets[lane] = incl - c;
+    }
+    if (lane == E - 1) {
+      s_off[E] = incl;
+      offsets[E] = incl;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < R) {
+    const int a = threadIdx.x, e = s_ids[a];
+    int before = 0;
+    for (int b = 0; b < a; ++b) before += s_ids[b] == e;
+    s_dst[a] = s_off[e] + before;
+    dst[a] = s_off[e] + before;
+  }
+  __syncthreads();
+  // xs[dst[a]] = normalised row of token a / k, from LDS
+  for (int a = 0; a < R; ++a) {
+    const int t = a / k, row = s_dst[a];
+    for (int v = threadIdx.x; v < nv; v += MDR_NT)
+      reinterpret_cast<uint4*>(xs + (long long)row * d)[v] = s_xn[t * (MDR_D / 8) + v];
+  }
+}
+
+// moe_combine + add_prep in one launch (decode, experts all local): resid[t] += sum_j w[t][j] Y[dst[t][j]];
+// xw[t] = bf16(resid[t] * w_next); ss[t][p] = sum of resid[t]^2 over column part p (grid (T, P): one 8-column
+// vector per thread, one load round trip per workgroup; the consumer's deferred norm sums the P partials)
+__global__ __launch_bounds__(64) void moe_combine_prep_kernel(LinOut y, int R, const int* __restrict__ dst,
+                                                              const int* __restrict__ ids, int E,
+                                                              const float* __restrict__ w, int k, int d,
+                                                              float* __restrict__ resid,
+                                                              const bf16* __restrict__ w_next, bf16* __restrict__ xw,
+                                                              float* __restrict__ ss) {
+  const int t = blockIdx.x, P = gridDim.y, vp = d / 8 / P;
+  float sq = 0.f;
+  for (int i = blockIdx.y * vp + threadIdx.x; i < (blockIdx.y + 1) * vp; i += 64) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < k; ++j) {
+      const int row = dst[t * k + j];
+      const int ex = ids[t * k + j];
+      if (row < 0 || row >= R || ex < 0 || ex >= E) continue;
+      const float wj = w[t * k + j];
+      float v[8];
+      linout_load8(y, (long long)row * d + i * 8, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += wj * v[q];
+    }
+    float* rp = resid + (long long)t * d + i * 8;
+    float r[8], g[8];
+    load8f(rp, r);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) r[q] += acc[q];
+    store8f(rp, r);
+    load8(w_next + i * 8, g);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      sq += r[q] * r[q];
+      g[q] *= r[q];
+    }
+    store8(xw + (long long)t * d + i * 8, g);
+  }
+  sq = wave_sum(sq);
+  if (threadIdx.x == 0) ss[t * P + blockIdx.y] = sq;
+}
+
 }  // namespace
+
+void launch_moe_decode_route(const float* resid, const bf16* lnw, float eps, const bf16* Wr, int T, int d, int E, int k,
+                             int* ids, float* w, int* counts, int* offsets, int* cursor, bf16* xs, int* dst,
+                             hipStream_t s) {
+  if (T == 0) return;
+  moe_decode_route_kernel<<<1, MDR_NT, 0, s>>>(resid, lnw, eps, Wr, T, d, E, k, ids, w, counts, offsets, cursor, xs,
+                                             dst);
+}
+
+void launch_moe_combine_prep(LinOut y, int R, const int* dst, const int* ids, int E, const float* w, int T, int k, int d,
+                             float* resid, const bf16* w_next, bf16* xw, float* ss, int parts, hipStream_t s) {
+  if (T == 0) return;
+  moe_combine_prep_kernel<<<dim3(T, parts), 64, 0, s>>>(y, R, dst, ids, E, w, k, d, resid, w_next, xw, ss);
+}
 
 void launch_moe_route(LinOut logits, int ld, int T, int E, int k, int* ids, float* w, hipStream_t s) {
   if (T == 0) return;

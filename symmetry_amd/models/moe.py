@@ -38,6 +38,12 @@ A2A_ROWS = int(os.environ.get("SYMMETRY_MOE_A2A_ROWS", "128"))
 GROUPED = os.environ.get("SYMMETRY_MOE_GROUPED", "1") != "0"  # A/B: 0 = per-expert library GEMMs (host sync)
 # count the all-to-all bytes this rank pushes (reads the device counts: a host sync per layer -- tests / benches)
 A2A_STATS = os.environ.get("SYMMETRY_MOE_A2A_STATS", "0") == "1"
+# decode steps: routing in one launch and the combine fused with the residual prep (A/B: 0 = five routing launches
+# + combine + add_prep; profiles/r4/moe_decode_fused.jsonl)
+DECODE_FUSED = os.environ.get("SYMMETRY_MOE_DECODE_FUSED", "1") != "0"
+# rows up to which the routing runs as the one-workgroup launch: 8.8 vs 12.0 us at 1 row, 12.8 vs 14.0 at 4,
+# 17.8 vs 14.1 at 8 (profiles/r4/moe_decode_fused.jsonl)
+ROUTE_FUSED_ROWS = int(os.environ.get("SYMMETRY_MOE_ROUTE_FUSED_ROWS", "4"))
 
 
 class MoEBlock:
@@ -78,6 +84,49 @@ class MoEBlock:
             return self.forward_a2a(i, x)
         self.calls["allreduce"] += 1
         return self._forward_local(i, x, reduce=self.ep > 1)
+
+    def decode_fused_ok(self, T: int, d: int) -> bool:
+        """The one-launch routing (+ fused combine / residual prep) of a decode step applies."""
+        return (DECODE_FUSED and T <= 8 and not self.use_a2a(T) and self.E <= 64 and self.k <= 8 and d % 8 == 0
+                and d <= 4096)
+
+    def forward_decode(self, i: int, resid, lnw, eps: float, w_next, xw, ss_1) -> torch.Tensor:
+        """A decode step's MoE block straight off the fp32 residual stream: ONE routing launch (RMSNorm + router
+        + top-k + segments + permuted rows, ``ops.moe_decode_route``), the grouped expert GEMMs, and the weighted
+        combine fused with the residual add + next-norm prep (``ops.moe_combine_prep``); under expert
+        parallelism the combine stays separate (its partial sum is all-reduced first).  resid += MoE(RMSNorm(
+        resid)); xw and the returned sum-of-squares partials ([T, P]; ``ss_1`` [T, 1] under EP): the next layer's
+        deferred-norm inputs."""
+        self.calls["allreduce"] += 1
+        T, d = resid.shape
+        k, E = self.k, self.E
+        R = T * k
+        ids = self._buf("ids", (R,), torch.int32)
+        w = self._buf("w", (R,), torch.float32)
+        dst = self._buf("dst", (R,), torch.int32)
+        counts = self._buf("counts", (E,), torch.int32)
+        offsets = self._buf("offsets", (E + 1,), torch.int32)
+        cursor = self._buf("cursor", (E,), torch.int32)
+        xs = self._buf("xs", (R, d), torch.bfloat16)
+        if T <= ROUTE_FUSED_ROWS:
+            ops.moe_decode_route(resid, lnw, eps, self.router[i][:E], k, ids, w, counts, offsets, cursor, xs, dst)
+        else:  # the one-workgroup routing launch stops paying off past a few rows (bench_moe_decode.py)
+            xn = self._buf("xn", (T, d), torch.bfloat16)
+            ops.rms_norm(resid, lnw, eps, xn)
+            logits = self.m._linear("router", xn, self.router[i])
+            ops.moe_route_permute(logits, xn, k, E, ids, w, counts, offsets, cursor, xs, dst)
+        y2 = self._experts(i, xs, offsets, self.e_lo, self.E_local, out_f32=True)
+        if self.ep > 1:
+            out = self._buf("out", (T, d), torch.float32)
+            ops.moe_combine(y2, dst, ids, self.e_lo, self.e_hi, w, k, out)
+            self.comm.all_reduce(out)
+            ops.add_prep(out, resid, w_next, xw, ss_1)
+            return ss_1
+        nv = d // 8
+        P = nv // 64 if nv % 64 == 0 and nv >= 64 else 1  # one 8-column vector per thread of a 64-thread part
+        ss = self._buf("ss_parts", (T, P), torch.float32)
+        ops.moe_combine_prep(y2, dst, ids, E, w, k, resid, w_next, xw, ss)
+        return ss
 
     # ------------------------------------------------------------------------------------------
     def _route(self, i, x):

@@ -403,11 +403,14 @@ class TransformerLM:
             ss = self._resid_proj("o", attn2d, self._dgw(i, "wo"), resid, w.layer(i, "ln2"), xw, ss_t, ss_1,
                                   w.layer(i, "wo"))
             if cfg.is_moe:
-                # router + experts are not decode GEMMs: materialise RMSNorm(resid) (one bf16 rounding)
-                xn = self._buf("x", (T, d), torch.bfloat16)
-                ops.rms_norm(resid, w.layer(i, "ln2"), eps, xn)
-                ops.add_prep(self.moe.forward(i, xn), resid, nxt, xw, ss_1)
-                ss = ss_1
+                if self.moe.decode_fused_ok(T, d):
+                    ss = self.moe.forward_decode(i, resid, w.layer(i, "ln2"), eps, nxt, xw, ss_1)
+                else:
+                    # router + experts are not decode GEMMs: materialise RMSNorm(resid) (one bf16 rounding)
+                    xn = self._buf("x", (T, d), torch.bfloat16)
+                    ops.rms_norm(resid, w.layer(i, "ln2"), eps, xn)
+                    ops.add_prep(self.moe.forward(i, xn), resid, nxt, xw, ss_1)
+                    ss = ss_1
             else:
                 w_gu, shg = self._dgw(i, "w_gu")
                 act = self._buf("act", (T, w_gu.shape[0] // 2), torch.bfloat16)

@@ -299,6 +299,22 @@ def grouped_skinny(xs, W, offsets, e0, y):
     return reference.grouped_skinny(xs, W, offsets, e0, y)
 
 
+def moe_decode_route(resid, lnw, eps, Wr, k, ids, w, counts, offsets, cursor, xs, dst):
+    """Decode MoE routing in one launch: RMSNorm(resid) rows -> router logits -> top-k -> expert segments ->
+    xs (the normalised rows permuted into their segments, token order within a segment)."""
+    if _gpu(resid):
+        return _native.ops().moe_decode_route(resid, lnw, float(eps), Wr, int(k), ids, w, counts, offsets, cursor,
+                                              xs, dst)
+    return reference.moe_decode_route(resid, lnw, eps, Wr, k, ids, w, counts, offsets, cursor, xs, dst)
+
+
+def moe_combine_prep(y, dst, ids, E, w, k, resid, w_next, xw, ss):
+    """moe_combine over every expert fused with add_prep (decode, experts all on this rank)."""
+    if _gpu(resid):
+        return _native.ops().moe_combine_prep(y, dst, ids, int(E), w, int(k), resid, w_next, xw, ss)
+    return reference.moe_combine_prep(y, dst, ids, E, w, k, resid, w_next, xw, ss)
+
+
 def moe_combine(y, dst, ids, e_lo, e_hi, w, k, out, accumulate=False):
     if _gpu(out):
         return _native.ops().moe_combine(y, dst, ids, int(e_lo), int(e_hi), w, int(k), out, bool(accumulate))

@@ -484,3 +484,20 @@ def sample_filtered(logits, temps, top_k, top_p, seeds, step, out_ids) -> None:
         v = l / t - torch.log(-torch.log(u.to(l.device)))
         v = torch.where(l >= thr, v, torch.full_like(v, -float("inf")))
         out_ids[r] = int(torch.argmax(v))
+
+
+def moe_decode_route(resid, lnw, eps, Wr, k: int, ids, w, counts, offsets, cursor, xs, dst) -> None:
+    """rms_norm + router logits + moe_route_permute (the fused decode routing kernel's contract)."""
+    T, d = resid.shape
+    xn = torch.empty(T, d, dtype=torch.bfloat16)
+    rms_norm(resid, lnw, eps, xn)
+    logits = _mm(xn, Wr)
+    moe_route_permute(logits, xn, k, Wr.shape[0], ids, w, counts, offsets, cursor, xs, dst)
+
+
+def moe_combine_prep(y, dst, ids, E: int, w, k: int, resid, w_next, xw, ss) -> None:
+    """moe_combine over every expert + add_prep (one sum-of-squares partial per row)."""
+    T, d = resid.shape
+    out = torch.empty(T, d, dtype=torch.float32)
+    moe_combine(y, dst, ids, 0, E, w, k, out, False)
+    add_prep(out, resid, w_next, xw, ss)

@@ -251,6 +251,50 @@ def test_moe_kernels_vs_reference(gpu):
     assert torch.allclose(out.cpu(), c_out, atol=1e-3, rtol=1e-3)
 
 
+@pytest.mark.parametrize("T,d,E,k", [(4, 4096, 8, 2), (8, 512, 8, 2), (1, 256, 64, 8), (7, 1024, 16, 4),
+                                     (3, 4000, 20, 2)])
+def test_moe_decode_fused_vs_reference(gpu, T, d, E, k):
+    """The one-launch decode routing (RMSNorm + router + top-k + segments + permuted rows) and the combine fused
+    with the residual prep against their fp32 compositions (reference.rms_norm / router / moe_route_permute;
+    moe_combine + add_prep)."""
+    g = torch.Generator(device=gpu).manual_seed(T * 31 + E)
+    resid = torch.randn(T, d, device=gpu, generator=g) * 3
+    lnw = (torch.rand(d, device=gpu, generator=g) + 0.5).bfloat16()
+    Wr = (torch.randn(E, d, device=gpu, generator=g) * 0.05).bfloat16()
+    R = T * k
+    ids = torch.empty(R, dtype=torch.int32, device=gpu)
+    w = torch.empty(R, device=gpu)
+    dst = torch.empty(R, dtype=torch.int32, device=gpu)
+    counts = torch.empty(E, dtype=torch.int32, device=gpu)
+    offsets = torch.empty(E + 1, dtype=torch.int32, device=gpu)
+    cursor = torch.full((E,), 7, dtype=torch.int32, device=gpu)
+    xs = torch.empty(R, d, dtype=torch.bfloat16, device=gpu)
+    ops.moe_decode_route(resid, lnw, 1e-5, Wr, k, ids, w, counts, offsets, cursor, xs, dst)
+    c_ids, c_w, c_dst = torch.empty(R, dtype=torch.int32), torch.empty(R), torch.empty(R, dtype=torch.int32)
+    c_cnt, c_off = torch.empty(E, dtype=torch.int32), torch.empty(E + 1, dtype=torch.int32)
+    c_cur, c_xs = torch.empty(E, dtype=torch.int32), torch.empty(R, d, dtype=torch.bfloat16)
+    ref.moe_decode_route(resid.cpu(), lnw.cpu(), 1e-5, Wr.cpu(), k, c_ids, c_w, c_cnt, c_off, c_cur, c_xs, c_dst)
+    assert torch.equal(ids.cpu(), c_ids)  # random logits: no near-ties at this scale
+    assert torch.allclose(w.cpu(), c_w, atol=1e-5)
+    assert torch.equal(offsets.cpu(), c_off) and torch.equal(counts.cpu(), c_cnt)
+    assert torch.equal(dst.cpu(), c_dst)  # segment rows in token order, like the reference
+    assert int(cursor.abs().sum()) == 0
+    assert (xs.cpu().float() - c_xs.float()).abs().max() <= 0.02 * c_xs.float().abs().max()
+    # combine + residual prep (every expert local)
+    y = torch.randn(2, R, d, device=gpu, generator=g)
+    w_next = (torch.rand(d, device=gpu, generator=g) + 0.5).bfloat16()
+    xw = torch.empty(T, d, dtype=torch.bfloat16, device=gpu)
+    P = d // 8 // 64 if (d // 8) % 64 == 0 else 1
+    ss = torch.empty(T, P, device=gpu)
+    r0 = resid.clone()
+    ops.moe_combine_prep(y, dst, ids, E, w, k, resid, w_next, xw, ss)
+    c_r, c_xw, c_ss = r0.cpu().clone(), torch.empty(T, d, dtype=torch.bfloat16), torch.empty(T, P)
+    ref.moe_combine_prep(y.cpu(), dst.cpu(), ids.cpu(), E, w.cpu(), k, c_r, w_next.cpu(), c_xw, c_ss)
+    assert torch.allclose(resid.cpu(), c_r, atol=1e-4, rtol=1e-5)
+    assert torch.allclose(xw.cpu().float(), c_xw.float(), atol=2e-2, rtol=1e-2)
+    assert torch.allclose(ss.cpu(), c_ss, rtol=1e-4)
+
+
 def test_rccl_single_rank_allreduce_and_capture(gpu):
     import socket
 
