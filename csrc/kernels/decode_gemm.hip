@@ -732,7 +732,17 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
       else if (M > 1 && N <= 8192 && K >= 3072 && K % 256 == 0) v = 4;
       else v = 0;
     } else if (M <= 4) {
-      v = 0;
+      // row-major (models too large for a preshuffled copy: Llama-3-70B on one GPU) at <= 4 rows: two row tiles
+      // per 8-wave workgroup when that grid is a whole number of rounds over the CUs, else 4 waves per tile
+      // (profiles/r4/dg_70b_row.jsonl, 4 rows: gate_up 179.4 -> 163.4 us, down 92.6 -> 85.7, o 31.1 -> 29.8,
+      // qkv 41.2 -> 40.1)
+      if (g_num_cus == 0) {
+        int dev = 0;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+        g_num_cus = std::max(1, g_num_cus);
+      }
+      v = (N % 32 == 0 && (N / 32) % g_num_cus == 0) ? 3 : (K >= 4096 && K % 256 == 0 ? 4 : 0);
     } else if (N >= 12288) {
       // row-major wide N above 16 rows (the lm_head, whose weights are never preshuffled): 4 row tiles per
       // workgroup, lm_head 268 -> 224 us at M = 24, 421 -> 335 at M = 64 (profiles/decode_gemm_bigm_row_r1.jsonl)
