@@ -714,8 +714,9 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
       // sharing of multi-tile workgroups unnecessary; wide N prefers 4 waves per tile
       // x-resident persistent tiles (profiles/decode_gemm_xres_r1.jsonl, M = 10: gate_up 49.1 -> 40.9 us,
       // qkv 15.6 -> 13.4, lm_head 205.9 -> 190.5; = variant 2 on the one-tile-per-CU O projection), except
-      // the vocabulary projection at <= 4 rows where the 8-wave split stays ahead
-      if (M <= 16 && K % 1024 == 0 && K <= 4096 && !(N >= 65536 && M <= 4)) v = 11;
+      // the vocabulary projection at <= 2 rows where the 8-wave split stays ahead (lm_head 171 vs 177-183 us;
+      // at 4 rows the walk wins, 179 vs 186: profiles/r4/dg_lm_head_small_m.jsonl)
+      if (M <= 16 && K % 1024 == 0 && K <= 4096 && !(N >= 65536 && M <= 2)) v = 11;
       // wide N at 2..16 rows otherwise (Llama-3-70B at TP <= 4: gate_up, lm_head; K = 8192): 4 waves per tile.
       // (The round-1 pick, 7 resident 4-wave workgroups per CU -- variant 8, launch bounds (256, 7) -- now spills
       // 32 VGPRs to scratch with the grown epilogues: 70B gate_up 293-317 vs 165-204 us at 8-16 rows,
@@ -723,7 +724,7 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
       // above 16 rows (profiles/decode_gemm_bigm_r1.jsonl, M = 64): wide N shares each x fragment over
       // four row tiles (gate_up 93.6 -> 76.7 us, lm_head 367 -> 307), qkv over two (43.7 -> 33.3)
       // (eight row tiles from 25 rows: gate_up 77.0 -> 69.1 us at M = 64, profiles/decode_gemm_rt8_r1.jsonl)
-      else if (N >= 12288) v = M > 16 ? (M > 24 ? 14 : 3) : (M == 1 ? 0 : 4);
+      else if (N >= 12288) v = M > 16 ? (M > 24 ? 14 : 3) : (M <= 2 ? 0 : 4);
       else if (M > 16 && N > 4096) v = 3;
       else if (N <= 4096 && K % 1024 == 0) v = K > 4096 ? 4 : 2;  // few row tiles: split K (down_proj: 4 waves,
                                                                   // 24.2 vs 25.7 us at M = 10)
