@@ -726,8 +726,9 @@ void launch_mt(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEp
       // (eight row tiles from 25 rows: gate_up 77.0 -> 69.1 us at M = 64, profiles/decode_gemm_rt8_r1.jsonl)
       else if (N >= 12288) v = M > 16 ? (M > 24 ? 14 : 3) : (M <= 2 ? 0 : 4);
       else if (M > 16 && N > 4096) v = 3;
-      else if (N <= 4096 && K % 1024 == 0) v = K > 4096 ? 4 : 2;  // few row tiles: split K (down_proj: 4 waves,
-                                                                  // 24.2 vs 25.7 us at M = 10)
+      else if (N <= 4096 && K % 1024 == 0) v = K > 4096 ? (M <= 4 ? 0 : 4) : 2;  // few row tiles: split K
+        // (down_proj: 4 waves, 24.2 vs 25.7 us at M = 10; at <= 4 rows 8 waves: 24.2 vs 26.0 at 1 row,
+        // profiles/r4/dg_sweep_8b.jsonl)
       // Llama-3-70B TP = 8 gate_up (7168 x 8192) and down (8192 x 3584) at 2..16 rows: 4 waves per tile
       // (profiles/r4/dg_tile_ksplit.jsonl, variant 4 vs -1: 27.6 vs 29.4 us and 15.2 vs 16.5 at M = 10)
       else if (M > 1 && N <= 8192 && K >= 3072 && K % 256 == 0) v = 4;
