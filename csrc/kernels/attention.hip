@@ -474,6 +474,7 @@ __global__ __launch_bounds__(128 * HPW) void attn_prefill_lds_kernel(
   const int qstart = cu_q[seq], qlen = cu_q[seq + 1] - qstart;
   const int ctx = ctx_lens[seq];
   const int pos0 = ctx - qlen;
+  if (qrow0 >= qlen) return;  // padding tile (graph-captured prefill buckets): workgroup-uniform, before any barrier
   const int* bt = block_tables + (long long)seq * max_blocks;
   // keys visible to any row of the workgroup / of this wave
   const int kend_wg = min(ctx, pos0 + min(qrow0 + 64, qlen));
@@ -680,6 +681,7 @@ __global__ __launch_bounds__(512, 2) void attn_prefill_m32p_kernel(
   const int qstart = cu_q[seq], qlen = cu_q[seq + 1] - qstart;
   const int ctx = ctx_lens[seq];
   const int pos0 = ctx - qlen;
+  if (qrow0 >= qlen) return;  // padding tile (graph-captured prefill buckets): workgroup-uniform, before any barrier
   const int* bt = block_tables + (long long)seq * max_blocks;
   const int row0 = qrow0 + 32 * half;
   const int kend_wg = min(ctx, pos0 + min(qrow0 + 64, qlen));

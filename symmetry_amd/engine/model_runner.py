@@ -36,7 +36,16 @@ MAX_DECODE_ROWS = 256  # decode rows per step (past FUSED_DECODE_ROWS: the gener
 FUSED_DECODE_ROWS = 64
 CTX_BUCKETS = (512, 2048, 8192, 32768, 131072)  # tokens (multiples of the 512-token attention partition)
 CMD_STOP, CMD_CAPTURE, CMD_SYNC = -1, 2, 3  # control headers of the rank-0 -> worker metadata plane
+KIND_DECODE, KIND_PREFILL, KIND_PREFILL_GRAPH = 0, 1, 4  # header[0] of a step
 HEADER_LEN = 7  # kind, T, rows, max_blocks, prefill tiles, real seqs, filtered-sampling flag
+# Short prefills replay a hipGraph too: T padded up to one of these token buckets, the sequence count to 1/2/4.
+# A 128-token Llama-3-8B prefill is ~300 launches whose host enqueue (~4.8 ms) outlasts its GPU time (~3 ms):
+# the single-client TTFT was host-bound.  SYMMETRY_PREFILL_GRAPH_TOKENS (0: off) bounds the bucket.
+PREFILL_GRAPH_BUCKETS = (16, 32, 64, 128, 192, 256)
+PREFILL_GRAPH_SEQS = (1, 2, 4)
+PREFILL_GRAPH_TOKENS = int(os.environ.get("SYMMETRY_PREFILL_GRAPH_TOKENS", "256"))
+PREFILL_GRAPH_MAX = 48  # captured prefill graphs at most (lazily, per bucket); past that, eager
+_PAD_TILE_ROW = 1 << 24  # query row of a padding attention tile: past every qlen, so its workgroups exit
 _SEED_MIX = 0x9E3779B97F4A7C15
 
 
@@ -119,6 +128,8 @@ class ModelRunner:
         self.ctx_blocks = [b for b in self.ctx_blocks if b <= self.max_blocks]
         self.is_gpu = self.device.type != "cpu"
         self.use_graphs = use_graphs and self.is_gpu
+        # pad short prefills to the graph buckets (without use_graphs -- CPU tests -- they then run eagerly)
+        self.prefill_graphs = self.use_graphs
         self.tp_size, self.tp_rank = tp_size, tp_rank
         self.cpu_group = cpu_group
         self.graphs: dict[tuple, tuple] = {}
@@ -254,8 +265,10 @@ class ModelRunner:
         for i, seq in enumerate(seqs):
             btv[i, :len(seq.block_table)] = seq.block_table
         if lay.prefill:
-            cu = np.zeros(lay.nseq + 1, dtype=np.int64)
-            cu[1:] = np.cumsum(counts)
+            # padding sequences of a graph bucket: qlen 0 (cu_q repeats the real total), context 1, last row 0
+            cu = np.full(lay.nseq + 1, len(ids), dtype=np.int64)
+            cu[0] = 0
+            cu[1:nreal + 1] = np.cumsum(counts, dtype=np.int64)
             host[lay.cu:lay.cu + lay.nseq + 1] = cu
             tiles = []
             for i, n in enumerate(counts):
@@ -264,8 +277,11 @@ class ModelRunner:
             # in the first wave of attention workgroups instead of finishing last
             if len(tiles) > 1:
                 tiles.sort(key=lambda t: -(ctx[t[0]] - counts[t[0]] + min(t[1] + 64, counts[t[0]])))
-            host[lay.tiles:lay.tiles + 2 * len(tiles)] = np.asarray(tiles, dtype=np.int32).reshape(-1)
-            host[lay.last:lay.last + 2 * lay.nseq] = (cu[1:] - 1).astype(np.int64).view(np.int32)
+            if tiles:
+                host[lay.tiles:lay.tiles + 2 * len(tiles)] = np.asarray(tiles, dtype=np.int32).reshape(-1)
+            if lay.ntiles > len(tiles):  # padding tiles (graph buckets): row past every qlen -> workgroup exits
+                host[lay.tiles + 2 * len(tiles) + 1:lay.tiles + 2 * lay.ntiles:2] = _PAD_TILE_ROW
+            host[lay.last:lay.last + 2 * lay.nseq] = np.maximum(cu[1:] - 1, 0).astype(np.int64).view(np.int32)
 
     def _forward_batch(self, kind: str, lay: _Layout, dev: torch.Tensor, nseq: int, need_logits=False,
                        filtered=False):
@@ -288,22 +304,28 @@ class ModelRunner:
         token is that step's (not yet host-visible) sample."""
         seqs, counts = batch.seqs, batch.num_new_tokens
         t0 = time.perf_counter()
+        filt = int(self._filtered(seqs))
+        nseq = len(seqs)
         if batch.kind == "decode":
-            nseq = len(seqs)
             bucket = self._bucket(nseq)
             need = max(len(s.block_table) for s in seqs)
             lay = _Layout(bucket, bucket, self._ctx_bucket(need), prefill=False)
+            kind = KIND_DECODE
         else:
-            nseq = len(seqs)
-            ntiles = sum((n + 63) // 64 for n in counts)
+            T = sum(counts)
             max_blocks = max(len(s.block_table) for s in seqs)
-            lay = _Layout(sum(counts), nseq, max_blocks, prefill=True, ntiles=ntiles)
+            shape = self._prefill_graph_shape(T, nseq, max_blocks, filt)
+            if shape is not None:
+                lay, kind = _Layout(*shape, prefill=True, ntiles=self._pad_tiles(shape[0], shape[1])), \
+                    KIND_PREFILL_GRAPH
+            else:
+                ntiles = sum((n + 63) // 64 for n in counts)
+                lay, kind = _Layout(T, nseq, max_blocks, prefill=True, ntiles=ntiles), KIND_PREFILL
         self._parity ^= 1
         host_t = self._host(lay.size, f"{batch.kind}{self._parity}")  # double-buffered: the previous
         host = host_t.numpy()                                          # step's H2D may still be queued
         self._fill(lay, host, seqs, counts, prev_rows)
-        header = np.array([0 if batch.kind == "decode" else 1, lay.T, lay.nseq, lay.max_blocks, lay.ntiles, nseq,
-                           int(self._filtered(seqs))], dtype=np.int32)
+        header = np.array([kind, lay.T, lay.nseq, lay.max_blocks, lay.ntiles, nseq, filt], dtype=np.int32)
         t1 = time.perf_counter()
         if self.meta is not None:
             self._broadcast(header, host_t)
@@ -345,6 +367,26 @@ class ModelRunner:
         self.timing["forward"] += time.perf_counter() - handle["t0"]
         return ids[:handle["nseq"]]
 
+    @staticmethod
+    def _pad_tiles(T: int, nseq: int) -> int:
+        """Attention tiles of a prefill bucket: sum(ceil(n_i / 64)) <= (T + 63 * nseq) / 64 for any split."""
+        return (T + 63 * nseq) // 64
+
+    def _prefill_graph_shape(self, T: int, nseq: int, nblocks: int, filt: int):
+        """(T bucket, sequence bucket, block-table bucket) of a prefill that replays a hipGraph, or None (eager).
+        One GPU, dense models: a TP prefill's collectives and the MoE dispatch stay eager."""
+        if not (self.prefill_graphs and PREFILL_GRAPH_TOKENS > 0 and self.tp_size == 1 and not self.model.cfg.is_moe):
+            return None
+        Tb = next((b for b in PREFILL_GRAPH_BUCKETS if T <= b <= PREFILL_GRAPH_TOKENS), None)
+        nb = next((b for b in PREFILL_GRAPH_SEQS if nseq <= b), None)
+        if Tb is None or nb is None or nblocks > self.max_blocks:
+            return None
+        mb = self._ctx_bucket(nblocks)
+        key = ("prefill", Tb, nb, mb, self._pad_tiles(Tb, nb), bool(filt))
+        if key not in self.graphs and sum(isinstance(k[0], str) for k in self.graphs) >= PREFILL_GRAPH_MAX:
+            return None
+        return Tb, nb, mb
+
     def _bucket(self, n: int) -> int:
         for b in self.buckets:
             if b >= n:
@@ -358,14 +400,20 @@ class ModelRunner:
         raise ValueError(f"sequence needs {nblocks} blocks > max {self.max_blocks}")
 
     def _run(self, header: np.ndarray, host_t: torch.Tensor) -> torch.Tensor:
-        kind = "decode" if header[0] == 0 else "prefill"
+        kind = "decode" if header[0] == KIND_DECODE else "prefill"
         T, nseq_l, max_blocks, ntiles, nseq, filt = (int(x) for x in header[1:HEADER_LEN])
         lay = _Layout(T, nseq_l, max_blocks, prefill=kind == "prefill", ntiles=ntiles)
-        if kind == "decode" and self.use_graphs:
-            key = (T, max_blocks, bool(filt))
+        if self.use_graphs and (kind == "decode" or header[0] == KIND_PREFILL_GRAPH):
+            if kind == "decode":
+                key = (T, max_blocks, bool(filt))
+            else:
+                key = ("prefill", T, nseq_l, max_blocks, ntiles, bool(filt))
             g = self.graphs.get(key)
             if g is None:
-                self._capture(T, max_blocks, bool(filt))
+                if kind == "decode":
+                    self._capture(T, max_blocks, bool(filt))
+                else:
+                    self._capture(T, max_blocks, bool(filt), prefill=lay)
                 g = self.graphs[key]
             graph, dev, out, exec_ = g
             if exec_:
@@ -388,16 +436,19 @@ class ModelRunner:
         return ids
 
     # ------------------------------------------------------------------------------------------
-    def _capture(self, bucket: int, max_blocks: int, filtered: bool = False) -> None:
+    def _capture(self, bucket: int, max_blocks: int, filtered: bool = False, prefill: _Layout | None = None) -> None:
         """Capture the decode forward for `bucket` rows and a `max_blocks`-wide block table, with or
-        without the top-k / top-p resampler (largest first avoids workspace growth)."""
-        lay = _Layout(bucket, bucket, max_blocks, prefill=False)
+        without the top-k / top-p resampler (largest first avoids workspace growth).  ``prefill``: capture
+        that padded prefill layout instead (the warmup and capture run on all-padding metadata: no cache
+        slot is written, every attention tile exits)."""
+        lay = prefill if prefill is not None else _Layout(bucket, bucket, max_blocks, prefill=False)
+        kind = "prefill" if prefill is not None else "decode"
         dev = torch.zeros(lay.size, dtype=torch.int32, device=self.device)
         host = self._host(lay.size, "capture")
         hn = host.numpy()
         self._fill(lay, hn, [], [])
         dev.copy_(host[:lay.size])
-        fb = self._forward_batch("decode", lay, dev, bucket, filtered=filtered)
+        fb = self._forward_batch(kind, lay, dev, lay.nseq, filtered=filtered)
         # eager warmup: allocates workspace and loads kernels outside the capture
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -418,7 +469,9 @@ class ModelRunner:
                 exec_ = int(g.raw_cuda_graph_exec())
             except Exception:  # noqa: BLE001 -- older torch: replay() it is
                 exec_ = 0
-        self.graphs[(bucket, max_blocks, filtered)] = (g, dev, out, exec_)
+        key = (bucket, max_blocks, filtered) if prefill is None else \
+            ("prefill", lay.T, lay.nseq, lay.max_blocks, lay.ntiles, filtered)
+        self.graphs[key] = (g, dev, out, exec_)
 
     def capture_all(self) -> float:
         """Rank 0: capture every (batch, context) decode graph; under TP each capture is mirrored by the

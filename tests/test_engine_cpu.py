@@ -57,6 +57,40 @@ def test_continuous_batching_matches_reference():
         _agree(eng.weights, p, s.output_ids, tol=0.05)
 
 
+def test_padded_prefill_buckets_match_reference():
+    """The hipGraph prefill buckets' padded metadata (token rows with slot -1, sequences with qlen 0, padding
+    attention tiles), run eagerly here: prompts of 3..256 tokens, one to three per step and a prefix-cache tail
+    agree with the fp32 forward, and the buckets were taken (a 300-token step stays unpadded)."""
+    from symmetry_amd.engine import model_runner as mr
+
+    eng = _engine(max_num_seqs=4, max_model_len=1024, max_num_batched_tokens=512)
+    eng.runner.prefill_graphs = True
+    shapes = []
+    orig = eng.runner._prefill_graph_shape
+
+    def spy(T, nseq, nblocks, filt):
+        s = orig(T, nseq, nblocks, filt)
+        shapes.append((T, nseq, s))
+        return s
+
+    eng.runner._prefill_graph_shape = spy
+    groups = [_prompts(1, seed=1, lo=3, hi=4), _prompts(1, seed=2, lo=17, hi=18), _prompts(3, seed=3, lo=20, hi=70),
+              _prompts(1, seed=4, lo=250, hi=251), _prompts(2, seed=5, lo=150, hi=151)]
+    groups.append([groups[3][0][:120] + [9, 8, 7]])  # prefix-cache hit: only the tail is prefilled
+    for group in groups:
+        seqs = [eng.add_request(f"p{len(shapes)}-{j}", p, SamplingParams(max_tokens=5, ignore_eos=True))
+                for j, p in enumerate(group)]
+        while eng.has_unfinished():
+            eng.step()
+        for p, s in zip(group, seqs):
+            assert len(s.output_ids) == 5
+            _agree(eng.weights, p, s.output_ids, tol=0.05)
+    taken = [s for s in shapes if s[2] is not None]
+    assert any(s[1] == 3 and s[2][1] == 4 for s in taken), shapes  # three sequences padded to four
+    assert all(s[2][0] in mr.PREFILL_GRAPH_BUCKETS and s[2][0] >= s[0] for s in taken)
+    assert any(s[2] is None and s[0] == 300 for s in shapes)  # steps past 256 tokens stay eager
+
+
 def test_chunked_prefill_and_staggered_arrivals():
     eng = _engine(max_num_batched_tokens=24)
     prompts = _prompts(4, seed=3, lo=40, hi=90)

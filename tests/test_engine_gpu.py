@@ -343,7 +343,8 @@ def test_top_k_one_in_graph_equals_greedy(gpu):
     a = eng.generate(prompt, SamplingParams(max_tokens=10, temperature=0.9, top_p=0.8, seed=3, ignore_eos=True))
     b = eng.generate(prompt, SamplingParams(max_tokens=10, temperature=0.9, top_p=0.8, seed=3, ignore_eos=True))
     assert a == b
-    assert any(k[2] for k in eng.runner.graphs)  # the filtered graph variant was captured and used
+    # the filtered graph variant was captured and used (decode keys: (rows, blocks, filtered))
+    assert any(k[2] for k in eng.runner.graphs if not isinstance(k[0], str))
 
 
 def test_staggered_arrivals_mixed_steps_and_pipelining_match_oracle(gpu):
@@ -415,6 +416,44 @@ def test_llama3_8b_shapes_two_layers_match_oracle(gpu, monkeypatch, path):
     for p, s in zip(prompts, seqs):
         assert len(s.output_ids) == 8
         _agree(eng.weights, p, s.output_ids, tol=0.1)
+
+
+def test_prefill_graphs_match_oracle(gpu, monkeypatch):
+    """Short prefills replay hipGraphs captured per padded (tokens, sequences, context) bucket: padding token
+    rows write no cache slot, padding sequences have no queries, padding attention tiles exit.  One- and
+    two-sequence prefills of 3..256 tokens (bucket edges included), a prefix-cache hit, and a bucket replayed
+    a second time all agree with the fp32 oracle; the eager engine (buckets off) captures no prefill graph."""
+    from symmetry_amd.engine import model_runner
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+
+    groups = [[list(range(300, 303))], [list(range(10, 26))], [list(range(40, 57))], [list(range(60, 160))],
+              [list(range(500, 756))], [list(range(900, 940)), list(range(1200, 1271))],
+              [list(range(60, 160)) + [5, 6, 7]], [list(range(2000, 2090))]]
+
+    def run(tokens):
+        monkeypatch.setattr(model_runner, "PREFILL_GRAPH_TOKENS", tokens)
+        eng = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", max_num_seqs=4, max_model_len=1024,
+                                     num_kv_blocks=64, block_size=32, use_graphs=True))
+        outs = []
+        for gi, group in enumerate(groups):
+            seqs = [eng.add_request(f"g{gi}-{j}", p, SamplingParams(max_tokens=6, ignore_eos=True))
+                    for j, p in enumerate(group)]
+            while eng.has_unfinished():
+                eng.step()
+            outs.append([list(s.output_ids) for s in seqs])
+        return eng, outs
+
+    eng, got = run(256)
+    keys = [k for k in eng.runner.graphs if isinstance(k[0], str)]
+    assert any(k[2] == 1 for k in keys) and any(k[2] == 2 for k in keys), keys
+    assert {k[1] for k in keys} >= {16, 32, 128, 256}, keys
+    for group, outs in zip(groups, got):
+        for p, o in zip(group, outs):
+            assert len(o) == 6
+            _agree(eng.weights, p, o, tol=0.08)
+    eager, _ = run(0)
+    assert not any(isinstance(k[0], str) for k in eager.runner.graphs)
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
