@@ -6,8 +6,10 @@
 // returns that supports the problem; one JSON line with both times and the best algorithm's index.
 //
 //   hipcc -O2 --offload-arch=gfx950 bench/kernels/blaslt_algos.cpp -lhipblaslt -o /tmp/blaslt_algos
-//   /tmp/blaslt_algos [max_algos] [shape] [M] [out: bf16|f32]   (operands: random bf16 in [-1, 1): data-dependent
-//   MFMA power draw moves the clock, so constant fills overstate throughput)
+//   /tmp/blaslt_algos [max_algos] [shape] [M] [out: bf16|f32] [layout: tn|nn]
+//   (layout nn: the weights stored transposed, [K][N] row-major, i.e. the N x K column-major A operand)
+//   (operands: random bf16 in [-1, 1): data-dependent MFMA power draw moves the clock, so constant fills
+//   overstate throughput)
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt-ext.hpp>
 #include <hipblaslt/hipblaslt.h>
@@ -77,6 +79,7 @@ int main(int argc, char** argv) {
   const std::string only = argc > 2 ? argv[2] : "";
   const int only_m = argc > 3 ? atoi(argv[3]) : 0;
   const std::string only_out = argc > 4 ? argv[4] : "";
+  const bool nn = argc > 5 && std::string(argv[5]) == "nn";
   const Shape shapes[] = {{"qkv", 6144, 4096}, {"o", 4096, 4096}, {"gate_up", 28672, 4096}, {"down", 4096, 14336}};
   const int Ms[] = {512, 768, 1024, 1280};
   hipblasLtHandle_t h;
@@ -106,11 +109,12 @@ int main(int argc, char** argv) {
         const hipDataType tD = outf ? HIP_R_32F : HIP_R_16BF;
         hipblasLtMatmulDesc_t desc;
         CK(hipblasLtMatmulDescCreate(&desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
-        hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
+        hipblasOperation_t ta = nn ? HIPBLAS_OP_N : HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
         CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)));
         CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)));
         hipblasLtMatrixLayout_t la, lb, lc;
-        CK(hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, sh.K, sh.N, sh.K));
+        if (nn) CK(hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, sh.N, sh.K, sh.N));
+        else CK(hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, sh.K, sh.N, sh.K));
         CK(hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, sh.K, M, sh.K));
         CK(hipblasLtMatrixLayoutCreate(&lc, tD, sh.N, M, sh.N));
         hipblasLtMatmulPreference_t pref;
@@ -148,10 +152,10 @@ int main(int argc, char** argv) {
         }
         // re-time the best one like the default (9 reps)
         double flops = 2.0 * M * sh.N * sh.K;
-        printf("{\"shape\": \"%s\", \"M\": %d, \"N\": %d, \"K\": %d, \"out\": \"%s\", \"default_us\": %.2f, "
+        printf("{\"layout\": \"%s\", \"shape\": \"%s\", \"M\": %d, \"N\": %d, \"K\": %d, \"out\": \"%s\", \"default_us\": %.2f, "
                "\"default_index\": %d, \"default_tflops\": %.1f, \"best_us\": %.2f, \"best_index\": %d, "
                "\"best_tflops\": %.1f, \"algos_tried\": %d, \"algos_listed\": %zu, \"best_kernel\": \"%s\"}\n",
-               sh.name, M, sh.N, sh.K, outf ? "f32" : "bf16", t_def, def_idx, flops / t_def / 1e6, best, best_idx,
+               nn ? "nn" : "tn", sh.name, M, sh.N, sh.K, outf ? "f32" : "bf16", t_def, def_idx, flops / t_def / 1e6, best, best_idx,
                flops / best / 1e6, tried, all.size(), best_name.substr(0, 90).c_str());
         fflush(stdout);
         CK(hipblasLtMatmulPreferenceDestroy(pref));
