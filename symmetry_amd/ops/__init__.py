@@ -336,9 +336,12 @@ def logits_argmax(logits, temps, seeds, step, out_keys, out_ids, n_offset=0):
     return reference.logits_argmax(logits, temps, seeds, step, out_keys, out_ids, n_offset)
 
 
-def _load_blaslt_table() -> dict:
+def _load_blaslt_table(force: bool = False) -> dict:
     """{(N, K): sorted [(M, solution index)]} from blaslt_table.json (tools/blaslt_table.py); empty when off."""
-    if os.environ.get("SYMMETRY_BLASLT_TUNED", "1") == "0":
+    # OFF by default: the isolated-GEMM gains of the sweep (gate_up 512 rows 113.8 -> 95.0 us) did not show in
+    # the prefill steps (profiles/r4/blaslt_tuned_ab.jsonl, alternating runs: 384 / 512 / 640-token steps and the
+    # 128-token prefill within run-to-run noise); SYMMETRY_BLASLT_TUNED=1 turns the table on
+    if os.environ.get("SYMMETRY_BLASLT_TUNED", "0") != "1" and not force:
         return {}
     import json
 
