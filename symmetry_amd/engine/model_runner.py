@@ -39,12 +39,15 @@ CMD_STOP, CMD_CAPTURE, CMD_SYNC = -1, 2, 3  # control headers of the rank-0 -> w
 KIND_DECODE, KIND_PREFILL, KIND_PREFILL_GRAPH = 0, 1, 4  # header[0] of a step
 HEADER_LEN = 7  # kind, T, rows, max_blocks, prefill tiles, real seqs, filtered-sampling flag
 # Short prefills replay a hipGraph too: T padded up to one of these token buckets, the sequence count to 1/2/4.
-# A 128-token Llama-3-8B prefill is ~300 launches whose host enqueue (~4.8 ms) outlasts its GPU time (~3 ms):
-# the single-client TTFT was host-bound.  SYMMETRY_PREFILL_GRAPH_TOKENS (0: off) bounds the bucket.
+# A 128-token Llama-3-8B prefill is ~300 launches whose eager host enqueue (3.9 ms) held the GPU back; replayed,
+# 0.19 ms (one-client TTFT 8.4 -> 7.4 ms).  SYMMETRY_PREFILL_GRAPH_TOKENS (0: off) bounds the bucket.
+# Captured at start-up only (capture_all: every token bucket x one sequence x every context bucket): a bucket
+# captured lazily in serving cost its first request ~14 ms of TTFT (multi-turn turn 2: 6.7 -> 21 ms,
+# profiles/r4/multiturn_prefill_graph_ab.jsonl); a step whose bucket was not captured runs eagerly.
 PREFILL_GRAPH_BUCKETS = (16, 32, 64, 128, 192, 256)
-PREFILL_GRAPH_SEQS = (1, 2, 4)
+PREFILL_GRAPH_SEQS = (1, 2, 4)  # padding buckets of the sequence count
+PREFILL_CAPTURE_SEQS = (1,)     # the ones captured at start-up
 PREFILL_GRAPH_TOKENS = int(os.environ.get("SYMMETRY_PREFILL_GRAPH_TOKENS", "256"))
-PREFILL_GRAPH_MAX = 48  # captured prefill graphs at most (lazily, per bucket); past that, eager
 _PAD_TILE_ROW = 1 << 24  # query row of a padding attention tile: past every qlen, so its workgroups exit
 _SEED_MIX = 0x9E3779B97F4A7C15
 
@@ -130,6 +133,7 @@ class ModelRunner:
         self.use_graphs = use_graphs and self.is_gpu
         # pad short prefills to the graph buckets (without use_graphs -- CPU tests -- they then run eagerly)
         self.prefill_graphs = self.use_graphs
+        self.prefill_graph_replays = 0
         self.tp_size, self.tp_rank = tp_size, tp_rank
         self.cpu_group = cpu_group
         self.graphs: dict[tuple, tuple] = {}
@@ -375,7 +379,7 @@ class ModelRunner:
     def _prefill_graph_shape(self, T: int, nseq: int, nblocks: int, filt: int):
         """(T bucket, sequence bucket, block-table bucket) of a prefill that replays a hipGraph, or None (eager).
         One GPU, dense models: a TP prefill's collectives and the MoE dispatch stay eager."""
-        if not (self.prefill_graphs and PREFILL_GRAPH_TOKENS > 0 and self.tp_size == 1 and not self.model.cfg.is_moe):
+        if not self._prefill_graphs_on():
             return None
         Tb = next((b for b in PREFILL_GRAPH_BUCKETS if T <= b <= PREFILL_GRAPH_TOKENS), None)
         nb = next((b for b in PREFILL_GRAPH_SEQS if nseq <= b), None)
@@ -383,9 +387,12 @@ class ModelRunner:
             return None
         mb = self._ctx_bucket(nblocks)
         key = ("prefill", Tb, nb, mb, self._pad_tiles(Tb, nb), bool(filt))
-        if key not in self.graphs and sum(isinstance(k[0], str) for k in self.graphs) >= PREFILL_GRAPH_MAX:
+        if self.use_graphs and key not in self.graphs:  # replay only what start-up captured
             return None
         return Tb, nb, mb
+
+    def _prefill_graphs_on(self) -> bool:
+        return self.prefill_graphs and PREFILL_GRAPH_TOKENS > 0 and self.tp_size == 1 and not self.model.cfg.is_moe
 
     def _bucket(self, n: int) -> int:
         for b in self.buckets:
@@ -408,6 +415,7 @@ class ModelRunner:
                 key = (T, max_blocks, bool(filt))
             else:
                 key = ("prefill", T, nseq_l, max_blocks, ntiles, bool(filt))
+                self.prefill_graph_replays += 1
             g = self.graphs.get(key)
             if g is None:
                 if kind == "decode":
@@ -485,6 +493,13 @@ class ModelRunner:
                             self._broadcast(np.array([CMD_CAPTURE, b, b, mb, 0, b, 0], dtype=np.int32),
                                             torch.zeros(0, dtype=torch.int32))
                         self._capture(b, mb)
+            if self._prefill_graphs_on():
+                for mb in sorted(self.ctx_blocks, reverse=True):
+                    for T in sorted((b for b in PREFILL_GRAPH_BUCKETS if b <= PREFILL_GRAPH_TOKENS), reverse=True):
+                        for n in PREFILL_CAPTURE_SEQS:
+                            lay = _Layout(T, n, mb, prefill=True, ntiles=self._pad_tiles(T, n))
+                            if ("prefill", T, n, mb, lay.ntiles, False) not in self.graphs:
+                                self._capture(T, mb, False, prefill=lay)
         return time.perf_counter() - t0
 
     # ------------------------------------------------------------------------------------------

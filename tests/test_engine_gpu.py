@@ -419,10 +419,10 @@ def test_llama3_8b_shapes_two_layers_match_oracle(gpu, monkeypatch, path):
 
 
 def test_prefill_graphs_match_oracle(gpu, monkeypatch):
-    """Short prefills replay hipGraphs captured per padded (tokens, sequences, context) bucket: padding token
-    rows write no cache slot, padding sequences have no queries, padding attention tiles exit.  One- and
-    two-sequence prefills of 3..256 tokens (bucket edges included), a prefix-cache hit, and a bucket replayed
-    a second time all agree with the fp32 oracle; the eager engine (buckets off) captures no prefill graph."""
+    """Short prefills replay hipGraphs captured at start-up per padded (tokens, context) bucket: padding token
+    rows write no cache slot, padding attention tiles exit.  One-sequence prefills of 3..256 tokens (bucket edges
+    included), a prefix-cache tail and a bucket replayed a second time, plus a two-sequence step (eager: not
+    captured), all agree with the fp32 oracle; with the buckets off nothing is captured or replayed."""
     from symmetry_amd.engine import model_runner
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
     from symmetry_amd.engine.sequence import SamplingParams
@@ -435,6 +435,7 @@ def test_prefill_graphs_match_oracle(gpu, monkeypatch):
         monkeypatch.setattr(model_runner, "PREFILL_GRAPH_TOKENS", tokens)
         eng = LLMEngine(EngineConfig(model="small-llama", device="cuda:0", max_num_seqs=4, max_model_len=1024,
                                      num_kv_blocks=64, block_size=32, use_graphs=True))
+        eng.warmup([16, 128])  # start-up capture: decode graphs + one-sequence prefill buckets
         outs = []
         for gi, group in enumerate(groups):
             seqs = [eng.add_request(f"g{gi}-{j}", p, SamplingParams(max_tokens=6, ignore_eos=True))
@@ -446,14 +447,15 @@ def test_prefill_graphs_match_oracle(gpu, monkeypatch):
 
     eng, got = run(256)
     keys = [k for k in eng.runner.graphs if isinstance(k[0], str)]
-    assert any(k[2] == 1 for k in keys) and any(k[2] == 2 for k in keys), keys
-    assert {k[1] for k in keys} >= {16, 32, 128, 256}, keys
+    assert {k[1] for k in keys} == set(model_runner.PREFILL_GRAPH_BUCKETS) and {k[2] for k in keys} == {1}, keys
+    # every one-sequence group replayed a start-up graph (the two-sequence one ran eagerly: not captured)
+    assert eng.runner.prefill_graph_replays >= 7, eng.runner.prefill_graph_replays
     for group, outs in zip(groups, got):
         for p, o in zip(group, outs):
             assert len(o) == 6
             _agree(eng.weights, p, o, tol=0.08)
     eager, _ = run(0)
-    assert not any(isinstance(k[0], str) for k in eager.runner.graphs)
+    assert not any(isinstance(k[0], str) for k in eager.runner.graphs) and eager.runner.prefill_graph_replays == 0
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
