@@ -5,7 +5,9 @@ Metric and config come from BASELINE.json ("streamed tokens/sec + p50 TTFT per
 client, Llama-3-8B provider, 1/2/4/8 MI355X"; config 3: maxConnections=10
 concurrent clients, continuous batching, greedy decode).
 
-One process per GPU (launched by torch.distributed.run for N > 1), bf16,
+One process per GPU for N > 1: either under ``torch.distributed.run`` (the
+driver's form) or as plain ``python bench.py --gpus N``, which starts its own
+torchrun child with N ranks (``_self_launch``).  bf16,
 random-init weights of the real Llama-3-8B architecture, synthetic 128-token
 prompts (no network for checkpoints/datasets).
 
@@ -75,8 +77,74 @@ def _args():
     return ap.parse_args()
 
 
+SHARED_GPU_ENV = "SYMMETRY_BENCH_SHARED_GPU"
+
+
+def _fail(args, msg: str) -> int:
+    """One JSON line with an ``error`` (never a silently smaller measurement) and a non-zero exit."""
+    print(json.dumps({"metric": METRIC, "value": None, "unit": "tokens/s per client", "n_gpus": args.gpus,
+                      "steps": args.steps, "warmup": args.warmup, "error": msg}), flush=True)
+    return 2
+
+
+def visible_gpus() -> int:
+    """GPUs this process may use, counted without initialising the HIP runtime (``device_count()`` only
+    enumerates on this stack; ``HIP_VISIBLE_DEVICES`` restricts it)."""
+    import torch
+
+    return int(torch.cuda.device_count())
+
+
+def launch_plan(args_argv: list, n: int, port: int) -> list:
+    """argv of the ONE torchrun child that runs ``n`` ranks of this bench (one per GPU, 127.0.0.1 rendezvous)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), *args_argv]
+
+
+def _self_launch(args) -> int | None:
+    """``python bench.py --gpus N`` (N > 1) outside a launcher: check the GPUs, then start the N ranks as one
+    ``torch.distributed.run`` child -- before this process makes any GPU call, never an exec -- relay its output
+    and exit with its return code.  Under a launcher: ``WORLD_SIZE`` must equal ``--gpus``.
+
+    No GPUs visible (CPU container): the ranks run on the CPU (gloo), the rehearsal the tests use.  Fewer GPUs
+    than asked: an error line, unless ``SYMMETRY_BENCH_SHARED_GPU=1`` lets the ranks share the visible GPUs
+    (a one-GPU rehearsal: host-staged gloo collectives + the xGMI kernels between the processes + decode
+    hipGraphs)."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != args.gpus:
+            return _fail(args, f"--gpus {args.gpus} but the launcher started {world} ranks")
+        return None
+    if args.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+
+    n = visible_gpus()
+    env = dict(os.environ)
+    if 0 < n < args.gpus:
+        if os.environ.get(SHARED_GPU_ENV) != "1":
+            return _fail(args, f"--gpus {args.gpus} needs {args.gpus} GPUs, {n} visible "
+                               f"({SHARED_GPU_ENV}=1 rehearses the ranks on the visible GPUs)")
+        for k, v in (("SYMMETRY_TP_COMM", "gloo"), ("SYMMETRY_XGMI", "1"), ("SYMMETRY_XGMI_GRAPHS", "1"),
+                     ("SYMMETRY_DIST_BACKEND", "gloo")):
+            env.setdefault(k, v)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    p = subprocess.Popen(launch_plan(sys.argv[1:], args.gpus, port), env=env)
+    try:
+        return abs(p.wait())
+    except KeyboardInterrupt:
+        p.terminate()
+        return abs(p.wait())
+
+
 def main() -> int:
     args = _args()
+    code = _self_launch(args)
+    if code is not None:
+        return code
     import torch
     import torch.distributed as dist
 

@@ -65,3 +65,39 @@ def test_bench_torchrun_two_ranks_dp():
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
            "--parallel", "dp"] + ARGS
     _check(_run(cmd), 2, "dp")
+
+
+def test_bench_plain_gpus_two_launches_its_ranks_tp():
+    """``python bench.py --gpus 2`` with no launcher starts its own 2-rank torchrun child (the driver's BENCH
+    form must not silently time one GPU)."""
+    _check(_run([sys.executable, "bench.py", "--gpus", "2"] + ARGS), 2, "tp")
+
+
+def test_bench_plain_gpus_two_launches_its_ranks_dp():
+    _check(_run([sys.executable, "bench.py", "--gpus", "2", "--parallel", "dp"] + ARGS), 2, "dp")
+
+
+def test_bench_world_size_mismatch_fails_loudly():
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2"] + ARGS, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert "error" in line and line["value"] is None and line["n_gpus"] == 2
+
+
+def test_bench_too_few_gpus_is_an_error(monkeypatch, capsys):
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv(bench.SHARED_GPU_ENV, raising=False)
+    monkeypatch.setattr(bench, "visible_gpus", lambda: 1)
+    args = type("A", (), {"gpus": 8, "steps": 3, "warmup": 1})()
+    assert bench._self_launch(args) == 2
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert "8 GPUs, 1 visible" in line["error"] and line["value"] is None
+    plan = bench.launch_plan(["--gpus", "8"], 8, 29555)
+    assert "--nproc-per-node=8" in plan and "--master-addr" in plan and "127.0.0.1" in plan
