@@ -582,7 +582,6 @@ void go_xres_ks(const bf16* x, const bf16* W, int M, int N, int K, const DecodeE
 template <int EPI>
 bool go_xres(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, hipStream_t s) {
   if (M > 16 || K % 1024 || K > 4096) return false;
-  if (EPI == DECODE_EPI_XAR && N / 16 > XAR_MAX_TILES * 64) return false;  // (per-workgroup epoch slots)
   if (!g_num_cus) {
     int dev = 0;
     hipGetDevice(&dev);
@@ -592,6 +591,9 @@ bool go_xres(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi&
   const int C = g_num_cus;
   const int ntiles = N / 16;
   const int per = (ntiles + C - 1) / C;  // whole tiles: equal tile count per workgroup
+  // XAR keeps one epoch slot per walked tile in LDS: the real tiles-per-workgroup count (a partitioned GPU has
+  // fewer CUs) must fit, else the caller falls back to the gemm_tile variant
+  if (EPI == DECODE_EPI_XAR && per > XAR_MAX_TILES) return false;
   int grid = (ntiles + per - 1) / per, NF = ntiles, P = 0, KS = 1;
   // remainder split: weight bytes on the busiest CU, f K + q K / KS, must drop >= 10 % (<= 4 parts per
   // workgroup, >= 4 waves per part)

@@ -498,6 +498,9 @@ class LLMEngine:
         return list(seq.output_ids)
 
     def shutdown(self) -> None:
+        if self.health is not None:
+            # an orderly stop: the workers leaving after the stop broadcast is not a fault
+            self.health.stop()
         self.runner.broadcast_stop()
 
 

@@ -48,6 +48,7 @@ class BlockManager:
         self.ref = [0] * num_blocks
         self.block_hash: dict[int, bytes] = {}      # block -> content key (registered blocks)
         self.cached: dict[bytes, int] = {}          # content key -> block
+        self.cache_gen = 0                          # blocks ever registered (queued misses re-look when it grows)
         self.evictable: collections.OrderedDict[int, None] = collections.OrderedDict()  # ref 0, LRU order
         self.hit_tokens = 0
         self.query_tokens = 0
@@ -101,11 +102,14 @@ class BlockManager:
         """Adopt the cached blocks of the longest matching full-block prefix of a sequence that has no
         KV yet; returns the number of tokens whose prefill is skipped.  At least one prompt token is
         always left to compute (its logits give the first output token)."""
-        if not self.prefix_caching or seq.block_table or seq.num_computed or seq.prefix_checked:
+        if not self.prefix_caching or seq.block_table or seq.num_computed:
             return 0
-        # once per fresh KV state (again after a preemption): a miss is not re-queried on every schedule(),
-        # which kept the hit-rate denominator growing while a prompt waited
-        seq.prefix_checked = True
+        # a miss is not re-queried on every schedule() (which kept the hit-rate denominator growing while a
+        # prompt waited) unless blocks were cached since the last look: a queued prompt that missed while a
+        # same-scope prefix was still being prefilled finds it once that prefill registered its blocks
+        if seq.prefix_checked and seq.prefix_epoch == self.cache_gen:
+            return 0
+        seq.prefix_checked, seq.prefix_epoch = True, self.cache_gen
         tokens = seq.token_ids
         target = seq.prefill_target
         nfull = max(0, target - 1) // self.block_size  # >= 1 token left to prefill
@@ -138,6 +142,7 @@ class BlockManager:
                 continue
             self.block_hash[b] = h
             self.cached[h] = b
+            self.cache_gen += 1
 
     def release(self, seq: Sequence) -> None:
         self.register(seq)

@@ -84,6 +84,7 @@ class Sequence:
     output_text: str = ""
     cache_scope: bytes = b""       # prefix-cache namespace (client identity)
     prefix_checked: bool = False   # the prefix cache was consulted for the current (fresh) KV state
+    prefix_epoch: int = -1         # the prefix cache's size at that look (a grown cache is re-queried)
 
     @property
     def token_ids(self) -> list:

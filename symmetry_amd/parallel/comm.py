@@ -218,24 +218,30 @@ class XgmiComm(Comm):
         want = self.world * (self.world + 1) / 2
         return int(self.ops.xgmi_error(self.handle)) == 0 and bool((t == want).all())
 
-    def xar_self_test(self, d: int) -> bool:
+    def xar_self_test(self, d: int, ks=(256,), rows=(4,), layouts=(False,)) -> bool:
         """The fused row-parallel projection + all-reduce + residual launch on exactly representable data
-        (x = 1, W = (rank + 1) / 256, K = 256, residual 0.5): True when every row came back as 0.5 + sum of
-        (rank + 1), the launch fit (co-resident grid) and no rank gave up waiting."""
+        (x = 1, W = (rank + 1) / 256, residual 0.5) for every (K, M, layout) given -- the production shapes (the
+        row-parallel K of o and down, M = 1 and 16, row-major and preshuffled: a constant matrix is its own
+        preshuffle) reach the launch variants the decode step will pick.  True when every row came back as
+        0.5 + K / 256 * sum of (rank + 1), every launch fit (co-resident grid) and no rank gave up waiting."""
         dev = torch.device("cuda", torch.cuda.current_device())
-        M, K = 4, 256
-        x = torch.ones(M, K, device=dev, dtype=torch.bfloat16)
-        W = torch.full((d, K), (self.rank + 1) / 256, device=dev, dtype=torch.bfloat16)
-        resid = torch.full((M, d), 0.5, device=dev)
         w_next = torch.ones(d, device=dev, dtype=torch.bfloat16)
-        xw = torch.empty(M, d, device=dev, dtype=torch.bfloat16)
-        ss = torch.empty(M, d // 16, device=dev)
-        if not self.gemm_ar_resid(x, W, False, resid, w_next, xw, ss):
-            return False
-        torch.cuda.synchronize(dev)
-        self.calls["gemm_ar"] -= 1
-        want = 0.5 + self.world * (self.world + 1) / 2
-        return int(self.ops.xgmi_error(self.xar.handle)) == 0 and bool((resid == want).all())
+        for K in ks:
+            W = torch.full((d, K), (self.rank + 1) / 256, device=dev, dtype=torch.bfloat16)
+            for M in rows:
+                for wshuf in layouts:
+                    x = torch.ones(M, K, device=dev, dtype=torch.bfloat16)
+                    resid = torch.full((M, d), 0.5, device=dev)
+                    xw = torch.empty(M, d, device=dev, dtype=torch.bfloat16)
+                    ss = torch.empty(M, d // 16, device=dev)
+                    if not self.gemm_ar_resid(x, W, wshuf, resid, w_next, xw, ss):
+                        return False
+                    torch.cuda.synchronize(dev)
+                    self.calls["gemm_ar"] -= 1
+                    want = 0.5 + K / 256 * self.world * (self.world + 1) / 2
+                    if int(self.ops.xgmi_error(self.xar.handle)) != 0 or not bool((resid == want).all()):
+                        return False
+        return True
 
     def _fits(self, t) -> bool:
         return (t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous()
@@ -261,7 +267,8 @@ class XgmiComm(Comm):
         ``row_bytes`` each (+ counts and side ints) for :meth:`a2a_rows`.  Mixtral prefill: cap = ceil(max
         tokens / N) * top_k rows, row_bytes = d * 4 (the fp32 return) -- ~0.5 GB of uncached HBM per rank."""
         slot = (int(self.ops.xgmi_a2a_slot(int(cap), int(row_bytes))) + 255) // 256 * 256
-        self.a2a = XgmiComm(self.inner, group, torch.device("cuda", torch.cuda.current_device()), slot_bytes=slot)
+        self.a2a = XgmiComm(self.inner, group, torch.device("cuda", torch.cuda.current_device()), slot_bytes=slot,
+                            barrier=False)  # the caller votes, then barriers (parallel/launch.py)
         self.a2a_cap, self.a2a_row_bytes = int(cap), int(row_bytes)
         self.calls["a2a"] = 0
 
@@ -279,7 +286,7 @@ class XgmiComm(Comm):
         """Collective (every rank): the communicator of the fused row-parallel decode projections -- slots of
         ``rows`` x ``d`` epoch-tagged 8-B granules (csrc/kernels/decode_epi.h, xar_push / xar_collect)."""
         self.xar = XgmiComm(self.inner, group, torch.device("cuda", torch.cuda.current_device()),
-                            slot_bytes=(int(rows) * int(d) * 8 + 255) // 256 * 256)
+                            slot_bytes=(int(rows) * int(d) * 8 + 255) // 256 * 256, barrier=False)
 
     def gemm_ar_resid(self, x, W, wshuf, resid, w_next, xw, ss) -> bool:
         """Row-parallel decode projection + all-reduce + residual add + next-norm prep as ONE launch

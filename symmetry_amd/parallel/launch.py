@@ -98,24 +98,58 @@ def _vote(ok: bool, group) -> bool:
     return int(t[0]) == 1
 
 
-def _attach_xar_checked(comm, group, d: int) -> None:
+def _attach_xar_checked(comm, group, d: int, ks=(256,)) -> None:
     """attach_xar + its startup self-test on every rank; on any failure every rank drops the fused path (the
     decode step then runs GEMM + the one-shot all-reduce)."""
     import sys
 
-    passed, err = False, None
+    attached, passed, err = False, False, None
     try:
         comm.attach_xar(group, 64, d)
-        passed = comm.xar_self_test(d)
+        attached = True
     except Exception as exc:  # noqa: BLE001
         err = exc
-    if _vote(passed, group):
-        return
+    if _vote(attached, group):
+        dist.barrier(group=group)  # every rank mapped every peer slot before the first fused launch
+        try:
+            # the production shapes: the row-parallel K of o and down, 1 and 16 rows, both weight layouts
+            passed = comm.xar_self_test(d, ks=ks, rows=(1, 16), layouts=(False, True))
+        except Exception as exc:  # noqa: BLE001
+            err = exc
+        if _vote(passed, group):
+            return
     print(f"symmetry: fused GEMM + all-reduce launches disabled ({err or 'startup self-test failed'})",
           file=sys.stderr, flush=True)
     if comm.xar is not None:
         comm.xar.destroy(inner_too=False)
         comm.xar = None
+
+
+def a2a_capacity(tokens: int, top_k: int, num_experts: int, world: int) -> int:
+    """Rows one rank may push to one token-slice owner in the replicated-token expert exchange: every token of
+    the owner's slice (ceil(T / N)) routed to up to min(k, E / N) of this rank's experts."""
+    return -(-int(tokens) // world) * min(int(top_k), int(num_experts) // world)
+
+
+def _attach_a2a_checked(comm, group, tokens: int, mcfg, world: int) -> None:
+    """attach_a2a on every rank or on none: a rank whose uncached allocation or IPC mapping fails votes no over
+    gloo, every rank drops the communicator, and MoE prefill combines by all-reduce instead."""
+    import sys
+
+    ok, err = False, None
+    try:
+        comm.attach_a2a(group, a2a_capacity(tokens, mcfg.top_k, mcfg.num_experts, world), mcfg.hidden_size * 4)
+        ok = True
+    except Exception as exc:  # noqa: BLE001
+        err = exc
+    if _vote(ok, group):
+        dist.barrier(group=group)  # every rank mapped every peer slot before the first exchange
+        return
+    print(f"symmetry: xGMI expert all-to-all unavailable ({err or 'a peer failed to attach'}); "
+          "MoE prefill combines by all-reduce", file=sys.stderr, flush=True)
+    if comm.a2a is not None:
+        comm.a2a.destroy(inner_too=False)
+        comm.a2a = None
 
 
 def init_tp_engine(ecfg):
@@ -148,11 +182,14 @@ def init_tp_engine(ecfg):
         # when ranks share a GPU (the one-GPU rehearsal): a fused launch's workgroups wait for the other ranks'
         # tiles while holding their CUs, and one rank's grid can fill the whole device before the other's starts
         # (SYMMETRY_XGMI_FUSED=force: a test whose grids are small enough to be co-resident anyway)
-        _attach_xar_checked(comm, cpu_group, mcfg.hidden_size)
+        ks = {mcfg.num_heads * mcfg.head_dim // world}
+        if not mcfg.is_moe:
+            ks.add(mcfg.intermediate_size // world)
+        _attach_xar_checked(comm, cpu_group, mcfg.hidden_size, ks=tuple(sorted(k for k in ks if k % 256 == 0)) or (256,))
     if ep_comm is not None and isinstance(comm, XgmiComm) and os.environ.get("SYMMETRY_MOE_XGMI_A2A", "1") != "0":
-        # the unpadded expert all-to-all (prefill dispatch / return of routed rows) on its own peer buffers
-        tokens = max(ecfg.max_num_batched_tokens, 8192)
-        comm.attach_a2a(cpu_group, -(-tokens // world) * mcfg.top_k, mcfg.hidden_size * 4)
+        # the unpadded expert all-to-all (prefill: expert results pushed to the token-slice owners) on its own
+        # peer buffers, sized by the largest prefill step
+        _attach_a2a_checked(comm, cpu_group, ecfg.max_num_batched_tokens, mcfg, world)
     engine = LLMEngine(ecfg, tp_comm=comm, ep_comm=ep_comm, cpu_group=cpu_group)
     if rank == 0 and world > 1:
         # fault containment: a lost worker takes the provider offline within ~0.1 s (parallel/health.py)

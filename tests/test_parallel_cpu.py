@@ -129,6 +129,7 @@ def _xar_vote_worker(rank, world):
 
     class FakeComm:
         xar = None
+        a2a = None
 
         def __init__(self, fail_attach=False, fail_test=False):
             self.fail_attach, self.fail_test = fail_attach, fail_test
@@ -138,8 +139,13 @@ def _xar_vote_worker(rank, world):
                 raise RuntimeError("ipc mapping refused")
             self.xar = FakeSub()
 
-        def xar_self_test(self, d):
+        def xar_self_test(self, d, ks=(256,), rows=(4,), layouts=(False,)):
             return not self.fail_test
+
+        def attach_a2a(self, group, cap, row_bytes):
+            if self.fail_attach:
+                raise RuntimeError("uncached allocation failed")
+            self.a2a = FakeSub()
 
     group = dist.new_group(backend="gloo")
     out = []
@@ -147,12 +153,26 @@ def _xar_vote_worker(rank, world):
         c = FakeComm(*fail)
         launch._attach_xar_checked(c, group, 64)
         out.append(c.xar is not None)
+    # the expert all-to-all communicator: attached on every rank or on none
+    cfg = type("M", (), {"top_k": 2, "num_experts": 8, "hidden_size": 64})()
+    for fail in (False, rank == 1):
+        c = FakeComm(fail)
+        launch._attach_a2a_checked(c, group, 4096, cfg, world)
+        out.append(c.a2a is not None)
     return out
+
+
+def test_a2a_capacity():
+    from symmetry_amd.parallel.launch import a2a_capacity
+
+    # Mixtral EP=8: one expert per rank, so a token reaches one rank at most once: ceil(T / 8) rows per owner
+    assert a2a_capacity(8192, 2, 8, 8) == 1024
+    assert a2a_capacity(1000, 2, 8, 2) == 1000  # 4 experts per rank: both of a token's experts can be local
 
 
 def test_fused_path_startup_check_is_all_ranks_or_none():
     res = _run(_xar_vote_worker, world=2)
-    assert [r[1] for r in res] == [[True, False, False], [True, False, False]]
+    assert [r[1] for r in res] == [[True, False, False, True, False], [True, False, False, True, False]]
 
 
 def _tp_worker(rank, world, model="tiny-llama"):
