@@ -267,52 +267,6 @@ void mgemm(const Tensor& x, const Tensor& w, Tensor& y, int64_t rw) {
   launch_mgemm(ptr<bf16>(x), ptr<bf16>(w), ptr<float>(y), (int)M, (int)N, (int)K, (int)S, (int)rw, cur_stream(x));
 }
 
-// Library prefill GEMM y [M, N] = x [M, K] . w [N, K]^T on a tuned hipBLASLt solution (blaslt.hip).  Returns
-// false when the solution does not support the problem (the caller runs the library heuristic instead).
-bool blaslt_gemm(const Tensor& x, const Tensor& w, Tensor& y, int64_t algo_index) {
-  check_gpu(x, "x");
-  check_gpu(w, "w");
-  check_gpu(y, "y");
-  check_dtype(x, at::kBFloat16, "x");
-  check_dtype(w, at::kBFloat16, "w");
-  TORCH_CHECK(y.scalar_type() == at::kBFloat16 || y.scalar_type() == at::kFloat, "blaslt_gemm: y bf16 or fp32");
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "blaslt_gemm: x [M,K], w [N,K], y [M,N]");
-  TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && y.is_contiguous(), "blaslt_gemm: contiguous operands");
-  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K && y.size(0) == M && y.size(1) == N, "blaslt_gemm: shape mismatch");
-  const at::OptionalDeviceGuard g(x.device());
-  const int st = launch_blaslt_gemm(x.data_ptr(), w.data_ptr(), y.data_ptr(), y.scalar_type() == at::kFloat ? 1 : 0,
-                                    (int)M, (int)N, (int)K, (int)algo_index, cur_stream(x));
-  if (st < 0) {  // the library refused the call: the caller runs the heuristic path instead (reported once)
-    static bool warned = false;
-    if (!warned) TORCH_WARN("blaslt_gemm: hipBLASLt error (M=", M, " N=", N, " K=", K, " algo ", algo_index, ")");
-    warned = true;
-  }
-  return st == 0;
-}
-
-// Tuning sweep (bench/kernels/blaslt_tune.py): [best index, default index, supported count] and [best us,
-// default us] for y = x . w^T with the weight rotating over the copies in ws.
-std::tuple<std::vector<int64_t>, std::vector<double>> blaslt_tune_op(const Tensor& x, const std::vector<Tensor>& ws,
-                                                                     Tensor& y) {
-  check_gpu(x, "x");
-  TORCH_CHECK(!ws.empty() && x.dim() == 2 && y.dim() == 2, "blaslt_tune: x [M,K], ws [N,K]..., y [M,N]");
-  const int64_t M = x.size(0), K = x.size(1), N = ws[0].size(0);
-  std::vector<const void*> wp;
-  for (const auto& w : ws) {
-    TORCH_CHECK(w.size(0) == N && w.size(1) == K && w.is_contiguous() && w.scalar_type() == at::kBFloat16,
-                "blaslt_tune: weight copies [N, K] bf16");
-    wp.push_back(w.data_ptr());
-  }
-  const at::OptionalDeviceGuard g(x.device());
-  int out[3] = {-1, -1, 0};
-  float us[2] = {-1.f, -1.f};
-  const int st = blaslt_tune(x.data_ptr(), wp.data(), (int)wp.size(), y.data_ptr(), y.scalar_type() == at::kFloat,
-                             (int)M, (int)N, (int)K, out, us, cur_stream(x));
-  TORCH_CHECK(st == 0, "blaslt_tune failed");
-  return {std::vector<int64_t>{out[0], out[1], out[2]}, std::vector<double>{us[0], us[1]}};
-}
-
 void lm_head_sample(const Tensor& x, const Tensor& w, const Tensor& temps, const Tensor& seeds, const Tensor& step,
                     Tensor& tile_keys, Tensor& out_keys, Tensor& out_ids, int64_t n_offset,
                     const c10::optional<Tensor>& logits) {
@@ -955,8 +909,6 @@ TORCH_LIBRARY(symmetry_amd, m) {
       &attn_prefill);
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) y, int variant=0) -> ()", &skinny_gemm);
   m.def("mgemm(Tensor x, Tensor w, Tensor(a!) y, int rw) -> ()", &mgemm);
-  m.def("blaslt_gemm(Tensor x, Tensor w, Tensor(a!) y, int algo_index) -> bool", &blaslt_gemm);
-  m.def("blaslt_tune(Tensor x, Tensor[] ws, Tensor(a!) y) -> (int[], float[])", &blaslt_tune_op);
   m.def("mgemm_nt(int on) -> ()", [](int64_t on) { set_mgemm_nt((int)on); });
   m.def("decode_halves(int on) -> ()", [](int64_t on) { set_decode_halves((int)on); });
   m.def("attn_stream_min(int tokens) -> ()", [](int64_t t) { set_attn_stream_min((int)t); });

@@ -114,13 +114,6 @@ void launch_rownorm(const bf16* xw, const float* ss, int ss_tiles, float eps, bf
 // mgemm.hip -- medium-M (65..256 tokens) projection into fp32 split-K slabs y[S][M][N]; W is the
 // MFMA-preshuffled weight copy, 64 * rw | N, 64 * S | K
 void launch_mgemm(const bf16* x, const bf16* Wshuf, float* y, int M, int N, int K, int S, int rw, hipStream_t s);
-// y [M][N] (bf16, or fp32 if out_f32) = x [M][K] . W[N][K]^T on hipBLASLt solution `algo_index` (blaslt.hip):
-// 0 enqueued, 1 solution does not support the problem, -1 hipBLASLt error
-int launch_blaslt_gemm(const void* x, const void* w, void* y, int out_f32, int M, int N, int K, int algo_index,
-                       hipStream_t s);
-// offline solution sweep in this process's hipBLASLt (blaslt.hip): out {best, default, supported}, us {best, default}
-int blaslt_tune(const void* x, const void* const* ws, int nw, void* y, int out_f32, int M, int N, int K, int* out,
-                float* us, hipStream_t s);
 // mgemm with a fused consumer epilogue (DECODE_EPI_QKV / RESID / SWIGLU / F32 of decode_epi.h): y is the
 // [S][M][N] fp32 slab scratch (S > 1: in-launch split-K reduction by the last workgroup of each column group),
 // counters [N / (64 rw)] ints, zero before the first launch (re-armed by the kernel)

@@ -123,7 +123,7 @@ def build_kernels(verbose: bool = False, force: bool = False) -> str:
     if force or jobs or _newer(KERNEL_SO, objs):
         cmd = [HIPCC, "-shared", "-o", KERNEL_SO] + objs + [
             f"--offload-arch={ARCH}", "-L", tlib, "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch",
-            "-lrccl", "-lhipblaslt",
+            "-lrccl",
             f"-Wl,-rpath,{tlib}",
         ]
         _run(cmd, verbose)

@@ -336,49 +336,9 @@ def logits_argmax(logits, temps, seeds, step, out_keys, out_ids, n_offset=0):
     return reference.logits_argmax(logits, temps, seeds, step, out_keys, out_ids, n_offset)
 
 
-def _load_blaslt_table(force: bool = False) -> dict:
-    """{(N, K): sorted [(M, solution index)]} from blaslt_table.json (tools/blaslt_table.py); empty when off."""
-    # OFF by default: the isolated-GEMM gains of the sweep (gate_up 512 rows 113.8 -> 95.0 us) did not show in
-    # the prefill steps (profiles/r4/blaslt_tuned_ab.jsonl, alternating runs: 384 / 512 / 640-token steps and the
-    # 128-token prefill within run-to-run noise); SYMMETRY_BLASLT_TUNED=1 turns the table on
-    if os.environ.get("SYMMETRY_BLASLT_TUNED", "0") != "1" and not force:
-        return {}
-    import json
-
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "blaslt_table.json")
-    if not os.path.exists(path):
-        return {}
-    with open(path) as f:
-        raw = json.load(f).get("table", {})
-    out = {}
-    for key, rows in raw.items():
-        n, k = (int(v) for v in key.split(","))
-        out[(n, k)] = sorted((int(m), int(r["index"])) for m, r in rows.items())
-    return out
-
-
-_BLASLT = _load_blaslt_table()
-
-
-def blaslt_solution(M: int, N: int, K: int) -> int | None:
-    """Tuned hipBLASLt solution for an [M, K] x [N, K]^T bf16 GEMM: the entry of the nearest tuned M (log scale,
-    within 1.5x of the tuned range), -1 for "the heuristic is best there", None for an untuned shape."""
-    rows = _BLASLT.get((N, K))
-    if not rows or M < rows[0][0] / 1.5 or M > rows[-1][0] * 1.5:
-        return None
-    import math
-
-    return min(rows, key=lambda r: abs(math.log(M / r[0])))[1]
-
-
 def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """Plain library GEMM ``x @ w.T`` for prefill-sized M: hipBLASLt on the tuned solution of this shape when the
-    sweep found one (csrc/kernels/blaslt.hip: the heuristic's pick is 12-30 % off at 512-768 rows for some
-    Llama-3-8B projections), else via torch (the library heuristic)."""
-    if out is not None and x.is_cuda and out.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous():
-        algo = blaslt_solution(x.shape[0], w.shape[0], w.shape[1])
-        if algo is not None and algo >= 0 and _native.ops().blaslt_gemm(x, w, out, algo):
-            return out
+    """Plain library GEMM ``x @ w.T`` for prefill-sized M (hipBLASLt through torch, the library heuristic; a
+    tuned-solution table measured neutral end to end and was removed: profiles/r4/blaslt_tuned_ab.jsonl)."""
     return torch.matmul(x, w.t(), out=out)
 
 

@@ -260,50 +260,6 @@ def test_mgemm(gpu, M, N, K, rw, S):
         _close(y[s], ref_s, atol=2e-3 * math.sqrt(kc) * 0.1 + 1e-3, rtol=1e-3)
 
 
-def _tuned_cases():
-    cases = []
-    for (N, K), rows in sorted(ops._load_blaslt_table(force=True).items()):
-        tuned = [(m, i) for m, i in rows if i >= 0]
-        if tuned:
-            m = tuned[len(tuned) // 2][0]
-            cases += [(N, K, m), (N, K, m - 13)]  # the tuned M and a ragged M near it (same solution)
-    return cases[:8]
-
-
-@pytest.mark.parametrize("N,K,M", _tuned_cases() or [pytest.param(0, 0, 0, marks=pytest.mark.skip("no table"))])
-def test_blaslt_tuned_linear(gpu, N, K, M):
-    """The tuned hipBLASLt solutions of the table (csrc/kernels/blaslt.hip; used by ops.linear under
-    SYMMETRY_BLASLT_TUNED=1) against the fp32 product; the native call must have taken the problem (no silent
-    fallback to the heuristic for a tuned shape)."""
-    g = torch.Generator(device=gpu).manual_seed(N + M)
-    x = torch.randn(M, K, device=gpu, generator=g).bfloat16()
-    w = (torch.randn(N, K, device=gpu, generator=g) * 0.02).bfloat16()
-    y = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
-    from symmetry_amd.ops import _native
-
-    table = ops._load_blaslt_table(force=True)[(N, K)]
-    algo = min(table, key=lambda r: abs(math.log(M / r[0])))[1]
-    assert algo >= 0
-
-    assert _native.ops().blaslt_gemm(x, w, y, algo)
-    _close(y.float(), x.float() @ w.float().t(), atol=2e-3 * math.sqrt(K) * 0.1 + 2e-2, rtol=1e-2)
-    if ops.blaslt_solution(M, N, K) == algo:  # (SYMMETRY_BLASLT_TUNED=1) ops.linear takes the same solution
-        y2 = torch.empty_like(y)
-        ops.linear(x, w, out=y2)
-        assert torch.equal(y, y2)
-
-
-def test_blaslt_unsupported_solution_falls_back(gpu):
-    """A solution index that does not fit the problem reports False (the caller then runs the heuristic)."""
-    from symmetry_amd.ops import _native
-
-    x = torch.randn(8, 256, device=gpu).bfloat16()
-    w = torch.randn(96, 256, device=gpu).bfloat16()
-    y = torch.empty(8, 96, device=gpu, dtype=torch.bfloat16)
-    ok = _native.ops().blaslt_gemm(x, w, y, 1 << 30)
-    assert ok is False
-
-
 def test_lm_head_sample(gpu):
     M, N, K = 10, 128256 // 16 * 16, 4096
     g = torch.Generator(device=gpu).manual_seed(7)
