@@ -477,6 +477,57 @@ void moe_combine(const Tensor& y, const Tensor& dst, const Tensor& ids, int64_t 
                      (int)k, (int)d, ptr<float>(out), accumulate ? 1 : 0, cur_stream(out));
 }
 
+// Expert parallelism over replicated tokens (moe.hip moe_owner_*): y = the expert outputs of this rank's routed
+// rows ([R, d] or fp32 slabs), dst / ids / w [T*k] of ALL T tokens; send fp32 [N*cap, d], side int32 [N*cap],
+// cursor int32 [N] (zeroed here): the weighted partial of every token with a local expert, grouped by slice owner.
+void moe_owner_pack(const Tensor& y, const Tensor& dst, const Tensor& ids, const Tensor& w, int64_t e_lo, int64_t e_hi,
+                    int64_t k, int64_t S, Tensor& cursor, Tensor& send, Tensor& side) {
+  for (const Tensor* t : {&dst, &ids, (const Tensor*)&cursor, (const Tensor*)&side}) {
+    check_gpu(*t, "moe_owner_pack index");
+    check_dtype(*t, at::kInt, "moe_owner_pack index");
+  }
+  check_gpu(w, "w");
+  check_dtype(w, at::kFloat, "w");
+  check_gpu(send, "send");
+  check_dtype(send, at::kFloat, "send");
+  TORCH_CHECK(send.dim() == 2 && send.is_contiguous(), "moe_owner_pack: send [N * cap, d]");
+  const int64_t N = cursor.numel(), d = send.size(1), T = dst.numel() / k;
+  TORCH_CHECK(N >= 1 && send.size(0) % N == 0 && side.numel() >= send.size(0), "moe_owner_pack: send / side blocks");
+  const int64_t cap = send.size(0) / N;
+  TORCH_CHECK(S >= 1 && cap >= S && N * S >= T && d % 8 == 0, "moe_owner_pack: capacity / slice shapes");
+  TORCH_CHECK(ids.numel() >= T * k && w.numel() >= T * k, "moe_owner_pack: ids / w too small");
+  const int64_t R = y.dim() == 3 ? y.size(1) : y.size(0);
+  TORCH_CHECK((y.dim() == 3 ? y.size(2) : y.size(1)) == d, "moe_owner_pack: y width");
+  const at::OptionalDeviceGuard g(send.device());
+  (void)hipMemsetAsync(cursor.data_ptr(), 0, N * sizeof(int), cur_stream(send));
+  launch_moe_owner_pack(linout(y, R, d, "y"), (int)R, ptr<int>(dst), ptr<int>(ids), ptr<float>(w), (int)e_lo, (int)e_hi,
+                        (int)T, (int)k, (int)d, (int)S, (int)cap, ptr<int>(cursor), ptr<float>(send), ptr<int>(side),
+                        cur_stream(send));
+}
+
+// The slice owner's combine: recv fp32 [N*cap, d] (block s: source s's rows, rcnt[s] of them, side ints = slice
+// token), pos int32 [N*S] scratch, out bf16 [S, d] = rank-ordered sums, rows >= Tr zero.
+void moe_owner_combine(const Tensor& recv, const Tensor& side, const Tensor& rcnt, int64_t Tr, Tensor& pos,
+                       Tensor& out) {
+  check_gpu(recv, "recv");
+  check_dtype(recv, at::kFloat, "recv");
+  check_gpu(out, "out");
+  check_dtype(out, at::kBFloat16, "out");
+  for (const Tensor* t : {&side, &rcnt, (const Tensor*)&pos}) {
+    check_gpu(*t, "moe_owner_combine index");
+    check_dtype(*t, at::kInt, "moe_owner_combine index");
+  }
+  TORCH_CHECK(recv.dim() == 2 && out.dim() == 2 && out.size(1) == recv.size(1) && out.is_contiguous(),
+              "moe_owner_combine: recv [N * cap, d], out [S, d]");
+  const int64_t N = rcnt.numel(), d = recv.size(1), S = out.size(0);
+  TORCH_CHECK(N >= 1 && recv.size(0) % N == 0 && side.numel() >= recv.size(0), "moe_owner_combine: blocks");
+  const int64_t cap = recv.size(0) / N;
+  TORCH_CHECK(pos.numel() >= N * S && Tr >= 0 && Tr <= S && d % 8 == 0, "moe_owner_combine: shapes");
+  const at::OptionalDeviceGuard g(out.device());
+  launch_moe_owner_combine(ptr<float>(recv), ptr<int>(side), ptr<int>(rcnt), (int)N, (int)cap, (int)S, (int)Tr, (int)d,
+                           ptr<int>(pos), ptr<bf16>(out), cur_stream(out));
+}
+
 // Decode MoE routing in one launch: resid fp32 [T, d] (T <= 16) -> ids / w [T*k], counts / offsets / cursor,
 // xs [T*k, d] (the normalised rows, expert segments in token order), dst [T*k]
 void moe_decode_route(const Tensor& resid, const Tensor& lnw, double eps, const Tensor& Wr, int64_t k, Tensor& ids,
@@ -965,6 +1016,10 @@ TORCH_LIBRARY(symmetry_amd, m) {
       "moe_scatter(Tensor x, Tensor ids, int k, int G, Tensor offsets, Tensor(a!) cursor, Tensor(b!) xs, Tensor(c!) dst, "
       "Tensor(d!)? src_tok=None) -> ()",
       &moe_scatter);
+  m.def("moe_owner_pack(Tensor y, Tensor dst, Tensor ids, Tensor w, int e_lo, int e_hi, int k, int S, "
+        "Tensor(a!) cursor, Tensor(b!) send, Tensor(c!) side) -> ()", &moe_owner_pack);
+  m.def("moe_owner_combine(Tensor recv, Tensor side, Tensor rcnt, int Tr, Tensor(a!) pos, Tensor(b!) out) -> ()",
+        &moe_owner_combine);
   m.def(
       "moe_combine(Tensor y, Tensor dst, Tensor ids, int e_lo, int e_hi, Tensor w, int k, Tensor(a!) out, "
       "bool accumulate) -> ()",

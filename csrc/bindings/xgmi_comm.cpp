@@ -238,11 +238,13 @@ bool xgmi_gemm_ar_resid(const Tensor& a, const Tensor& W, bool wshuf, Tensor& re
 // test-only: every rank of this process in one launch (grid z = rank); xres: the x-resident walk
 bool xgmi_gemm_ar_resid_multi(std::vector<Tensor> xs, const Tensor& W, bool wshuf, std::vector<Tensor> resids,
                               const Tensor& w_next, std::vector<Tensor> xws, std::vector<Tensor> sss,
-                              std::vector<int64_t> comms, bool xres) {
+                              std::vector<int64_t> comms, bool xres, int64_t delay_rank, int64_t delay_us) {
   const int world = (int)comms.size();
   TORCH_CHECK(world >= 1 && world <= XAR_MULTI_MAX && (int)xs.size() == world && (int)resids.size() == world &&
                   (int)xws.size() == world && (int)sss.size() == world, "xgmi_gemm_ar_resid_multi: one set per rank");
   XarMulti m{};
+  m.delay_rank = (int)delay_rank;
+  m.delay_ticks = (unsigned long long)std::max<int64_t>(delay_us, 0) * 100ull;  // 100 MHz wall clock
   for (int r = 0; r < world; ++r) {
     Xgmi* x = get(comms[r]);
     TORCH_CHECK(x->args.rank == r && x->args.world == world, "xgmi_gemm_ar_resid_multi: communicator order");
@@ -473,7 +475,7 @@ TORCH_LIBRARY_FRAGMENT(symmetry_amd, m) {
       &xgmi_gemm_ar_resid);
   m.def(
       "xgmi_gemm_ar_resid_multi(Tensor[] xs, Tensor W, bool wshuf, Tensor(a!)[] resids, Tensor w_next, "
-      "Tensor(b!)[] xws, Tensor(c!)[] sss, int[] comms, bool xres) -> bool",
+      "Tensor(b!)[] xws, Tensor(c!)[] sss, int[] comms, bool xres, int delay_rank=-1, int delay_us=0) -> bool",
       &xgmi_gemm_ar_resid_multi);
   m.def("xgmi_keys_max_multi(Tensor[] keys, Tensor(a!)[] ids, int[] comms, int delay_rank=-1, int delay_us=0) -> ()",
         &xgmi_keys_max_multi);

@@ -854,6 +854,7 @@ template <int MT, int NW, int U>
 __global__ __launch_bounds__(NW * 64) void decode_gemm_xar_multi_kernel(XarMulti m, const bf16* __restrict__ W,
                                                                        int M, int N, int K) {
   const int r = blockIdx.z;
+  if (r == m.delay_rank) xg_delay(m.delay_ticks);
   gemm_tile<MT, NW, U, 1, DECODE_EPI_XAR>(m.x[r], W, M, N, K, m.e[r], blockIdx.x);
 }
 
@@ -861,6 +862,7 @@ template <int U>
 __global__ __launch_bounds__(1024) void decode_gemm_xar_multi_xres_kernel(XarMulti m, const bf16* __restrict__ W,
                                                                           int M, int N, int K) {
   const int r = blockIdx.z;
+  if (r == m.delay_rank) xg_delay(m.delay_ticks);
   xres_body<U, 1, DECODE_EPI_XAR>(m.x[r], W, M, N, K, m.e[r], N / 16, 0, blockIdx.x, gridDim.x);
 }
 

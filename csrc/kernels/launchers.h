@@ -100,6 +100,8 @@ constexpr int XAR_MULTI_MAX = 8;
 struct XarMulti {
   const bf16* x[XAR_MULTI_MAX];
   DecodeEpi e[XAR_MULTI_MAX];
+  int delay_rank = -1;                 // test hook: this rank's workgroups start delay_ticks late (a slow peer)
+  unsigned long long delay_ticks = 0;
 };
 bool launch_decode_gemm_xar_multi(const XarMulti& m, int world, const bf16* W, int M, int N, int K, int xres,
                                   hipStream_t s);
@@ -182,6 +184,12 @@ void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_l
 void launch_moe_decode_route(const float* resid, const bf16* lnw, float eps, const bf16* Wr, int T, int d, int E, int k,
                              int* ids, float* w, int* counts, int* offsets, int* cursor, bf16* xs, int* dst,
                              hipStream_t s);
+// expert parallelism over replicated tokens (moe.hip): the weighted partial of each token's local experts pushed
+// to its slice owner (cursor[N] zeroed by the caller), and the owner's rank-ordered sum as bf16 [S][d]
+void launch_moe_owner_pack(LinOut y, int R, const int* dst, const int* ids, const float* w, int e_lo, int e_hi, int T,
+                           int k, int d, int S, int cap, int* cursor, float* send, int* side, hipStream_t s);
+void launch_moe_owner_combine(const float* recv, const int* side, const int* rcnt, int N, int cap, int S, int Tr,
+                              int d, int* pos, bf16* out, hipStream_t s);
 // decode, every expert local: moe_combine + add_prep as one launch (ss [T, parts]: partials over column parts)
 void launch_moe_combine_prep(LinOut y, int R, const int* dst, const int* ids, int E, const float* w, int T, int k, int d,
                              float* resid, const bf16* w_next, bf16* xw, float* ss, int parts, hipStream_t s);

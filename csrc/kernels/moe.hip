@@ -612,6 +612,88 @@ __global__ __launch_bounds__(64) void moe_combine_prep_kernel(LinOut y, int R, c
   if (threadIdx.x == 0) ss[t * P + blockIdx.y] = sq;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Expert parallelism over REPLICATED tokens (attention is tensor-parallel, so every rank holds all T rows):
+// every rank routes all T tokens, runs its own experts on its own routed rows, and then
+//  (1) moe_owner_pack: for each token with >= 1 local expert, the weighted partial sum over its local experts
+//      (fp32, j order) becomes ONE row pushed to the token's slice owner (owner = t / S), in owner-grouped
+//      blocks of capacity S with the token's slice-local index beside it (the xGMI a2a kernel moves only the
+//      counted rows);
+//  (2) moe_owner_index: the owner turns the received side ints into pos[s][t] = row of source s's partial
+//      for its token t (or -1);
+//  (3) moe_owner_combine: out[t] = sum over sources in rank order (deterministic), written as bf16 straight
+//      into the all-gather's send rows (rows past the slice's token count are zero).
+// ---------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void moe_owner_pack_kernel(LinOut y, int R, const int* __restrict__ dst,
+                                                             const int* __restrict__ ids, const float* __restrict__ w,
+                                                             int e_lo, int e_hi, int k, int d, int S, int cap,
+                                                             int* __restrict__ cursor, float* __restrict__ send,
+                                                             int* __restrict__ side) {
+  const int t = blockIdx.x;
+  bool any = false;
+  for (int j = 0; j < k; ++j) {
+    const int ex = ids[t * k + j];
+    any = any || (ex >= e_lo && ex < e_hi);
+  }
+  if (!any) return;  // uniform across the block
+  const int owner = t / S;
+  __shared__ int slot;
+  if (threadIdx.x == 0) {
+    slot = atomicAdd(&cursor[owner], 1);
+    if (slot < cap) side[(long long)owner * cap + slot] = t - owner * S;
+  }
+  __syncthreads();
+  if (slot >= cap) return;  // (cannot happen: a token sends at most one row)
+  float* o = send + ((long long)owner * cap + slot) * d;
+  for (int i = threadIdx.x; i < d / 8; i += 256) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < k; ++j) {
+      const int row = dst[t * k + j];
+      const int ex = ids[t * k + j];
+      if (row < 0 || row >= R || ex < e_lo || ex >= e_hi) continue;
+      const float wj = w[t * k + j];
+      float v[8];
+      linout_load8(y, (long long)row * d + i * 8, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += wj * v[q];
+    }
+    store8f(o + i * 8, acc);
+  }
+}
+
+// pos [N][S] (-1 from the op's memset first): the row of source s's partial for slice token t; grid
+// (N, ceil(cap / 256))
+__global__ __launch_bounds__(256) void moe_owner_index_kernel(const int* __restrict__ side,
+                                                              const int* __restrict__ rcnt, int cap, int S,
+                                                              int* __restrict__ pos) {
+  const int s = blockIdx.x;
+  const int i = blockIdx.y * 256 + threadIdx.x;
+  if (i >= min(rcnt[s], cap)) return;
+  const int t = side[(long long)s * cap + i];
+  if (t >= 0 && t < S) pos[(long long)s * S + t] = i;
+}
+
+// out bf16 [S][d]: row t = sum_s recv[s cap + pos[s][t]] (sources in rank order); t >= Tr: zeros
+__global__ __launch_bounds__(256) void moe_owner_combine_kernel(const float* __restrict__ recv,
+                                                                const int* __restrict__ pos, int N, int cap, int S,
+                                                                int Tr, int d, bf16* __restrict__ out) {
+  const int t = blockIdx.x;
+  for (int i = threadIdx.x; i < d / 8; i += 256) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (t < Tr) {
+      for (int s = 0; s < N; ++s) {
+        const int p = pos[(long long)s * S + t];
+        if (p < 0 || p >= cap) continue;
+        float v[8];
+        load8f(recv + ((long long)s * cap + p) * d + i * 8, v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] += v[q];
+      }
+    }
+    store8(out + (long long)t * d + i * 8, acc);
+  }
+}
+
 }  // namespace
 
 void launch_moe_decode_route(const float* resid, const bf16* lnw, float eps, const bf16* Wr, int T, int d, int E, int k,
@@ -669,4 +751,17 @@ void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_l
                         int d, float* out, int accumulate, hipStream_t s) {
   if (T == 0) return;
   moe_combine_kernel<<<T, 256, 0, s>>>(y, R, dst, ids, e_lo, e_hi, w, k, d, out, accumulate);
+}
+
+void launch_moe_owner_pack(LinOut y, int R, const int* dst, const int* ids, const float* w, int e_lo, int e_hi, int T,
+                           int k, int d, int S, int cap, int* cursor, float* send, int* side, hipStream_t s) {
+  if (T == 0) return;
+  moe_owner_pack_kernel<<<T, 256, 0, s>>>(y, R, dst, ids, w, e_lo, e_hi, k, d, S, cap, cursor, send, side);
+}
+
+void launch_moe_owner_combine(const float* recv, const int* side, const int* rcnt, int N, int cap, int S, int Tr,
+                              int d, int* pos, bf16* out, hipStream_t s) {
+  (void)hipMemsetAsync(pos, 0xff, (size_t)N * S * sizeof(int), s);  // -1: no partial from that source
+  moe_owner_index_kernel<<<dim3(N, (cap + 255) / 256), 256, 0, s>>>(side, rcnt, cap, S, pos);
+  if (S > 0) moe_owner_combine_kernel<<<S, 256, 0, s>>>(recv, pos, N, cap, S, Tr, d, out);
 }

@@ -134,6 +134,7 @@ class ModelRunner:
         # pad short prefills to the graph buckets (without use_graphs -- CPU tests -- they then run eagerly)
         self.prefill_graphs = self.use_graphs
         self.prefill_graph_replays = 0
+        self.graph_replays = 0  # decode steps run as a replayed hipGraph
         self.tp_size, self.tp_rank = tp_size, tp_rank
         self.cpu_group = cpu_group
         self.graphs: dict[tuple, tuple] = {}
@@ -413,6 +414,7 @@ class ModelRunner:
         if self.use_graphs and (kind == "decode" or header[0] == KIND_PREFILL_GRAPH):
             if kind == "decode":
                 key = (T, max_blocks, bool(filt))
+                self.graph_replays += 1
             else:
                 key = ("prefill", T, nseq_l, max_blocks, ntiles, bool(filt))
                 self.prefill_graph_replays += 1

@@ -12,17 +12,14 @@ every rank holds the same T tokens when the block starts):
 * all-reduce combine (``mode="allreduce"``, and ``"auto"`` below ``A2A_ROWS`` rows -- decode steps): each
   rank applies its own experts to all routed rows and one all-reduce sums the partial outputs (on the
   one-shot xGMI kernel at decode sizes);
-* expert all-to-all (``mode="a2a"``, and ``"auto"`` from ``A2A_ROWS`` rows -- prefill): rank r takes token
-  slice r (S = ceil(T / N) rows), routes it, DISPATCHES each routed row to the rank owning its expert, the
-  owners run their grouped GEMMs, the results RETURN to the slice owners, who combine their slice; an
-  all-gather rebuilds the [T, d] output on every rank.  Rows are grouped by owner into blocks of capacity
-  S * k with the expert id beside each row, and no count is ever read on the host.  On an xGMI node
-  (``XgmiComm.a2a_rows``, ``csrc/kernels/xgmi_ar.hip`` xgmi_a2a_kernel) each rank pushes ONLY its routed
-  rows straight into the owners' peer buffers -- S k d x 2 B dispatched (bf16) and S k d x 4 B returned
-  (fp32) per rank, i.e. T k d x 2 / N each way -- with the device-side counts travelling beside them.
-  Elsewhere (RCCL / gloo) the blocks move whole: N x the routed rows, empty slots marked -1.
-* :meth:`MoEBlock.forward_tokens` is the same exchange for ranks that hold DIFFERENT tokens (data-parallel
-  attention in front of expert-parallel MoE): dispatch, expert GEMMs, return, combine, no gather.
+* owner exchange (``mode="a2a"``, and ``"auto"`` from ``A2A_ROWS`` rows -- prefill; :meth:`forward_a2a`):
+  no dispatch leg (every rank already holds the tokens) -- every rank routes all T tokens and runs its own
+  experts on its own routed rows; per token with a local expert ONE fp32 row (the weighted partial over those
+  experts) goes to the token's slice owner (``XgmiComm.a2a_rows``: only counted rows cross the links, counts
+  on the device); the owners sum in rank order and a bf16 all-gather rebuilds [T, d].  Elsewhere (RCCL / gloo)
+  whole capacity blocks move, empty slots marked -1.
+* :meth:`MoEBlock.forward_tokens` is the exchange for ranks that hold DIFFERENT tokens (data-parallel attention
+  in front of expert-parallel MoE): dispatch of routed rows to their owners, expert GEMMs, return, combine.
 """
 from __future__ import annotations
 
@@ -60,7 +57,7 @@ class MoEBlock:
         self.mode = mode or os.environ.get("SYMMETRY_MOE_MODE", "auto")
         self.F = cfg.intermediate_size
         self.calls = {"allreduce": 0, "a2a": 0}
-        self.a2a_bytes = {"dispatch": 0, "return": 0, "routed_rows": 0, "padded_dispatch": 0}
+        self.a2a_bytes = {"dispatch": 0, "return": 0, "routed_rows": 0, "padded_dispatch": 0, "gather": 0}
         # router rows padded to a multiple of 16 for the skinny GEMM (padded logits are never read)
         self.router = {}
         Ep = (self.E + 15) // 16 * 16
@@ -199,16 +196,50 @@ class MoEBlock:
 
     # ------------------------------------------------------------------------------------------
     def forward_a2a(self, i: int, x: torch.Tensor) -> torch.Tensor:
-        """Expert all-to-all over token slices (x [T, d] identical on every rank; see the module note)."""
+        """Expert parallelism over REPLICATED tokens (x [T, d] identical on every rank: the attention is tensor-
+        parallel).  No dispatch leg: every rank routes all T tokens (deterministic kernels, identical routing),
+        runs its own experts on its own routed rows, and pushes, per token with a local expert, ONE fp32 row --
+        the weighted partial over its local experts -- to the token's slice owner (rank t // S, S = ceil(T / N));
+        the owner sums the partials in rank order and a bf16 all-gather rebuilds [T, d] on every rank.  Bytes
+        per rank: ~T k / N rows x d x 4 to the owners (only counted rows cross the links on the xGMI
+        communicator) + (N - 1) / N x T x d x 2 gathered, against 2 (N - 1) / N x T x d x 4 for the fp32
+        all-reduce combine.  Elsewhere (RCCL / gloo) whole capacity blocks move, empty slots marked -1."""
         T, d = x.shape
-        N, r = self.ep, self.ep_rank
+        N, r, k = self.ep, self.ep_rank, self.k
         S = -(-T // N)
         lo, hi = min(T, r * S), min(T, (r + 1) * S)
-        out_s = self.forward_tokens(i, x[lo:hi], S)
-        full = self._buf("a2a.slice", (S, d), torch.float32)
-        if hi > lo:
-            full[: hi - lo].copy_(out_s)
-        g = self.comm.all_gather(full)  # [N * S, d]
+        ids, w, dst, offsets, xs = self._route(i, x)
+        y = self._experts(i, xs, offsets, self.e_lo, self.E_local, out_f32=True)
+        cap = S  # a token sends at most one (pre-combined) row to its owner
+        send = self._buf("own.send", (N * cap, d), torch.float32)
+        side = self._buf("own.side", (N * cap,), torch.int32)
+        cursor = self._buf("own.cursor", (N,), torch.int32)
+        xg = getattr(self.comm, "a2a_fits", None)
+        xg = xg is not None and xg(cap, d * 4)
+        if not xg:
+            side.fill_(-1)  # whole blocks move: slots past each owner's count must read "empty"
+        ops.moe_owner_pack(y, dst, ids, w, self.e_lo, self.e_hi, k, S, cursor, send, side)
+        if xg:
+            recv = self._buf("own.recv", (N * cap, d), torch.float32)
+            rside = self._buf("own.rside", (N * cap,), torch.int32)
+            rcnt = self._buf("own.rcnt", (N,), torch.int32)
+            self.comm.a2a_rows(send, cursor, side, recv, rside, rcnt)
+            if A2A_STATS:
+                sent = int(cursor.sum()) - int(cursor[r])  # rows that left this GPU
+                self.a2a_bytes["return"] += sent * d * 4
+                self.a2a_bytes["routed_rows"] += int(cursor.sum())
+        else:
+            splits = [cap] * N
+            recv = self.comm.all_to_all_rows(send, splits, splits)
+            rside = self.comm.all_to_all_rows(side.view(-1, 1), splits, splits).view(-1)
+            rcnt = self._buf("own.rcnt_full", (N,), torch.int32)
+            rcnt.fill_(cap)
+        pos = self._buf("own.pos", (N * S,), torch.int32)
+        mine = self._buf("own.slice", (S, d), torch.bfloat16)
+        ops.moe_owner_combine(recv, rside, rcnt, hi - lo, pos, mine)
+        g = self.comm.all_gather(mine)  # [N * S, d] bf16
+        if A2A_STATS:
+            self.a2a_bytes["gather"] += (N - 1) * S * d * 2
         return g[:T]
 
     def forward_tokens(self, i: int, x: torch.Tensor, S: int) -> torch.Tensor:

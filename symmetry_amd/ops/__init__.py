@@ -321,6 +321,21 @@ def moe_combine(y, dst, ids, e_lo, e_hi, w, k, out, accumulate=False):
     return reference.moe_combine(y, dst, ids, e_lo, e_hi, w, k, out, accumulate)
 
 
+def moe_owner_pack(y, dst, ids, w, e_lo, e_hi, k, S, cursor, send, side):
+    """Expert parallelism over replicated tokens: the weighted partial of each token's local experts, one fp32
+    row per token, grouped by slice owner (t // S) into ``send`` [N * cap, d]; ``cursor`` [N] = rows per owner."""
+    if _gpu(send):
+        return _native.ops().moe_owner_pack(y, dst, ids, w, int(e_lo), int(e_hi), int(k), int(S), cursor, send, side)
+    return reference.moe_owner_pack(y, dst, ids, w, e_lo, e_hi, k, S, cursor, send, side)
+
+
+def moe_owner_combine(recv, side, rcnt, Tr, pos, out):
+    """The slice owner's rank-ordered sum of the received partials -> bf16 [S, d] (rows >= Tr zero)."""
+    if _gpu(out):
+        return _native.ops().moe_owner_combine(recv, side, rcnt, int(Tr), pos, out)
+    return reference.moe_owner_combine(recv, side, rcnt, Tr, pos, out)
+
+
 def sample_filtered(logits, temps, top_k, top_p, seeds, step, out_ids):
     """Resample rows that request top-k / top-p (temperature > 0) from full-vocab fp32 logits."""
     if _gpu(logits):

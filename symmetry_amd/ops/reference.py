@@ -453,6 +453,52 @@ def moe_combine(y, dst, ids, e_lo: int, e_hi: int, w, k: int, out, accumulate: b
         out.copy_(res)
 
 
+def moe_owner_pack(y, dst, ids, w, e_lo: int, e_hi: int, k: int, S: int, cursor, send, side) -> None:
+    """Weighted partial over each token's local experts ([e_lo, e_hi)), one row per token that has one, pushed
+    into its slice owner's block (owner = t // S; token order here, arrival order on the GPU: the owner's
+    combine does not depend on it); side = the token's index in the owner's slice."""
+    N = cursor.numel()
+    cap = send.shape[0] // N
+    T = dst.numel() // k
+    yy = linout_sum(y)
+    cursor.zero_()
+    for t in range(T):
+        row = None
+        for j in range(k):
+            a = t * k + j
+            e = int(ids[a])
+            if e_lo <= e < e_hi and int(dst[a]) >= 0:
+                v = float(w[a]) * yy[int(dst[a])]
+                row = v if row is None else row + v
+        if row is None:
+            continue
+        o = t // S
+        c = int(cursor[o])
+        cursor[o] += 1
+        send[o * cap + c] = row
+        side[o * cap + c] = t - o * S
+
+
+def moe_owner_combine(recv, side, rcnt, Tr: int, pos, out) -> None:
+    """out [S, d] bf16: row t = sum over sources (rank order) of the received partial for slice token t."""
+    N = rcnt.numel()
+    cap = recv.shape[0] // N
+    S, d = out.shape
+    acc = torch.zeros(S, d, dtype=torch.float32)
+    pos.view(-1)[: N * S] = -1
+    for s in range(N):
+        for i in range(min(int(rcnt[s]), cap)):
+            t = int(side[s * cap + i])
+            if 0 <= t < S:
+                pos[s * S + t] = i
+    for t in range(Tr):
+        for s in range(N):
+            p = int(pos[s * S + t])
+            if p >= 0:
+                acc[t] += recv[s * cap + p].float()
+    out.copy_(acc.to(out.dtype))
+
+
 def sample_filtered(logits, temps, top_k, top_p, seeds, step, out_ids) -> None:
     """Temperature + top-k + top-p (nucleus) resampling of full-vocab rows (csrc/kernels/sampling.hip).
 

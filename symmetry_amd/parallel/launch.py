@@ -125,10 +125,10 @@ def _attach_xar_checked(comm, group, d: int, ks=(256,)) -> None:
         comm.xar = None
 
 
-def a2a_capacity(tokens: int, top_k: int, num_experts: int, world: int) -> int:
-    """Rows one rank may push to one token-slice owner in the replicated-token expert exchange: every token of
-    the owner's slice (ceil(T / N)) routed to up to min(k, E / N) of this rank's experts."""
-    return -(-int(tokens) // world) * min(int(top_k), int(num_experts) // world)
+def a2a_capacity(tokens: int, world: int) -> int:
+    """Rows one rank may push to one token-slice owner in the replicated-token expert exchange: one pre-combined
+    row per token of the owner's slice, ceil(T / N) (models/moe.py forward_a2a)."""
+    return -(-int(tokens) // world)
 
 
 def _attach_a2a_checked(comm, group, tokens: int, mcfg, world: int) -> None:
@@ -138,7 +138,7 @@ def _attach_a2a_checked(comm, group, tokens: int, mcfg, world: int) -> None:
 
     ok, err = False, None
     try:
-        comm.attach_a2a(group, a2a_capacity(tokens, mcfg.top_k, mcfg.num_experts, world), mcfg.hidden_size * 4)
+        comm.attach_a2a(group, a2a_capacity(tokens, world), mcfg.hidden_size * 4)
         ok = True
     except Exception as exc:  # noqa: BLE001
         err = exc

@@ -321,3 +321,53 @@ def test_swiglu(gpu):
     ops.swiglu(gb, out)
     ref.swiglu(gb.cpu(), out_r)
     _close(out, out_r, atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("N,T,E,k", [(2, 243, 8, 2), (8, 1000, 8, 2), (4, 37, 8, 2)])
+def test_moe_owner_pack_and_combine(gpu, N, T, E, k):
+    """Replicated-token expert exchange kernels (moe.hip moe_owner_*): every rank packs the weighted partials of
+    its local experts by slice owner; routing them like the xGMI a2a would (block s of rank q's send -> block q
+    of rank s's recv) and combining must give each owner exactly the fp32 full MoE combine of its slice (up to
+    one bf16 rounding), whatever order the atomics placed the rows in."""
+    from symmetry_amd.ops import reference
+
+    d = 256
+    S = -(-T // N)
+    g = torch.Generator(device="cpu").manual_seed(T + N)
+    R = T * k
+    ids = torch.stack([torch.randperm(E, generator=g)[:k] for _ in range(T)]).view(-1).int()
+    w = torch.rand(R, generator=g)
+    dst = torch.randperm(R, generator=g).int()  # row of each (token, slot) in the expert-sorted buffer
+    y = torch.randn(R, d, generator=g)
+    full = torch.zeros(T, d)
+    reference.moe_combine(y, dst, ids, 0, E, w, k, full, False)
+    El = E // N
+    sends, sides, counts = [], [], []
+    for q in range(N):
+        send = torch.full((N * S, d), float("nan"), device=gpu)
+        side = torch.full((N * S,), -1, dtype=torch.int32, device=gpu)
+        cursor = torch.full((N,), 99, dtype=torch.int32, device=gpu)
+        ops.moe_owner_pack(y.to(gpu), dst.to(gpu), ids.to(gpu), w.to(gpu), q * El, (q + 1) * El, k, S, cursor, send,
+                           side)
+        torch.cuda.synchronize()
+        sends.append(send.cpu())
+        sides.append(side.cpu())
+        counts.append(cursor.cpu())
+    for s in range(N):  # owner s
+        recv = torch.zeros(N * S, d)
+        rside = torch.full((N * S,), -1, dtype=torch.int32)
+        rcnt = torch.zeros(N, dtype=torch.int32)
+        for q in range(N):
+            n = int(counts[q][s])
+            recv[q * S:q * S + n] = sends[q][s * S:s * S + n]
+            rside[q * S:q * S + n] = sides[q][s * S:s * S + n]
+            rcnt[q] = n
+        lo, hi = min(T, s * S), min(T, (s + 1) * S)
+        out = torch.full((S, d), float("nan"), device=gpu, dtype=torch.bfloat16)
+        pos = torch.empty(N * S, dtype=torch.int32, device=gpu)
+        ops.moe_owner_combine(recv.to(gpu), rside.to(gpu), rcnt.to(gpu), hi - lo, pos, out)
+        torch.cuda.synchronize()
+        want = full[lo:hi]
+        got = out[: hi - lo].float().cpu()
+        assert ((got - want).abs() <= 1e-5 + want.abs() * 2.0 ** -8).all(), float((got - want).abs().max())
+        assert (out[hi - lo:] == 0).all()

@@ -165,9 +165,9 @@ def _xar_vote_worker(rank, world):
 def test_a2a_capacity():
     from symmetry_amd.parallel.launch import a2a_capacity
 
-    # Mixtral EP=8: one expert per rank, so a token reaches one rank at most once: ceil(T / 8) rows per owner
-    assert a2a_capacity(8192, 2, 8, 8) == 1024
-    assert a2a_capacity(1000, 2, 8, 2) == 1000  # 4 experts per rank: both of a token's experts can be local
+    # one pre-combined row per token of the owner's slice
+    assert a2a_capacity(8192, 8) == 1024
+    assert a2a_capacity(1000, 3) == 334
 
 
 def test_fused_path_startup_check_is_all_ranks_or_none():
@@ -316,13 +316,15 @@ def _ep_worker(rank, world, model="tiny-mixtral"):
     ref = ref_model.moe.forward(0, x_all[0]).clone()
     ep_model.moe.mode = "allreduce"
     outs["allreduce"] = torch.allclose(ep_model.moe.forward(0, x_all[0]), ref, atol=1e-4)
-    # expert all-to-all over token slices: identical tokens, each rank routes and combines its slice
+    # owner exchange over token slices: identical tokens, every rank's local-expert partials go to the slice
+    # owners, a bf16 all-gather rebuilds the output (within one bf16 rounding of the fp32 local block)
     ep_model.moe.mode = "a2a"
     for name, x in (("a2a", x_all[0]), ("a2a_long", x_long), ("a2a_short", x_long[:max(1, world - 2)])):
         ref_r = ref_model.moe.forward(1, x).clone()
         got = ep_model.moe.forward(1, x)
-        outs[name] = torch.allclose(got, ref_r, atol=1e-4)
-        outs[name + "_err"] = float((got - ref_r).abs().max())
+        outs[name] = got.dtype == torch.bfloat16 and bool(
+            ((got.float() - ref_r).abs() <= 1e-5 + ref_r.abs() * 2.0 ** -8).all())
+        outs[name + "_err"] = float((got.float() - ref_r).abs().max())
     # expert all-to-all with DIFFERENT tokens per rank (data-parallel attention in front of EP)
     ref_t = ref_model.moe.forward(1, x_all[rank]).clone()
     got_t = ep_model.moe.forward_tokens(1, x_all[rank], 6)
@@ -344,7 +346,8 @@ def test_expert_parallel_modes_match_local_moe(world):
 
 
 def test_expert_parallel_a2a_world8():
-    """EP = 8, one expert per rank (Mixtral's layout at full width): all-to-all dispatch / return."""
+    """EP = 8, one expert per rank (Mixtral's layout at full width): the owner exchange and the dispatch /
+    return exchange of different tokens per rank."""
     res = _run(_ep8_worker, world=8)
     for _, r in res:
         assert all(v for k, v in r.items() if not k.endswith("_err")), str(r)

@@ -27,7 +27,7 @@ def _port():
     return p
 
 
-def _entry(model, rank, world, port, q, xgmi="0", prompts=None):
+def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False):
     import traceback
 
     prompts = prompts or PROMPTS
@@ -35,14 +35,16 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None):
                       LOCAL_RANK="0", SYMMETRY_TP_COMM="gloo", SYMMETRY_XGMI=xgmi, SYMMETRY_MOE_A2A_STATS="1",
                       # the fused GEMM + all-reduce launches between the two processes: the small test models' grids
                       # (<= 64 workgroups per rank) are co-resident on the one GPU
-                      SYMMETRY_XGMI_FUSED="force")
+                      SYMMETRY_XGMI_FUSED="force",
+                      # graphs: decode steps captured and replayed with every collective on the xGMI kernels
+                      SYMMETRY_XGMI_GRAPHS="1" if graphs else "0")
     try:
         from symmetry_amd.engine.llm_engine import EngineConfig
         from symmetry_amd.engine.sequence import SamplingParams
         from symmetry_amd.parallel.launch import init_tp_engine
 
         ecfg = EngineConfig(model=model, device="cuda", max_num_seqs=4, max_model_len=512, num_kv_blocks=64,
-                            use_graphs=False, weight_init="full")
+                            use_graphs=graphs, weight_init="full")
         eng, r = init_tp_engine(ecfg)
         if xgmi == "1":
             from symmetry_amd.parallel.comm import XgmiComm
@@ -59,6 +61,8 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None):
                 eng.step()
         finally:
             eng.shutdown()  # the worker leaves its loop whatever happened here
+        if graphs:
+            assert eng.runner.use_graphs and eng.runner.graph_replays > 0, "decode steps did not replay graphs"
         if xgmi == "1":
             calls = eng.runner.model.tp.calls
             # decode steps ran the peer-memory all-reduce: fused into the row-parallel GEMMs (one XAR launch each:
@@ -83,13 +87,13 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None):
             dist.destroy_process_group()
 
 
-def _run(model, world=2, xgmi="0", prompts=None, extra=False):
+def _run(model, world=2, xgmi="0", prompts=None, extra=False, graphs=False):
     import torch.multiprocessing as mp
 
     port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    procs = [ctx.Process(target=_entry, args=(model, r, world, port, q, xgmi, prompts)) for r in range(world)]
+    procs = [ctx.Process(target=_entry, args=(model, r, world, port, q, xgmi, prompts, graphs)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get() for _ in range(world))
@@ -128,18 +132,25 @@ LONG_PROMPTS = [list(range(300, 420)), list(range(400, 490)), list(range(7, 40))
 
 
 def test_tp2_mixtral_unpadded_a2a_on_one_gpu(gpu):
-    """tiny-mixtral attention TP=2 + EP=2 with a 243-token prefill step (>= A2A_ROWS): the expert all-to-all runs
-    on the xGMI kernel between the two processes (IPC-mapped buffers on one GPU), pushing only routed rows --
-    rank 0's dispatch bytes are exactly its routed rows x d x 2 (bf16), ~1/N of RCCL's padded blocks -- and every
-    token agrees with the fp32 oracle."""
+    """tiny-mixtral attention TP=2 + EP=2 with a 243-token prefill step (>= A2A_ROWS): the replicated-token owner
+    exchange (models/moe.py forward_a2a) on the xGMI a2a kernel between the two processes (IPC-mapped buffers on
+    one GPU) -- no dispatch leg, at most one pre-combined fp32 row per token leaves a rank, the slices come back
+    by a bf16 all-gather -- fewer bytes than the fp32 all-reduce combine, and every token agrees with the fp32
+    oracle."""
     outs, extra = _run("tiny-mixtral", xgmi="1", prompts=LONG_PROMPTS, extra=True)
     assert extra["moe_calls"]["a2a"] > 0 and extra["xgmi_a2a"] > 0, extra
     b = extra["a2a_bytes"]
     from symmetry_amd.models.config import resolve
 
-    d = resolve("tiny-mixtral").hidden_size
-    assert b["dispatch"] == b["routed_rows"] * d * 2, b
-    assert 0 < b["dispatch"] <= b["padded_dispatch"] / 2 + 1, b  # N = 2: at most half the padded blocks
+    cfg = resolve("tiny-mixtral")
+    d = cfg.hidden_size
+    T = sum(len(p) for p in LONG_PROMPTS)
+    calls = extra["moe_calls"]["a2a"]
+    assert b["dispatch"] == 0 and b["return"] > 0 and b["gather"] > 0, b
+    # a token sends at most one row to its (one) other owner: at most T/2 rows per call leave rank 0 at N = 2
+    assert b["return"] <= calls * (T // 2 + 1) * d * 4, b
+    allreduce = calls * 2 * (2 - 1) / 2 * T * d * 4  # ring all-reduce of the fp32 [T, d] partials, per rank
+    assert b["return"] + b["gather"] < allreduce, (b, allreduce)
     _check_oracle("tiny-mixtral", LONG_PROMPTS, outs)
 
 
@@ -161,3 +172,12 @@ def test_tp2_on_one_gpu_matches_oracle(gpu, model, xgmi):
             row = lg[len(p) - 1 + j]
             # bf16 kernels + a different reduction order than the fp32 oracle: near-ties may flip
             assert float(row.max() - row[t]) <= 0.08, (j, t, int(row.argmax()), float(row.max() - row[t]))
+
+
+def test_tp2_fused_xar_under_hipgraphs_on_one_gpu(gpu):
+    """The default 8-GPU decode path end to end between two processes: small-llama TP=2 with every decode step
+    captured into a hipGraph and replayed, the o / down projections as fused GEMM + xGMI all-reduce + residual
+    launches (``SYMMETRY_XGMI_FUSED=force``) on the shared per-tile epoch counters, IPC-mapped peer buffers;
+    every token within bf16 noise of the fp32 oracle."""
+    outs = _run("small-llama", xgmi="1", graphs=True)
+    _check_oracle("small-llama", PROMPTS, outs)

@@ -324,3 +324,47 @@ def test_xgmi_gemm_all_reduce_resid_one_launch(gpu, world, M, form):
     finally:
         for h in hs:
             ops.xgmi_destroy(h)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("xres", [False, True])
+def test_xgmi_gemm_ar_resid_skewed_alternating(gpu, world, xres):
+    """The default 8-GPU decode path's fused launches as a decode step issues them: o-shaped and down-shaped
+    row-parallel projections alternating on ONE communicator (they share its per-output-tile epoch counters,
+    N = d for both), 6 consecutive launches (both slot parities, three times), a rotating rank held back 40 us
+    before its workgroups start.  Each launch's residual feeds the next (a stale or mixed-epoch granule shows
+    up as a wrong sum downstream); every rank bit-identical; fp32 torch reference per launch."""
+    from symmetry_amd.models.layout import preshuffle
+    from symmetry_amd.ops import _native
+
+    ops = _native.ops()
+    N = 1024
+    # (K, preshuffled) of the o- and down-shaped calls: the x-resident walk needs K % 1024 == 0 and preshuffled W
+    shapes = [(1024, True), (2048, True)] if xres else [(512, False), (1792, False)]
+    M = 4
+    hs = _comms(ops, world, slot_bytes=16 * N * 8 + 256)
+    g = torch.Generator(device="cpu").manual_seed(world * 7 + int(xres))
+    try:
+        wn = (torch.rand(N, generator=g) + 0.5).to(gpu, torch.bfloat16)
+        r = torch.randn(M, N, generator=g).to(gpu)
+        resids = [r.clone() for _ in range(world)]
+        for it in range(6):
+            K, shuf = shapes[it % 2]
+            W = (torch.randn(N, K, generator=g) * K ** -0.5).to(gpu, torch.bfloat16)
+            xs = [torch.randn(M, K, generator=g).to(gpu, torch.bfloat16) for _ in range(world)]
+            xws = [torch.empty(M, N, dtype=torch.bfloat16, device=gpu) for _ in range(world)]
+            sss = [torch.empty(M, N // 16, device=gpu) for _ in range(world)]
+            before = resids[0].clone()
+            ok = ops.xgmi_gemm_ar_resid_multi(xs, preshuffle(W) if shuf else W, shuf, resids, wn, xws, sss, hs, xres,
+                                              it % world, 40)
+            if not ok:
+                pytest.skip("grid not co-resident for this world size")
+            torch.cuda.synchronize()
+            want = before + sum(x.float() @ W.float().t() for x in xs)
+            for q in range(world):
+                assert ops.xgmi_error(hs[q]) == 0, (it, q)
+                torch.testing.assert_close(resids[q], want, rtol=2e-3, atol=2e-3)
+                assert torch.equal(resids[q], resids[0]) and torch.equal(sss[q], sss[0]), (it, q)
+    finally:
+        for h in hs:
+            ops.xgmi_destroy(h)
