@@ -95,6 +95,54 @@ void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int
 // (DECODE_EPI_XAR).  false (nothing launched): no variant whose whole grid is co-resident on this GPU (the
 // workgroups wait on their peers' tiles) -- the caller runs the two-launch form.
 bool launch_decode_gemm_xar(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, hipStream_t s);
+// decode_layers.hip -- the persistent decode-step engine for tensor-parallel shards: ONE launch runs every layer's
+// QKV -> attention -> O (+ all-reduce) -> gate_up -> down (+ all-reduce) with in-launch edges and each phase's
+// weights streamed into registers before the edge it waits on (see the file header)
+struct DLLayer {  // one layer's operands (a device array of L of them)
+  const bf16* wqkv;   // MFMA-preshuffled [Nq][d] (q / k head rows permuted, models/layout.py)
+  const bf16* wo;     // preshuffled [d][Hq * 128]
+  const bf16* wgu;    // preshuffled [2 Fl][d] (gate / up interleaved per 16-row tile)
+  const bf16* wdown;  // preshuffled [d][Fl]
+  const bf16* ln2;    // O epilogue's next-norm weight [d]
+  const bf16* lnn;    // down epilogue's next-norm weight [d] (the next layer's ln1, or the final norm)
+  bf16* k_cache;      // this layer's [NB][Hkv][BS][128]
+  bf16* v_cache;      // [NB][Hkv][128][BS]
+};
+struct DLArgs {
+  const DLLayer* layers = nullptr;
+  int L = 0;
+  int M = 0, d = 0, Hq = 0, Hkv = 0, Fl = 0;  // rows (<= 16), hidden, local q / kv heads, local intermediate
+  int KSq = 1;                                 // k-splits of the QKV projection (fp32 slabs, summed by attention)
+  int cq = 0, co = 0, cg = 0, cd = 0;          // 32-deep k pieces per streamer wave per unit, per projection
+  const int* positions = nullptr;
+  const int* slots = nullptr;
+  const int* block_tables = nullptr;
+  const int* ctx_lens = nullptr;
+  int BS = 0, max_blocks = 0;
+  const float* cos_sin = nullptr;
+  float scale_log2 = 0.f, eps = 0.f;
+  float* resid = nullptr;    // [M][d] fp32 residual stream
+  bf16* xw = nullptr;        // [M][d] bf16 normed-input numerators (deferred RMSNorm)
+  float* ss = nullptr;       // [M][d / 16] sum-of-squares partials
+  const float* ss0 = nullptr;  // layer 0's partials (embed_prep: [M][ss0_tiles])
+  int ss0_tiles = 0;
+  float* qkv_ws = nullptr;   // [KSq][M][Nq] fp32
+  bf16* attn = nullptr;      // [M][Hq * 128]
+  bf16* act = nullptr;       // [M][Fl]
+  unsigned* edge = nullptr;  // [L * 5][8] arrival counters (zeroed by the launcher before every launch)
+  int* fault = nullptr;      // device word: an edge wait gave up (sticky for the launch)
+  int G = 0;                 // workgroups of this rank (one per CU)
+  int wnt = 1;               // non-temporal weight loads
+  XgmiArgs xp;               // world > 1: the fused all-reduce communicator (decode_epi.h granules)
+  unsigned* xar_ctr = nullptr;
+};
+// false: shapes outside the engine (the caller runs the per-layer launches); the launch itself is checked
+bool launch_decode_layers(const DLArgs& a, hipStream_t s);
+// test-only: up to 8 ranks of this process in ONE launch (grid z = rank), each with its own args
+constexpr int DL_MULTI_MAX = 8;
+bool launch_decode_layers_multi(const DLArgs* a, int world, hipStream_t s);
+int decode_layers_pieces_ok(int cq, int co, int cg, int cd);  // 1 if this shape class is built
+
 // test-only: every rank of this process in ONE launch (grid z = rank; co-residency checked)
 constexpr int XAR_MULTI_MAX = 8;
 struct XarMulti {

@@ -75,6 +75,13 @@ ROPE_DECODE_ROWS = os.environ.get("SYMMETRY_ROPE_DECODE_ROWS", "1") != "0"
 MG_FUSED_MODE = os.environ.get("SYMMETRY_MG_FUSED", "gu")
 MG_FUSED = MG_FUSED_MODE in ("1", "all")
 MG_FUSED_GU = MG_FUSED_MODE == "gu"
+# Dense decode steps of <= 16 rows run every layer as ONE persistent launch (csrc/kernels/decode_layers.hip: QKV ->
+# attention -> O (+ all-reduce) -> gate_up -> down with in-launch edges, each phase's weights streamed into registers
+# before the edge it waits on).  "auto": tensor-parallel shards (TP >= 2), where the per-layer launches sit at their
+# floors; "1": wherever the shape class is built (also TP = 1); "0": the per-layer launches.
+DECODE_ENGINE = os.environ.get("SYMMETRY_DECODE_ENGINE", "0")
+# workgroups of the engine's grid (one per CU; a one-GPU multi-rank rehearsal gives each rank a share)
+ENGINE_GRID = int(os.environ.get("SYMMETRY_ENGINE_GRID", "0"))
 # MFMA-preshuffled copy of the lm_head for the fused decode path's dg_argmax (1 KB per wave load like the layer
 # weights; +1 GB for Llama-3-8B): SYMMETRY_LMHEAD_SHUF=0 keeps the row-major stream
 LMHEAD_SHUF = os.environ.get("SYMMETRY_LMHEAD_SHUF", "1") != "0"
@@ -191,6 +198,8 @@ class TransformerLM:
             ops.decode_ks_ws(self.device)  # allocated before any graph capture (stable address)
         self.dgw = self._decode_copies(decode_weights)
         self.tp_reduced_bytes: dict[str, int] = {}  # bytes per rank of the last general-path all-reduce
+        self.engine_steps = 0  # forward passes (incl. graph captures) that ran the decode-step engine
+        self._engine_cache: dict = {}  # its plan and layer tables (per KV cache)
 
     def _decode_copies(self, mode: str) -> dict:
         """MFMA-preshuffled copies of the decode-GEMM weights (1 KB contiguous per wave load:
@@ -382,6 +391,68 @@ class TransformerLM:
         ops.dg_resid(x, W, resid, w_next, xw, ss_t, wshuf=sh)
         return ss_t
 
+    def _engine_plan(self, b: ForwardBatch, kv: KVCache):
+        """(KSq, pieces, grid, xar handle) of the decode-step engine for this step, or None (per-layer launches)."""
+        if (DECODE_ENGINE == "0" or self.device.type == "cpu" or self.cfg.is_moe or not self.dgw
+                or b.kind != "decode" or b.num_tokens > 16 or b.num_tokens != b.num_seqs):
+            return None
+        xar = -1
+        if self._tp_active():
+            get = getattr(self.tp, "engine_xar_handle", None)
+            xar = get() if get is not None else None
+            if xar is None:
+                return None  # the engine all-reduces in-launch: needs the peer-memory communicator
+        elif DECODE_ENGINE == "auto":
+            return None
+        bs = kv.block_size
+        if bs < 32 or bs & (bs - 1) or (self.hq // self.hkv) > 8 or (self.hq % self.hkv):
+            return None
+        plan = self._engine_cache.get("plan")
+        if plan is None:
+            d = self.cfg.hidden_size
+            Fl = self.w.layer(0, "w_gu").shape[0] // 2
+            G = ENGINE_GRID or torch.cuda.get_device_properties(self.device).multi_processor_count
+            ntq = (self.hq + 2 * self.hkv) * self.D // 16
+            ksq = 1
+            while ntq * ksq * 2 <= G and d % (ksq * 2 * 256) == 0:
+                ksq *= 2
+            pieces = (d // ksq // 256, self.hq * self.D // 256, d // 256, Fl // 256)
+            ok = (d % (ksq * 256) == 0 and (self.hq * self.D) % 256 == 0 and Fl % 256 == 0
+                  and ops.decode_layers_built(*pieces))
+            plan = (ksq, Fl, G) if ok else ()
+            self._engine_cache["plan"] = plan
+        if not plan:
+            return None
+        return plan + (xar,)
+
+    def _engine_table(self, kv: KVCache) -> torch.Tensor:
+        """int64 [L, 8] device table of every layer's engine operands (csrc/kernels/launchers.h DLLayer)."""
+        key = ("table", kv.k.data_ptr(), kv.v.data_ptr())
+        t = self._engine_cache.get(key)
+        if t is None:
+            w, L = self.w, self.cfg.num_layers
+            rows = []
+            for i in range(L):
+                lnn = w.layer(i + 1, "ln1") if i + 1 < L else w["norm"]
+                rows.append([self.dgw[(i, "wqkv")].data_ptr(), self.dgw[(i, "wo")].data_ptr(),
+                             self.dgw[(i, "w_gu")].data_ptr(), self.dgw[(i, "w_down")].data_ptr(),
+                             w.layer(i, "ln2").data_ptr(), lnn.data_ptr(), kv.k[i].data_ptr(), kv.v[i].data_ptr()])
+            t = torch.tensor(rows, dtype=torch.int64, device=self.device)
+            self._engine_cache[key] = t
+        return t
+
+    def _run_engine(self, b: ForwardBatch, kv: KVCache, plan, resid, xw, ss_t, ss_1, attn) -> bool:
+        ksq, Fl, G, xar = plan
+        T, L = b.num_tokens, self.cfg.num_layers
+        nq = (self.hq + 2 * self.hkv) * self.D
+        qkv_ws = self._buf("dl.qkv", (ksq * T * nq,), torch.float32)
+        act = self._buf("act", (T, Fl), torch.bfloat16)
+        edge = self.ws.get("dl.edge", (L * 5 * 8,), torch.int32, self.device, zeros=True)
+        fault = self.ws.get("dl.fault", (1,), torch.int32, self.device, zeros=True)
+        return ops.decode_layers(self._engine_table(kv), self.hq, self.hkv, Fl, ksq, b.positions, b.slot_mapping,
+                                 b.block_tables, b.ctx_lens, kv.block_size, self.cos_sin, self.scale, self.cfg.rms_eps,
+                                 resid, xw, ss_t, ss_1, qkv_ws, attn.view(T, -1), act, edge, fault, G, xar)
+
     def _forward_fused(self, b: ForwardBatch, kv: KVCache) -> torch.Tensor:
         cfg, w = self.cfg, self.w
         T, d, eps = b.num_tokens, cfg.hidden_size, cfg.rms_eps
@@ -393,7 +464,14 @@ class TransformerLM:
         attn = self._buf("attn", (T, self.hq, self.D), torch.bfloat16)
         ops.embed_prep(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), xw, ss_1, b.src, self.last_ids)
         ss = ss_1
-        for i in range(cfg.num_layers):
+        plan = self._engine_plan(b, kv)
+        if plan is not None and self._run_engine(b, kv, plan, resid, xw, ss_t, ss_1, attn):
+            self.engine_steps += 1
+            layers = range(0)  # every layer ran in the engine's launch
+            ss = ss_t
+        else:
+            layers = range(cfg.num_layers)
+        for i in layers:
             wq, shq = self._dgw(i, "wqkv")
             attn2d = attn.view(T, self.hq * self.D)
             nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]

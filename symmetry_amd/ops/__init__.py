@@ -238,6 +238,24 @@ def dg_argmax(x, W, ss_in, eps, temps, seeds, step, tile_keys, out_keys, out_ids
                                out_keys, out_ids, n_offset, logits)
 
 
+def decode_layers_built(cq: int, co: int, cg: int, cd: int) -> bool:
+    """Is the decode-step engine instantiated for this shape class (k pieces per wave of QKV / O / gate_up / down
+    units, csrc/kernels/decode_layers.hip DL_SHAPES)?"""
+    return native_available() and bool(_native.ops().decode_layers_pieces(int(cq), int(co), int(cg), int(cd)))
+
+
+def decode_layers(table, Hq, Hkv, Fl, KSq, positions, slots, block_tables, ctx_lens, BS, cos_sin, scale, eps, resid,
+                  xw, ss, ss0, qkv_ws, attn, act, edge, fault, G, xar=-1) -> bool:
+    """Every layer of a dense decode step in ONE persistent launch (csrc/kernels/decode_layers.hip): QKV ->
+    attention -> O (+ all-reduce on the ``xar`` communicator, -1 = world 1) -> gate_up -> down, edges in-launch,
+    next-phase weights streamed before each edge.  resid / xw / ss: the residual stream and the deferred-norm
+    inputs (layer 0's partials in ``ss0``), updated in place to the last layer's outputs.  False: the shape class is
+    not built or the grid would not be resident (nothing launched; run the per-layer launches)."""
+    return bool(_native.ops().decode_layers(table, int(Hq), int(Hkv), int(Fl), int(KSq), positions, slots,
+                                            block_tables, ctx_lens, int(BS), cos_sin, float(scale), float(eps), resid,
+                                            xw, ss, ss0, qkv_ws, attn, act, edge, fault, int(G), int(xar)))
+
+
 def embed_prep(ids, table, resid, w, xw, ss, src=None, prev=None):
     """Embedding gather + deferred-norm prep; with ``src``/``prev`` a row whose src >= 0 takes its token
     from ``prev[src]`` (the previous step's device-resident samples: pipelined decode)."""

@@ -27,7 +27,7 @@ def _port():
     return p
 
 
-def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False):
+def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False, engine=False):
     import traceback
 
     prompts = prompts or PROMPTS
@@ -37,7 +37,10 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False):
                       # (<= 64 workgroups per rank) are co-resident on the one GPU
                       SYMMETRY_XGMI_FUSED="force",
                       # graphs: decode steps captured and replayed with every collective on the xGMI kernels
-                      SYMMETRY_XGMI_GRAPHS="1" if graphs else "0")
+                      SYMMETRY_XGMI_GRAPHS="1" if graphs else "0",
+                      # engine: every decode step as ONE persistent launch per rank, 128 workgroups each (both ranks'
+                      # grids co-resident on the one GPU)
+                      SYMMETRY_DECODE_ENGINE="auto" if engine else "0", SYMMETRY_ENGINE_GRID="128")
     try:
         from symmetry_amd.engine.llm_engine import EngineConfig
         from symmetry_amd.engine.sequence import SamplingParams
@@ -63,6 +66,8 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False):
             eng.shutdown()  # the worker leaves its loop whatever happened here
         if graphs:
             assert eng.runner.use_graphs and eng.runner.graph_replays > 0, "decode steps did not replay graphs"
+        if engine:
+            assert eng.runner.model.engine_steps > 0, "the decode-step engine never ran"
         if xgmi == "1":
             calls = eng.runner.model.tp.calls
             # decode steps ran the peer-memory all-reduce: fused into the row-parallel GEMMs (one XAR launch each:
@@ -87,13 +92,14 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False):
             dist.destroy_process_group()
 
 
-def _run(model, world=2, xgmi="0", prompts=None, extra=False, graphs=False):
+def _run(model, world=2, xgmi="0", prompts=None, extra=False, graphs=False, engine=False):
     import torch.multiprocessing as mp
 
     port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    procs = [ctx.Process(target=_entry, args=(model, r, world, port, q, xgmi, prompts, graphs)) for r in range(world)]
+    procs = [ctx.Process(target=_entry, args=(model, r, world, port, q, xgmi, prompts, graphs, engine))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get() for _ in range(world))
@@ -180,4 +186,12 @@ def test_tp2_fused_xar_under_hipgraphs_on_one_gpu(gpu):
     launches (``SYMMETRY_XGMI_FUSED=force``) on the shared per-tile epoch counters, IPC-mapped peer buffers;
     every token within bf16 noise of the fp32 oracle."""
     outs = _run("small-llama", xgmi="1", graphs=True)
+    _check_oracle("small-llama", PROMPTS, outs)
+
+
+def test_tp2_decode_engine_on_one_gpu(gpu):
+    """The decode-step engine under TP = 2 between two processes on one GPU: one persistent launch per rank per
+    decode step (128 workgroups each), the O / down all-reduces pushed through the fused communicator's peer slots
+    inside it, decode steps captured into hipGraphs; every token within bf16 noise of the fp32 oracle."""
+    outs = _run("small-llama", xgmi="1", graphs=True, engine=True)
     _check_oracle("small-llama", PROMPTS, outs)
