@@ -283,7 +283,8 @@ DLArgs dl_args(const Tensor& table, int64_t Hq, int64_t Hkv, int64_t Fl, int64_t
   TORCH_CHECK(ss0.dim() == 2 && ss0.size(0) >= M, "decode_layers: ss0 [M, P]");
   TORCH_CHECK(qkv_ws.numel() >= KSq * M * Nq && attn.numel() >= M * Hq * 128 && act.numel() >= M * Fl,
               "decode_layers: workspace too small");
-  TORCH_CHECK(edge.numel() >= L * 5 * 8 && fault.numel() >= 1, "decode_layers: edge [L * 5 * 8], fault [1]");
+  TORCH_CHECK(edge.numel() >= L * 5 * 8 * 32 && edge.numel() >= (G + 255) / 256 * 256 && fault.numel() >= 1,
+              "decode_layers: edge [max(L * 5 * 8 * 32, G rounded to 256)], fault [1]");
   TORCH_CHECK(positions.numel() >= M && slots.numel() >= M && ctx_lens.numel() >= M && block_tables.dim() == 2 &&
                   block_tables.size(0) >= M, "decode_layers: step metadata rows");
   TORCH_CHECK(d % KSq == 0 && (d / KSq) % 256 == 0 && (Hq * 128) % 256 == 0 && d % 256 == 0 && Fl % 256 == 0,
@@ -322,6 +323,16 @@ DLArgs dl_args(const Tensor& table, int64_t Hq, int64_t Hkv, int64_t Fl, int64_t
   a.fault = fault.data_ptr<int>();
   a.G = (int)G;
   a.wnt = 1;
+  static const int edge_mode = [] {  // A/B knob: SYMMETRY_ENGINE_EDGE=0 sharded counters (default), 1 flag board
+    const char* k = getenv("SYMMETRY_ENGINE_EDGE");
+    return k ? atoi(k) : 0;
+  }();
+  a.edge_mode = edge_mode;
+  static const int ctl_prefetch = [] {  // A/B knob: SYMMETRY_ENGINE_CTL_PREFETCH=0 (profiles/r5/engine_ab.jsonl)
+    const char* k = getenv("SYMMETRY_ENGINE_CTL_PREFETCH");
+    return k ? atoi(k) : 1;
+  }();
+  a.ctl_prefetch = ctl_prefetch;
   if (xar >= 0) {
     Xgmi* x = get(xar);
     check_ready(x, resid);
@@ -337,9 +348,14 @@ bool decode_layers(const Tensor& table, int64_t Hq, int64_t Hkv, int64_t Fl, int
                    const Tensor& slots, const Tensor& block_tables, const Tensor& ctx_lens, int64_t BS,
                    const Tensor& cos_sin, double scale, double eps, Tensor& resid, Tensor& xw, Tensor& ss,
                    const Tensor& ss0, Tensor& qkv_ws, Tensor& attn, Tensor& act, Tensor& edge, Tensor& fault, int64_t G,
-                   int64_t xar) {
-  const DLArgs a = dl_args(table, Hq, Hkv, Fl, KSq, positions, slots, block_tables, ctx_lens, BS, cos_sin, scale, eps,
-                           resid, xw, ss, ss0, qkv_ws, attn, act, edge, fault, G, xar);
+                   int64_t xar, const c10::optional<Tensor>& stamps) {
+  DLArgs a = dl_args(table, Hq, Hkv, Fl, KSq, positions, slots, block_tables, ctx_lens, BS, cos_sin, scale, eps,
+                     resid, xw, ss, ss0, qkv_ws, attn, act, edge, fault, G, xar);
+  if (stamps.has_value() && stamps->defined()) {
+    dl_check_t(*stamps, at::kLong, "stamps");
+    TORCH_CHECK(stamps->numel() >= G * a.L * 5 * 8, "decode_layers: stamps [G * L * 5 * 8]");
+    a.stamps = reinterpret_cast<unsigned long long*>(stamps->data_ptr());
+  }
   return launch_decode_layers(a, stream_of(resid));
 }
 
@@ -596,7 +612,7 @@ TORCH_LIBRARY_FRAGMENT(symmetry_amd, m) {
       "decode_layers(Tensor table, int Hq, int Hkv, int Fl, int KSq, Tensor positions, Tensor slots, "
       "Tensor block_tables, Tensor ctx_lens, int BS, Tensor cos_sin, float scale, float eps, Tensor(a!) resid, "
       "Tensor(b!) xw, Tensor(c!) ss, Tensor ss0, Tensor(d!) qkv_ws, Tensor(e!) attn, Tensor(f!) act, "
-      "Tensor(g!) edge, Tensor(h!) fault, int G, int xar) -> bool",
+      "Tensor(g!) edge, Tensor(h!) fault, int G, int xar, Tensor(i!)? stamps=None) -> bool",
       &decode_layers);
   m.def(
       "decode_layers_multi(Tensor[] tables, int Hq, int Hkv, int Fl, int KSq, Tensor positions, Tensor slots, "

@@ -129,12 +129,15 @@ struct DLArgs {
   float* qkv_ws = nullptr;   // [KSq][M][Nq] fp32
   bf16* attn = nullptr;      // [M][Hq * 128]
   bf16* act = nullptr;       // [M][Fl]
-  unsigned* edge = nullptr;  // [L * 5][8] arrival counters (zeroed by the launcher before every launch)
+  unsigned* edge = nullptr;  // edge words (decode_layers.hip: edge_mode), zeroed by the launcher before every launch
+  int edge_mode = 0;         // 0: sharded arrival counters [L * 5][8] x 128 B; 1: flag board [G] (rounded to 1 KB)
   int* fault = nullptr;      // device word: an edge wait gave up (sticky for the launch)
   int G = 0;                 // workgroups of this rank (one per CU)
   int wnt = 1;               // non-temporal weight loads
+  int ctl_prefetch = 1;      // the control wave prefetches its weight pieces too (its edge poll then waits for them)
   XgmiArgs xp;               // world > 1: the fused all-reduce communicator (decode_epi.h granules)
   unsigned* xar_ctr = nullptr;
+  unsigned long long* stamps = nullptr;  // diagnostics: [G][L][5][8] wall clock: edge passed, signalled, sub-phases
 };
 // false: shapes outside the engine (the caller runs the per-layer launches); the launch itself is checked
 bool launch_decode_layers(const DLArgs& a, hipStream_t s);

@@ -200,6 +200,7 @@ class TransformerLM:
         self.tp_reduced_bytes: dict[str, int] = {}  # bytes per rank of the last general-path all-reduce
         self.engine_steps = 0  # forward passes (incl. graph captures) that ran the decode-step engine
         self._engine_cache: dict = {}  # its plan and layer tables (per KV cache)
+        self.engine_stamps = None  # diagnostics: int64 [G * L * 5 * 8] per-phase wall clock (bench/kernels/bench_engine.py)
 
     def _decode_copies(self, mode: str) -> dict:
         """MFMA-preshuffled copies of the decode-GEMM weights (1 KB contiguous per wave load:
@@ -447,11 +448,13 @@ class TransformerLM:
         nq = (self.hq + 2 * self.hkv) * self.D
         qkv_ws = self._buf("dl.qkv", (ksq * T * nq,), torch.float32)
         act = self._buf("act", (T, Fl), torch.bfloat16)
-        edge = self.ws.get("dl.edge", (L * 5 * 8,), torch.int32, self.device, zeros=True)
+        edge = self.ws.get("dl.edge", (max(L * 5 * 8 * 32, (G + 255) // 256 * 256),), torch.int32, self.device,
+                           zeros=True)
         fault = self.ws.get("dl.fault", (1,), torch.int32, self.device, zeros=True)
         return ops.decode_layers(self._engine_table(kv), self.hq, self.hkv, Fl, ksq, b.positions, b.slot_mapping,
                                  b.block_tables, b.ctx_lens, kv.block_size, self.cos_sin, self.scale, self.cfg.rms_eps,
-                                 resid, xw, ss_t, ss_1, qkv_ws, attn.view(T, -1), act, edge, fault, G, xar)
+                                 resid, xw, ss_t, ss_1, qkv_ws, attn.view(T, -1), act, edge, fault, G, xar,
+                                 self.engine_stamps)
 
     def _forward_fused(self, b: ForwardBatch, kv: KVCache) -> torch.Tensor:
         cfg, w = self.cfg, self.w

@@ -245,15 +245,17 @@ def decode_layers_built(cq: int, co: int, cg: int, cd: int) -> bool:
 
 
 def decode_layers(table, Hq, Hkv, Fl, KSq, positions, slots, block_tables, ctx_lens, BS, cos_sin, scale, eps, resid,
-                  xw, ss, ss0, qkv_ws, attn, act, edge, fault, G, xar=-1) -> bool:
+                  xw, ss, ss0, qkv_ws, attn, act, edge, fault, G, xar=-1, stamps=None) -> bool:
     """Every layer of a dense decode step in ONE persistent launch (csrc/kernels/decode_layers.hip): QKV ->
     attention -> O (+ all-reduce on the ``xar`` communicator, -1 = world 1) -> gate_up -> down, edges in-launch,
     next-phase weights streamed before each edge.  resid / xw / ss: the residual stream and the deferred-norm
-    inputs (layer 0's partials in ``ss0``), updated in place to the last layer's outputs.  False: the shape class is
-    not built or the grid would not be resident (nothing launched; run the per-layer launches)."""
+    inputs (layer 0's partials in ``ss0``), updated in place to the last layer's outputs.  ``stamps`` (int64
+    [G * L * 5 * 8], diagnostics): every workgroup's wall clock when each phase's edge passed / it signalled the
+    phase.  False: the shape class is not built or the grid would not be resident (nothing launched; run the
+    per-layer launches)."""
     return bool(_native.ops().decode_layers(table, int(Hq), int(Hkv), int(Fl), int(KSq), positions, slots,
                                             block_tables, ctx_lens, int(BS), cos_sin, float(scale), float(eps), resid,
-                                            xw, ss, ss0, qkv_ws, attn, act, edge, fault, int(G), int(xar)))
+                                            xw, ss, ss0, qkv_ws, attn, act, edge, fault, int(G), int(xar), stamps))
 
 
 def embed_prep(ids, table, resid, w, xw, ss, src=None, prev=None):

@@ -68,7 +68,7 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False, en
             assert eng.runner.use_graphs and eng.runner.graph_replays > 0, "decode steps did not replay graphs"
         if engine:
             assert eng.runner.model.engine_steps > 0, "the decode-step engine never ran"
-        if xgmi == "1":
+        if xgmi == "1" and not engine:
             calls = eng.runner.model.tp.calls
             # decode steps ran the peer-memory all-reduce: fused into the row-parallel GEMMs (one XAR launch each:
             # GEMM + all-reduce + residual) for the dense model, the fused add_prep kernel around the MoE block
