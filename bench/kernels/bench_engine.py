@@ -74,17 +74,29 @@ def main():
             edge_med.append(float(nxt.median() - signed.max()))
         # sub-phase stamps of the first unit (2: operands landed, 3: after the reduce barrier / rope barrier, 4: epilogue
         # done / merge barrier), relative to the edge, median over the workgroups that have them
-        sub = {}
+        sub, spread, split = {}, {}, {}
+        n_attn = C * model.hkv * 8  # workgroups with an attention unit (decode_layers.hip DL_APARTS = 8)
         for k in (2, 3, 4):
-            vals = []
+            vals, q10, q90, va, vo = [], [], [], [], []
             for l in mid:
                 v = s[:, l, p, k]
                 ok = v > 0
                 if ok.any():
-                    vals.append(float((v[ok] - s[ok, l, p, 0]).median()))
+                    rel = v[ok] - s[ok, l, p, 0]
+                    vals.append(float(rel.median()))
+                    q10.append(float(rel.quantile(0.1)))
+                    q90.append(float(rel.quantile(0.9)))
+                    idx = torch.nonzero(ok).flatten()
+                    ra, ro = rel[idx < n_attn], rel[idx >= n_attn]
+                    if len(ra) and len(ro):
+                        va.append(float(ra.median()))
+                        vo.append(float(ro.median()))
             if vals:
                 sub[str(k)] = round(sum(vals) / len(vals), 2)
-        rows[n] = {"sub_us": sub, "work_median_us": round(sum(work) / len(work), 2),
+                spread[str(k)] = [round(sum(q10) / len(q10), 2), round(sum(q90) / len(q90), 2)]
+            if va:
+                split[str(k)] = [round(sum(va) / len(va), 2), round(sum(vo) / len(vo), 2)]
+        rows[n] = {"sub_us": sub, "sub_p10_p90_us": spread, "sub_attn_wgs_vs_rest_us": split, "work_median_us": round(sum(work) / len(work), 2),
                    "last_signal_skew_us": round(sum(skew) / len(skew), 2),
                    "edge_release_first_us": round(sum(edge_first) / len(edge_first), 2),
                    "edge_release_median_us": round(sum(edge_med) / len(edge_med), 2)}

@@ -283,8 +283,6 @@ DLArgs dl_args(const Tensor& table, int64_t Hq, int64_t Hkv, int64_t Fl, int64_t
   TORCH_CHECK(ss0.dim() == 2 && ss0.size(0) >= M, "decode_layers: ss0 [M, P]");
   TORCH_CHECK(qkv_ws.numel() >= KSq * M * Nq && attn.numel() >= M * Hq * 128 && act.numel() >= M * Fl,
               "decode_layers: workspace too small");
-  TORCH_CHECK(edge.numel() >= L * 5 * 8 * 32 && edge.numel() >= (G + 255) / 256 * 256 && fault.numel() >= 1,
-              "decode_layers: edge [max(L * 5 * 8 * 32, G rounded to 256)], fault [1]");
   TORCH_CHECK(positions.numel() >= M && slots.numel() >= M && ctx_lens.numel() >= M && block_tables.dim() == 2 &&
                   block_tables.size(0) >= M, "decode_layers: step metadata rows");
   TORCH_CHECK(d % KSq == 0 && (d / KSq) % 256 == 0 && (Hq * 128) % 256 == 0 && d % 256 == 0 && Fl % 256 == 0,
@@ -322,17 +320,13 @@ DLArgs dl_args(const Tensor& table, int64_t Hq, int64_t Hkv, int64_t Fl, int64_t
   a.edge = reinterpret_cast<unsigned*>(edge.data_ptr());
   a.fault = fault.data_ptr<int>();
   a.G = (int)G;
-  a.wnt = 1;
   static const int edge_mode = [] {  // A/B knob: SYMMETRY_ENGINE_EDGE=0 sharded counters (default), 1 flag board
     const char* k = getenv("SYMMETRY_ENGINE_EDGE");
     return k ? atoi(k) : 0;
   }();
   a.edge_mode = edge_mode;
-  static const int ctl_prefetch = [] {  // A/B knob: SYMMETRY_ENGINE_CTL_PREFETCH=0 (profiles/r5/engine_ab.jsonl)
-    const char* k = getenv("SYMMETRY_ENGINE_CTL_PREFETCH");
-    return k ? atoi(k) : 1;
-  }();
-  a.ctl_prefetch = ctl_prefetch;
+  TORCH_CHECK(edge.numel() >= dl_edge_words((int)L, (int)M, (int)Hq, (int)Hkv, (int)G, edge_mode) &&
+                  fault.numel() >= 1, "decode_layers: edge [decode_layers_edge_words(...)], fault [1]");
   if (xar >= 0) {
     Xgmi* x = get(xar);
     check_ready(x, resid);
@@ -359,31 +353,13 @@ bool decode_layers(const Tensor& table, int64_t Hq, int64_t Hkv, int64_t Fl, int
   return launch_decode_layers(a, stream_of(resid));
 }
 
-// test-only: every rank of this process in ONE launch (grid z = rank); per-rank lists, shared step metadata
-bool decode_layers_multi(std::vector<Tensor> tables, int64_t Hq, int64_t Hkv, int64_t Fl, int64_t KSq,
-                         const Tensor& positions, const Tensor& slots, const Tensor& block_tables,
-                         const Tensor& ctx_lens, int64_t BS, const Tensor& cos_sin, double scale, double eps,
-                         std::vector<Tensor> resids, std::vector<Tensor> xws, std::vector<Tensor> sss,
-                         std::vector<Tensor> ss0s, std::vector<Tensor> qkv_wss, std::vector<Tensor> attns,
-                         std::vector<Tensor> acts, std::vector<Tensor> edges, std::vector<Tensor> faults, int64_t G,
-                         std::vector<int64_t> xars) {
-  const int world = (int)tables.size();
-  TORCH_CHECK(world >= 1 && world <= DL_MULTI_MAX && (int)resids.size() == world && (int)xws.size() == world &&
-                  (int)sss.size() == world && (int)ss0s.size() == world && (int)qkv_wss.size() == world &&
-                  (int)attns.size() == world && (int)acts.size() == world && (int)edges.size() == world &&
-                  (int)faults.size() == world && (int)xars.size() == world, "decode_layers_multi: one set per rank");
-  std::vector<DLArgs> as;
-  for (int r = 0; r < world; ++r) {
-    as.push_back(dl_args(tables[r], Hq, Hkv, Fl, KSq, positions, slots, block_tables, ctx_lens, BS, cos_sin, scale,
-                         eps, resids[r], xws[r], sss[r], ss0s[r], qkv_wss[r], attns[r], acts[r], edges[r], faults[r], G,
-                         xars[r]));
-    if (xars[r] >= 0) TORCH_CHECK(as[r].xp.rank == r && as[r].xp.world == world, "decode_layers_multi: comm order");
-  }
-  return launch_decode_layers_multi(as.data(), world, stream_of(resids[0]));
+int64_t decode_layers_edge_words(int64_t L, int64_t M, int64_t Hq, int64_t Hkv, int64_t G) {
+  const char* k = getenv("SYMMETRY_ENGINE_EDGE");
+  return dl_edge_words((int)L, (int)M, (int)Hq, (int)Hkv, (int)G, k ? atoi(k) : 0);
 }
 
-int64_t decode_layers_pieces(int64_t cq, int64_t co, int64_t cg, int64_t cd) {
-  return decode_layers_pieces_ok((int)cq, (int)co, (int)cg, (int)cd);
+int64_t decode_layers_pieces(int64_t cq, int64_t co, int64_t cg, int64_t cd, int64_t ks, int64_t gh) {
+  return decode_layers_pieces_ok((int)cq, (int)co, (int)cg, (int)cd, (int)ks, (int)gh);
 }
 
 // test-only: every rank of this process in one launch (grid slice per rank; see xgmi_ar.hip)
@@ -614,13 +590,8 @@ TORCH_LIBRARY_FRAGMENT(symmetry_amd, m) {
       "Tensor(b!) xw, Tensor(c!) ss, Tensor ss0, Tensor(d!) qkv_ws, Tensor(e!) attn, Tensor(f!) act, "
       "Tensor(g!) edge, Tensor(h!) fault, int G, int xar, Tensor(i!)? stamps=None) -> bool",
       &decode_layers);
-  m.def(
-      "decode_layers_multi(Tensor[] tables, int Hq, int Hkv, int Fl, int KSq, Tensor positions, Tensor slots, "
-      "Tensor block_tables, Tensor ctx_lens, int BS, Tensor cos_sin, float scale, float eps, Tensor(a!)[] resids, "
-      "Tensor(b!)[] xws, Tensor(c!)[] sss, Tensor[] ss0s, Tensor(d!)[] qkv_wss, Tensor(e!)[] attns, "
-      "Tensor(f!)[] acts, Tensor(g!)[] edges, Tensor(h!)[] faults, int G, int[] xars) -> bool",
-      &decode_layers_multi);
-  m.def("decode_layers_pieces(int cq, int co, int cg, int cd) -> int", &decode_layers_pieces);
+  m.def("decode_layers_pieces(int cq, int co, int cg, int cd, int ks, int gh) -> int", &decode_layers_pieces);
+  m.def("decode_layers_edge_words(int L, int M, int Hq, int Hkv, int G) -> int", &decode_layers_edge_words);
   m.def("xgmi_keys_max_multi(Tensor[] keys, Tensor(a!)[] ids, int[] comms, int delay_rank=-1, int delay_us=0) -> ()",
         &xgmi_keys_max_multi);
   m.def(

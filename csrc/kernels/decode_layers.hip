@@ -7,21 +7,28 @@
 // 54.5 MB, ~213 KB per CU) and each of the five launches per layer sits at its ~5-9 us floor -- launch boundary,
 // the first weight loads' latency, the tail (profiles/r4/prof_tp8_shard_xar.csv: 36.3 us per layer against an
 // 8.7 us weight floor).  Weights never depend on activations, so here every workgroup issues the weight loads of
-// its NEXT phase's first unit into registers right after it signalled the current phase, and they stream while
-// it waits on the edge: at TP = 8 a unit is a whole phase's share (QKV 32 KB, O 16 KB, gate_up 128 KB, down 56 KB
-// per CU), so after an edge only the activations' round trip, the MFMAs and the epilogue remain.
+// its NEXT phase's first unit into registers while it runs the current phase, and they stream across the edge:
+// at TP = 8 a unit is a whole phase's share (QKV 32 KB, O 16 KB, gate_up 128 KB, down 56 KB per CU), so after an
+// edge only the activations' round trip, the MFMAs and the epilogue remain.
 //
 // Geometry: one workgroup per CU (G of them, all co-resident: the edges wait on every workgroup), 8 waves (two per
 // SIMD: 256 VGPRs each, so a unit's weights AND activations fit in registers):
 //   * every wave streams: it owns the 32-deep k pieces w, w + 8, w + 16, ... of every GEMM unit (a 16-row weight
-//     tile x a k range; one 16 B load per lane per piece, MFMA-preshuffled weights: 1 KB contiguous per wave
-//     load), holds them AND the unit's activation fragments in registers, accumulates one
-//     v_mfma_f32_16x16x32_bf16 chain and hands its 16 x 16 partial to LDS; in the attention phase the 8 waves are
-//     the attention waves (one 32-token group each per pass);
+//     tile x a k range; one 16 B buffer load per lane per piece, MFMA-preshuffled weights: 1 KB contiguous per
+//     wave load), holds them AND the unit's activation fragments in registers, accumulates one
+//     v_mfma_f32_16x16x32_bf16 chain and hands its 16 x 16 partial to LDS;
 //   * wave 7 doubles as the control wave: it sums the 8 partials, runs the epilogue (every hand-off store is
 //     write-through: sc1), the xGMI all-reduce of O / down (push to every peer, collect in rank order,
-//     decode_epi.h xar_push / xar_collect), the row scales and the edges.  Next-phase weight loads are issued only
-//     after the phase's signal, so the drain before a signal waits for this phase's stores alone.
+//     decode_epi.h xar_push / xar_collect), the row scales and the edges;
+//   * attention is wave-level split-KV (dl_attn_wave): (sequence, kv head, context partition) units, one per wave,
+//     dealt over the workgroups first, the partitions merged by the last arriver.
+// Weight streaming: a wave's loads and stores retire in issue order (MI355X_MICROARCH.md, vmcnt), so the next
+// phase's weights are issued right AFTER this phase's activation loads (`after_x`), never before them, and the
+// streamer waves do not drain at a signal (they store nothing in a GEMM phase): the stream stays in flight across
+// the edge.  The control wave -- which polls and stores -- loads its own pieces after the edge instead.  Every load
+// is a buffer load with the per-piece offset in an SGPR and no branch between an MFMA's operands and the next
+// phase's loads, so the compiler's waits count exactly the operands (flat loads, or path-dependent load counts,
+// made it wait for everything).
 // Edges (MI355X_MICROARCH.md Valid forms, row 1): every storing wave drains (s_waitcnt vmcnt(0)), the workgroup
 // barriers, ONE lane adds to an agent-scope counter (sharded 8 ways by blockIdx & 7); the consumer's control wave
 // polls every shard with sc1 loads, the workgroup barriers, and every load of handed-off bytes is an sc1 (L1-
@@ -44,11 +51,21 @@ constexpr int DL_MAXP = 16;              // pieces per streamer wave per unit: u
 constexpr int DL_GMAX = 8;               // query heads per kv head
 constexpr int DL_MAXT = 64;              // O / down tiles per workgroup (epoch slots)
 constexpr int DL_MAXKS = 4;              // QKV k-slabs
+constexpr int DL_MAXL = 128;             // layers
 constexpr unsigned long long DL_WAIT_TICKS = 200000000ull;  // 2 s (100 MHz): an edge that never completes
 enum { DL_QKV = 0, DL_ATTN = 1, DL_O = 2, DL_GU = 3, DL_DOWN = 4, DL_PH = 5 };
 enum { EP_SLAB = 0, EP_RES = 1, EP_SWI = 2 };
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+// a pointer the wave holds in every lane (read from LDS): into SGPRs, so buffer descriptors built from it need
+// no waterfall loop
+template <typename T>
+SYM_DEV T* dl_uni(T* p) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return reinterpret_cast<T*>(((unsigned long long)hi << 32) | lo);
+}
 
 SYM_DEV rsrc_t dl_rsrc(const void* base, long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
@@ -91,9 +108,12 @@ SYM_DEV void dl_stamp_ctl(const DLArgs& a, int ev, int b, int which) {
 //      (16 B sc1 loads, 4 workgroups per lane) until all reached the event.
 constexpr int DL_SHARD_STRIDE = 32;  // u32 words between counter shards (128 B)
 
-// every thread: this workgroup's hand-off stores are drained, then ONE lane signals
-SYM_DEV void dl_signal(const DLArgs& a, int ev, int b) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// every thread: this workgroup's hand-off stores are drained, then ONE lane signals.  `drain`: this wave stored
+// hand-off data in the phase.  In a GEMM phase only the control wave stores (the epilogue); the streamer waves skip
+// the drain, so the next phase's weight loads they issued during this phase stay in flight across the signal (a
+// wave's loads and stores retire in order: draining would wait for that whole stream).
+SYM_DEV void dl_signal(const DLArgs& a, int ev, int b, bool drain = true) {
+  if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     if (a.edge_mode == 1)
@@ -144,21 +164,19 @@ SYM_DEV void dl_wait(const DLArgs& a, int ev) {
 // ---- GEMM units ---------------------------------------------------------------------------------------------
 // A unit = 16 weight rows (tile) x k range [k0, k0 + 256 CNT): streamer wave w owns pieces w + 8 i, i < CNT.
 template <int CNT>
-SYM_DEV void dl_load_w(Pack8 (&wa)[DL_MAXP], const bf16* __restrict__ W, int K, int tile, int k0, int wnt, int rot) {
+SYM_DEV void dl_load_w(Pack8 (&wa)[DL_MAXP], const bf16* __restrict__ W, int K, int tile, int k0, int rot,
+                       bool on = true) {
+  // buffer loads, nt (aux 2), no branches: the compiler's wait before an MFMA counts the loads issued after its
+  // operands, which needs the same instruction sequence on every path (loads through the generic pointers of the
+  // argument table were flat loads, after which it can only wait for everything -- the next phase's whole prefetch
+  // included).  !on: a zero-length descriptor -- every load returns 0 without touching memory.
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const bf16* p = W + ((long long)tile * (K / 32) + k0 / 32 + w) * 512 + lane * 8;
-  if (wnt) {
+  const rsrc_t rw = dl_rsrc(dl_uni(W) + ((long long)tile * (K / 32) + k0 / 32) * 512, on ? 0x7fffffffLL : 0LL);
+  const int off = (w * 512 + lane * 8) * 2;  // the lane's part in a VGPR, the piece's in an SGPR (soffset)
 #pragma unroll
-    for (int j = 0; j < CNT; ++j) {
-      const int i = CNT > 1 ? (j + rot) % CNT : 0;
-      wa[j].w = ld_nt16(p + (long long)i * DL_SW * 512);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < CNT; ++j) {
-      const int i = CNT > 1 ? (j + rot) % CNT : 0;
-      wa[j].u = *reinterpret_cast<const uint4*>(p + (long long)i * DL_SW * 512);
-    }
+  for (int j = 0; j < CNT; ++j) {
+    const int i = CNT > 1 ? (j + rot) % CNT : 0;
+    wa[j].w = __builtin_amdgcn_raw_buffer_load_b128(rw, off, __builtin_amdgcn_readfirstlane(i * DL_SW * 1024), 2);
   }
 }
 
@@ -174,7 +192,7 @@ SYM_DEV void dl_load_x(Pack8 (&xa)[DL_MAXP], rsrc_t rx, int K, int k0, int M, in
 #pragma unroll
   for (int j = 0; j < CNT; ++j) {
     const int i = CNT > 1 ? (j + rot) % CNT : 0;
-    xa[j].w = ld_sc1(rx, off + i * DL_SW * 64);
+    xa[j].w = __builtin_amdgcn_raw_buffer_load_b128(rx, off, __builtin_amdgcn_readfirstlane(i * DL_SW * 64), 16);
   }
 }
 
@@ -200,21 +218,17 @@ SYM_DEV void dl_unit_of(const DLPhase& ph, int u, int& tile, int& k0) {
   k0 = (u % ph.ksplit) * ph.kunit;
 }
 
-// (unconditional definitions of wa[0 .. CNT): a workgroup without a unit in the phase zeroes them, so no older
-// value of the array stays live across the phases in between -- across attention that cost ~50 VGPRs)
-// The control wave does not prefetch: its first vector load after the signal is the edge poll, which would
-// otherwise wait behind its weight loads (vmcnt retires in order; a 128 KB gate_up share took ~5 us to land); it
-// loads its pieces of the first unit with the activations, after the edge.
+// (every path issues the same loads -- zero-length descriptors where the workgroup has no unit -- so no older value
+// of the array stays live and the compiler's waits stay exact).  `with_ctl`: the control wave loads its pieces too.
+// It does at a signal (its poll then waits for its few pieces, issued before any later stream), not inside a
+// phase: there its epilogue drain would wait for the next phase's whole stream; it loads those pieces with the
+// activations after the edge instead (dl_gemm_phase `ctl_late`).
 template <int CNT>
-SYM_DEV void dl_prefetch(Pack8 (&wa)[DL_MAXP], const DLPhase& ph, int b, int wnt, int ctl_prefetch) {
-  if (b >= ph.nunits || (!ctl_prefetch && (threadIdx.x >> 6) == DL_CTL)) {
-#pragma unroll
-    for (int i = 0; i < CNT; ++i) wa[i].u = make_uint4(0, 0, 0, 0);
-    return;
-  }
-  int tile, k0;
-  dl_unit_of(ph, b, tile, k0);
-  dl_load_w<CNT>(wa, ph.W, ph.K, tile, k0, wnt, b);
+SYM_DEV void dl_prefetch(Pack8 (&wa)[DL_MAXP], const DLPhase& ph, int b, bool with_ctl, bool any = true) {
+  const bool on = any && b < ph.nunits && (with_ctl || (threadIdx.x >> 6) != DL_CTL);
+  int tile = 0, k0 = 0;
+  if (b < ph.nunits) dl_unit_of(ph, b, tile, k0);
+  dl_load_w<CNT>(wa, ph.W, ph.K, tile, k0, b, on);
 }
 
 // The control wave's view of a layer for the epilogues
@@ -304,34 +318,54 @@ SYM_DEV void dl_row_scales(const DLArgs& a, const float* __restrict__ ss, int ti
   }
 }
 
-// One GEMM phase: the workgroup's units b, b + G, ... (the first unit's weights already in flight in wa)
-template <int CNT, int EPI>
+struct DLNoHook {
+  SYM_DEV void operator()() const {}
+};
+
+// One GEMM phase: the workgroup's units b, b + G, ... (the first unit's weights already in flight in wa).
+// `after_x` runs right after the first unit's activation loads are issued: the NEXT phase's weight prefetch goes
+// there, behind this phase's operands (a wave's loads retire in order: weights issued before the activations --
+// at the previous signal -- made this phase's first MFMA wait for the next phase's whole stream).
+template <int CNT, int EPI, typename AfterX>
 SYM_DEV void dl_gemm_phase(const DLArgs& a, const DLPhase& ph, const DLEpi& ep, Pack8 (&wa)[DL_MAXP],
                            Pack8 (&xa)[DL_MAXP], int b, f32x4 (*red)[DL_SW][64], const float* rn_s,
-                           unsigned* xep_s, int ev) {
+                           unsigned* xep_s, int ev, bool ctl_late, AfterX after_x) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const bool ctl = wid == DL_CTL;
   const rsrc_t rx = dl_rsrc(ph.x, (long long)a.M * ph.K * 2);
-  int buf = 0, i = 0;
-  for (int u = b; u < ph.nunits; u += a.G, ++i) {
+  int buf = 0;
+  // (the first unit peeled: `after_x` defines the prefetch registers on every path, so no older value of them
+  // stays live through the phase -- a conditional definition inside the loop kept both and spilled)
+  auto unit = [&](int u, int i, auto hook) {
     int tile, k0;
     dl_unit_of(ph, u, tile, k0);
     {
-      if (ctl && i == 0 && !a.ctl_prefetch) dl_load_w<CNT>(wa, ph.W, ph.K, tile, k0, a.wnt, b);
+      if (ctl && i == 0 && ctl_late) dl_load_w<CNT>(wa, ph.W, ph.K, tile, k0, b);
       dl_load_x<CNT>(xa, rx, ph.K, k0, a.M, b);
-      const f32x4 acc = dl_mma<CNT>(wa, xa);
-      if (i == 0 && a.stamps != nullptr) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        dl_stamp_ctl(a, ev, b, 2);
+      if constexpr (!std::is_same_v<AfterX, DLNoHook>) {
+        // every wave's operand loads (the control wave's late weight pieces too) are queued before any wave's
+        // prefetch: a CU's vector memory path returns in issue order, so a load queued behind the next phase's
+        // stream waited for all of it (the control wave's -- whose partial every unit's epilogue needs -- ~3 us).
+        // A bare s_barrier: __syncthreads' fence would wait for the loads themselves.
+        __builtin_amdgcn_s_barrier();
+        hook();
       }
+      // every activation load issued before the first MFMA waits (left to itself the scheduler interleaved them
+      // with the MFMAs to save registers, one memory round trip per piece)
+      __builtin_amdgcn_sched_barrier(0);
+      const f32x4 acc = dl_mma<CNT>(wa, xa);
       // the next unit's weights behind this unit's MFMAs (same registers: no renamed second copy)
       __builtin_amdgcn_sched_barrier(0);
       if (u + a.G < ph.nunits) {
         int t2, k2;
         dl_unit_of(ph, u + a.G, t2, k2);
-        dl_load_w<CNT>(wa, ph.W, ph.K, t2, k2, a.wnt, b);
+        dl_load_w<CNT>(wa, ph.W, ph.K, t2, k2, b);
       }
       red[buf][wid][lane] = acc;
+      if (i == 0 && ctl && a.stamps != nullptr) {  // operands landed: the store above needed the MFMA result (no
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // vmcnt wait: it would also wait for the prefetch)
+        dl_stamp_ctl(a, ev, b, 2);
+      }
     }
     __syncthreads();
     if (i == 0) dl_stamp_ctl(a, ev, b, 3);
@@ -368,243 +402,288 @@ SYM_DEV void dl_gemm_phase(const DLArgs& a, const DLPhase& ph, const DLEpi& ep, 
     }
     if (i == 0) dl_stamp_ctl(a, ev, b, 4);
     buf ^= 1;
-  }
+  };
+  if (b < ph.nunits)
+    unit(b, 0, after_x);
+  else
+    after_x();
+  for (int u = b + a.G, i = 1; u < ph.nunits; u += a.G, ++i) unit(u, i, DLNoHook{});
 }
 
 // ---- attention ----------------------------------------------------------------------------------------------
-// The newest token's K / V come out of this step's QKV slabs; every OLDER token is in the paged cache since an
-// earlier launch.  So the old K / V do not wait for the QKV edge beyond one round trip: the block-table entries are
-// read before the edge and the K / V loads issue together with the slab loads right after it; the newest token
-// joins in the merge (its score and value from the rebuilt rows in LDS) and goes to the cache with plain stores for
-// the NEXT step (no drain, no read-back).  (Holding the whole first pass in registers across the edge spilled.)
-struct DLAttnLds {
-  float qkv[(DL_GMAX + 2) * 128];  // the unit's q / k / v rows (slab sums, not yet row-scaled; permuted order)
-  bf16 q[DL_GMAX][128];            // roped q, natural dim order
-  bf16 knew[128], vnew[128];       // the newest token's roped k and its v (bf16, as the cache holds them)
-  float cs[128];                   // RoPE cos (0..63) / sin (64..127) of the unit's position
-  float m[DL_SW][DL_GMAX], l[DL_SW][DL_GMAX];
-  float o[DL_SW][DL_GMAX][D + 4];
+// Wave-level split-KV: a (sequence, kv head) is DL_APARTS units, one per wave (partition p: the 32-token groups p,
+// p + DL_APARTS, ... of the old tokens), dealt over the workgroups first (at TP = 8, 10 sequences: 80 workgroups with
+// one attention wave each), so the old K / V stream in over 80 CUs' load paths instead of 10 (a 128 KB per-CU share
+// took ~8 us).  Every unit rebuilds the (small) q / k / v rows of its (sequence, kv head) from the QKV slabs (x the
+// row scale, RoPE through a lane shuffle: the partner row r ^ 8 sits two lanes away), publishes its partial
+// softmax state (sc1), drains, and bumps the (sequence, kv head) counter; the last arriver merges the partials with
+// the newest token (its score and value from its own rebuilt rows) and stores the head outputs (sc1: handed to O).
+// The newest token's K / V come out of this step's slabs; every OLDER token is in the paged cache since an earlier
+// launch, so the first group's block-table entry is read before the edge and its K / V loads issue together with
+// the slab loads right after it.  Partition 0 stores the newest K / V for the next step (kernel boundary: plain).
+struct DLWaveLds {  // per wave: the roped q rows and the newest token's k / v (bf16, natural dim order)
+  bf16 q[DL_GMAX][128];
+  bf16 knew[128], vnew[128];
 };
 
-// What a unit needs that does not depend on this step's QKV, read BEFORE the QKV edge: the sequence's context
-// length / cache slot / position, the block of wave w's first 32-token group of old tokens [0, ctx - 1) (-1: none),
-// and the position's RoPE cos / sin row (into LDS) -- so after the edge the unit's first loads (old K / V, the
-// slabs, the row scale's partials) all issue at once and nothing else waits on a round trip.
 struct DLAttnMeta {
   int ctx, slot, pos, bk0;
 };
 
-SYM_DEV DLAttnMeta dl_attn_meta(const DLArgs& a, int s, float* cs_lds) {
+SYM_DEV DLAttnMeta dl_attn_meta(const DLArgs& a, int s, int p) {
   DLAttnMeta mt;
   mt.ctx = a.ctx_lens[s];
   mt.slot = a.slots[s];
   mt.pos = a.positions[s];
-  const int tok0 = (threadIdx.x >> 6) * 32;
+  const int tok0 = 32 * p;
   mt.bk0 = tok0 < mt.ctx - 1 ? a.block_tables[(long long)s * a.max_blocks + (tok0 >> __builtin_ctz(a.BS))] : -1;
-  if (threadIdx.x < 32)
-    *reinterpret_cast<float4*>(cs_lds + 4 * threadIdx.x) =
-        *reinterpret_cast<const float4*>(a.cos_sin + (long long)mt.pos * 128 + 4 * threadIdx.x);
   return mt;
 }
 
-// One (sequence, kv head) unit on the 8 waves: rebuild its q / k / v rows from the QKV slabs (x the row scale,
-// RoPE), store the newest K / V for the next step, flash-decode over the old tokens (first pass from `pre` when
-// `use_pre`; wave w: 32-token groups w, w + 8, ...), merge the waves and the newest token through LDS, store the
-// head outputs (sc1: handed to O).
-SYM_DEV void dl_attn_unit(const DLArgs& a, const DLLayer& ly, int s, int g, const float* __restrict__ ss_in,
-                          int ss_tiles, DLAttnLds& L, DLAttnMeta mt, int stamp_ev) {
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int Hq = a.Hq, Hkv = a.Hkv, G = Hq / Hkv;
+// One 32-token group's K / V fragments (attn_decode.h load_group's layout) by buffer loads off the group's block
+SYM_DEV void dl_load_kv(const DLLayer& ly, int Hkv, int BS, int bk, int g, int tok0, KVFrag& f) {
+  const int lane = threadIdx.x & 63, r16 = lane & 15, h = lane >> 4;
+  const int boff = tok0 & (BS - 1);
+  const rsrc_t rk = dl_rsrc(dl_uni(ly.k_cache) + (((long long)bk * Hkv + g) * BS + boff) * D, 0x7fffffffLL);
+  const rsrc_t rv = dl_rsrc(dl_uni(ly.v_cache) + ((long long)bk * Hkv + g) * (long long)D * BS + boff, 0x7fffffffLL);
+#pragma unroll
+  for (int aa = 0; aa < 2; ++aa) {
+    const int trow = (r16 >> 2) * 8 + 4 * aa + (r16 & 3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      Pack8 t;
+      t.w = __builtin_amdgcn_raw_buffer_load_b128(rk, (trow * D + 32 * h + 8 * i) * 2, 0, 0);
+      f.k[aa][i] = t.v;
+    }
+  }
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    Pack8 t;
+    t.w = __builtin_amdgcn_raw_buffer_load_b128(rv, ((16 * dt + r16) * BS + 8 * h) * 2, 0, 0);
+    f.v[dt] = t.v;
+  }
+}
+
+// KS: QKV k-slabs, GH: query heads per kv head (4 or 8) -- template parameters of the shape class, so every
+// register array below has its exact size
+template <int KS, int GH>
+SYM_DEV void dl_attn_wave(const DLArgs& a, const DLLayer& ly, int sg, int p, const float* __restrict__ ss_in,
+                          int ss_tiles, DLWaveLds& W, DLAttnMeta mt, int stamp_ev) {
+  const int lane = threadIdx.x & 63;
+  constexpr int Gh = GH, R = (GH + 2) / 2;  // R: 256-value rounds of the unit's q / k / v rows
+  const int Hq = a.Hq, Hkv = a.Hkv;
+  const int s = sg / Hkv, g = sg % Hkv;
   const int Nq = (Hq + 2 * Hkv) * 128;
-  const int nval = (G + 2) * 128;
-  const int ctx = mt.ctx;
-  const int ctx_old = ctx - 1;
-  const int slot = mt.slot;
+  const int ctx = mt.ctx, ctx_old = ctx - 1, slot = mt.slot;
   const int c = lane & 15, h = lane >> 4;
-  // the first pass of old K / V (block known from before the edge: bk0), the slab rows (4 consecutive values per
-  // thread, every slab's 16 B at once) and, in every wave, the row scale from the residual's sum-of-squares
-  // partials (one 16 B load per lane for d / 16 partials) -- all issued together
   const int bsh = __builtin_ctz(a.BS);
   const int* bt = a.block_tables + (long long)s * a.max_blocks;
+  // ---- every load of the unit at once: the first group's old K / V, the slab rows (4 consecutive values per lane
+  // per round), the lane's RoPE cos / sin (the same 4 dims in every round), the row scale's partials
   KVFrag f;
-  int tok0 = wid * 32;
-  if (tok0 < ctx_old) {
-    const int bk = mt.bk0 >= 0 ? mt.bk0 : bt[tok0 >> bsh];
-    const int boff = tok0 & (a.BS - 1);
-    load_group(ly.k_cache + (((long long)bk * Hkv + g) * a.BS + boff) * D,
-               ly.v_cache + ((long long)bk * Hkv + g) * (long long)D * a.BS + boff, a.BS, f);
-  }
-  Pack8 q[DL_MAXKS];
-  const int t4 = threadIdx.x * 4;
-  const int row = t4 < G * 128 ? g * G * 128 + t4
-                               : (t4 < (G + 1) * 128 ? Hq * 128 + g * 128 + (t4 - G * 128)
-                                                     : (Hq + Hkv) * 128 + g * 128 + (t4 - (G + 1) * 128));
-  if (t4 < nval) {
-    const rsrc_t rq = dl_rsrc(a.qkv_ws, (long long)a.KSq * a.M * Nq * 4);
+  int tok0 = 32 * p;
+  if (tok0 < ctx_old) dl_load_kv(ly, Hkv, a.BS, mt.bk0, g, tok0, f);
+  Pack8 q[R][KS];
+  {
+    const rsrc_t rq = dl_rsrc(a.qkv_ws, (long long)KS * a.M * Nq * 4);
 #pragma unroll
-    for (int sp = 0; sp < DL_MAXKS; ++sp)
-      if (sp < a.KSq) q[sp].w = ld_sc1(rq, ((sp * a.M + s) * Nq + row) * 4);
+    for (int j = 0; j < R; ++j) {
+      const int t4 = 4 * lane + 256 * j;
+      const int row = t4 < Gh * 128 ? g * Gh * 128 + t4
+                                    : (t4 < (Gh + 1) * 128 ? Hq * 128 + g * 128 + (t4 - Gh * 128)
+                                                           : (Hq + Hkv) * 128 + g * 128 + (t4 - (Gh + 1) * 128));
+#pragma unroll
+      for (int sp = 0; sp < KS; ++sp) q[j][sp].w = ld_sc1(rq, ((sp * a.M + s) * Nq + row) * 4);
+    }
   }
+  const int r4 = (4 * lane) & 127;  // the lane's rows within a head (permuted order)
+  const bool lo = (r4 & 15) < 8;
+  const int dh0 = 8 * (r4 >> 4) + (r4 & 7);
+  const float4 co = *reinterpret_cast<const float4*>(a.cos_sin + (long long)mt.pos * 128 + dh0);
+  const float4 si = *reinterpret_cast<const float4*>(a.cos_sin + (long long)mt.pos * 128 + 64 + dh0);
   float ssum = 0.f;
   {
     const rsrc_t rs = dl_rsrc(ss_in, (long long)a.M * ss_tiles * 4);
     if ((ss_tiles & 3) == 0) {
       Pack8 sq[2];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int i = 4 * lane + 256 * c;
-        sq[c].w = i < ss_tiles ? ld_sc1(rs, (s * ss_tiles + i) * 4) : u32x4{0u, 0u, 0u, 0u};
+      for (int k = 0; k < 2; ++k) {
+        const int i = 4 * lane + 256 * k;
+        sq[k].w = i < ss_tiles ? ld_sc1(rs, (s * ss_tiles + i) * 4) : u32x4{0u, 0u, 0u, 0u};
       }
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+      for (int k = 0; k < 2; ++k)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ssum += __uint_as_float(sq[c].w[e]);
+        for (int e = 0; e < 4; ++e) ssum += __uint_as_float(sq[k].w[e]);
     } else {
       for (int i = lane; i < ss_tiles; i += 64) ssum += ldf_sc1(ss_in + (long long)s * ss_tiles + i);
     }
   }
   const float rn = rsqrtf(wave_sum(ssum) * (1.f / (float)a.d) + a.eps);
-  if (stamp_ev >= 0) {
+  if (stamp_ev >= 0 && a.stamps != nullptr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    dl_stamp_ctl(a, stamp_ev, blockIdx.x, 2);
+    if (lane == 0) a.stamps[((long long)blockIdx.x * a.L * DL_PH + stamp_ev) * 8 + 2] = wall_clock64();
   }
-  if (t4 < nval) {
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int sp = 0; sp < DL_MAXKS; ++sp)
-      if (sp < a.KSq)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += __uint_as_float(q[sp].w[e]);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) L.qkv[t4 + e] = v[e] * rn;
-  }
-  __syncthreads();
+  // ---- rebuild the rows (slab sum x row scale), RoPE on q / k, into the wave's LDS; partition 0 writes the cache
   {
-    const float* cs = L.cs;  // the position's cos / sin row (staged before the edge)
     const long long blk = slot >= 0 ? slot / a.BS : 0, off = slot >= 0 ? slot % a.BS : 0;
-    // q heads and the k head: RoPE over the permuted rows (partner row = r ^ 8); thread -> 8 consecutive dims of
-    // one head (natural order)
-    const int nqk = (G + 1) * 16;
-    if ((int)threadIdx.x < nqk) {
-      const int head = threadIdx.x >> 4, c8 = threadIdx.x & 15;  // dims 8 c8 .. 8 c8 + 7
-      const bool lo = c8 < 8;
-      Pack8 pk;
+    const float cof[4] = {co.x, co.y, co.z, co.w}, sif[4] = {si.x, si.y, si.z, si.w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int dim = 8 * c8 + e, dh = dim & 63, j = dh >> 3, c = (dh & 7) + (lo ? 0 : 8);
-        const int r = 16 * j + c;  // permuted row of this dim within the head
-        const float x = L.qkv[head * 128 + r], p = L.qkv[head * 128 + (r ^ 8)];
-        const float co = cs[dh], si = cs[64 + dh];
-        pk.h[e] = (bf16)(lo ? x * co - p * si : x * co + p * si);
+    for (int j = 0; j < R; ++j) {
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sp = 0; sp < KS; ++sp)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += __uint_as_float(q[j][sp].w[e]);
+      float pv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] *= rn;
+        pv[e] = __shfl_xor(v[e], 2, 64);
       }
-      if (head < G) {
-        *reinterpret_cast<uint4*>(&L.q[head][8 * c8]) = pk.u;
-      } else {
-        *reinterpret_cast<uint4*>(&L.knew[8 * c8]) = pk.u;
-        if (slot >= 0)  // for the next step (kernel boundary: plain stores)
-          *reinterpret_cast<uint4*>(ly.k_cache + ((blk * Hkv + g) * a.BS + off) * 128 + 8 * c8) = pk.u;
+      const int t4 = 4 * lane + 256 * j;
+      const int dim0 = dh0 + (lo ? 0 : 64);
+      Pack8 pk;
+      if (t4 < (Gh + 1) * 128) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk.h[e] = (bf16)(lo ? v[e] * cof[e] - pv[e] * sif[e] : v[e] * cof[e] + pv[e] * sif[e]);
+        const uint2 u = make_uint2(pk.w[0], pk.w[1]);
+        if (t4 < Gh * 128) {
+          *reinterpret_cast<uint2*>(&W.q[t4 >> 7][dim0]) = u;
+        } else {
+          *reinterpret_cast<uint2*>(&W.knew[dim0]) = u;
+          if (p == 0 && slot >= 0)
+            *reinterpret_cast<uint2*>(ly.k_cache + ((blk * Hkv + g) * a.BS + off) * 128 + dim0) = u;
+        }
+      } else {  // v: natural order; dim-major cache (one bf16 per line)
+        const int dim = t4 - (Gh + 1) * 128;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bf16 bv = (bf16)v[e];
+          W.vnew[dim + e] = bv;
+          if (p == 0 && slot >= 0) ly.v_cache[((blk * Hkv + g) * 128 + dim + e) * (long long)a.BS + off] = bv;
+        }
       }
-    } else if ((int)threadIdx.x < nqk + 128) {  // v: natural order; dim-major cache (one bf16 per line)
-      const int dim = threadIdx.x - nqk;
-      const bf16 bv = (bf16)L.qkv[(G + 1) * 128 + dim];
-      L.vnew[dim] = bv;
-      if (slot >= 0) ly.v_cache[((blk * Hkv + g) * 128 + dim) * (long long)a.BS + off] = bv;
     }
   }
-  __syncthreads();
-  if (stamp_ev >= 0) dl_stamp_ctl(a, stamp_ev, blockIdx.x, 3);
-  // old tokens [0, ctx - 1)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS rows, read back across lanes
+  // ---- old tokens of this partition
   f32x4 o[8];
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, lsum = 0.f;
-  {
-    bf16x8 qf[4];
-    if (c < G) {
+  bf16x8 qf[4];
+  if (c < Gh) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) qf[i] = *reinterpret_cast<const bf16x8*>(&L.q[c][32 * h + 8 * i]);
-    } else {
+    for (int i = 0; i < 4; ++i) qf[i] = *reinterpret_cast<const bf16x8*>(&W.q[c][32 * h + 8 * i]);
+  } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) qf[i] = zero8();
-    }
-    if (tok0 < ctx_old)
-      compute_group(f, qf, a.scale_log2, [&](int aa, int r) { return tok0 + 8 * h + 4 * aa + r < ctx_old; }, o, m,
-                    lsum);
-    tok0 += DL_SW * 32;
+    for (int i = 0; i < 4; ++i) qf[i] = zero8();
+  }
+  if (tok0 < ctx_old)
+    compute_group(f, qf, a.scale_log2, [&](int aa, int r) { return tok0 + 8 * h + 4 * aa + r < ctx_old; }, o, m, lsum);
+  tok0 += DL_APARTS * 32;
 #pragma unroll 1
-    for (; tok0 < ctx_old; tok0 += DL_SW * 32) {
-      const int bk = bt[tok0 >> bsh];
-      const int boff = tok0 & (a.BS - 1);
-      load_group(ly.k_cache + (((long long)bk * Hkv + g) * a.BS + boff) * D,
-                 ly.v_cache + ((long long)bk * Hkv + g) * (long long)D * a.BS + boff, a.BS, f);
-      compute_group(f, qf, a.scale_log2, [&](int aa, int r) { return tok0 + 8 * h + 4 * aa + r < ctx_old; }, o, m,
-                    lsum);
-    }
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
-    if (c < DL_GMAX) {
-      if (h == 0) {
-        L.m[wid][c] = m;
-        L.l[wid][c] = lsum;
-      }
+  for (; tok0 < ctx_old; tok0 += DL_APARTS * 32) {
+    dl_load_kv(ly, Hkv, a.BS, __builtin_amdgcn_readfirstlane(bt[tok0 >> bsh]), g, tok0, f);
+    compute_group(f, qf, a.scale_log2, [&](int aa, int r) { return tok0 + 8 * h + 4 * aa + r < ctx_old; }, o, m,
+                  lsum);
+  }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  // ---- publish the partial, count in; the last arriver merges
+  const int nused = ctx_old > 0 ? min(DL_APARTS, (ctx_old + 31) / 32) : 0;
+  const long long sync_w = dl_edge_sync_words(a.L, a.M, Hkv, a.G, a.edge_mode);
+  unsigned* cnt = a.edge + sync_w - (long long)a.M * Hkv * 32 + sg * 32;
+  float* po = reinterpret_cast<float*>(a.edge + sync_w);
+  float* pml = po + (long long)a.M * Hkv * DL_APARTS * Gh * 128;
+  const rsrc_t rpo = dl_rsrc(po, (long long)a.M * Hkv * DL_APARTS * Gh * 128 * 4);
+  const rsrc_t rpm = dl_rsrc(pml, (long long)a.M * Hkv * Gh * DL_APARTS * 2 * 4);
+  if (p < nused && c < Gh) {
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) L.o[wid][c][16 * dt + 4 * h + r] = o[dt][r];
+    for (int dt = 0; dt < 8; ++dt)
+      st_sc1(rpo, ((((sg * DL_APARTS + p) * Gh + c) * 128) + 16 * dt + 4 * h) * 4,
+             u32x4{__float_as_uint(o[dt][0]), __float_as_uint(o[dt][1]), __float_as_uint(o[dt][2]),
+                   __float_as_uint(o[dt][3])});
+    if (h == 0) {
+      stf_sc1(pml + ((sg * Gh + c) * DL_APARTS + p) * 2, m);
+      stf_sc1(pml + ((sg * Gh + c) * DL_APARTS + p) * 2 + 1, lsum);
     }
   }
-  __syncthreads();
-  if (stamp_ev >= 0) dl_stamp_ctl(a, stamp_ev, blockIdx.x, 4);
-  {  // thread (qq, d0): 8 dims of query head qq; the 16 threads of a head are 16 consecutive lanes
-    const int qq = threadIdx.x >> 4, d0 = (threadIdx.x & 15) * 8;
-    float sn = 0.f;  // the newest token's score: q . k_new over this thread's 8 dims, then over the 16 threads
-    if (qq < G) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0, 64);
+  if (old != DL_APARTS - 1) return;
+  if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next layer's
+  if (stamp_ev >= 0 && a.stamps != nullptr && lane == 0)
+    a.stamps[((long long)blockIdx.x * a.L * DL_PH + stamp_ev) * 8 + 3] = wall_clock64();
+  // ---- merge: lane -> head qq, 2 Gh consecutive dims
+  constexpr int LPH = 64 / Gh, DPL = 2 * Gh, CH = Gh / 2;
+  const int qq = lane / LPH, d0 = (lane % LPH) * DPL;
+  Pack8 mlv[DL_APARTS / 2];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sn += (float)L.q[qq][d0 + j] * (float)L.knew[d0 + j];
-    }
+  for (int i = 0; i < DL_APARTS / 2; ++i) mlv[i].w = ld_sc1(rpm, (((sg * Gh + qq) * DL_APARTS) * 2 + 4 * i) * 4);
+  Pack8 ov[DL_APARTS][CH];
 #pragma unroll
-    for (int o2 = 8; o2 > 0; o2 >>= 1) sn += __shfl_xor(sn, o2, 64);
-    if (qq < G) {
-      sn *= a.scale_log2;
-      const bool has_new = ctx >= 1;
-      float M_ = has_new ? sn : -INFINITY, Lsum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int pp = 0; pp < DL_APARTS; ++pp)
 #pragma unroll
-      for (int w = 0; w < DL_SW; ++w) M_ = fmaxf(M_, L.m[w][qq]);
+    for (int k = 0; k < CH; ++k)
+      ov[pp][k].w = pp < nused
+                        ? ld_sc1(rpo, ((((sg * DL_APARTS + pp) * Gh + qq) * 128) + d0 + 4 * k) * 4)
+                        : u32x4{0u, 0u, 0u, 0u};
+  float sn = 0.f;  // the newest token's score over the lane's dims, then over the head's lanes
 #pragma unroll
-      for (int w = 0; w < DL_SW; ++w) {
-        const float mw = L.m[w][qq];
-        const float f = (mw == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(mw - M_);
-        Lsum += L.l[w][qq] * f;
+  for (int j = 0; j < DPL; ++j) sn += (float)W.q[qq][d0 + j] * (float)W.knew[d0 + j];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += L.o[w][qq][d0 + j] * f;
-      }
-      if (has_new) {
-        const float f = __builtin_amdgcn_exp2f(sn - M_);
-        Lsum += f;
+  for (int x = LPH / 2; x > 0; x >>= 1) sn += __shfl_xor(sn, x, 64);
+  sn *= a.scale_log2;
+  const bool has_new = ctx >= 1;
+  float Mx = has_new ? sn : -INFINITY;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += f * (float)L.vnew[d0 + j];
-      }
-      const float inv = Lsum > 0.f ? 1.f / Lsum : 0.f;  // ctx == 0 (padding row): zeros
-      Pack8 pk;
+  for (int pp = 0; pp < DL_APARTS; ++pp)
+    if (pp < nused) Mx = fmaxf(Mx, __uint_as_float(mlv[pp / 2].w[(pp & 1) * 2]));
+  float Ls = 0.f, acc[DPL];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) pk.h[j] = (bf16)(acc[j] * inv);
-      const rsrc_t ro = dl_rsrc(a.attn, (long long)a.M * Hq * 128 * 2);
-      st_sc1(ro, ((s * Hq + g * G + qq) * 128 + d0) * 2, pk.w);
-    }
+  for (int j = 0; j < DPL; ++j) acc[j] = 0.f;
+#pragma unroll
+  for (int pp = 0; pp < DL_APARTS; ++pp) {
+    const float mp = __uint_as_float(mlv[pp / 2].w[(pp & 1) * 2]), lp = __uint_as_float(mlv[pp / 2].w[(pp & 1) * 2 + 1]);
+    const float fct = pp < nused ? __builtin_amdgcn_exp2f(mp - Mx) : 0.f;
+    Ls += pp < nused ? lp * fct : 0.f;
+#pragma unroll
+    for (int k = 0; k < CH; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[4 * k + e] += __uint_as_float(ov[pp][k].w[e]) * fct;
   }
-  __syncthreads();  // the LDS staging is reused by the next unit
+  if (has_new) {
+    const float fct = __builtin_amdgcn_exp2f(sn - Mx);
+    Ls += fct;
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) acc[j] += fct * (float)W.vnew[d0 + j];
+  }
+  const float inv = Ls > 0.f ? 1.f / Ls : 0.f;  // ctx == 0 (padding row): zeros
+  const rsrc_t ro = dl_rsrc(a.attn, (long long)a.M * Hq * 128 * 2);
+#pragma unroll
+  for (int k = 0; k < DPL / 8; ++k) {
+    Pack8 pk;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pk.h[j] = (bf16)(acc[8 * k + j] * inv);
+    st_sc1(ro, ((s * Hq + g * Gh + qq) * 128 + d0 + 8 * k) * 2, pk.w);
+  }
 }
 
 // ---- the step ---------------------------------------------------------------------------------------------
 // Specialised per shape class: the k pieces per streamer wave of the QKV, O, gate_up and down units are template
 // parameters, so every register array has its exact size (a runtime-dispatched form inlined every instantiation
 // into one body and spilled).
-template <int CQ, int CO, int CG, int CD>
+template <int CQ, int CO, int CG, int CD, int KS, int GH>
 SYM_DEV void dl_body(const DLArgs& a, int b) {
   __shared__ f32x4 red[2][DL_SW][64];
   __shared__ float rn_s[16];
   __shared__ unsigned xep_s[DL_MAXT];
-  __shared__ DLAttnLds lds_attn;
+  __shared__ DLWaveLds lds_wave[DL_SW];
+  __shared__ DLLayer lay_s[DL_MAXL];  // the layer table (LDS reads: no vector-memory wait behind streaming loads)
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool ctl = wid == DL_CTL;
   const int d = a.d, Nq = (a.Hq + 2 * a.Hkv) * 128;
@@ -612,6 +691,11 @@ SYM_DEV void dl_body(const DLArgs& a, int b) {
   // this workgroup's O / down tiles (b, b + G, ...): their all-reduce epochs, read once, bumped by every O and
   // every down phase, written back at exit (the per-tile counters of the fused launches, decode_gemm.hip)
   const int nmine = b < ntile_d ? (ntile_d - b + a.G - 1) / a.G : 0;
+  {
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(a.layers);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(lay_s);
+    for (int i = threadIdx.x; i < a.L * (int)(sizeof(DLLayer) / 8); i += DL_NT) dst[i] = src[i];
+  }
   if (ctl && a.xp.world > 1)
     for (int i = lane; i < nmine; i += 64) xep_s[i] = a.xar_ctr[b + i * a.G];
   __syncthreads();
@@ -619,80 +703,87 @@ SYM_DEV void dl_body(const DLArgs& a, int b) {
   // weight registers: wa = QKV / O units, wb = gate_up (prefetched at the attention signal, across O), wc = down
   // (prefetched at the O signal, across gate_up): each phase's stream starts as early as its registers allow
   Pack8 wa[DL_MAXP], wb[DL_MAXP], wc[DL_MAXP], xa[DL_MAXP];
+  // down's weights stream during gate_up when both shares fit the registers beside gate_up's activations (TP = 8:
+  // 16 + 7 pieces per wave); otherwise (TP = 4: 16 + 14 spilled ~190 VGPRs) from the gate_up signal on
+  constexpr bool kEarlyDown = CG + CD <= 24;
+  constexpr bool kEarlyQkv = CD + CQ <= 16;  // the next layer's QKV weights during down, likewise
   auto phase_of = [&](int l, int p) -> DLPhase {
-    const DLLayer& ly = a.layers[l];
+    const DLLayer& ly = lay_s[l];
     if (p == DL_QKV) return DLPhase{ly.wqkv, d, d / a.KSq, (Nq / 16) * a.KSq, a.KSq, a.xw};
     if (p == DL_O) return DLPhase{ly.wo, a.Hq * 128, a.Hq * 128, ntile_d, 1, a.attn};
     if (p == DL_GU) return DLPhase{ly.wgu, d, d, (2 * a.Fl) / 16, 1, a.xw};
     return DLPhase{ly.wdown, a.Fl, a.Fl, ntile_d, 1, a.act};
   };
-  dl_prefetch<CQ>(wa, phase_of(0, DL_QKV), b, a.wnt, a.ctl_prefetch);
+  dl_prefetch<CQ>(wa, phase_of(0, DL_QKV), b, true);
   for (int l = 0; l < a.L; ++l) {
-    const DLLayer& ly = a.layers[l];
+    const DLLayer& ly = lay_s[l];
     const int ev0 = l * DL_PH;
     // ---- QKV: split-K slabs (the row scale waits for the attention phase)
     if (l > 0) dl_wait(a, ev0 - DL_PH + DL_DOWN);
     dl_stamp(a, ev0 + DL_QKV, b, 0);
     dl_gemm_phase<CQ, EP_SLAB>(a, phase_of(l, DL_QKV), DLEpi{EP_SLAB, a.qkv_ws, Nq, nullptr, nullptr, Nq}, wa, xa, b,
-                               red, rn_s, xep_s, ev0 + DL_QKV);
-    dl_signal(a, ev0 + DL_QKV, b);
-    // ---- attention: the first unit's old K / V stream in before the edge
+                               red, rn_s, xep_s, ev0 + DL_QKV, l > 0 && kEarlyQkv, DLNoHook{});
+    dl_signal(a, ev0 + DL_QKV, b, ctl);
+    // ---- attention: wave-level units (sequence x kv head x partition), dealt over the workgroups first; the first
+    // unit's metadata read before the edge
     {
-      const bool have = b < a.M * a.Hkv;
+      const int nv = a.M * a.Hkv * DL_APARTS;
+      const int v0 = b + a.G * wid;
       DLAttnMeta mt{0, -1, 0, -1};
-      if (have) mt = dl_attn_meta(a, b / a.Hkv, lds_attn.cs);
-      dl_wait(a, ev0 + DL_QKV);  // (its barrier publishes the staged cos / sin row)
+      if (v0 < nv) mt = dl_attn_meta(a, v0 / DL_APARTS / a.Hkv, v0 % DL_APARTS);
+      dl_wait(a, ev0 + DL_QKV);
       dl_stamp(a, ev0 + DL_ATTN, b, 0);
       const float* ss_in = l == 0 ? a.ss0 : a.ss;
       const int ss_tiles = l == 0 ? a.ss0_tiles : ntile_d;
-      for (int u = b; u < a.M * a.Hkv; u += a.G) {
-        if (u != b) {  // a later unit of this workgroup: its own pre-stage (after the previous unit's last barrier)
-          mt = dl_attn_meta(a, u / a.Hkv, lds_attn.cs);
-          __syncthreads();
-        }
-        dl_attn_unit(a, ly, u / a.Hkv, u % a.Hkv, ss_in, ss_tiles, lds_attn, mt, u == b ? ev0 + DL_ATTN : -1);
+      for (int v = v0; v < nv; v += a.G * DL_SW) {
+        if (v != v0) mt = dl_attn_meta(a, v / DL_APARTS / a.Hkv, v % DL_APARTS);
+        dl_attn_wave<KS, GH>(a, ly, v / DL_APARTS, v % DL_APARTS, ss_in, ss_tiles, lds_wave[wid], mt,
+                             v == b ? ev0 + DL_ATTN : -1);
       }
     }
     dl_signal(a, ev0 + DL_ATTN, b);
-    dl_prefetch<CO>(wa, phase_of(l, DL_O), b, a.wnt, a.ctl_prefetch);
-    dl_prefetch<CG>(wb, phase_of(l, DL_GU), b, a.wnt, a.ctl_prefetch);
-    // ---- O (+ all-reduce, residual, ln2 prep)
+    dl_prefetch<CO>(wa, phase_of(l, DL_O), b, true);  // small (O: 16 KB per CU), before any later stream
+    // ---- O (+ all-reduce, residual, ln2 prep); gate_up's weights stream from here on
     dl_wait(a, ev0 + DL_ATTN);
     dl_stamp(a, ev0 + DL_O, b, 0);
     dl_gemm_phase<CO, EP_RES>(a, phase_of(l, DL_O), DLEpi{EP_RES, nullptr, 0, ly.ln2, nullptr, d}, wa, xa, b, red,
-                              rn_s, xep_s, ev0 + DL_O);
-    dl_signal(a, ev0 + DL_O, b);
-    dl_prefetch<CD>(wc, phase_of(l, DL_DOWN), b, a.wnt, a.ctl_prefetch);
+                              rn_s, xep_s, ev0 + DL_O, false,
+                              [&] { dl_prefetch<CG>(wb, phase_of(l, DL_GU), b, false); });
+    dl_signal(a, ev0 + DL_O, b, ctl);
     // ---- gate_up (+ row scale, SwiGLU)
     dl_wait(a, ev0 + DL_O);
     dl_stamp(a, ev0 + DL_GU, b, 0);
     dl_row_scales(a, a.ss, ntile_d, rn_s);  // published by the first unit's barrier, before any epilogue reads it
     dl_gemm_phase<CG, EP_SWI>(a, phase_of(l, DL_GU), DLEpi{EP_SWI, nullptr, 0, nullptr, a.act, 2 * a.Fl}, wb, xa, b,
-                              red, rn_s, xep_s, ev0 + DL_GU);
-    dl_signal(a, ev0 + DL_GU, b);
+                              red, rn_s, xep_s, ev0 + DL_GU, true, [&] {
+                                if constexpr (kEarlyDown) dl_prefetch<CD>(wc, phase_of(l, DL_DOWN), b, false);
+                              });
+    dl_signal(a, ev0 + DL_GU, b, ctl);
+    if constexpr (!kEarlyDown) dl_prefetch<CD>(wc, phase_of(l, DL_DOWN), b, true);
     // ---- down (+ all-reduce, residual, next-norm prep)
     dl_wait(a, ev0 + DL_GU);
     dl_stamp(a, ev0 + DL_DOWN, b, 0);
+    const int ln = l + 1 < a.L ? l + 1 : l;  // (the last layer issues zero-length loads: the same instructions)
     dl_gemm_phase<CD, EP_RES>(a, phase_of(l, DL_DOWN), DLEpi{EP_RES, nullptr, 0, ly.lnn, nullptr, d}, wc, xa, b, red,
-                              rn_s, xep_s, ev0 + DL_DOWN);
-    dl_signal(a, ev0 + DL_DOWN, b);
-    if (l + 1 < a.L) dl_prefetch<CQ>(wa, phase_of(l + 1, DL_QKV), b, a.wnt, a.ctl_prefetch);
+                              rn_s, xep_s, ev0 + DL_DOWN, kEarlyDown, [&] {
+                                if constexpr (kEarlyQkv) dl_prefetch<CQ>(wa, phase_of(ln, DL_QKV), b, false, ln != l);
+                              });
+    dl_signal(a, ev0 + DL_DOWN, b, ctl);
+    if constexpr (!kEarlyQkv) dl_prefetch<CQ>(wa, phase_of(ln, DL_QKV), b, true, ln != l);
   }
   if (ctl && a.xp.world > 1)
     for (int i = lane; i < nmine; i += 64) a.xar_ctr[b + i * a.G] = xep_s[i];
 }
 
-template <int CQ, int CO, int CG, int CD>
-__global__ __launch_bounds__(DL_NT) void decode_layers_kernel(DLArgs a) {
-  dl_body<CQ, CO, CG, CD>(a, blockIdx.x);
-}
-
-struct DLMulti {
-  DLArgs a[DL_MULTI_MAX];
+// (the arguments indexed by blockIdx.z, always 0 here: a dynamically indexed kernel argument is read from the
+// kernarg segment where used -- passed plainly, every field was hoisted into SGPRs at entry and ~300 of them
+// spilled, through VGPR lanes into scratch)
+struct DLOne {
+  DLArgs a[1];
 };
-template <int CQ, int CO, int CG, int CD>
-__global__ __launch_bounds__(DL_NT) void decode_layers_multi_kernel(DLMulti m) {
-  dl_body<CQ, CO, CG, CD>(m.a[blockIdx.z], blockIdx.x);
+template <int CQ, int CO, int CG, int CD, int KS, int GH>
+__global__ __launch_bounds__(DL_NT) void decode_layers_kernel(DLOne m) {
+  dl_body<CQ, CO, CG, CD, KS, GH>(m.a[blockIdx.z], blockIdx.x);
 }
 
 // The shape classes built (pieces per streamer wave = unit K / 256 for QKV (K = d / KSq), O (K = Hq x 128 / tp),
@@ -702,18 +793,17 @@ __global__ __launch_bounds__(DL_NT) void decode_layers_multi_kernel(DLMulti m) {
 //   Llama-3-8B TP = 2: QKV 2048 (KSq 2), O 2048, gate_up 4096, down 7168  -> (not built: down K > 4096)
 //   small-llama TP = 1 / 2 (tests): QKV 512 (KSq 2) / 256 (KSq 4), O 1024 / 512, gate_up 1024, down 3584 / 1792;
 //   its TP = 2 one-GPU rehearsal (128 workgroups per rank): QKV 512 (KSq 2)
-#define DL_SHAPES(X) X(4, 2, 16, 7) X(8, 4, 16, 14) X(2, 4, 4, 14) X(1, 2, 4, 7) X(2, 2, 4, 7)
+// (+ the QKV k-slabs and the query heads per kv head: 4 for both models)
+#define DL_SHAPES(X) X(4, 2, 16, 7, 4, 4) X(8, 4, 16, 14, 2, 4) X(2, 4, 4, 14, 2, 4) X(1, 2, 4, 7, 4, 4) X(2, 2, 4, 7, 2, 4)
 
 bool dl_check(const DLArgs& a) {
-  return a.M >= 1 && a.M <= 16 && a.L >= 1 && a.Hkv >= 1 && a.Hq % a.Hkv == 0 && a.Hq / a.Hkv <= DL_GMAX &&
+  return a.M >= 1 && a.M <= 16 && a.L >= 1 && a.Hkv >= 1 && a.Hq % a.Hkv == 0 && (a.Hq / a.Hkv == 4 || a.Hq / a.Hkv == 8) &&
          a.d % 256 == 0 && a.Fl % 256 == 0 && a.BS >= 32 && (a.BS & (a.BS - 1)) == 0 && a.G >= 1 &&
-         (a.d / 16 + a.G - 1) / a.G <= DL_MAXT && a.KSq >= 1 && a.KSq <= DL_MAXKS && a.d % (a.KSq * 256) == 0;
+         (a.d / 16 + a.G - 1) / a.G <= DL_MAXT && a.L <= DL_MAXL && a.KSq >= 1 && a.KSq <= DL_MAXKS && a.d % (a.KSq * 256) == 0;
 }
 
 // bytes of edge words one launch uses (zeroed before it)
-size_t dl_edge_bytes(const DLArgs& a) {
-  return a.edge_mode == 1 ? (size_t)(a.G + 255) / 256 * 1024 : (size_t)a.L * DL_PH * 8 * DL_SHARD_STRIDE * 4;
-}
+size_t dl_edge_bytes(const DLArgs& a) { return (size_t)dl_edge_sync_words(a.L, a.M, a.Hkv, a.G, a.edge_mode) * 4; }
 
 int g_dl_resident[16];  // per shape: workgroups per CU the kernel admits (occupancy query, once; 0 = unknown)
 
@@ -721,7 +811,7 @@ template <typename Kern>
 int dl_per_cu(Kern k, int& cache) {
   if (cache <= 0) {
     int n = 0;
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, DL_NT, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, DL_NT, 0);
     cache = n > 0 ? n : -1;
   }
   return cache;
@@ -739,9 +829,9 @@ int dl_cus() {
 
 }  // namespace
 
-int decode_layers_pieces_ok(int cq, int co, int cg, int cd) {
-#define DL_MATCH(A, B, C, D_) \
-  if (cq == A && co == B && cg == C && cd == D_) return 1;
+int decode_layers_pieces_ok(int cq, int co, int cg, int cd, int ks, int gh) {
+#define DL_MATCH(A, B, C, D_, KS, GH) \
+  if (cq == A && co == B && cg == C && cd == D_ && ks == KS && gh == GH) return 1;
   DL_SHAPES(DL_MATCH)
 #undef DL_MATCH
   return 0;
@@ -750,40 +840,15 @@ int decode_layers_pieces_ok(int cq, int co, int cg, int cd) {
 bool launch_decode_layers(const DLArgs& a, hipStream_t s) {
   if (!dl_check(a)) return false;
   int idx = 0;
-#define DL_LAUNCH(A, B, C, D_)                                                                          \
-  if (a.cq == A && a.co == B && a.cg == C && a.cd == D_) {                                               \
-    auto k = decode_layers_kernel<A, B, C, D_>;                                                          \
+#define DL_LAUNCH(A, B, C, D_, KS, GH)                                                                  \
+  if (a.cq == A && a.co == B && a.cg == C && a.cd == D_ && a.KSq == KS && a.Hq / a.Hkv == GH) {          \
+    auto k = decode_layers_kernel<A, B, C, D_, KS, GH>;                                                  \
     if (a.G > dl_cus() * dl_per_cu(k, g_dl_resident[idx])) return false; /* every workgroup resident */ \
     (void)hipMemsetAsync(a.edge, 0, dl_edge_bytes(a), s);                                               \
-    k<<<a.G, DL_NT, 0, s>>>(a);                                                                          \
+    k<<<a.G, DL_NT, 0, s>>>(DLOne{{a}});                                                                 \
     return true;                                                                                         \
   }                                                                                                      \
   ++idx;
-  DL_SHAPES(DL_LAUNCH)
-#undef DL_LAUNCH
-  return false;
-}
-
-bool launch_decode_layers_multi(const DLArgs* a, int world, hipStream_t s) {
-  if (world < 1 || world > DL_MULTI_MAX) return false;
-  DLMulti m{};
-  for (int r = 0; r < world; ++r) {
-    if (!dl_check(a[r]) || a[r].G != a[0].G || a[r].cq != a[0].cq || a[r].co != a[0].co || a[r].cg != a[0].cg ||
-        a[r].cd != a[0].cd)
-      return false;
-    m.a[r] = a[r];
-  }
-#define DL_LAUNCH(A, B, C, D_)                                                                      \
-  if (a[0].cq == A && a[0].co == B && a[0].cg == C && a[0].cd == D_) {                               \
-    auto k = decode_layers_multi_kernel<A, B, C, D_>;                                                \
-    int per_cu = 0;                                                                                  \
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, DL_NT, 0);                              \
-    if (per_cu < 1 || (long long)a[0].G * world > (long long)dl_cus() * per_cu) return false;        \
-    for (int r = 0; r < world; ++r)                                                                  \
-      (void)hipMemsetAsync(a[r].edge, 0, dl_edge_bytes(a[r]), s);                                   \
-    k<<<dim3(a[0].G, 1, world), DL_NT, 0, s>>>(m);                                                   \
-    return true;                                                                                     \
-  }
   DL_SHAPES(DL_LAUNCH)
 #undef DL_LAUNCH
   return false;

@@ -129,22 +129,30 @@ struct DLArgs {
   float* qkv_ws = nullptr;   // [KSq][M][Nq] fp32
   bf16* attn = nullptr;      // [M][Hq * 128]
   bf16* act = nullptr;       // [M][Fl]
-  unsigned* edge = nullptr;  // edge words (decode_layers.hip: edge_mode), zeroed by the launcher before every launch
+  unsigned* edge = nullptr;  // edge words + attention counters / partials (dl_edge_words); the launcher zeroes the
+                             // synchronisation words before every launch
   int edge_mode = 0;         // 0: sharded arrival counters [L * 5][8] x 128 B; 1: flag board [G] (rounded to 1 KB)
   int* fault = nullptr;      // device word: an edge wait gave up (sticky for the launch)
   int G = 0;                 // workgroups of this rank (one per CU)
-  int wnt = 1;               // non-temporal weight loads
-  int ctl_prefetch = 1;      // the control wave prefetches its weight pieces too (its edge poll then waits for them)
   XgmiArgs xp;               // world > 1: the fused all-reduce communicator (decode_epi.h granules)
   unsigned* xar_ctr = nullptr;
   unsigned long long* stamps = nullptr;  // diagnostics: [G][L][5][8] wall clock: edge passed, signalled, sub-phases
 };
+// The edge tensor holds, in order: the edge words (edge_mode 0: [L * 5][8] counters 128 B apart; 1: [G] flags
+// rounded to 256), one attention arrival counter per (sequence, kv head) 128 B apart (both zeroed by the launcher),
+// then the attention partials (fp32 o [M * Hkv][DL_APARTS][Hq / Hkv][128], m / l [M * Hkv][Hq / Hkv][DL_APARTS][2]).
+constexpr int DL_APARTS = 8;  // context partitions per (sequence, kv head): one wave each
+__host__ __device__ inline long long dl_edge_sync_words(int L, int M, int Hkv, int G, int edge_mode) {
+  return (edge_mode == 1 ? (long long)(G + 255) / 256 * 256 : (long long)L * 5 * 8 * 32) + (long long)M * Hkv * 32;
+}
+__host__ __device__ inline long long dl_edge_words(int L, int M, int Hq, int Hkv, int G, int edge_mode) {
+  return dl_edge_sync_words(L, M, Hkv, G, edge_mode) + (long long)M * Hq * DL_APARTS * 130;
+}
 // false: shapes outside the engine (the caller runs the per-layer launches); the launch itself is checked
 bool launch_decode_layers(const DLArgs& a, hipStream_t s);
-// test-only: up to 8 ranks of this process in ONE launch (grid z = rank), each with its own args
-constexpr int DL_MULTI_MAX = 8;
-bool launch_decode_layers_multi(const DLArgs* a, int world, hipStream_t s);
-int decode_layers_pieces_ok(int cq, int co, int cg, int cd);  // 1 if this shape class is built
+// 1 if this shape class (k pieces per wave of the QKV / O / gate_up / down units, QKV k-slabs, query heads per kv
+// head) is built
+int decode_layers_pieces_ok(int cq, int co, int cg, int cd, int ks, int gh);
 
 // test-only: every rank of this process in ONE launch (grid z = rank; co-residency checked)
 constexpr int XAR_MULTI_MAX = 8;

@@ -406,7 +406,7 @@ class TransformerLM:
         elif DECODE_ENGINE == "auto":
             return None
         bs = kv.block_size
-        if bs < 32 or bs & (bs - 1) or (self.hq // self.hkv) > 8 or (self.hq % self.hkv):
+        if bs < 32 or bs & (bs - 1) or (self.hq % self.hkv) or (self.hq // self.hkv) not in (4, 8):
             return None
         plan = self._engine_cache.get("plan")
         if plan is None:
@@ -419,7 +419,7 @@ class TransformerLM:
                 ksq *= 2
             pieces = (d // ksq // 256, self.hq * self.D // 256, d // 256, Fl // 256)
             ok = (d % (ksq * 256) == 0 and (self.hq * self.D) % 256 == 0 and Fl % 256 == 0
-                  and ops.decode_layers_built(*pieces))
+                  and ops.decode_layers_built(*pieces, ksq, self.hq // self.hkv))
             plan = (ksq, Fl, G) if ok else ()
             self._engine_cache["plan"] = plan
         if not plan:
@@ -448,8 +448,8 @@ class TransformerLM:
         nq = (self.hq + 2 * self.hkv) * self.D
         qkv_ws = self._buf("dl.qkv", (ksq * T * nq,), torch.float32)
         act = self._buf("act", (T, Fl), torch.bfloat16)
-        edge = self.ws.get("dl.edge", (max(L * 5 * 8 * 32, (G + 255) // 256 * 256),), torch.int32, self.device,
-                           zeros=True)
+        edge = self.ws.get("dl.edge", (ops.decode_layers_edge_words(L, T, self.hq, self.hkv, G),), torch.int32,
+                           self.device, zeros=True)
         fault = self.ws.get("dl.fault", (1,), torch.int32, self.device, zeros=True)
         return ops.decode_layers(self._engine_table(kv), self.hq, self.hkv, Fl, ksq, b.positions, b.slot_mapping,
                                  b.block_tables, b.ctx_lens, kv.block_size, self.cos_sin, self.scale, self.cfg.rms_eps,

@@ -238,10 +238,17 @@ def dg_argmax(x, W, ss_in, eps, temps, seeds, step, tile_keys, out_keys, out_ids
                                out_keys, out_ids, n_offset, logits)
 
 
-def decode_layers_built(cq: int, co: int, cg: int, cd: int) -> bool:
+def decode_layers_built(cq: int, co: int, cg: int, cd: int, ks: int, gh: int) -> bool:
     """Is the decode-step engine instantiated for this shape class (k pieces per wave of QKV / O / gate_up / down
-    units, csrc/kernels/decode_layers.hip DL_SHAPES)?"""
-    return native_available() and bool(_native.ops().decode_layers_pieces(int(cq), int(co), int(cg), int(cd)))
+    units, QKV k-slabs, query heads per kv head; csrc/kernels/decode_layers.hip DL_SHAPES)?"""
+    return native_available() and bool(_native.ops().decode_layers_pieces(int(cq), int(co), int(cg), int(cd), int(ks),
+                                                                           int(gh)))
+
+
+def decode_layers_edge_words(L: int, M: int, Hq: int, Hkv: int, G: int) -> int:
+    """int32 words of the engine's edge tensor: edge words, attention counters, attention partials
+    (csrc/kernels/launchers.h dl_edge_words)."""
+    return int(_native.ops().decode_layers_edge_words(int(L), int(M), int(Hq), int(Hkv), int(G)))
 
 
 def decode_layers(table, Hq, Hkv, Fl, KSq, positions, slots, block_tables, ctx_lens, BS, cos_sin, scale, eps, resid,
