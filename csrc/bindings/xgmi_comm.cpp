@@ -298,8 +298,12 @@ DLArgs dl_args(const Tensor& table, int64_t Hq, int64_t Hkv, int64_t Fl, int64_t
   a.KSq = (int)KSq;
   a.cq = (int)(d / KSq / 256);
   a.co = (int)(Hq * 128 / 256);
-  a.cg = (int)(d / 256);
-  a.cd = (int)(Fl / 256);
+  a.KSg = 1;  // gate_up units at most 4096 deep (16 pieces per wave): K = 8192 in two tile-major splits
+  while (d / a.KSg / 256 > 16 && d % (a.KSg * 2 * 256) == 0) a.KSg *= 2;
+  a.cg = (int)(d / a.KSg / 256);
+  a.KSd = 1;
+  while (Fl / a.KSd / 256 > 16 && Fl % (a.KSd * 2 * 256) == 0) a.KSd *= 2;
+  a.cd = (int)(Fl / a.KSd / 256);
   a.positions = positions.data_ptr<int>();
   a.slots = slots.data_ptr<int>();
   a.block_tables = block_tables.data_ptr<int>();

@@ -42,6 +42,8 @@
 #include "launchers.h"
 #include "xgmi_proto.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int DL_SW = 8;                 // streamer / attention waves
@@ -206,16 +208,31 @@ SYM_DEV f32x4 dl_mma(const Pack8 (&wa)[DL_MAXP], const Pack8 (&xa)[DL_MAXP]) {
 
 struct DLPhase {  // one GEMM phase of one layer
   const bf16* W;
-  int K;        // weight row length (the projection's full K)
-  int kunit;    // k range of one unit (K for whole-K units, K / KSq for the QKV slabs)
-  int nunits;   // units dealt round-robin over the G workgroups (u = b, b + G, ...)
-  int ksplit;   // QKV: units per tile (u -> tile u / ksplit, split u % ksplit)
+  int K;          // weight row length (the projection's full K)
+  int kunit;      // k range of one unit (K / ksplit)
+  int ntiles;     // 16-row output tiles
+  int ksplit;     // units per tile
+  int tile_major; // 0: the ntiles x ksplit units dealt round-robin (QKV slabs: each split its own fp32 slab);
+                  // 1: the TILES dealt round-robin, a tile's splits consecutive on one workgroup, summed by its control
+                  //    wave (gate_up at K = 8192: two 4096-deep units per tile)
   const bf16* x;  // activations [M][K]
 };
 
-SYM_DEV void dl_unit_of(const DLPhase& ph, int u, int& tile, int& k0) {
-  tile = u / ph.ksplit;
-  k0 = (u % ph.ksplit) * ph.kunit;
+SYM_DEV int dl_units(const DLPhase& ph, int b, int G) {  // units of workgroup b
+  if (ph.tile_major) return b < ph.ntiles ? ph.ksplit * ((ph.ntiles - b + G - 1) / G) : 0;
+  const int n = ph.ntiles * ph.ksplit;
+  return b < n ? (n - b + G - 1) / G : 0;
+}
+
+SYM_DEV void dl_unit_at(const DLPhase& ph, int b, int i, int G, int& tile, int& split) {
+  if (ph.tile_major) {
+    tile = b + (i / ph.ksplit) * G;
+    split = i % ph.ksplit;
+  } else {
+    const int u = b + i * G;
+    tile = u / ph.ksplit;
+    split = u % ph.ksplit;
+  }
 }
 
 // (every path issues the same loads -- zero-length descriptors where the workgroup has no unit -- so no older value
@@ -223,12 +240,18 @@ SYM_DEV void dl_unit_of(const DLPhase& ph, int u, int& tile, int& k0) {
 // It does at a signal (its poll then waits for its few pieces, issued before any later stream), not inside a
 // phase: there its epilogue drain would wait for the next phase's whole stream; it loads those pieces with the
 // activations after the edge instead (dl_gemm_phase `ctl_late`).
-template <int CNT>
+template <int CNT, bool LOAD = true>
 SYM_DEV void dl_prefetch(Pack8 (&wa)[DL_MAXP], const DLPhase& ph, int b, bool with_ctl, bool any = true) {
-  const bool on = any && b < ph.nunits && (with_ctl || (threadIdx.x >> 6) != DL_CTL);
-  int tile = 0, k0 = 0;
-  if (b < ph.nunits) dl_unit_of(ph, b, tile, k0);
-  dl_load_w<CNT>(wa, ph.W, ph.K, tile, k0, b, on);
+  if constexpr (!LOAD) {  // the control wave's instance inside a phase: defined, nothing issued
+#pragma unroll
+    for (int i = 0; i < CNT; ++i) wa[i].u = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  const bool have = dl_units(ph, b, gridDim.x) > 0;
+  const bool on = any && have && (with_ctl || (threadIdx.x >> 6) != DL_CTL);
+  int tile = 0, split = 0;
+  if (have) dl_unit_at(ph, b, 0, gridDim.x, tile, split);
+  dl_load_w<CNT>(wa, ph.W, ph.K, tile, split * ph.kunit, b, on);
 }
 
 // The control wave's view of a layer for the epilogues
@@ -244,22 +267,35 @@ struct DLEpi {
 // Residual epilogue of one O / down tile on the control wave: resid += all_reduce(v); xw = bf16(resid * w_next);
 // ss[m][tile] = sum over the tile's 16 columns of resid^2.  All rows of resid / xw / ss of this tile belong to
 // this workgroup in both phases; xw / ss are handed to the next phase (sc1).
-SYM_DEV void dl_epi_res(const DLArgs& a, f32x4 v, int tile, const bf16* __restrict__ w_next, unsigned ep) {
+struct DLResIn {  // the residual epilogue's loads, issued with the unit's activations (before any prefetch)
+  f32x4 r;
+  uint2 w;
+};
+SYM_DEV DLResIn dl_epi_res_load(const DLArgs& a, int tile, const bf16* __restrict__ w_next) {
+  const int lane = threadIdx.x & 63, r16 = lane & 15, h = lane >> 4;
+  const int m = r16, d = a.d, n = tile * 16 + 4 * h;
+  const rsrc_t rr = dl_rsrc(a.resid, m < a.M ? (long long)a.M * d * 4 : 0LL);  // rows >= M: zeros, no traffic
+  const rsrc_t rw = dl_rsrc(dl_uni(w_next), (long long)d * 2);
+  DLResIn in;
+  Pack8 t;
+  t.w = ld_sc1(rr, (m * d + n) * 4);
+  in.r = f32x4{__uint_as_float(t.w[0]), __uint_as_float(t.w[1]), __uint_as_float(t.w[2]), __uint_as_float(t.w[3])};
+  const unsigned long long wv = __builtin_bit_cast(unsigned long long,
+                                                   __builtin_amdgcn_raw_buffer_load_b64(rw, n * 2, 0, 0));
+  in.w = make_uint2((unsigned)wv, (unsigned)(wv >> 32));
+  return in;
+}
+
+SYM_DEV void dl_epi_res(const DLArgs& a, f32x4 v, int tile, DLResIn in, unsigned ep) {
   const int lane = threadIdx.x & 63, r16 = lane & 15, h = lane >> 4;
   const int m = r16, d = a.d, n = tile * 16 + 4 * h;
   const bool mok = m < a.M;
   const rsrc_t rr = dl_rsrc(a.resid, (long long)a.M * d * 4);
-  f32x4 r = {0.f, 0.f, 0.f, 0.f};
-  uint2 wraw = make_uint2(0, 0);
+  const f32x4 r = in.r;
+  const uint2 wraw = in.w;
   const long long goff = xar_goff(m, d, n);
   const bool xar = a.xp.world > 1;
-  if (mok) {
-    Pack8 t;
-    t.w = ld_sc1(rr, (m * d + n) * 4);
-    r = f32x4{__uint_as_float(t.w[0]), __uint_as_float(t.w[1]), __uint_as_float(t.w[2]), __uint_as_float(t.w[3])};
-    wraw = *reinterpret_cast<const uint2*>(w_next + n);
-    if (xar) xar_push(a.xp, v, goff, ep);
-  }
+  if (mok && xar) xar_push(a.xp, v, goff, ep);
   f32x4 s = v;
   if (xar) s = mok ? xar_collect(a.xp, v, goff, ep) : f32x4{0.f, 0.f, 0.f, 0.f};
   float sq = 0.f;
@@ -326,23 +362,33 @@ struct DLNoHook {
 // `after_x` runs right after the first unit's activation loads are issued: the NEXT phase's weight prefetch goes
 // there, behind this phase's operands (a wave's loads retire in order: weights issued before the activations --
 // at the previous signal -- made this phase's first MFMA wait for the next phase's whole stream).
-template <int CNT, int EPI, typename AfterX>
+// `tail` runs after the LAST unit's MFMAs instead of a next unit's weight loads: a next phase whose weights do not
+// fit beside this phase's registers streams from there, into this phase's own (then free) registers.
+template <int CNT, int EPI, typename AfterX, typename Tail>
 SYM_DEV void dl_gemm_phase(const DLArgs& a, const DLPhase& ph, const DLEpi& ep, Pack8 (&wa)[DL_MAXP],
                            Pack8 (&xa)[DL_MAXP], int b, f32x4 (*red)[DL_SW][64], const float* rn_s,
-                           unsigned* xep_s, int ev, bool ctl_late, AfterX after_x) {
+                           unsigned* xep_s, int ev, bool ctl_late, AfterX after_x, Tail tail) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const bool ctl = wid == DL_CTL;
   const rsrc_t rx = dl_rsrc(ph.x, (long long)a.M * ph.K * 2);
   int buf = 0;
   // (the first unit peeled: `after_x` defines the prefetch registers on every path, so no older value of them
   // stays live through the phase -- a conditional definition inside the loop kept both and spilled)
-  auto unit = [&](int u, int i, auto hook) {
-    int tile, k0;
-    dl_unit_of(ph, u, tile, k0);
+  const int nu = dl_units(ph, b, a.G);
+  f32x4 gacc = {0.f, 0.f, 0.f, 0.f};  // tile-major: the control wave's running sum over a tile's splits
+  auto unit = [&](int i, auto hook) {
+    int tile, split;
+    dl_unit_at(ph, b, i, a.G, tile, split);
+    const int k0 = split * ph.kunit;
+    DLResIn res_in{};
     {
       if (ctl && i == 0 && ctl_late) dl_load_w<CNT>(wa, ph.W, ph.K, tile, k0, b);
+      // (reloaded per unit even where the k range repeats: kept live across the epilogue they spilled; behind the
+      // rolled-in weights they cost no extra wait)
       dl_load_x<CNT>(xa, rx, ph.K, k0, a.M, b);
-      if constexpr (!std::is_same_v<AfterX, DLNoHook>) {
+      if constexpr (EPI == EP_RES)
+        if (ctl) res_in = dl_epi_res_load(a, tile, ep.w_next);
+      if constexpr (!std::is_same_v<decltype(hook), DLNoHook>) {
         // every wave's operand loads (the control wave's late weight pieces too) are queued before any wave's
         // prefetch: a CU's vector memory path returns in issue order, so a load queued behind the next phase's
         // stream waited for all of it (the control wave's -- whose partial every unit's epilogue needs -- ~3 us).
@@ -354,12 +400,17 @@ SYM_DEV void dl_gemm_phase(const DLArgs& a, const DLPhase& ph, const DLEpi& ep, 
       // with the MFMAs to save registers, one memory round trip per piece)
       __builtin_amdgcn_sched_barrier(0);
       const f32x4 acc = dl_mma<CNT>(wa, xa);
-      // the next unit's weights behind this unit's MFMAs (same registers: no renamed second copy)
+      // the next unit's weights behind this unit's MFMAs (same registers: no renamed second copy; rolling each
+      // piece in right behind its MFMA measured slower: 70B TP = 8 4.30 -> 4.55 ms)
       __builtin_amdgcn_sched_barrier(0);
-      if (u + a.G < ph.nunits) {
-        int t2, k2;
-        dl_unit_of(ph, u + a.G, t2, k2);
-        dl_load_w<CNT>(wa, ph.W, ph.K, t2, k2, b);
+      if (i + 1 < nu) {
+        int t2, s2;
+        dl_unit_at(ph, b, i + 1, a.G, t2, s2);
+        dl_load_w<CNT>(wa, ph.W, ph.K, t2, s2 * ph.kunit, b);
+      } else if (ctl) {
+        tail(std::false_type{});
+      } else {
+        tail(std::true_type{});
       }
       red[buf][wid][lane] = acc;
       if (i == 0 && ctl && a.stamps != nullptr) {  // operands landed: the store above needed the MFMA result (no
@@ -376,17 +427,25 @@ SYM_DEV void dl_gemm_phase(const DLArgs& a, const DLPhase& ph, const DLEpi& ep, 
       const int r16 = lane & 15, h = lane >> 4;
       const int m = r16;
       const bool mok = m < a.M;
+      bool last = true;
+      if (ph.tile_major && ph.ksplit > 1) {
+        v += gacc;
+        last = split == ph.ksplit - 1;
+        gacc = last ? f32x4{0.f, 0.f, 0.f, 0.f} : v;
+      }
       if constexpr (EPI == EP_SLAB) {
         if (mok) {
           const rsrc_t rs = dl_rsrc(ep.slab, (long long)ph.ksplit * a.M * ep.Nq * 4);
-          const int off = (((u % ph.ksplit) * a.M + m) * ep.Nq + tile * 16 + 4 * h) * 4;
+          const int off = ((split * a.M + m) * ep.Nq + tile * 16 + 4 * h) * 4;
           st_sc1(rs, off, u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
                                 __float_as_uint(v[3])});
         }
       } else if constexpr (EPI == EP_RES) {
-        const unsigned e = ++xep_s[i];
-        dl_epi_res(a, v, tile, ep.w_next, e);
-      } else {  // EP_SWI: rows 0-7 gate, 8-15 up (interleaved per tile), row scale of the deferred norm
+        if (last) {
+          const unsigned e = ++xep_s[ph.tile_major ? i / ph.ksplit : i];
+          dl_epi_res(a, v, tile, res_in, e);
+        }
+      } else if (last) {  // EP_SWI: rows 0-7 gate, 8-15 up (interleaved per tile), row scale of the deferred norm
         const float sc = mok ? rn_s[m] : 1.f;
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] *= sc;
@@ -403,11 +462,25 @@ SYM_DEV void dl_gemm_phase(const DLArgs& a, const DLPhase& ph, const DLEpi& ep, 
     if (i == 0) dl_stamp_ctl(a, ev, b, 4);
     buf ^= 1;
   };
-  if (b < ph.nunits)
-    unit(b, 0, after_x);
-  else
-    after_x();
-  for (int u = b + a.G, i = 1; u < ph.nunits; u += a.G, ++i) unit(u, i, DLNoHook{});
+  // the control wave runs an instance whose hook issues nothing: its epilogue loads and its drain must not queue
+  // behind the next phase's stream (the streamers' instance issues it)
+  const auto hook_load = [&] { after_x(std::true_type{}); };
+  const auto hook_none = [&] { after_x(std::false_type{}); };
+  if (nu > 0) {
+    if (ctl)
+      unit(0, hook_none);
+    else
+      unit(0, hook_load);
+  } else {
+    if (ctl) {
+      hook_none();
+      tail(std::false_type{});
+    } else {
+      hook_load();
+      tail(std::true_type{});
+    }
+  }
+  for (int i = 1; i < nu; ++i) unit(i, DLNoHook{});
 }
 
 // ---- attention ----------------------------------------------------------------------------------------------
@@ -466,9 +539,49 @@ SYM_DEV void dl_load_kv(const DLLayer& ly, int Hkv, int BS, int bk, int g, int t
 
 // KS: QKV k-slabs, GH: query heads per kv head (4 or 8) -- template parameters of the shape class, so every
 // register array below has its exact size
+// What a unit loads that does not depend on this step's QKV -- the row scale (the layer input's sum-of-squares
+// partials: published before the QKV phase began) and the RoPE cos / sin -- issued right after the QKV signal.
+struct DLAttnPre {
+  float4 co, si;
+  float rn;
+};
+
+SYM_DEV void dl_attn_pre(const DLArgs& a, int sg, const float* __restrict__ ss_in,
+                         int ss_tiles, DLAttnMeta mt, DLAttnPre& pre) {
+  const int lane = threadIdx.x & 63;
+  const int s = sg / a.Hkv;
+  const int r4 = (4 * lane) & 127;  // the lane's rows within a head (permuted order)
+  const int dh0 = 8 * (r4 >> 4) + (r4 & 7);
+  const rsrc_t rc = dl_rsrc(a.cos_sin + (long long)mt.pos * 128, 512);
+  Pack8 c, t;
+  c.w = __builtin_amdgcn_raw_buffer_load_b128(rc, dh0 * 4, 0, 0);
+  t.w = __builtin_amdgcn_raw_buffer_load_b128(rc, (64 + dh0) * 4, 0, 0);
+  float ssum = 0.f;
+  const rsrc_t rs = dl_rsrc(ss_in, (long long)a.M * ss_tiles * 4);
+  if ((ss_tiles & 3) == 0) {
+    Pack8 sq[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = 4 * lane + 256 * k;
+      sq[k].w = i < ss_tiles ? ld_sc1(rs, (s * ss_tiles + i) * 4) : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ssum += __uint_as_float(sq[k].w[e]);
+  } else {
+    for (int i = lane; i < ss_tiles; i += 64) ssum += ldf_sc1(ss_in + (long long)s * ss_tiles + i);
+  }
+  pre.co = make_float4(__uint_as_float(c.w[0]), __uint_as_float(c.w[1]), __uint_as_float(c.w[2]),
+                       __uint_as_float(c.w[3]));
+  pre.si = make_float4(__uint_as_float(t.w[0]), __uint_as_float(t.w[1]), __uint_as_float(t.w[2]),
+                       __uint_as_float(t.w[3]));
+  pre.rn = rsqrtf(wave_sum(ssum) * (1.f / (float)a.d) + a.eps);
+}
+
 template <int KS, int GH>
-SYM_DEV void dl_attn_wave(const DLArgs& a, const DLLayer& ly, int sg, int p, const float* __restrict__ ss_in,
-                          int ss_tiles, DLWaveLds& W, DLAttnMeta mt, int stamp_ev) {
+SYM_DEV void dl_attn_wave(const DLArgs& a, const DLLayer& ly, int sg, int p, DLWaveLds& W, DLAttnMeta mt,
+                          const DLAttnPre& pre, int stamp_ev) {
   const int lane = threadIdx.x & 63;
   constexpr int Gh = GH, R = (GH + 2) / 2;  // R: 256-value rounds of the unit's q / k / v rows
   const int Hq = a.Hq, Hkv = a.Hkv;
@@ -478,8 +591,8 @@ SYM_DEV void dl_attn_wave(const DLArgs& a, const DLLayer& ly, int sg, int p, con
   const int c = lane & 15, h = lane >> 4;
   const int bsh = __builtin_ctz(a.BS);
   const int* bt = a.block_tables + (long long)s * a.max_blocks;
-  // ---- every load of the unit at once: the first group's old K / V, the slab rows (4 consecutive values per lane
-  // per round), the lane's RoPE cos / sin (the same 4 dims in every round), the row scale's partials
+  // ---- after the edge: the first group's old K / V and the slab rows (4 consecutive values per lane per round),
+  // all at once (the old K / V held across the edge instead spilled)
   KVFrag f;
   int tok0 = 32 * p;
   if (tok0 < ctx_old) dl_load_kv(ly, Hkv, a.BS, mt.bk0, g, tok0, f);
@@ -496,30 +609,11 @@ SYM_DEV void dl_attn_wave(const DLArgs& a, const DLLayer& ly, int sg, int p, con
       for (int sp = 0; sp < KS; ++sp) q[j][sp].w = ld_sc1(rq, ((sp * a.M + s) * Nq + row) * 4);
     }
   }
-  const int r4 = (4 * lane) & 127;  // the lane's rows within a head (permuted order)
+  const int r4 = (4 * lane) & 127;
   const bool lo = (r4 & 15) < 8;
   const int dh0 = 8 * (r4 >> 4) + (r4 & 7);
-  const float4 co = *reinterpret_cast<const float4*>(a.cos_sin + (long long)mt.pos * 128 + dh0);
-  const float4 si = *reinterpret_cast<const float4*>(a.cos_sin + (long long)mt.pos * 128 + 64 + dh0);
-  float ssum = 0.f;
-  {
-    const rsrc_t rs = dl_rsrc(ss_in, (long long)a.M * ss_tiles * 4);
-    if ((ss_tiles & 3) == 0) {
-      Pack8 sq[2];
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int i = 4 * lane + 256 * k;
-        sq[k].w = i < ss_tiles ? ld_sc1(rs, (s * ss_tiles + i) * 4) : u32x4{0u, 0u, 0u, 0u};
-      }
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) ssum += __uint_as_float(sq[k].w[e]);
-    } else {
-      for (int i = lane; i < ss_tiles; i += 64) ssum += ldf_sc1(ss_in + (long long)s * ss_tiles + i);
-    }
-  }
-  const float rn = rsqrtf(wave_sum(ssum) * (1.f / (float)a.d) + a.eps);
+  const float4 co = pre.co, si = pre.si;
+  const float rn = pre.rn;
   if (stamp_ev >= 0 && a.stamps != nullptr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) a.stamps[((long long)blockIdx.x * a.L * DL_PH + stamp_ev) * 8 + 2] = wall_clock64();
@@ -700,76 +794,93 @@ SYM_DEV void dl_body(const DLArgs& a, int b) {
     for (int i = lane; i < nmine; i += 64) xep_s[i] = a.xar_ctr[b + i * a.G];
   __syncthreads();
 
-  // weight registers: wa = QKV / O units, wb = gate_up (prefetched at the attention signal, across O), wc = down
-  // (prefetched at the O signal, across gate_up): each phase's stream starts as early as its registers allow
+  // Weight registers.  A phase's weights stream as early as the registers allow: "early" into a register set of
+  // their own during the previous phase (right behind its first unit's activations: TP = 8, whose units are a whole
+  // phase's share), otherwise from the previous phase's last MFMAs on, into that phase's (then free) set ("tail").
+  //   O: wa (from the attention signal); gate_up: wb early / wa; down: wc early / gate_up's; the next layer's QKV:
+  //   wa early / down's.
   Pack8 wa[DL_MAXP], wb[DL_MAXP], wc[DL_MAXP], xa[DL_MAXP];
-  // down's weights stream during gate_up when both shares fit the registers beside gate_up's activations (TP = 8:
-  // 16 + 7 pieces per wave); otherwise (TP = 4: 16 + 14 spilled ~190 VGPRs) from the gate_up signal on
-  constexpr bool kEarlyDown = CG + CD <= 24;
-  constexpr bool kEarlyQkv = CD + CQ <= 16;  // the next layer's QKV weights during down, likewise
+  constexpr bool kEarlyGu = CO + CG <= 24;    // TP = 8 / 4: O 2-4 pieces beside gate_up's 16
+  constexpr bool kEarlyDown = CG + CD <= 24;  // TP = 8: 16 + 7 (TP = 4's 16 + 14 spilled ~190 VGPRs)
+  constexpr bool kEarlyQkv = CD + CQ <= 16 && (kEarlyDown || kEarlyGu);  // (down's set must not be wa)
+  Pack8(&w_gu)[DL_MAXP] = kEarlyGu ? wb : wa;
+  Pack8(&w_dn)[DL_MAXP] = kEarlyDown ? wc : w_gu;
+  Pack8(&w_qkv)[DL_MAXP] = kEarlyQkv ? wa : w_dn;
   auto phase_of = [&](int l, int p) -> DLPhase {
     const DLLayer& ly = lay_s[l];
-    if (p == DL_QKV) return DLPhase{ly.wqkv, d, d / a.KSq, (Nq / 16) * a.KSq, a.KSq, a.xw};
-    if (p == DL_O) return DLPhase{ly.wo, a.Hq * 128, a.Hq * 128, ntile_d, 1, a.attn};
-    if (p == DL_GU) return DLPhase{ly.wgu, d, d, (2 * a.Fl) / 16, 1, a.xw};
-    return DLPhase{ly.wdown, a.Fl, a.Fl, ntile_d, 1, a.act};
+    if (p == DL_QKV) return DLPhase{ly.wqkv, d, d / a.KSq, Nq / 16, a.KSq, 0, a.xw};
+    if (p == DL_O) return DLPhase{ly.wo, a.Hq * 128, a.Hq * 128, ntile_d, 1, 0, a.attn};
+    if (p == DL_GU) return DLPhase{ly.wgu, d, d / a.KSg, (2 * a.Fl) / 16, a.KSg, 1, a.xw};
+    return DLPhase{ly.wdown, a.Fl, a.Fl / a.KSd, ntile_d, a.KSd, 1, a.act};
   };
-  dl_prefetch<CQ>(wa, phase_of(0, DL_QKV), b, true);
+  const auto none = [](auto) {};
+  dl_prefetch<CQ>(w_qkv, phase_of(0, DL_QKV), b, true);
   for (int l = 0; l < a.L; ++l) {
     const DLLayer& ly = lay_s[l];
     const int ev0 = l * DL_PH;
     // ---- QKV: split-K slabs (the row scale waits for the attention phase)
     if (l > 0) dl_wait(a, ev0 - DL_PH + DL_DOWN);
     dl_stamp(a, ev0 + DL_QKV, b, 0);
-    dl_gemm_phase<CQ, EP_SLAB>(a, phase_of(l, DL_QKV), DLEpi{EP_SLAB, a.qkv_ws, Nq, nullptr, nullptr, Nq}, wa, xa, b,
-                               red, rn_s, xep_s, ev0 + DL_QKV, l > 0 && kEarlyQkv, DLNoHook{});
+    dl_gemm_phase<CQ, EP_SLAB>(a, phase_of(l, DL_QKV), DLEpi{EP_SLAB, a.qkv_ws, Nq, nullptr, nullptr, Nq}, w_qkv, xa,
+                               b, red, rn_s, xep_s, ev0 + DL_QKV, l > 0, none, none);
     dl_signal(a, ev0 + DL_QKV, b, ctl);
     // ---- attention: wave-level units (sequence x kv head x partition), dealt over the workgroups first; the first
     // unit's metadata read before the edge
     {
       const int nv = a.M * a.Hkv * DL_APARTS;
       const int v0 = b + a.G * wid;
-      DLAttnMeta mt{0, -1, 0, -1};
-      if (v0 < nv) mt = dl_attn_meta(a, v0 / DL_APARTS / a.Hkv, v0 % DL_APARTS);
-      dl_wait(a, ev0 + DL_QKV);
-      dl_stamp(a, ev0 + DL_ATTN, b, 0);
       const float* ss_in = l == 0 ? a.ss0 : a.ss;
       const int ss_tiles = l == 0 ? a.ss0_tiles : ntile_d;
+      DLAttnMeta mt{0, -1, 0, -1};
+      DLAttnPre pre;
+      if (v0 < nv) {
+        mt = dl_attn_meta(a, v0 / DL_APARTS / a.Hkv, v0 % DL_APARTS);
+        dl_attn_pre(a, v0 / DL_APARTS, ss_in, ss_tiles, mt, pre);
+      }
+      dl_wait(a, ev0 + DL_QKV);
+      dl_stamp(a, ev0 + DL_ATTN, b, 0);
       for (int v = v0; v < nv; v += a.G * DL_SW) {
-        if (v != v0) mt = dl_attn_meta(a, v / DL_APARTS / a.Hkv, v % DL_APARTS);
-        dl_attn_wave<KS, GH>(a, ly, v / DL_APARTS, v % DL_APARTS, ss_in, ss_tiles, lds_wave[wid], mt,
-                             v == b ? ev0 + DL_ATTN : -1);
+        if (v != v0) {
+          mt = dl_attn_meta(a, v / DL_APARTS / a.Hkv, v % DL_APARTS);
+          dl_attn_pre(a, v / DL_APARTS, ss_in, ss_tiles, mt, pre);
+        }
+        dl_attn_wave<KS, GH>(a, ly, v / DL_APARTS, v % DL_APARTS, lds_wave[wid], mt, pre, v == b ? ev0 + DL_ATTN : -1);
       }
     }
     dl_signal(a, ev0 + DL_ATTN, b);
-    dl_prefetch<CO>(wa, phase_of(l, DL_O), b, true);  // small (O: 16 KB per CU), before any later stream
-    // ---- O (+ all-reduce, residual, ln2 prep); gate_up's weights stream from here on
+    dl_prefetch<CO>(wa, phase_of(l, DL_O), b, true);  // before any later stream
+    // ---- O (+ all-reduce, residual, ln2 prep)
     dl_wait(a, ev0 + DL_ATTN);
     dl_stamp(a, ev0 + DL_O, b, 0);
-    dl_gemm_phase<CO, EP_RES>(a, phase_of(l, DL_O), DLEpi{EP_RES, nullptr, 0, ly.ln2, nullptr, d}, wa, xa, b, red,
-                              rn_s, xep_s, ev0 + DL_O, false,
-                              [&] { dl_prefetch<CG>(wb, phase_of(l, DL_GU), b, false); });
+    dl_gemm_phase<CO, EP_RES>(
+        a, phase_of(l, DL_O), DLEpi{EP_RES, nullptr, 0, ly.ln2, nullptr, d}, wa, xa, b, red, rn_s, xep_s, ev0 + DL_O,
+        false, [&](auto load) { if constexpr (kEarlyGu) dl_prefetch<CG, load>(wb, phase_of(l, DL_GU), b, false); },
+        [&](auto load) { if constexpr (!kEarlyGu) dl_prefetch<CG, load>(wa, phase_of(l, DL_GU), b, false); });
     dl_signal(a, ev0 + DL_O, b, ctl);
     // ---- gate_up (+ row scale, SwiGLU)
     dl_wait(a, ev0 + DL_O);
     dl_stamp(a, ev0 + DL_GU, b, 0);
     dl_row_scales(a, a.ss, ntile_d, rn_s);  // published by the first unit's barrier, before any epilogue reads it
-    dl_gemm_phase<CG, EP_SWI>(a, phase_of(l, DL_GU), DLEpi{EP_SWI, nullptr, 0, nullptr, a.act, 2 * a.Fl}, wb, xa, b,
-                              red, rn_s, xep_s, ev0 + DL_GU, true, [&] {
-                                if constexpr (kEarlyDown) dl_prefetch<CD>(wc, phase_of(l, DL_DOWN), b, false);
-                              });
+    dl_gemm_phase<CG, EP_SWI>(
+        a, phase_of(l, DL_GU), DLEpi{EP_SWI, nullptr, 0, nullptr, a.act, 2 * a.Fl}, w_gu, xa, b, red, rn_s, xep_s,
+        ev0 + DL_GU, true,
+        [&](auto load) { if constexpr (kEarlyDown) dl_prefetch<CD, load>(wc, phase_of(l, DL_DOWN), b, false); },
+        [&](auto load) { if constexpr (!kEarlyDown) dl_prefetch<CD, load>(w_gu, phase_of(l, DL_DOWN), b, false); });
     dl_signal(a, ev0 + DL_GU, b, ctl);
-    if constexpr (!kEarlyDown) dl_prefetch<CD>(wc, phase_of(l, DL_DOWN), b, true);
     // ---- down (+ all-reduce, residual, next-norm prep)
     dl_wait(a, ev0 + DL_GU);
     dl_stamp(a, ev0 + DL_DOWN, b, 0);
     const int ln = l + 1 < a.L ? l + 1 : l;  // (the last layer issues zero-length loads: the same instructions)
-    dl_gemm_phase<CD, EP_RES>(a, phase_of(l, DL_DOWN), DLEpi{EP_RES, nullptr, 0, ly.lnn, nullptr, d}, wc, xa, b, red,
-                              rn_s, xep_s, ev0 + DL_DOWN, kEarlyDown, [&] {
-                                if constexpr (kEarlyQkv) dl_prefetch<CQ>(wa, phase_of(ln, DL_QKV), b, false, ln != l);
-                              });
+    dl_gemm_phase<CD, EP_RES>(
+        a, phase_of(l, DL_DOWN), DLEpi{EP_RES, nullptr, 0, ly.lnn, nullptr, d}, w_dn, xa, b, red, rn_s, xep_s,
+        ev0 + DL_DOWN, true,
+        [&](auto load) {
+          if constexpr (kEarlyQkv) dl_prefetch<CQ, load>(wa, phase_of(ln, DL_QKV), b, false, ln != l);
+        },
+        [&](auto load) {
+          if constexpr (!kEarlyQkv) dl_prefetch<CQ, load>(w_dn, phase_of(ln, DL_QKV), b, false, ln != l);
+        });
     dl_signal(a, ev0 + DL_DOWN, b, ctl);
-    if constexpr (!kEarlyQkv) dl_prefetch<CQ>(wa, phase_of(ln, DL_QKV), b, true, ln != l);
   }
   if (ctl && a.xp.world > 1)
     for (int i = lane; i < nmine; i += 64) a.xar_ctr[b + i * a.G] = xep_s[i];
@@ -790,16 +901,22 @@ __global__ __launch_bounds__(DL_NT) void decode_layers_kernel(DLOne m) {
 // gate_up (K = d), down (K = F / tp)):
 //   Llama-3-8B TP = 8: QKV 1024 (KSq 4), O 512, gate_up 4096, down 1792   -> (4, 2, 16, 7)
 //   Llama-3-8B TP = 4: QKV 2048 (KSq 2), O 1024, gate_up 4096, down 3584  -> (8, 4, 16, 14)
-//   Llama-3-8B TP = 2: QKV 2048 (KSq 2), O 2048, gate_up 4096, down 7168  -> (not built: down K > 4096)
 //   small-llama TP = 1 / 2 (tests): QKV 512 (KSq 2) / 256 (KSq 4), O 1024 / 512, gate_up 1024, down 3584 / 1792;
 //   its TP = 2 one-GPU rehearsal (128 workgroups per rank): QKV 512 (KSq 2)
 // (+ the QKV k-slabs and the query heads per kv head: 4 for both models)
-#define DL_SHAPES(X) X(4, 2, 16, 7, 4, 4) X(8, 4, 16, 14, 2, 4) X(2, 4, 4, 14, 2, 4) X(1, 2, 4, 7, 4, 4) X(2, 2, 4, 7, 2, 4)
+//   Llama-3-70B TP = 8: QKV 4096 (KSq 2), O 1024, gate_up 2 x 4096 (KSg 2, tile-major), down 3584 -> (16, 4, 16, 14)
+//   Llama-3-8B TP = 1: QKV 2048 (KSq 2), O 4096, gate_up 4096, down 4 x 3584 (KSd 4, tile-major) -> (8, 16, 16, 14)
+//   Llama-3-8B TP = 2: QKV 1024 (KSq 4), O 2048, gate_up 4096, down 2 x 3584 (KSd 2)              -> (4, 8, 16, 14)
+#define DL_SHAPES(X)                                                                                        \
+  X(4, 2, 16, 7, 4, 4) X(8, 4, 16, 14, 2, 4) X(2, 4, 4, 14, 2, 4) X(1, 2, 4, 7, 4, 4) X(2, 2, 4, 7, 2, 4) \
+  X(16, 4, 16, 14, 2, 8) X(8, 16, 16, 14, 2, 4) X(4, 8, 16, 14, 4, 4)
 
 bool dl_check(const DLArgs& a) {
   return a.M >= 1 && a.M <= 16 && a.L >= 1 && a.Hkv >= 1 && a.Hq % a.Hkv == 0 && (a.Hq / a.Hkv == 4 || a.Hq / a.Hkv == 8) &&
          a.d % 256 == 0 && a.Fl % 256 == 0 && a.BS >= 32 && (a.BS & (a.BS - 1)) == 0 && a.G >= 1 &&
-         (a.d / 16 + a.G - 1) / a.G <= DL_MAXT && a.L <= DL_MAXL && a.KSq >= 1 && a.KSq <= DL_MAXKS && a.d % (a.KSq * 256) == 0;
+         (a.d / 16 + a.G - 1) / a.G <= DL_MAXT && a.L <= DL_MAXL && a.KSq >= 1 && a.KSq <= DL_MAXKS &&
+         a.d % (a.KSq * 256) == 0 && a.KSg >= 1 && a.d % (a.KSg * 256) == 0 && a.KSd >= 1 &&
+         a.Fl % (a.KSd * 256) == 0;
 }
 
 // bytes of edge words one launch uses (zeroed before it)

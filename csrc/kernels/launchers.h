@@ -113,6 +113,8 @@ struct DLArgs {
   int L = 0;
   int M = 0, d = 0, Hq = 0, Hkv = 0, Fl = 0;  // rows (<= 16), hidden, local q / kv heads, local intermediate
   int KSq = 1;                                 // k-splits of the QKV projection (fp32 slabs, summed by attention)
+  int KSg = 1;                                 // k-splits of gate_up (consecutive units of one workgroup)
+  int KSd = 1;                                 // k-splits of down (likewise)
   int cq = 0, co = 0, cg = 0, cd = 0;          // 32-deep k pieces per streamer wave per unit, per projection
   const int* positions = nullptr;
   const int* slots = nullptr;

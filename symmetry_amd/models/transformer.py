@@ -414,10 +414,18 @@ class TransformerLM:
             Fl = self.w.layer(0, "w_gu").shape[0] // 2
             G = ENGINE_GRID or torch.cuda.get_device_properties(self.device).multi_processor_count
             ntq = (self.hq + 2 * self.hkv) * self.D // 16
-            ksq = 1
-            while ntq * ksq * 2 <= G and d % (ksq * 2 * 256) == 0:
-                ksq *= 2
-            pieces = (d // ksq // 256, self.hq * self.D // 256, d // 256, Fl // 256)
+            # QKV k-slabs: the fewest weight bytes on the busiest workgroup (units dealt round-robin), then the
+            # fewest slabs (TP = 8: 48 tiles -> 4 slabs, every unit 1024 deep; TP = 1: 384 tiles -> 2 slabs, 3
+            # units per workgroup instead of 2 whole-K ones on half of them)
+            cands = [k for k in (1, 2, 4) if d % (k * 256) == 0 and d // k // 256 <= 16]
+            ksq = min(cands, key=lambda k: (-(-ntq * k // G)) / k)
+            ksg = 1  # gate_up / down k-splits (csrc/bindings/xgmi_comm.cpp dl_args: units at most 4096 deep)
+            while d // ksg // 256 > 16 and d % (ksg * 2 * 256) == 0:
+                ksg *= 2
+            ksd = 1
+            while Fl // ksd // 256 > 16 and Fl % (ksd * 2 * 256) == 0:
+                ksd *= 2
+            pieces = (d // ksq // 256, self.hq * self.D // 256, d // ksg // 256, Fl // ksd // 256)
             ok = (d % (ksq * 256) == 0 and (self.hq * self.D) % 256 == 0 and Fl % 256 == 0
                   and ops.decode_layers_built(*pieces, ksq, self.hq // self.hkv))
             plan = (ksq, Fl, G) if ok else ()

@@ -66,3 +66,43 @@ def test_engine_tokens_match_per_layer_launches(gpu, monkeypatch):
                 top = lg[len(p) - 1 + j].topk(2).values
                 assert float(top[0] - top[1]) < 0.05, (j, a, b)
                 break
+
+
+def test_engine_70b_tp8_shard_matches_per_layer_launches(gpu, monkeypatch):
+    """Llama-3-70B's TP = 8 rank-0 shard (2 layers; shape class (16, 4, 16, 14): QKV 2 k-slabs of 4096, gate_up
+    K = 8192 as two tile-major 4096-deep units per tile, O / down two output tiles per workgroup, 8 query heads per
+    kv head) on a world-1 xGMI communicator (bench/tp_shard.py LocalXgmi): the first engine decode step picks the
+    same greedy token as the per-layer launches for (nearly) every sequence (a shard's logits are not a model's,
+    so no oracle; a broken engine agrees by chance only)."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench"))
+    from tp_shard import LocalXgmi
+
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+    from symmetry_amd.models import transformer as tr
+    from symmetry_amd.models.config import resolve
+
+    mc = resolve("llama3:70b").replace(num_layers=2)
+    prompts = [[(97 * i + 13 * k) % 100000 + 300 for k in range(40 + 7 * i)] for i in range(8)]
+    toks, steps = {}, {}
+    for mode in ("0", "1"):
+        monkeypatch.setattr(tr, "DECODE_ENGINE", mode)
+        dev = torch.device("cuda:0")
+        eng = LLMEngine(EngineConfig(model="llama3:70b", model_config=mc, device="cuda:0", max_num_seqs=8,
+                                     max_model_len=512, num_kv_blocks=64, tp_size=8, tp_rank=0, weight_init="shard",
+                                     use_graphs=False, seed=3), tp_comm=LocalXgmi(dev, 8))
+        seqs = [eng.add_request(f"s{i}", p, SamplingParams(max_tokens=3, ignore_eos=True))
+                for i, p in enumerate(prompts)]
+        while eng.has_unfinished():
+            eng.step()
+        toks[mode] = [s.output_ids for s in seqs]
+        steps[mode] = eng.model.engine_steps
+        del eng
+        torch.cuda.empty_cache()
+    assert steps["0"] == 0 and steps["1"] > 0, steps
+    assert all(a[0] == b[0] for a, b in zip(toks["0"], toks["1"])), toks  # the prefill token: no engine
+    same = sum(a[1] == b[1] for a, b in zip(toks["0"], toks["1"]))
+    assert same >= 7, (same, toks)
