@@ -1,12 +1,14 @@
 #!/bin/bash
-# rocprofv3 kernel trace of one TP rank's decode shard on one GPU (bench/tp_shard.py) -> per-kernel CSV.
-#   TP=8 TAG=tp8 bash tools/prof_tp_shard.sh
+# rocprofv3 kernel trace of one TP-shard decode run (bench/tp_shard.py) with the per-layer launches and with the
+# decode-step engine; per-kernel stats CSVs under gpurun_out/prof_tp_shard_e{0,1}/.
 set -o pipefail
-tag=${TAG:-tp${TP:-8}}
-root=$(pwd)
-mkdir -p "$root/gpurun_out"
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format rocpd -d /tmp/prof_$tag -o run -- \
-  python3 "$root/bench/tp_shard.py" --tp ${TP:-8} --clients ${CLIENTS:-10} --model ${MODEL:-llama3:8b} > "$root/gpurun_out/prof_$tag.log" 2>&1 || exit $?
-db=$(ls /tmp/prof_$tag/*/*.db /tmp/prof_$tag/*.db 2>/dev/null | head -1)
-cd "$root" && python3 tools/prof_summary.py "$db" "gpurun_out/prof_$tag.csv" --last-ms ${LAST_MS:-30} > "gpurun_out/prof_$tag.txt"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+MODEL=${1:-llama3:8b}
+TP=${2:-8}
+C=${3:-10}
+for e in 0 1; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_tp_shard_e$e -o run -- \
+    python3 bench/tp_shard.py --model $MODEL --tp $TP --clients $C --engine $e --steps 32 --warmup 4 \
+    > gpurun_out/prof_tp_shard_e$e.log 2>&1 || exit $?
+  grep '^{' gpurun_out/prof_tp_shard_e$e.log | cut -c1-200
+done
