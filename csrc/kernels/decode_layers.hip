@@ -206,6 +206,58 @@ SYM_DEV f32x4 dl_mma(const Pack8 (&wa)[DL_MAXP], const Pack8 (&xa)[DL_MAXP]) {
   return acc;
 }
 
+// One unit's MFMA chain with the NEXT unit's weights rolled in behind it: piece j's register is reloaded with the
+// next unit's piece j right after its MFMA read it, so a workgroup walking several units keeps about a unit of
+// pieces in flight instead of draining the pipe at every unit boundary.  Only with the activations resident
+// (loaded once per phase): a per-unit reload queued behind the rolled weights would wait for all of them (that
+// form measured slower).  No next unit: a zero-length descriptor (the same instructions, no traffic).
+template <int CNT>
+SYM_DEV f32x4 dl_mma_roll(Pack8 (&wa)[DL_MAXP], const Pack8 (&xa)[DL_MAXP], const bf16* W_next, int rot, bool roll) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const rsrc_t rw = dl_rsrc(dl_uni(W_next), roll ? 0x7fffffffLL : 0LL);
+  const int off = (w * 512 + lane * 8) * 2;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < CNT; ++j) {
+    acc = mfma16(wa[j].v, xa[j].v, acc);
+    const int i = CNT > 1 ? (j + rot) % CNT : 0;
+    wa[j].w = __builtin_amdgcn_raw_buffer_load_b128(rw, off, __builtin_amdgcn_readfirstlane(i * DL_SW * 1024), 2);
+  }
+  return acc;
+}
+
+// Activations resident in LDS for a rolled phase: rows m < M of x[:, k0 : k0 + kunit], row stride kunit + 8
+// bf16 (16 B of padding: the 16 rows of a fragment read fall on different banks).  DL_XS: 16 rows x 4104.
+constexpr int DL_XPAD = 8;
+constexpr int DL_XS = 16 * (4096 + DL_XPAD);
+
+// stage x[:M, k0 : k0 + kunit] into LDS by LDS-DMA (sc1: hand-off data), no registers: 1 KB per wave instruction
+// (64 lanes x 16 B of one row), instructions dealt over the waves; kunit % 512 == 0.  The caller waits
+// (vmcnt(0)) and barriers before the rows are read.
+typedef __attribute__((address_space(3))) void dl_lds_t;
+SYM_DEV void dl_xs_dma(const DLArgs& a, const bf16* x, int K, int k0, int kunit, bf16* xs) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ipr = kunit / 512;  // instructions per row
+  const rsrc_t rx = dl_rsrc(x, (long long)a.M * K * 2);
+  for (int q = w; q < a.M * ipr; q += DL_SW) {  // wave-uniform
+    const int row = q / ipr, part = q - row * ipr;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (dl_lds_t*)(xs + row * (kunit + DL_XPAD) + part * 512), 16,
+                                             ((row * K + k0) * 2 + part * 1024) + lane * 16, 0, 0, 16);
+  }
+}
+// the wave's fragments of one unit from LDS (piece order as dl_load_x)
+template <int CNT>
+SYM_DEV void dl_xs_frags(Pack8 (&xa)[DL_MAXP], const bf16* xs, int kunit, int rot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r16 = lane & 15, h = lane >> 4;
+  const bf16* p = xs + r16 * (kunit + DL_XPAD) + w * 32 + 8 * h;
+#pragma unroll
+  for (int j = 0; j < CNT; ++j) {
+    const int i = CNT > 1 ? (j + rot) % CNT : 0;
+    xa[j].u = *reinterpret_cast<const uint4*>(p + i * DL_SW * 32);
+  }
+}
+
 struct DLPhase {  // one GEMM phase of one layer
   const bf16* W;
   int K;          // weight row length (the projection's full K)
@@ -364,10 +416,10 @@ struct DLNoHook {
 // at the previous signal -- made this phase's first MFMA wait for the next phase's whole stream).
 // `tail` runs after the LAST unit's MFMAs instead of a next unit's weight loads: a next phase whose weights do not
 // fit beside this phase's registers streams from there, into this phase's own (then free) registers.
-template <int CNT, int EPI, typename AfterX, typename Tail>
+template <int CNT, int EPI, bool ROLL = false, typename AfterX, typename Tail>
 SYM_DEV void dl_gemm_phase(const DLArgs& a, const DLPhase& ph, const DLEpi& ep, Pack8 (&wa)[DL_MAXP],
                            Pack8 (&xa)[DL_MAXP], int b, f32x4 (*red)[DL_SW][64], const float* rn_s,
-                           unsigned* xep_s, int ev, bool ctl_late, AfterX after_x, Tail tail) {
+                           unsigned* xep_s, int ev, bool ctl_late, AfterX after_x, Tail tail, bf16* xs = nullptr) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const bool ctl = wid == DL_CTL;
   const rsrc_t rx = dl_rsrc(ph.x, (long long)a.M * ph.K * 2);
@@ -383,27 +435,46 @@ SYM_DEV void dl_gemm_phase(const DLArgs& a, const DLPhase& ph, const DLEpi& ep, 
     DLResIn res_in{};
     {
       if (ctl && i == 0 && ctl_late) dl_load_w<CNT>(wa, ph.W, ph.K, tile, k0, b);
-      // (reloaded per unit even where the k range repeats: kept live across the epilogue they spilled; behind the
-      // rolled-in weights they cost no extra wait)
-      dl_load_x<CNT>(xa, rx, ph.K, k0, a.M, b);
+      // ROLL (round-robin phases: every unit of the workgroup has the same k range): the activations are staged
+      // into LDS once, by the first unit, and every unit reads its fragments there
+      constexpr bool first = !std::is_same_v<decltype(hook), DLNoHook>;
+      if constexpr (ROLL) {
+        if constexpr (first) dl_xs_dma(a, ph.x, ph.K, k0, ph.kunit, xs);
+      } else {
+        dl_load_x<CNT>(xa, rx, ph.K, k0, a.M, b);
+      }
       if constexpr (EPI == EP_RES)
         if (ctl) res_in = dl_epi_res_load(a, tile, ep.w_next);
-      if constexpr (!std::is_same_v<decltype(hook), DLNoHook>) {
+      if constexpr (first) {
         // every wave's operand loads (the control wave's late weight pieces too) are queued before any wave's
         // prefetch: a CU's vector memory path returns in issue order, so a load queued behind the next phase's
         // stream waited for all of it (the control wave's -- whose partial every unit's epilogue needs -- ~3 us).
-        // A bare s_barrier: __syncthreads' fence would wait for the loads themselves.
-        __builtin_amdgcn_s_barrier();
+        // A bare s_barrier: __syncthreads' fence would wait for the loads themselves.  Staged activations: every
+        // wave's DMA landed, then the barrier publishes the rows (MI355X_MICROARCH.md, LDS-DMA).
+        if constexpr (ROLL) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+        } else {
+          __builtin_amdgcn_s_barrier();
+        }
         hook();
       }
+      if constexpr (ROLL) dl_xs_frags<CNT>(xa, xs, ph.kunit, b);
       // every activation load issued before the first MFMA waits (left to itself the scheduler interleaved them
       // with the MFMAs to save registers, one memory round trip per piece)
       __builtin_amdgcn_sched_barrier(0);
-      const f32x4 acc = dl_mma<CNT>(wa, xa);
-      // the next unit's weights behind this unit's MFMAs (same registers: no renamed second copy; rolling each
-      // piece in right behind its MFMA measured slower: 70B TP = 8 4.30 -> 4.55 ms)
+      f32x4 acc;
+      if constexpr (ROLL) {
+        int t2 = 0, s2 = 0;
+        if (i + 1 < nu) dl_unit_at(ph, b, i + 1, a.G, t2, s2);
+        acc = dl_mma_roll<CNT>(wa, xa, ph.W + ((long long)t2 * (ph.K / 32) + s2 * ph.kunit / 32) * 512, b, i + 1 < nu);
+      } else {
+        acc = dl_mma<CNT>(wa, xa);
+      }
+      // the next unit's weights behind this unit's MFMAs (same registers: no renamed second copy)
       __builtin_amdgcn_sched_barrier(0);
-      if (i + 1 < nu) {
+      if (ROLL && i + 1 < nu) {
+      } else if (i + 1 < nu) {
         int t2, s2;
         dl_unit_at(ph, b, i + 1, a.G, t2, s2);
         dl_load_w<CNT>(wa, ph.W, ph.K, t2, s2 * ph.kunit, b);
@@ -776,7 +847,11 @@ SYM_DEV void dl_body(const DLArgs& a, int b) {
   __shared__ f32x4 red[2][DL_SW][64];
   __shared__ float rn_s[16];
   __shared__ unsigned xep_s[DL_MAXT];
-  __shared__ DLWaveLds lds_wave[DL_SW];
+  // the attention phase's per-wave rows and a rolled GEMM phase's resident activations share the space
+  __shared__ __attribute__((aligned(16))) char lds_u[DL_XS * 2 > (int)sizeof(DLWaveLds) * DL_SW ? DL_XS * 2
+                                                                                               : sizeof(DLWaveLds) * DL_SW];
+  DLWaveLds* lds_wave = reinterpret_cast<DLWaveLds*>(lds_u);
+  bf16* xs = reinterpret_cast<bf16*>(lds_u);
   __shared__ DLLayer lay_s[DL_MAXL];  // the layer table (LDS reads: no vector-memory wait behind streaming loads)
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool ctl = wid == DL_CTL;
@@ -803,6 +878,12 @@ SYM_DEV void dl_body(const DLArgs& a, int b) {
   constexpr bool kEarlyGu = CO + CG <= 24;    // TP = 8 / 4: O 2-4 pieces beside gate_up's 16
   constexpr bool kEarlyDown = CG + CD <= 24;  // TP = 8: 16 + 7 (TP = 4's 16 + 14 spilled ~190 VGPRs)
   constexpr bool kEarlyQkv = CD + CQ <= 16 && (kEarlyDown || kEarlyGu);  // (down's set must not be wa)
+  // Phases whose workgroups walk several units of one k range run with their activations resident in LDS and the
+  // next unit's weights rolled in behind the MFMAs (dl_mma_roll): 8B TP = 1 QKV (3 units) and gate_up (7), 8B
+  // TP = 4 gate_up (2), 70B TP = 8 O and down (2 each).  Not 70B gate_up, whose tile-major units change k range;
+  // not single-unit phases (the LDS staging step would only add latency there).
+  constexpr bool kTp1 = CO == 16 && GH == 4, kTp4 = CO == 4 && GH == 4, k70 = GH == 8;
+  constexpr bool kRollQkv = kTp1, kRollO = k70, kRollGu = kTp1 || kTp4, kRollDown = k70;
   Pack8(&w_gu)[DL_MAXP] = kEarlyGu ? wb : wa;
   Pack8(&w_dn)[DL_MAXP] = kEarlyDown ? wc : w_gu;
   Pack8(&w_qkv)[DL_MAXP] = kEarlyQkv ? wa : w_dn;
@@ -821,8 +902,8 @@ SYM_DEV void dl_body(const DLArgs& a, int b) {
     // ---- QKV: split-K slabs (the row scale waits for the attention phase)
     if (l > 0) dl_wait(a, ev0 - DL_PH + DL_DOWN);
     dl_stamp(a, ev0 + DL_QKV, b, 0);
-    dl_gemm_phase<CQ, EP_SLAB>(a, phase_of(l, DL_QKV), DLEpi{EP_SLAB, a.qkv_ws, Nq, nullptr, nullptr, Nq}, w_qkv, xa,
-                               b, red, rn_s, xep_s, ev0 + DL_QKV, l > 0, none, none);
+    dl_gemm_phase<CQ, EP_SLAB, kRollQkv>(a, phase_of(l, DL_QKV), DLEpi{EP_SLAB, a.qkv_ws, Nq, nullptr, nullptr, Nq},
+                                         w_qkv, xa, b, red, rn_s, xep_s, ev0 + DL_QKV, l > 0, none, none, xs);
     dl_signal(a, ev0 + DL_QKV, b, ctl);
     // ---- attention: wave-level units (sequence x kv head x partition), dealt over the workgroups first; the first
     // unit's metadata read before the edge
@@ -852,26 +933,27 @@ SYM_DEV void dl_body(const DLArgs& a, int b) {
     // ---- O (+ all-reduce, residual, ln2 prep)
     dl_wait(a, ev0 + DL_ATTN);
     dl_stamp(a, ev0 + DL_O, b, 0);
-    dl_gemm_phase<CO, EP_RES>(
+    dl_gemm_phase<CO, EP_RES, kRollO>(
         a, phase_of(l, DL_O), DLEpi{EP_RES, nullptr, 0, ly.ln2, nullptr, d}, wa, xa, b, red, rn_s, xep_s, ev0 + DL_O,
         false, [&](auto load) { if constexpr (kEarlyGu) dl_prefetch<CG, load>(wb, phase_of(l, DL_GU), b, false); },
-        [&](auto load) { if constexpr (!kEarlyGu) dl_prefetch<CG, load>(wa, phase_of(l, DL_GU), b, false); });
+        [&](auto load) { if constexpr (!kEarlyGu) dl_prefetch<CG, load>(wa, phase_of(l, DL_GU), b, false); }, xs);
     dl_signal(a, ev0 + DL_O, b, ctl);
     // ---- gate_up (+ row scale, SwiGLU)
     dl_wait(a, ev0 + DL_O);
     dl_stamp(a, ev0 + DL_GU, b, 0);
     dl_row_scales(a, a.ss, ntile_d, rn_s);  // published by the first unit's barrier, before any epilogue reads it
-    dl_gemm_phase<CG, EP_SWI>(
+    dl_gemm_phase<CG, EP_SWI, kRollGu>(
         a, phase_of(l, DL_GU), DLEpi{EP_SWI, nullptr, 0, nullptr, a.act, 2 * a.Fl}, w_gu, xa, b, red, rn_s, xep_s,
         ev0 + DL_GU, true,
         [&](auto load) { if constexpr (kEarlyDown) dl_prefetch<CD, load>(wc, phase_of(l, DL_DOWN), b, false); },
-        [&](auto load) { if constexpr (!kEarlyDown) dl_prefetch<CD, load>(w_gu, phase_of(l, DL_DOWN), b, false); });
+        [&](auto load) { if constexpr (!kEarlyDown) dl_prefetch<CD, load>(w_gu, phase_of(l, DL_DOWN), b, false); },
+        xs);
     dl_signal(a, ev0 + DL_GU, b, ctl);
     // ---- down (+ all-reduce, residual, next-norm prep)
     dl_wait(a, ev0 + DL_GU);
     dl_stamp(a, ev0 + DL_DOWN, b, 0);
     const int ln = l + 1 < a.L ? l + 1 : l;  // (the last layer issues zero-length loads: the same instructions)
-    dl_gemm_phase<CD, EP_RES>(
+    dl_gemm_phase<CD, EP_RES, kRollDown>(
         a, phase_of(l, DL_DOWN), DLEpi{EP_RES, nullptr, 0, ly.lnn, nullptr, d}, w_dn, xa, b, red, rn_s, xep_s,
         ev0 + DL_DOWN, true,
         [&](auto load) {
@@ -879,7 +961,8 @@ SYM_DEV void dl_body(const DLArgs& a, int b) {
         },
         [&](auto load) {
           if constexpr (!kEarlyQkv) dl_prefetch<CQ, load>(w_dn, phase_of(ln, DL_QKV), b, false, ln != l);
-        });
+        },
+        xs);
     dl_signal(a, ev0 + DL_DOWN, b, ctl);
   }
   if (ctl && a.xp.world > 1)

@@ -73,6 +73,8 @@ ROPE_DECODE_ROWS = os.environ.get("SYMMETRY_ROPE_DECODE_ROWS", "1") != "0"
 #   the in-launch reduction's tail (one of S workgroups per column group sums the slabs) costs o / down /
 #   qkv more than the separate consumer kernel they save.
 MG_FUSED_MODE = os.environ.get("SYMMETRY_MG_FUSED", "gu")
+# prefill steps of <= 256 tokens on the fused general path too (A/B knob)
+MG_FUSED_PREFILL = os.environ.get("SYMMETRY_MG_FUSED_PREFILL", "0") != "0"
 MG_FUSED = MG_FUSED_MODE in ("1", "all")
 MG_FUSED_GU = MG_FUSED_MODE == "gu"
 # Dense decode steps of <= 16 rows run every layer as ONE persistent launch (csrc/kernels/decode_layers.hip: QKV ->
@@ -323,6 +325,8 @@ class TransformerLM:
         if self.fused and b.num_tokens <= SKINNY_MAX_M and not self._general_rows(b.num_tokens):
             return self._forward_fused(b, kv)
         mgs = self._mg_plan(b)
+        if mgs is None and MG_FUSED_PREFILL and b.kind != "decode":
+            mgs = self._mg_plan(b, any_kind=True)
         if mgs is not None:
             return self._forward_general_fused(b, kv, mgs)
         return self._forward_general(b, kv)
@@ -343,7 +347,7 @@ class TransformerLM:
         for name, (N, K) in shapes.items():
             if name not in names:
                 continue
-            pick = ops.choose_mgemm(T, N, K)
+            pick = ops.choose_mgemm(T, N, K, fused=True)
             if pick is None:
                 if need_all:
                     return None

@@ -129,7 +129,10 @@ def mgemm(x, w_shuf, y, rw: int):
     return reference.skinny_gemm(x, reference.unshuffled(w_shuf, True), y)
 
 
-def choose_mgemm(M: int, N: int, K: int, cus: int = 256):
+_MG_GU_WIDE = os.environ.get("SYMMETRY_MG_GU_WIDE", "0") != "0"  # A/B: the wide gate_up (+ SwiGLU) on mgemm
+
+
+def choose_mgemm(M: int, N: int, K: int, cus: int = 256, fused: bool = False):
     """(rw, S) of mgemm for an [M, K] x [N, K]^T projection, or None where another kernel is the better
     choice.  Measured on MI355X (profiles/mgemm_r2.jsonl, mgemm_small_r2.jsonl; each arm followed by its
     real consumer kernel): up to 64 rows mgemm beats both the split-K skinny GEMM and hipBLASLt on every
@@ -142,7 +145,8 @@ def choose_mgemm(M: int, N: int, K: int, cus: int = 256):
     workgroup spread over the grid."""
     if not _MGEMM_ON or M > MGEMM_MAX_M or K % 64:
         return None
-    if M > 64 and (N > 8192 or (M > 192 and K < 8192 and N < 6144)):
+    wide = fused and _MG_GU_WIDE and N > 8192  # fused epilogue: no fp32 slabs to write / re-read at S = 1
+    if M > 64 and not wide and (N > 8192 or (M > 192 and K < 8192 and N < 6144)):
         return None
     mt = 2 if M <= 32 else 4 if M <= 64 else 8 if M <= 128 else 16
     a_us_mb, b_us_mb = {2: (11.5, 2.2), 4: (11.5, 2.2), 8: (20.0, 1.0), 16: (30.0, 1.0)}[mt]
@@ -156,7 +160,8 @@ def choose_mgemm(M: int, N: int, K: int, cus: int = 256):
             wgs = N // (64 * rw) * S
             if wgs < cus // 2 or wgs > cus:
                 continue
-            t = (a_us_mb * (64 * rw + M) * (K // S) * 2 / 1e6 + b_us_mb * S * M * N * 4 / 1e6
+            slabs = 0 if (wide and S == 1) else b_us_mb * S * M * N * 4 / 1e6
+            t = (a_us_mb * (64 * rw + M) * (K // S) * 2 / 1e6 + slabs
                  + 1000.0 / wgs)  # per-workgroup fixed cost (prologue, epilogue), spread over the grid
             if best is None or t < best[0]:
                 best = (t, rw, S)
