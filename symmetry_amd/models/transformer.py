@@ -79,10 +79,10 @@ MG_FUSED = MG_FUSED_MODE in ("1", "all")
 MG_FUSED_GU = MG_FUSED_MODE == "gu"
 # Dense decode steps of <= 16 rows run every layer as ONE persistent launch (csrc/kernels/decode_layers.hip: QKV ->
 # attention -> O (+ all-reduce) -> gate_up -> down with in-launch edges, each phase's weights streamed into registers
-# before the edge it waits on).  "auto" (default): tensor-parallel shards (TP >= 2) with a GPU per rank, where the
-# per-layer launches sit at their floors (one shard on one GPU, bench/tp_shard.py: 8B TP = 8 1.20 -> 0.92 ms, TP = 4
-# 1.45 -> 1.27, 70B TP = 8 4 clients 4.93 -> 4.30; profiles/r5/engine_tp_shard.jsonl); "1": wherever the shape class
-# is built (also TP = 1, where it is slower); "0": the per-layer launches.
+# before the edge it waits on).  "auto" (default): wherever the shape class is built, under TP with a GPU per rank
+# (bench/tp_shard.py, 10 clients, profiles/r5/engine_tp_shard_rolled.jsonl: 8B TP = 1 3.10 -> 2.74 ms, TP = 4
+# 1.45 -> 1.18, TP = 8 1.20 -> 0.91, 70B TP = 8 4 clients 4.94 -> 4.17); "1": also ranks sharing a GPU; "0": the
+# per-layer launches.
 DECODE_ENGINE = os.environ.get("SYMMETRY_DECODE_ENGINE", "auto")
 # workgroups of the engine's grid (one per CU; a one-GPU multi-rank rehearsal gives each rank a share)
 ENGINE_GRID = int(os.environ.get("SYMMETRY_ENGINE_GRID", "0"))
@@ -413,8 +413,7 @@ class TransformerLM:
                 # ranks sharing a GPU (one-GPU rehearsals): two whole-GPU persistent grids whose edges wait on each
                 # other's all-reduce granules cannot both be resident -- only with an explicit per-rank grid
                 return None
-        elif DECODE_ENGINE == "auto":
-            return None  # TP = 1: the per-layer launches measured faster (3.10 vs 3.16 ms, profiles/r5)
+
         bs = kv.block_size
         if bs < 32 or bs & (bs - 1) or (self.hq % self.hkv) or (self.hq // self.hkv) not in (4, 8):
             return None
