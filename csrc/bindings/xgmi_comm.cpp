@@ -274,7 +274,9 @@ DLArgs dl_args(const Tensor& table, int64_t Hq, int64_t Hkv, int64_t Fl, int64_t
   for (const Tensor* t : {(const Tensor*)&xw, (const Tensor*)&attn, (const Tensor*)&act})
     dl_check_t(*t, at::kBFloat16, "bf16 operand");
   dl_check_t(edge, at::kInt, "edge");
-  dl_check_t(fault, at::kInt, "fault");
+  // the fault word: device memory, or a pinned host word the host reads after every step without a sync
+  TORCH_CHECK(fault.scalar_type() == at::kInt && fault.is_contiguous() && (fault.is_cuda() || fault.is_pinned()),
+              "decode_layers: fault must be an int32 GPU tensor or pinned host word");
   TORCH_CHECK(table.dim() == 2 && table.size(1) == 8, "decode_layers: table [L, 8]");
   TORCH_CHECK(resid.dim() == 2 && xw.sizes() == resid.sizes(), "decode_layers: resid / xw [M, d]");
   const int64_t L = table.size(0), M = resid.size(0), d = resid.size(1);

@@ -86,7 +86,7 @@ SYM_DEV void stbf_sc1(bf16* p, float v) {
 
 // ---- edges --------------------------------------------------------------------------------------------------
 SYM_DEV bool dl_faulted(const DLArgs& a) {
-  return __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+  return __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 ||
          (a.xp.err != nullptr && __hip_atomic_load(a.xp.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0);
 }
 
@@ -150,7 +150,7 @@ SYM_DEV void dl_wait(const DLArgs& a, int ev) {
       if (__all(ok)) break;
       if ((it & 63) == 63 && (dl_faulted(a) || wall_clock64() - t0 > DL_WAIT_TICKS)) {
         if (lane == 0) {
-          __hip_atomic_store(a.fault, 1 + ev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.fault, 1 + ev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           // under TP the host polls the communicator's (host-mapped) error word after every step
           if (a.xp.err != nullptr && __hip_atomic_load(a.xp.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0)
             __hip_atomic_store(a.xp.err, 0x100 + ev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -84,6 +84,8 @@ MG_FUSED_GU = MG_FUSED_MODE == "gu"
 # 1.45 -> 1.18, TP = 8 1.20 -> 0.91, 70B TP = 8 4 clients 4.94 -> 4.17); "1": also ranks sharing a GPU; "0": the
 # per-layer launches.
 DECODE_ENGINE = os.environ.get("SYMMETRY_DECODE_ENGINE", "auto")
+# "auto" at TP = 1 too (under investigation: a replayed-hipGraph mismatch at the 8B TP = 1 shape)
+ENGINE_TP1 = os.environ.get("SYMMETRY_ENGINE_TP1", "0") != "0"
 # workgroups of the engine's grid (one per CU; a one-GPU multi-rank rehearsal gives each rank a share)
 ENGINE_GRID = int(os.environ.get("SYMMETRY_ENGINE_GRID", "0"))
 # MFMA-preshuffled copy of the lm_head for the fused decode path's dg_argmax (1 KB per wave load like the layer
@@ -413,6 +415,8 @@ class TransformerLM:
                 # ranks sharing a GPU (one-GPU rehearsals): two whole-GPU persistent grids whose edges wait on each
                 # other's all-reduce granules cannot both be resident -- only with an explicit per-rank grid
                 return None
+        elif DECODE_ENGINE == "auto" and not ENGINE_TP1:
+            return None
 
         bs = kv.block_size
         if bs < 32 or bs & (bs - 1) or (self.hq % self.hkv) or (self.hq // self.hkv) not in (4, 8):
@@ -467,11 +471,24 @@ class TransformerLM:
         act = self._buf("act", (T, Fl), torch.bfloat16)
         edge = self.ws.get("dl.edge", (ops.decode_layers_edge_words(L, T, self.hq, self.hkv, G),), torch.int32,
                            self.device, zeros=True)
-        fault = self.ws.get("dl.fault", (1,), torch.int32, self.device, zeros=True)
+        fault = self._engine_cache.get("fault")
+        if fault is None:  # pinned host word: the runner reads it after every step without a sync
+            fault = self._engine_cache["fault"] = torch.zeros(1, dtype=torch.int32).pin_memory()
         return ops.decode_layers(self._engine_table(kv), self.hq, self.hkv, Fl, ksq, b.positions, b.slot_mapping,
                                  b.block_tables, b.ctx_lens, kv.block_size, self.cos_sin, self.scale, self.cfg.rms_eps,
                                  resid, xw, ss_t, ss_1, qkv_ws, attn.view(T, -1), act, edge, fault, G, xar,
                                  self.engine_stamps)
+
+    def engine_fault(self) -> int:
+        """Nonzero (1 + the phase event) once an engine edge gave up waiting: that step's outputs are invalid.
+        Read after the step's completion event; re-armed by the reader."""
+        f = self._engine_cache.get("fault")
+        if f is None:
+            return 0
+        v = int(f[0])
+        if v:
+            f.zero_()
+        return v
 
     def _forward_fused(self, b: ForwardBatch, kv: KVCache) -> torch.Tensor:
         cfg, w = self.cfg, self.w

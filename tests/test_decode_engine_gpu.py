@@ -68,12 +68,15 @@ def test_engine_tokens_match_per_layer_launches(gpu, monkeypatch):
                 break
 
 
-def test_engine_70b_tp8_shard_matches_per_layer_launches(gpu, monkeypatch):
-    """Llama-3-70B's TP = 8 rank-0 shard (2 layers; shape class (16, 4, 16, 14): QKV 2 k-slabs of 4096, gate_up
-    K = 8192 as two tile-major 4096-deep units per tile, O / down two output tiles per workgroup, 8 query heads per
-    kv head) on a world-1 xGMI communicator (bench/tp_shard.py LocalXgmi): the first engine decode step picks the
-    same greedy token as the per-layer launches for (nearly) every sequence (a shard's logits are not a model's,
-    so no oracle; a broken engine agrees by chance only)."""
+@pytest.mark.parametrize("model,tp", [("llama3:70b", 8), ("llama3:8b", 8), ("llama3:8b", 4), ("llama3:8b", 2),
+                                      ("llama3:8b", 1)])
+def test_engine_shard_matches_per_layer_launches(gpu, monkeypatch, model, tp):
+    """Every built shape class of the real models, on a TP rank-0 shard (2 layers) with a world-1 xGMI
+    communicator (bench/tp_shard.py LocalXgmi): 70B TP = 8 (16, 4, 16, 14) -- QKV 2 k-slabs of 4096, gate_up
+    K = 8192 as two tile-major 4096-deep units per tile, O / down two rolled units per workgroup, 8 query heads per
+    kv head; 8B TP = 8 / 4 / 2 / 1 -- TP = 1 with 3 rolled QKV units, 7 rolled gate_up units, down as 4 tile-major
+    k splits.  The first engine decode step picks the same greedy token as the per-layer launches for (nearly)
+    every sequence (a shard's logits are not a model's, so no oracle; a broken engine agrees by chance only)."""
     import os
     import sys
 
@@ -85,15 +88,15 @@ def test_engine_70b_tp8_shard_matches_per_layer_launches(gpu, monkeypatch):
     from symmetry_amd.models import transformer as tr
     from symmetry_amd.models.config import resolve
 
-    mc = resolve("llama3:70b").replace(num_layers=2)
+    mc = resolve(model).replace(num_layers=2)
     prompts = [[(97 * i + 13 * k) % 100000 + 300 for k in range(40 + 7 * i)] for i in range(8)]
     toks, steps = {}, {}
     for mode in ("0", "1"):
         monkeypatch.setattr(tr, "DECODE_ENGINE", mode)
         dev = torch.device("cuda:0")
-        eng = LLMEngine(EngineConfig(model="llama3:70b", model_config=mc, device="cuda:0", max_num_seqs=8,
-                                     max_model_len=512, num_kv_blocks=64, tp_size=8, tp_rank=0, weight_init="shard",
-                                     use_graphs=False, seed=3), tp_comm=LocalXgmi(dev, 8))
+        eng = LLMEngine(EngineConfig(model=model, model_config=mc, device="cuda:0", max_num_seqs=8,
+                                     max_model_len=512, num_kv_blocks=64, tp_size=tp, tp_rank=0, weight_init="shard",
+                                     use_graphs=False, seed=3), tp_comm=LocalXgmi(dev, tp))
         seqs = [eng.add_request(f"s{i}", p, SamplingParams(max_tokens=3, ignore_eos=True))
                 for i, p in enumerate(prompts)]
         while eng.has_unfinished():
