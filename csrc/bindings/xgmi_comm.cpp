@@ -326,13 +326,8 @@ DLArgs dl_args(const Tensor& table, int64_t Hq, int64_t Hkv, int64_t Fl, int64_t
   a.edge = reinterpret_cast<unsigned*>(edge.data_ptr());
   a.fault = fault.data_ptr<int>();
   a.G = (int)G;
-  static const int edge_mode = [] {  // A/B knob: SYMMETRY_ENGINE_EDGE=0 sharded counters (default), 1 flag board
-    const char* k = getenv("SYMMETRY_ENGINE_EDGE");
-    return k ? atoi(k) : 0;
-  }();
-  a.edge_mode = edge_mode;
-  TORCH_CHECK(edge.numel() >= dl_edge_words((int)L, (int)M, (int)Hq, (int)Hkv, (int)G, edge_mode) &&
-                  fault.numel() >= 1, "decode_layers: edge [decode_layers_edge_words(...)], fault [1]");
+  TORCH_CHECK(edge.numel() >= dl_edge_words((int)L, (int)M, (int)Hq, (int)Hkv) && fault.numel() >= 1,
+              "decode_layers: edge [decode_layers_edge_words(...)], fault [1]");
   if (xar >= 0) {
     Xgmi* x = get(xar);
     check_ready(x, resid);
@@ -360,8 +355,8 @@ bool decode_layers(const Tensor& table, int64_t Hq, int64_t Hkv, int64_t Fl, int
 }
 
 int64_t decode_layers_edge_words(int64_t L, int64_t M, int64_t Hq, int64_t Hkv, int64_t G) {
-  const char* k = getenv("SYMMETRY_ENGINE_EDGE");
-  return dl_edge_words((int)L, (int)M, (int)Hq, (int)Hkv, (int)G, k ? atoi(k) : 0);
+  (void)G;
+  return dl_edge_words((int)L, (int)M, (int)Hq, (int)Hkv);
 }
 
 int64_t decode_layers_pieces(int64_t cq, int64_t co, int64_t cg, int64_t cd, int64_t ks, int64_t gh) {

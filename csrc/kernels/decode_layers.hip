@@ -102,13 +102,20 @@ SYM_DEV void dl_stamp_ctl(const DLArgs& a, int ev, int b, int which) {
     a.stamps[((long long)b * a.L * DL_PH + ev) * 8 + which] = wall_clock64();
 }
 
-// Edge forms (DLArgs.edge_mode; the launcher zeroes the words before every launch):
-//   0  arrival counters, one per (event, shard), 8 shards by blockIdx & 7, each on its own 128 B line: ONE lane
-//      per workgroup adds (agent scope); the control wave's lanes 0..7 poll one shard each;
-//   1  a flag board: one u32 per workgroup holding the last event it signalled + 1 (a write-through store, no
-//      read-modify-write, no serialisation on a shared address); the control wave sweeps every workgroup's flag
-//      (16 B sc1 loads, 4 workgroups per lane) until all reached the event.
+// Edge counters, one per (event, shard), 8 shards by blockIdx & 7, each on its own 128 B line: ONE lane per
+// workgroup adds (agent scope); the control wave's lanes 0..7 poll one shard each.  The counters are never
+// cleared: launch E (the E-th launch on this buffer) waits for (E + 1) x the shard's workgroups.  E comes from the
+// LAST event's shard-0 counter read at kernel start (every earlier launch completed, no workgroup of this one has
+// reached that event yet).  (The first form zeroed them with a memset node in front of every launch: once another
+// hipGraph was captured, the replayed memset of an earlier decode graph no longer cleared them -- its waits then
+// passed at once and the step computed garbage.)
 constexpr int DL_SHARD_STRIDE = 32;  // u32 words between counter shards (128 B)
+
+SYM_DEV unsigned dl_epoch(const DLArgs& a) {
+  const unsigned c = __hip_atomic_load(a.edge + ((a.L * DL_PH - 1) * 8) * DL_SHARD_STRIDE, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return c / (unsigned)((a.G + 7) / 8);
+}
 
 // every thread: this workgroup's hand-off stores are drained, then ONE lane signals.  `drain`: this wave stored
 // hand-off data in the phase.  In a GEMM phase only the control wave stores (the epilogue); the streamer waves skip
@@ -117,33 +124,21 @@ constexpr int DL_SHARD_STRIDE = 32;  // u32 words between counter shards (128 B)
 SYM_DEV void dl_signal(const DLArgs& a, int ev, int b, bool drain = true) {
   if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    if (a.edge_mode == 1)
-      __hip_atomic_store(a.edge + b, (unsigned)(ev + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-      __hip_atomic_fetch_add(a.edge + (ev * 8 + (b & 7)) * DL_SHARD_STRIDE, 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(a.edge + (ev * 8 + (b & 7)) * DL_SHARD_STRIDE, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
   dl_stamp(a, ev, b, 1);
 }
 
-// every thread: returns once every workgroup signalled `ev`
-SYM_DEV void dl_wait(const DLArgs& a, int ev) {
+// every thread: returns once every workgroup signalled `ev` (epoch: dl_epoch, read by the control wave at start)
+SYM_DEV void dl_wait(const DLArgs& a, int ev, unsigned epoch) {
   if ((threadIdx.x >> 6) == DL_CTL) {
     const int lane = threadIdx.x & 63;
     const unsigned long long t0 = wall_clock64();
-    const rsrc_t rf = dl_rsrc(a.edge, (long long)((a.G + 255) / 256) * 1024);
     for (int it = 0;; ++it) {
       bool ok = true;
-      if (a.edge_mode == 1) {
-        for (int w0 = 4 * lane; w0 < a.G; w0 += 256) {
-          Pack8 f;
-          f.w = ld_sc1(rf, w0 * 4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) ok = ok && (w0 + e >= a.G || f.w[e] >= (unsigned)(ev + 1));
-        }
-      } else if (lane < 8) {
-        const unsigned want = (unsigned)((a.G - lane + 7) / 8);
+      if (lane < 8) {
+        const unsigned want = (epoch + 1u) * (unsigned)((a.G - lane + 7) / 8);
         ok = __hip_atomic_load(a.edge + (ev * 8 + lane) * DL_SHARD_STRIDE, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT) >= want;
       }
@@ -758,8 +753,8 @@ SYM_DEV void dl_attn_wave(const DLArgs& a, const DLLayer& ly, int sg, int p, DLW
   lsum += __shfl_xor(lsum, 32, 64);
   // ---- publish the partial, count in; the last arriver merges
   const int nused = ctx_old > 0 ? min(DL_APARTS, (ctx_old + 31) / 32) : 0;
-  const long long sync_w = dl_edge_sync_words(a.L, a.M, Hkv, a.G, a.edge_mode);
-  unsigned* cnt = a.edge + sync_w - (long long)a.M * Hkv * 32 + sg * 32;
+  const long long sync_w = dl_edge_sync_words(a.L, a.M, Hkv);
+  unsigned* cnt = a.edge + (long long)a.L * DL_PH * 8 * DL_SHARD_STRIDE + sg * 32;
   float* po = reinterpret_cast<float*>(a.edge + sync_w);
   float* pml = po + (long long)a.M * Hkv * DL_APARTS * Gh * 128;
   const rsrc_t rpo = dl_rsrc(po, (long long)a.M * Hkv * DL_APARTS * Gh * 128 * 4);
@@ -860,6 +855,7 @@ SYM_DEV void dl_body(const DLArgs& a, int b) {
   // this workgroup's O / down tiles (b, b + G, ...): their all-reduce epochs, read once, bumped by every O and
   // every down phase, written back at exit (the per-tile counters of the fused launches, decode_gemm.hip)
   const int nmine = b < ntile_d ? (ntile_d - b + a.G - 1) / a.G : 0;
+  const unsigned epoch = ctl ? dl_epoch(a) : 0u;  // (read before this workgroup's first signal)
   {
     const unsigned long long* src = reinterpret_cast<const unsigned long long*>(a.layers);
     unsigned long long* dst = reinterpret_cast<unsigned long long*>(lay_s);
@@ -900,7 +896,7 @@ SYM_DEV void dl_body(const DLArgs& a, int b) {
     const DLLayer& ly = lay_s[l];
     const int ev0 = l * DL_PH;
     // ---- QKV: split-K slabs (the row scale waits for the attention phase)
-    if (l > 0) dl_wait(a, ev0 - DL_PH + DL_DOWN);
+    if (l > 0) dl_wait(a, ev0 - DL_PH + DL_DOWN, epoch);
     dl_stamp(a, ev0 + DL_QKV, b, 0);
     dl_gemm_phase<CQ, EP_SLAB, kRollQkv>(a, phase_of(l, DL_QKV), DLEpi{EP_SLAB, a.qkv_ws, Nq, nullptr, nullptr, Nq},
                                          w_qkv, xa, b, red, rn_s, xep_s, ev0 + DL_QKV, l > 0, none, none, xs);
@@ -918,7 +914,7 @@ SYM_DEV void dl_body(const DLArgs& a, int b) {
         mt = dl_attn_meta(a, v0 / DL_APARTS / a.Hkv, v0 % DL_APARTS);
         dl_attn_pre(a, v0 / DL_APARTS, ss_in, ss_tiles, mt, pre);
       }
-      dl_wait(a, ev0 + DL_QKV);
+      dl_wait(a, ev0 + DL_QKV, epoch);
       dl_stamp(a, ev0 + DL_ATTN, b, 0);
       for (int v = v0; v < nv; v += a.G * DL_SW) {
         if (v != v0) {
@@ -931,7 +927,7 @@ SYM_DEV void dl_body(const DLArgs& a, int b) {
     dl_signal(a, ev0 + DL_ATTN, b);
     dl_prefetch<CO>(wa, phase_of(l, DL_O), b, true);  // before any later stream
     // ---- O (+ all-reduce, residual, ln2 prep)
-    dl_wait(a, ev0 + DL_ATTN);
+    dl_wait(a, ev0 + DL_ATTN, epoch);
     dl_stamp(a, ev0 + DL_O, b, 0);
     dl_gemm_phase<CO, EP_RES, kRollO>(
         a, phase_of(l, DL_O), DLEpi{EP_RES, nullptr, 0, ly.ln2, nullptr, d}, wa, xa, b, red, rn_s, xep_s, ev0 + DL_O,
@@ -939,7 +935,7 @@ SYM_DEV void dl_body(const DLArgs& a, int b) {
         [&](auto load) { if constexpr (!kEarlyGu) dl_prefetch<CG, load>(wa, phase_of(l, DL_GU), b, false); }, xs);
     dl_signal(a, ev0 + DL_O, b, ctl);
     // ---- gate_up (+ row scale, SwiGLU)
-    dl_wait(a, ev0 + DL_O);
+    dl_wait(a, ev0 + DL_O, epoch);
     dl_stamp(a, ev0 + DL_GU, b, 0);
     dl_row_scales(a, a.ss, ntile_d, rn_s);  // published by the first unit's barrier, before any epilogue reads it
     dl_gemm_phase<CG, EP_SWI, kRollGu>(
@@ -950,7 +946,7 @@ SYM_DEV void dl_body(const DLArgs& a, int b) {
         xs);
     dl_signal(a, ev0 + DL_GU, b, ctl);
     // ---- down (+ all-reduce, residual, next-norm prep)
-    dl_wait(a, ev0 + DL_GU);
+    dl_wait(a, ev0 + DL_GU, epoch);
     dl_stamp(a, ev0 + DL_DOWN, b, 0);
     const int ln = l + 1 < a.L ? l + 1 : l;  // (the last layer issues zero-length loads: the same instructions)
     dl_gemm_phase<CD, EP_RES, kRollDown>(
@@ -1002,8 +998,6 @@ bool dl_check(const DLArgs& a) {
          a.Fl % (a.KSd * 256) == 0;
 }
 
-// bytes of edge words one launch uses (zeroed before it)
-size_t dl_edge_bytes(const DLArgs& a) { return (size_t)dl_edge_sync_words(a.L, a.M, a.Hkv, a.G, a.edge_mode) * 4; }
 
 int g_dl_resident[16];  // per shape: workgroups per CU the kernel admits (occupancy query, once; 0 = unknown)
 
@@ -1044,7 +1038,6 @@ bool launch_decode_layers(const DLArgs& a, hipStream_t s) {
   if (a.cq == A && a.co == B && a.cg == C && a.cd == D_ && a.KSq == KS && a.Hq / a.Hkv == GH) {          \
     auto k = decode_layers_kernel<A, B, C, D_, KS, GH>;                                                  \
     if (a.G > dl_cus() * dl_per_cu(k, g_dl_resident[idx])) return false; /* every workgroup resident */ \
-    (void)hipMemsetAsync(a.edge, 0, dl_edge_bytes(a), s);                                               \
     k<<<a.G, DL_NT, 0, s>>>(DLOne{{a}});                                                                 \
     return true;                                                                                         \
   }                                                                                                      \

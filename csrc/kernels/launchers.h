@@ -131,24 +131,25 @@ struct DLArgs {
   float* qkv_ws = nullptr;   // [KSq][M][Nq] fp32
   bf16* attn = nullptr;      // [M][Hq * 128]
   bf16* act = nullptr;       // [M][Fl]
-  unsigned* edge = nullptr;  // edge words + attention counters / partials (dl_edge_words); the launcher zeroes the
-                             // synchronisation words before every launch
-  int edge_mode = 0;         // 0: sharded arrival counters [L * 5][8] x 128 B; 1: flag board [G] (rounded to 1 KB)
+  unsigned* edge = nullptr;  // edge counters + attention counters / partials (dl_edge_words), zero at allocation
   int* fault = nullptr;      // device word: an edge wait gave up (sticky for the launch)
   int G = 0;                 // workgroups of this rank (one per CU)
   XgmiArgs xp;               // world > 1: the fused all-reduce communicator (decode_epi.h granules)
   unsigned* xar_ctr = nullptr;
   unsigned long long* stamps = nullptr;  // diagnostics: [G][L][5][8] wall clock: edge passed, signalled, sub-phases
 };
-// The edge tensor holds, in order: the edge words (edge_mode 0: [L * 5][8] counters 128 B apart; 1: [G] flags
-// rounded to 256), one attention arrival counter per (sequence, kv head) 128 B apart (both zeroed by the launcher),
-// then the attention partials (fp32 o [M * Hkv][DL_APARTS][Hq / Hkv][128], m / l [M * Hkv][Hq / Hkv][DL_APARTS][2]).
+// The edge tensor holds, in order: the edge counters ([L * 5][8], 128 B apart), one attention arrival counter per
+// (sequence, kv head) 128 B apart, then the attention partials (fp32 o [M * Hkv][DL_APARTS][Hq / Hkv][128], m / l
+// [M * Hkv][Hq / Hkv][DL_APARTS][2]).  Zero when allocated and never cleared again (decode_layers.hip: epochs).
 constexpr int DL_APARTS = 8;  // context partitions per (sequence, kv head): one wave each
-__host__ __device__ inline long long dl_edge_sync_words(int L, int M, int Hkv, int G, int edge_mode) {
-  return (edge_mode == 1 ? (long long)(G + 255) / 256 * 256 : (long long)L * 5 * 8 * 32) + (long long)M * Hkv * 32;
+// (the attention counters are laid out for 16 rows whatever M: graphs of different batch buckets share the buffer,
+// and a smaller bucket's partials must not land on a larger one's counters)
+__host__ __device__ inline long long dl_edge_sync_words(int L, int M, int Hkv) {
+  (void)M;
+  return (long long)L * 5 * 8 * 32 + 16LL * Hkv * 32;
 }
-__host__ __device__ inline long long dl_edge_words(int L, int M, int Hq, int Hkv, int G, int edge_mode) {
-  return dl_edge_sync_words(L, M, Hkv, G, edge_mode) + (long long)M * Hq * DL_APARTS * 130;
+__host__ __device__ inline long long dl_edge_words(int L, int M, int Hq, int Hkv) {
+  return dl_edge_sync_words(L, M, Hkv) + (long long)M * Hq * DL_APARTS * 130;
 }
 // false: shapes outside the engine (the caller runs the per-layer launches); the launch itself is checked
 bool launch_decode_layers(const DLArgs& a, hipStream_t s);

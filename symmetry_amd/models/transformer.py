@@ -79,12 +79,13 @@ MG_FUSED = MG_FUSED_MODE in ("1", "all")
 MG_FUSED_GU = MG_FUSED_MODE == "gu"
 # Dense decode steps of <= 16 rows run every layer as ONE persistent launch (csrc/kernels/decode_layers.hip: QKV ->
 # attention -> O (+ all-reduce) -> gate_up -> down with in-launch edges, each phase's weights streamed into registers
-# before the edge it waits on).  "auto" (default): wherever the shape class is built, under TP with a GPU per rank
-# (bench/tp_shard.py, 10 clients, profiles/r5/engine_tp_shard_rolled.jsonl: 8B TP = 1 3.10 -> 2.74 ms, TP = 4
-# 1.45 -> 1.18, TP = 8 1.20 -> 0.91, 70B TP = 8 4 clients 4.94 -> 4.17); "1": also ranks sharing a GPU; "0": the
-# per-layer launches.
-DECODE_ENGINE = os.environ.get("SYMMETRY_DECODE_ENGINE", "auto")
-# "auto" at TP = 1 too (under investigation: a replayed-hipGraph mismatch at the 8B TP = 1 shape)
+# before the edge it waits on).  Off by default: with correct in-launch edges under hipGraphs it does not beat the
+# per-layer launches (one shard on one GPU, bench/tp_shard.py, 10 clients, profiles/r5/engine_tp_shard_epoch.jsonl:
+# 8B TP = 8 1.206 vs 1.201 ms, TP = 4 1.55 vs 1.45, TP = 1 3.44 vs 3.11, 70B TP = 8 4 clients 5.59 vs 4.93; the
+# faster numbers measured earlier came from replayed graphs whose edge-counter memset had stopped working).
+# "auto": TP >= 2 with a GPU per rank (SYMMETRY_ENGINE_TP1=1: also TP = 1); "1": wherever the shape class is built;
+# "0" (default): the per-layer launches.
+DECODE_ENGINE = os.environ.get("SYMMETRY_DECODE_ENGINE", "0")
 ENGINE_TP1 = os.environ.get("SYMMETRY_ENGINE_TP1", "0") != "0"
 # workgroups of the engine's grid (one per CU; a one-GPU multi-rank rehearsal gives each rank a share)
 ENGINE_GRID = int(os.environ.get("SYMMETRY_ENGINE_GRID", "0"))

@@ -68,9 +68,10 @@ def test_engine_tokens_match_per_layer_launches(gpu, monkeypatch):
                 break
 
 
+@pytest.mark.parametrize("graphs", [False, True])
 @pytest.mark.parametrize("model,tp", [("llama3:70b", 8), ("llama3:8b", 8), ("llama3:8b", 4), ("llama3:8b", 2),
                                       ("llama3:8b", 1)])
-def test_engine_shard_matches_per_layer_launches(gpu, monkeypatch, model, tp):
+def test_engine_shard_matches_per_layer_launches(gpu, monkeypatch, model, tp, graphs):
     """Every built shape class of the real models, on a TP rank-0 shard (2 layers) with a world-1 xGMI
     communicator (bench/tp_shard.py LocalXgmi): 70B TP = 8 (16, 4, 16, 14) -- QKV 2 k-slabs of 4096, gate_up
     K = 8192 as two tile-major 4096-deep units per tile, O / down two rolled units per workgroup, 8 query heads per
@@ -96,7 +97,7 @@ def test_engine_shard_matches_per_layer_launches(gpu, monkeypatch, model, tp):
         dev = torch.device("cuda:0")
         eng = LLMEngine(EngineConfig(model=model, model_config=mc, device="cuda:0", max_num_seqs=8,
                                      max_model_len=512, num_kv_blocks=64, tp_size=tp, tp_rank=0, weight_init="shard",
-                                     use_graphs=False, seed=3), tp_comm=LocalXgmi(dev, tp))
+                                     use_graphs=graphs, seed=3), tp_comm=LocalXgmi(dev, tp))
         seqs = [eng.add_request(f"s{i}", p, SamplingParams(max_tokens=3, ignore_eos=True))
                 for i, p in enumerate(prompts)]
         while eng.has_unfinished():
