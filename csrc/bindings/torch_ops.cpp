@@ -423,8 +423,10 @@ void grouped_gemm(const Tensor& xs, const Tensor& W, const Tensor& offsets, int6
   check_dtype(xs, at::kBFloat16, "xs");
   check_dtype(W, at::kBFloat16, "W");
   check_dtype(offsets, at::kInt, "offsets");
+  const bool pre = (mode & 4) != 0;  // W MFMA-preshuffled per expert (models/layout.py::preshuffle)
+  mode &= 3;
   check_dtype(y, mode == 1 ? at::kFloat : at::kBFloat16, "y");
-  TORCH_CHECK(mode >= 0 && mode <= 2, "grouped_gemm: mode 0 (bf16), 1 (fp32), 2 (SwiGLU)");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "grouped_gemm: mode 0 (bf16), 1 (fp32), 2 (SwiGLU) [+4: preshuffled W]");
   TORCH_CHECK(W.dim() == 3 && xs.dim() == 2 && y.dim() == 2 && xs.is_contiguous() && W.is_contiguous() &&
                   y.is_contiguous(), "grouped_gemm: W [E, N, K], xs [R, K], y [R, N], contiguous");
   const int64_t E = W.size(0), K = W.size(2), R = xs.size(0);
@@ -432,9 +434,10 @@ void grouped_gemm(const Tensor& xs, const Tensor& W, const Tensor& offsets, int6
   TORCH_CHECK(xs.size(1) == K && y.size(0) >= R && y.size(1) == N, "grouped_gemm: shape mismatch");
   TORCH_CHECK(K % 64 == 0 && (mode == 2 ? N % 64 == 0 : N % 128 == 0), "grouped_gemm: K % 64, N % 128 (SwiGLU: F % 64)");
   TORCH_CHECK(E >= 1 && E <= 64 && e0 >= 0 && offsets.numel() >= e0 + E + 1, "grouped_gemm: offsets must cover e0..e0+E");
+  TORCH_CHECK(!pre || E <= 8, "grouped_gemm: preshuffled weights take the streaming path (<= 8 local experts)");
   const at::OptionalDeviceGuard g(xs.device());
   launch_grouped_gemm(ptr<bf16>(xs), ptr<bf16>(W), ptr<int>(offsets), y.data_ptr(), (int)R, (int)E, (int)e0, (int)N,
-                      (int)K, (int)mode, cur_stream(xs));
+                      (int)K, (int)mode, cur_stream(xs), (int)(offsets.numel() - 1), pre);
 }
 
 void grouped_skinny(const Tensor& xs, const Tensor& W, const Tensor& offsets, int64_t e0, Tensor& y) {
@@ -1010,6 +1013,7 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("decode_gemm_nt(int on) -> ()", [](int64_t on) { set_decode_gemm_nt((int)on); });
   m.def("grouped_skinny(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y) -> ()", &grouped_skinny);
   m.def("grouped_gemm(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y, int mode) -> ()", &grouped_gemm);
+  m.def("grouped_stream_policy(int p) -> ()", [](int64_t p) { set_grouped_stream_policy((int)p); });
   m.def("moe_route(Tensor logits, int T, int k, int E, Tensor(a!) ids, Tensor(b!) w) -> ()", &moe_route);
   m.def("moe_align(Tensor ids, int G, Tensor(a!) counts, Tensor(b!) offsets, Tensor(c!) cursor) -> ()", &moe_align);
   m.def(

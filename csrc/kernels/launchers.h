@@ -236,8 +236,12 @@ void launch_moe_route(LinOut logits, int ld, int T, int E, int k, int* ids, floa
 void launch_moe_align(const int* ids, int n, int E, int* counts, int* offsets, int* cursor, hipStream_t s);
 void launch_moe_scatter(const bf16* x, int T, int d, int k, int E, const int* ids, const int* offsets, int* cursor,
                         bf16* xs, int R, int* dst, int* src_tok, hipStream_t s);
+// E_all: experts in the global numbering of `offsets` (sizes the streaming path's row blocks); 0 = E.
+// pre: W MFMA-preshuffled per expert (the weight-streaming path only)
 void launch_grouped_gemm(const bf16* xs, const bf16* W, const int* offsets, void* y, int R, int E, int e0, int N,
-                         int K, int out, hipStream_t s);
+                         int K, int out, hipStream_t s, int E_all = 0, bool pre = false);
+// grouped_gemm's weight-streaming path: 0 never, 1 medium routed batches (default), 2 always
+void set_grouped_stream_policy(int p);
 void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, float* y, int R, int E, int e0, int N,
                            int K, int S, hipStream_t s);
 void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_lo, int e_hi, const float* w, int T, int k,

@@ -344,6 +344,333 @@ __global__ __launch_bounds__(GG_THREADS, 2) void grouped_gemm_kernel(const bf16*
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Weight-streaming grouped GEMM for medium routed batches (K12, ~32-256 rows per expert: Mixtral prefill
+// of a few prompts).  There the expert weights (Mixtral: 2.8 GB per layer) are read once and the routed
+// rows are few, so the 128 x 128 tile kernel above -- every tile re-stages its activation rows and pays a
+// prologue / epilogue per tile, 2 waves per CU -- streams the weights at ~3 TB/s
+// (profiles/r5/prof_mixtral_prefill_4x128.csv).  This kernel is mgemm.hip's weight stream made grouped and
+// persistent:
+//
+//   * a unit = (expert, block of up to 16 MT routed rows, n-block of 64 RW weight rows) over the whole K;
+//     units are numbered n-block-major, so with one row block per expert and a grid that is a multiple of 8
+//     every workgroup keeps ONE expert (blockIdx % 8 is the XCD: that expert's activation rows stay in its
+//     L2) and walks the n-blocks; the unit -> (expert, rows) map is computed on the device from the
+//     segment offsets (graph-capturable, no host sync);
+//   * one workgroup per CU, 4 waves x RW 16-row weight tiles; activation rows and weight rows stream
+//     through ONE LDS ring of 64-deep chunks by LDS-DMA (buffer loads: activation rows past the segment
+//     read as zeros without memory traffic), the ring continuing across unit boundaries, so the next
+//     unit's first chunks are in flight while this one's last chunks and its epilogue run;
+//   * both LDS images are [rows][128 B] with the 16-B chunk c stored at c ^ ((row >> 1) & 7) (swizzled on
+//     the DMA source), so fragment reads are conflict-free; the weight tile is the A operand of
+//     v_mfma_f32_16x16x32_bf16 (a lane ends with 4 consecutive features of one routed row), MFMAs on
+//     16-row token tiles past the segment are skipped (uniform branch);
+//   * OUT 2 (SwiGLU, W = [gate; up] rows): a wave's tiles alternate gate / up of the same 16 features, so
+//     act = silu(gate) * up is formed in registers -- the [R, 2F] intermediate never exists.
+// ---------------------------------------------------------------------------------------------------
+constexpr int GS_THR = 256, GS_EMAX = 8, GS_LDS = 160 * 1024;
+typedef __attribute__((address_space(3))) void lds_t;
+
+template <int MT, int RW, int D>
+struct GsCfg {
+  static constexpr int BM = 16 * MT;                         // routed rows per unit
+  static constexpr int XB = BM * 128;                        // activation bytes of one 64-deep chunk (LDS slot)
+  static constexpr int NX = MT / 2;                          // activation DMA instructions per wave per chunk
+  static constexpr int NW = 2 * RW;                          // weight load instructions per wave per chunk
+  // younger vector-memory ops when chunk g's activation DMA must have landed: W(g+1 .. g+D-1), X(g+1 .. g+D-2)
+  static constexpr int VM_KEEP = (D - 1) * NW + (D - 2) * NX;
+  static_assert(MT % 4 == 0 && D >= 3 && D * XB <= GS_LDS && VM_KEEP <= 63, "grouped stream config");
+};
+
+SYM_DEV __amdgpu_buffer_rsrc_t gs_rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL), 0x00020000);
+}
+
+// (the LDS-DMA builtin behind a device function: called directly inside the kernel's lambda, it makes the host
+// pass drop the kernel's launch stub)
+SYM_DEV void gs_dma(__amdgpu_buffer_rsrc_t r, int voff, int soff, char* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_t*)lds, 16, voff, soff, 0, 0);
+}
+
+SYM_DEV void gs_dma_nt(__amdgpu_buffer_rsrc_t r, int voff, int soff, char* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_t*)lds, 16, voff, soff, 0, 2);
+}
+
+SYM_DEV bf16x8 gs_ldw(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 2);  // nt: weights are read once
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+struct GsUnit {
+  int e, row0, rows, nb;
+};
+
+// unit u -> (expert, rows, n-block); a[] / nrb[] hold the segment starts and row-block counts (uniform)
+SYM_DEV GsUnit gs_unit(int u, int ERB, const int (&a)[GS_EMAX], const int (&n)[GS_EMAX], const int (&nrb)[GS_EMAX],
+                       int E, int BM) {
+  GsUnit r{0, 0, 0, u / ERB};
+  int j = u - r.nb * ERB;
+  bool found = false;
+#pragma unroll
+  for (int i = 0; i < GS_EMAX; ++i) {
+    if (i < E && !found) {
+      if (j < nrb[i]) {
+        found = true;
+        r.e = i;
+        r.row0 = a[i] + j * BM;
+        r.rows = min(BM, n[i] - j * BM);
+      } else {
+        j -= nrb[i];
+      }
+    }
+  }
+  return r;
+}
+
+// Nw: weight rows per expert (SwiGLU: 2 Ny); Ny: output columns.  PRE: W MFMA-preshuffled per expert
+// (models/layout.py::preshuffle: a wave's fragment load reads 1 KB contiguous instead of 16 rows x 64 B).
+//
+// Pipeline (one workgroup per CU): the weight fragments go straight into VGPRs (a register ring of D chunks
+// per wave, no LDS), the activation rows through an LDS ring of D slots, so a CU keeps D x (16 RW KB of weights
+// + 2 MT KB of activations) in flight -- the LDS alone (weights and activations both staged) held 96-128 KB,
+// and the activation bytes queued in front of the weights capped the stream at ~3 TB/s from 128 rows.
+// Per chunk g: wait for X(g) (W(g) is older), barrier, DMA X(g+D-1) into the slot chunk g-1 freed, MFMAs of
+// chunk g, then load W(g+D) into the register slot chunk g freed.  The chunk count is padded to a multiple of D
+// and loads past the last unit use a zero-range descriptor, so every iteration issues the same instructions
+// and one constant vmcnt covers every wait.
+template <int MT, int RW, int D, int OUT, bool PRE>
+__global__ __launch_bounds__(GS_THR, 1) void grouped_stream_kernel(const bf16* __restrict__ xs,
+                                                                   const bf16* __restrict__ W,
+                                                                   const int* __restrict__ offsets,
+                                                                   void* __restrict__ y, int R, int Nw, int Ny, int K,
+                                                                   int E, int e0) {
+  using C = GsCfg<MT, RW, D>;
+  __shared__ __attribute__((aligned(1024))) char smem[D * C::XB];
+  asm volatile("" ::: "a0");  // accumulators may live in AGPRs
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+
+  // ---- segment table (uniform) and the unit count
+  int a[GS_EMAX], n[GS_EMAX], nrb[GS_EMAX];
+  int ERB = 0;
+#pragma unroll
+  for (int i = 0; i < GS_EMAX; ++i) {
+    a[i] = 0;
+    n[i] = 0;
+    nrb[i] = 0;
+    if (i < E) {
+      a[i] = offsets[e0 + i];
+      n[i] = max(0, min(offsets[e0 + i + 1], R) - a[i]);
+      nrb[i] = (n[i] + C::BM - 1) / C::BM;
+      ERB += nrb[i];
+    }
+  }
+  const int rows_nb = OUT == 2 ? 32 * RW : 64 * RW;  // expert-local weight rows per n-block (SwiGLU: gate rows)
+  const int NB = (OUT == 2 ? Ny : Nw) / rows_nb;
+  const int U = NB * ERB;
+  const int G = gridDim.x;
+  if ((int)blockIdx.x >= U) return;  // uniform: the whole workgroup
+  const int nch = K / 64;
+  const int T = ((U - 1 - (int)blockIdx.x) / G + 1) * nch;  // chunks this workgroup streams
+  const int TP = (T + D - 1) / D * D;                       // padded to whole ring turns
+
+  // ---- per-lane offsets (unit-invariant: the unit lives in the descriptor bases)
+  int vx[C::NX];
+#pragma unroll
+  for (int i = 0; i < C::NX; ++i) {
+    const int row = (C::NX * wid + i) * 8 + (lane >> 3);
+    vx[i] = row * K * 2 + 16 * ((lane & 7) ^ ((row >> 1) & 7));
+  }
+  int vw[RW];  // k-step 0 of chunk 0; k-step 1 adds 64 B (row-major) / 1 KB (preshuffled)
+#pragma unroll
+  for (int rt = 0; rt < RW; ++rt) {
+    const int row0 = OUT == 2 ? (rt & 1) * Ny + 16 * (wid * (RW / 2) + rt / 2) : 16 * (wid * RW + rt);
+    if constexpr (PRE) vw[rt] = (row0 >> 4) * (K / 32) * 1024 + lane * 16;
+    else vw[rt] = (row0 + (lane & 15)) * K * 2 + 16 * (lane >> 4);
+  }
+  char* const dx = smem + (C::NX * wid) * 1024;
+
+  // ---- issue cursors: activations (unit xu, chunk xc) and weights (unit wu, chunk wc)
+  int xu = blockIdx.x, xc = 0, wu = blockIdx.x, wc = 0;
+  const bf16* xb = xs;
+  const bf16* wb = W;
+  long long xbytes = 0, wbytes = 0;
+  auto bind_x = [&](int u) {
+    xbytes = 0;
+    if (u < U) {
+      const GsUnit un = gs_unit(u, ERB, a, n, nrb, E, C::BM);
+      xb = xs + (long long)un.row0 * K;
+      xbytes = (long long)un.rows * K * 2;
+    }
+  };
+  auto bind_w = [&](int u) {
+    wbytes = 0;
+    if (u < U) {
+      const GsUnit un = gs_unit(u, ERB, a, n, nrb, E, C::BM);
+      const long long wrow = (long long)un.e * Nw + (long long)un.nb * rows_nb;
+      wb = W + wrow * K;
+      wbytes = ((long long)un.e * Nw + Nw - wrow) * K * 2;
+    }
+  };
+  bind_x(xu);
+  bind_w(wu);
+  auto issue_x = [&](int slot) {
+    const __amdgpu_buffer_rsrc_t rx = gs_rsrc(xb, xbytes);
+#pragma unroll
+    for (int i = 0; i < C::NX; ++i) gs_dma(rx, vx[i], xc * 128, dx + slot * C::XB + i * 1024);
+    if (++xc == nch) {
+      xc = 0;
+      xu += G;
+      bind_x(xu);
+    }
+  };
+  bf16x8 wr[D][RW][2];
+  auto issue_w = [&](bf16x8 (&dst)[RW][2]) {
+    const __amdgpu_buffer_rsrc_t rw = gs_rsrc(wb, wbytes);
+    const int so = PRE ? wc * 2048 : wc * 128;
+#pragma unroll
+    for (int rt = 0; rt < RW; ++rt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        dst[rt][s] = gs_ldw(rw, vw[rt] + (PRE ? s * 1024 : s * 64), so);
+    if (++wc == nch) {
+      wc = 0;
+      wu += G;
+      bind_w(wu);
+    }
+  };
+
+  // ---- fragment offsets of the activation image: row fr of a 16-row tile, global chunk 4 s + (lane >> 4)
+  const int fr = lane & 15;
+  const int fo0 = fr * 128 + 16 * ((lane >> 4) ^ ((fr >> 1) & 7));
+  const int fo1 = fr * 128 + 16 * ((4 + (lane >> 4)) ^ ((fr >> 1) & 7));
+
+  f32x4 acc[RW][MT];
+#pragma unroll
+  for (int rt = 0; rt < RW; ++rt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int cu = blockIdx.x, cc = 0;
+  GsUnit cun = gs_unit(cu, ERB, a, n, nrb, E, C::BM);
+  int mact = (cun.rows + 15) / 16;
+
+  // prologue in the steady state's order: W(0), then X(c), W(c + 1) for c = 0 .. D-2
+  issue_w(wr[0]);
+#pragma unroll
+  for (int c = 0; c < D - 1; ++c) {
+    issue_x(c);
+    issue_w(wr[c + 1]);
+  }
+
+  for (int g0 = 0; g0 < TP; g0 += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::VM_KEEP) : "memory");
+      __builtin_amdgcn_s_barrier();
+      issue_x((j + D - 1) % D);  // X(g + D - 1) into the slot chunk g - 1 freed (every wave is past its reads)
+      const char* const sb = smem + j * C::XB;
+      // token tiles in groups of 4 under one uniform skip branch: a group's 4 fragment reads are issued together
+      // (a read per tile under its own branch exposed the LDS latency once per tile: 1.3 us per chunk at 128 rows),
+      // and a unit sized for the largest segment costs the LDS reads / MFMAs of its actual rows only
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int g4 = 0; g4 < MT / 4; ++g4) {
+          if (4 * g4 < mact) {
+            bf16x8 xf[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) xf[q] = *(const bf16x8*)(sb + (4 * g4 + q) * 2048 + (s ? fo1 : fo0));
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+              for (int rt = 0; rt < RW; ++rt) acc[rt][4 * g4 + q] = mfma16(wr[j][rt][s], xf[q], acc[rt][4 * g4 + q]);
+          }
+        }
+      }
+      issue_w(wr[j]);  // W(g + D) into the register slot chunk g freed
+      if (++cc < nch || cu >= U) continue;
+      // ---- unit done: epilogue, lane holds features 4 (lane >> 4) .. + 3 of routed row 16 mt + (lane & 15)
+      cc = 0;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = 16 * mt + (lane & 15);
+        if (mt < mact && m < cun.rows) {
+          const long long yrow = (long long)(cun.row0 + m) * Ny;
+          if constexpr (OUT == 2) {
+#pragma unroll
+            for (int p = 0; p < RW / 2; ++p) {
+              const f32x4 gt = acc[2 * p][mt], up = acc[2 * p + 1][mt];
+              const int f = cun.nb * rows_nb + 16 * (wid * (RW / 2) + p) + 4 * (lane >> 4);
+              float o[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) o[q] = gt[q] / (1.f + __expf(-gt[q])) * up[q];
+              bf16x4 pk = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+              *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(y) + yrow + f) = pk;
+            }
+          } else {
+#pragma unroll
+            for (int rt = 0; rt < RW; ++rt) {
+              const f32x4 v = acc[rt][mt];
+              const int f = cun.nb * rows_nb + 16 * (wid * RW + rt) + 4 * (lane >> 4);
+              if constexpr (OUT == 1) {
+                *reinterpret_cast<float4*>(reinterpret_cast<float*>(y) + yrow + f) = make_float4(v[0], v[1], v[2], v[3]);
+              } else {
+                bf16x4 pk = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+                *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(y) + yrow + f) = pk;
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int rt = 0; rt < RW; ++rt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      cu += G;
+      if (cu < U) {
+        cun = gs_unit(cu, ERB, a, n, nrb, E, C::BM);
+        mact = (cun.rows + 15) / 16;
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup's LDS is released
+}
+
+template <int MT, int RW, int D, int OUT>
+void gs_launch(const bf16* xs, const bf16* W, const int* offsets, void* y, int R, int E, int e0, int Nw, int Ny, int K,
+               int G, bool pre, hipStream_t s) {
+  if (pre) grouped_stream_kernel<MT, RW, D, OUT, true><<<G, GS_THR, 0, s>>>(xs, W, offsets, y, R, Nw, Ny, K, E, e0);
+  else grouped_stream_kernel<MT, RW, D, OUT, false><<<G, GS_THR, 0, s>>>(xs, W, offsets, y, R, Nw, Ny, K, E, e0);
+}
+
+template <int MT, int RW, int D>
+void gs_launch_out(int out, const bf16* xs, const bf16* W, const int* offsets, void* y, int R, int E, int e0, int Nw,
+                   int Ny, int K, int G, bool pre, hipStream_t s) {
+  if (out == 2) gs_launch<MT, RW, D, 2>(xs, W, offsets, y, R, E, e0, Nw, Ny, K, G, pre, s);
+  else if (out == 1) gs_launch<MT, RW, D, 1>(xs, W, offsets, y, R, E, e0, Nw, Ny, K, G, pre, s);
+  else gs_launch<MT, RW, D, 0>(xs, W, offsets, y, R, E, e0, Nw, Ny, K, G, pre, s);
+}
+
+int g_gs_policy = 1;  // grouped_stream with row-major weights: 0 never, 1 where it measured faster, 2 always
+int g_gs_rw = 0;      // weight tiles per wave: 0 = by the unit count, 2, 4
+int g_gs_cus = 0;
+
+// E_all: experts of the global numbering (the routed rows R spread over them)
+bool launch_grouped_stream(const bf16* xs, const bf16* W, const int* offsets, void* y, int R, int E, int E_all, int e0,
+                           int N, int K, int out) {
+  (void)y;
+  if (g_gs_policy == 0 || E > GS_EMAX || K % 64 || K > (1 << 16)) return false;
+  const int RW = 2;
+  const int Nw = out == 2 ? 2 * N : N;
+  if ((out == 2 ? N % (32 * RW) : N % (64 * RW)) != 0) return false;
+  if ((long long)Nw * K * 2 >= 0x7fffffffLL) return false;  // one expert's weights within one buffer descriptor
+  const int avg = (R + E_all - 1) / std::max(1, E_all);
+  // auto, row-major weights (bench/kernels/bench_grouped.py, profiles/r5/grouped_stream.jsonl): the stream beats
+  // the tile kernel on w2-shaped launches up to ~80 rows per expert (fragment loads of 16 rows x 64 B), never
+  // clearly on SwiGLU gate/up; preshuffled weights always take the stream (launch_grouped_gemm's `pre`)
+  if (g_gs_policy == 1 && (out == 2 || avg > 80)) return false;
+  return true;
+}
+
 // out[t] (fp32 [T][d]) = sum_j w[t][j] * y[dst[t][j]] over assignments whose expert is in
 // [e_lo, e_hi) (the experts this rank computed); y is a LinOut over R rows
 __global__ __launch_bounds__(256) void moe_combine_kernel(LinOut y, int R, const int* __restrict__ dst,
@@ -733,9 +1060,45 @@ void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, fl
 }
 
 // out: 0 bf16 [R][N], 1 fp32 [R][N], 2 SwiGLU act bf16 [R][N] with W holding 2N rows per expert
+void set_grouped_stream_policy(int p) {
+  g_gs_policy = p % 10;
+  g_gs_rw = p / 10;  // tens digit: weight tiles per wave (0 = auto)
+}
+
 void launch_grouped_gemm(const bf16* xs, const bf16* W, const int* offsets, void* y, int R, int E, int e0, int N,
-                         int K, int out, hipStream_t s) {
+                         int K, int out, hipStream_t s, int E_all, bool pre) {
   if (R == 0) return;
+  if (pre || launch_grouped_stream(xs, W, offsets, y, R, E, E_all > 0 ? E_all : E, e0, N, K, out)) {
+    if (!g_gs_cus) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&g_gs_cus, hipDeviceAttributeMultiprocessorCount, dev);
+      g_gs_cus = std::max(8, g_gs_cus);
+    }
+    const int Nw = out == 2 ? 2 * N : N;
+    const int avg = (R + std::max(1, E_all > 0 ? E_all : E) - 1) / std::max(1, E_all > 0 ? E_all : E);
+    // unit rows: twice the mean segment (routing is uneven: a segment past the unit streams its weights again,
+    // and extra units leave a partial last round), the compute skipping the unit's empty token tiles
+    const int want = 2 * avg;
+    const int MT = want <= 128 ? 8 : want <= 192 ? 12 : 16;
+    // RW = 4 halves the activation LDS reads per weight byte, but its units (256 weight rows) must still
+    // give every CU work: taken when there are >= 3 units per CU, at 128-row units (it spills at 192)
+    const int rows4 = out == 2 ? 128 : 256;
+    int RW = g_gs_rw;
+    if (RW != 2 && RW != 4) RW = MT == 8 && (long long)((out == 2 ? N : Nw) / rows4) * E >= 3LL * g_gs_cus ? 4 : 2;
+    if (MT != 8 || (out == 2 ? N : Nw) % rows4) RW = 2;
+    const int NB = (out == 2 ? N : Nw) / (RW == 4 ? rows4 : rows4 / 2);
+    const long long upper = (long long)NB * ((R + 16 * MT - 1) / (16 * MT) + E);
+    const int G = (int)std::min<long long>(g_gs_cus, upper);
+    if (RW == 4 && MT == 8) {
+      gs_launch_out<8, 4, 4>(out, xs, W, offsets, y, R, E, e0, Nw, N, K, G, pre, s);
+    } else {
+      if (MT == 8) gs_launch_out<8, 2, 8>(out, xs, W, offsets, y, R, E, e0, Nw, N, K, G, pre, s);
+      else if (MT == 12) gs_launch_out<12, 2, 5>(out, xs, W, offsets, y, R, E, e0, Nw, N, K, G, pre, s);
+      else gs_launch_out<16, 2, 4>(out, xs, W, offsets, y, R, E, e0, Nw, N, K, G, pre, s);
+    }
+    return;
+  }
   const int ntile = out == 2 ? N / 64 : N / GG_BN;
   const dim3 grid(ntile, (R + GG_BM - 1) / GG_BM + E);
   const size_t lds = 4 * GG_TILE_BYTES;

@@ -30,6 +30,11 @@ import torch
 from .. import ops
 
 SKINNY_ROWS = 64
+# mean routed rows per expert up to which prefill takes the weight-streaming grouped GEMM on the preshuffled expert
+# copies (bench/kernels/bench_grouped.py, profiles/r5/grouped_stream.jsonl: at 64 rows w13 469 -> 358 us, w2 300 ->
+# 165; from ~128 rows the tile kernel is as fast on w13, and on w2 once uneven routing spills segments past the
+# 256-row unit: Mixtral 4 x 128-token prefill w2 324 vs 318 us, profiles/r5/prof_mixtral_prefill_4x128_stream.csv)
+PRE_ROWS = int(os.environ.get("SYMMETRY_MOE_PRE_ROWS", "100"))
 # "auto": expert all-to-all from this many tokens (prefill); decode steps (<= 64 rows under MoE) all-reduce
 A2A_ROWS = int(os.environ.get("SYMMETRY_MOE_A2A_ROWS", "128"))
 GROUPED = os.environ.get("SYMMETRY_MOE_GROUPED", "1") != "0"  # A/B: 0 = per-expert library GEMMs (host sync)
@@ -60,12 +65,43 @@ class MoEBlock:
         self.a2a_bytes = {"dispatch": 0, "return": 0, "routed_rows": 0, "padded_dispatch": 0, "gather": 0}
         # router rows padded to a multiple of 16 for the skinny GEMM (padded logits are never read)
         self.router = {}
+        self.pre = self._preshuffled_copies(model)
+        pol = os.environ.get("SYMMETRY_MOE_STREAM_POLICY")  # A/B: grouped_gemm's row-major streaming policy
+        if pol is not None and model.device.type == "cuda":
+            ops.grouped_stream_policy(int(pol))
         Ep = (self.E + 15) // 16 * 16
         for i in range(cfg.num_layers):
             r = model.w.layer(i, "router")
             pad = torch.zeros(Ep, r.shape[1], dtype=r.dtype, device=r.device)
             pad[: self.E] = r
             self.router[i] = pad
+
+    @staticmethod
+    def _preshuffled_copies(model) -> dict:
+        """MFMA-preshuffled copies of the expert weights for the weight-streaming grouped GEMM of prefill-sized
+        routed batches (csrc/kernels/moe.hip grouped_stream_kernel: fragment loads of 1 KB contiguous; Mixtral at
+        64-128 rows per expert: w2 303 -> 153 / 331 -> 212 us, w13 430 -> 352 us, profiles/r5/grouped_stream.jsonl).
+        The row-major tensors stay for decode (grouped skinny) and large batches (tile kernel), so this is one
+        extra copy: w2 first (the larger win), then w13, from 40 % of the free HBM (Mixtral on one GPU: w2 only)."""
+        mode = os.environ.get("SYMMETRY_MOE_PRESHUFFLE", "auto")
+        dev = model.device
+        if mode == "0" or dev.type != "cuda" or not GROUPED:
+            return {}
+        cfg = model.cfg
+        budget = float("inf") if mode == "1" else 0.4 * torch.cuda.mem_get_info(dev)[0]
+        out = {}
+        for name in ("w2", "w13"):
+            ws = [model.w.layer(i, name) for i in range(cfg.num_layers)]
+            if any(w.shape[1] % 16 or w.shape[2] % 32 for w in ws):
+                continue
+            need = sum(w.numel() * 2 for w in ws)
+            if need > budget:
+                break
+            budget -= need
+            for i, w in enumerate(ws):
+                E, N, K = w.shape
+                out[(i, name)] = w.reshape(E, N // 16, 16, K // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous().view(E, N, K)
+        return out
 
     def _buf(self, name, shape, dtype):
         return self.m._buf("moe." + name, shape, dtype)
@@ -164,10 +200,17 @@ class MoEBlock:
             ops.grouped_skinny(act, w2, offsets, e_lo, y2)
             return y2
         if self._grouped_ok(d):
-            # prefill-sized: grouped MFMA GEMMs, SwiGLU fused into the gate/up epilogue
-            ops.grouped_gemm(xs, w13, offsets, e_lo, act, ops.GROUPED_SWIGLU)
+            # prefill-sized: grouped MFMA GEMMs, SwiGLU fused into the gate/up epilogue; up to PRE_ROWS routed rows
+            # per expert the weight-streaming kernel on the preshuffled copies, beyond it the tile kernel
+            stream = R <= PRE_ROWS * self.E
+            p13 = self.pre.get((i, "w13")) if stream else None
+            p2 = self.pre.get((i, "w2")) if stream else None
+            ops.grouped_gemm(xs, w13 if p13 is None else p13, offsets, e_lo, act,
+                             ops.GROUPED_SWIGLU + (0 if p13 is None else ops.GROUPED_PRESHUFFLED))
             y2 = self._buf("y2f" if out_f32 else "y2b", (R, d), torch.float32 if out_f32 else torch.bfloat16)
-            ops.grouped_gemm(act, w2, offsets, e_lo, y2, ops.GROUPED_F32 if out_f32 else ops.GROUPED_BF16)
+            ops.grouped_gemm(act, w2 if p2 is None else p2, offsets, e_lo, y2,
+                             (ops.GROUPED_F32 if out_f32 else ops.GROUPED_BF16)
+                             + (0 if p2 is None else ops.GROUPED_PRESHUFFLED))
             return y2
         # shapes outside the grouped kernel's tiling (not the registered models): per-expert library GEMMs
         offs = offsets.tolist()

@@ -316,6 +316,7 @@ def moe_scatter(x, ids, k, G, offsets, cursor, xs, dst, src_tok=None):
 
 
 GROUPED_BF16, GROUPED_F32, GROUPED_SWIGLU = 0, 1, 2
+GROUPED_PRESHUFFLED = 4  # + mode: W MFMA-preshuffled per expert (models/layout.py::preshuffle)
 
 
 def grouped_gemm(xs, W, offsets, e0, y, mode):
@@ -323,6 +324,13 @@ def grouped_gemm(xs, W, offsets, e0, y, mode):
     if _gpu(xs):
         return _native.ops().grouped_gemm(xs, W, offsets, int(e0), y, int(mode))
     return reference.grouped_gemm(xs, W, offsets, e0, y, mode)
+
+
+def grouped_stream_policy(p: int) -> None:
+    """grouped_gemm's weight-streaming kernel on row-major weights (csrc/kernels/moe.hip grouped_stream_kernel):
+    0 never, 1 where it measured faster (default), 2 always (where the shapes tile); + 10 x (2 or 4): weight tiles
+    per wave instead of the automatic choice.  Preshuffled weights always take the streaming kernel."""
+    _native.ops().grouped_stream_policy(int(p))
 
 
 def grouped_skinny(xs, W, offsets, e0, y):

@@ -416,7 +416,13 @@ def moe_scatter(x, ids, k: int, G: int, offsets, cursor, xs, dst, src_tok=None) 
 
 
 def grouped_gemm(xs, W, offsets, e0: int, y, mode: int) -> None:
-    """Y[rows of e] = Xs[rows of e] . W[e]^T (mode 0 bf16 / 1 fp32), or SwiGLU of the [gate; up] product."""
+    """Y[rows of e] = Xs[rows of e] . W[e]^T (mode 0 bf16 / 1 fp32), or SwiGLU of the [gate; up] product;
+    mode + 4: W MFMA-preshuffled per expert."""
+    if mode & 4:
+        from ..models.layout import unshuffle
+
+        W = torch.stack([unshuffle(W[e]) for e in range(W.shape[0])])
+        mode &= 3
     for e in range(W.shape[0]):
         a, b = int(offsets[e0 + e]), int(offsets[e0 + e + 1])
         if b <= a:

@@ -458,12 +458,24 @@ def test_prefill_graphs_match_oracle(gpu, monkeypatch):
     assert not any(isinstance(k[0], str) for k in eager.runner.graphs) and eager.runner.prefill_graph_replays == 0
 
 
+@pytest.mark.parametrize("policy", [0, 2])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-@pytest.mark.parametrize("counts", [(300, 0, 129, 1, 640, 77, 0, 200), (3, 2, 1, 0, 0, 0, 0, 300)])
-def test_grouped_gemm_vs_fp32(gpu, mode, counts):
+@pytest.mark.parametrize("counts", [(300, 0, 129, 1, 640, 77, 0, 200), (3, 2, 1, 0, 0, 0, 0, 300),
+                                    (90, 60, 100, 70, 95, 85, 80, 96), (150, 170, 180, 120, 160, 175, 140, 190)])
+def test_grouped_gemm_vs_fp32(gpu, mode, counts, policy):
     """Grouped MFMA GEMM (K12) over uneven expert segments (empty ones, a 1-row one, multi-tile ones) with
     the segment bounds read on the device: bf16 / fp32 outputs and the fused SwiGLU epilogue, against fp32
-    products; rows outside every segment are never written."""
+    products; rows outside every segment are never written.  policy 0: the 128 x 128 tile kernel; 2: the
+    weight-streaming kernel (its 128 / 192 / 256-row unit variants by the mean segment, segments longer than
+    a unit split over several, an expert-parallel slice)."""
+    ops.grouped_stream_policy(policy)
+    try:
+        _grouped_case(gpu, mode, counts)
+    finally:
+        ops.grouped_stream_policy(1)
+
+
+def _grouped_case(gpu, mode, counts):
     E, d, F = 8, 512, 384
     g = torch.Generator(device=gpu).manual_seed(sum(counts) + mode)
     R = sum(counts)
@@ -492,6 +504,45 @@ def test_grouped_gemm_vs_fp32(gpu, mode, counts):
         torch.testing.assert_close(yc[a:b], p, atol=tol, rtol=tol)
         written[a:b] = True
     assert torch.all(yc[~written] == 7.0)
+
+
+@pytest.mark.parametrize("pre", [False, True])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_grouped_stream_mixtral_shapes(gpu, mode, pre):
+    """The weight-streaming grouped GEMM on Mixtral's expert shapes (K = 4096 for w13 with the SwiGLU
+    epilogue, K = 14336 for w2 with fp32 rows) at ~128 routed rows per expert, against fp32 products; row-major
+    and MFMA-preshuffled expert weights."""
+    E = 8
+    K, Nw = (4096, 2 * 512) if mode == 2 else (14336, 512)
+    counts = (131, 118, 140, 97, 126, 150, 110, 152)
+    g = torch.Generator(device=gpu).manual_seed(mode)
+    R = sum(counts)
+    off = torch.zeros(E + 1, dtype=torch.int32)
+    off[1:] = torch.cumsum(torch.tensor(counts), 0)
+    xs = torch.randn(R, K, device=gpu, generator=g).bfloat16()
+    W = (torch.randn(E, Nw, K, device=gpu, generator=g) * 0.02).bfloat16()
+    N = Nw // 2 if mode == 2 else Nw
+    y = torch.zeros(R, N, device=gpu, dtype=torch.float32 if mode == 1 else torch.bfloat16)
+    ops.grouped_stream_policy(2)
+    try:
+        if pre:
+            from symmetry_amd.models.layout import preshuffle
+
+            Wp = torch.stack([preshuffle(W[e]) for e in range(E)])
+            ops.grouped_gemm(xs, Wp, off.to(gpu), 0, y, mode + 4)
+        else:
+            ops.grouped_gemm(xs, W, off.to(gpu), 0, y, mode)
+        torch.cuda.synchronize()
+    finally:
+        ops.grouped_stream_policy(1)
+    yc, xc, Wc = y.float().cpu(), xs.float().cpu(), W.float().cpu()
+    for e in range(E):
+        a, b = int(off[e]), int(off[e + 1])
+        p = xc[a:b] @ Wc[e].t()
+        if mode == 2:
+            p = torch.nn.functional.silu(p[:, :N]) * p[:, N:]
+        tol = 2e-2 if mode == 2 else 2e-3
+        torch.testing.assert_close(yc[a:b], p, atol=tol, rtol=tol)
 
 
 def test_mixtral_prefill_grouped_path_matches_oracle(gpu):
