@@ -434,10 +434,39 @@ void grouped_gemm(const Tensor& xs, const Tensor& W, const Tensor& offsets, int6
   TORCH_CHECK(xs.size(1) == K && y.size(0) >= R && y.size(1) == N, "grouped_gemm: shape mismatch");
   TORCH_CHECK(K % 64 == 0 && (mode == 2 ? N % 64 == 0 : N % 128 == 0), "grouped_gemm: K % 64, N % 128 (SwiGLU: F % 64)");
   TORCH_CHECK(E >= 1 && E <= 64 && e0 >= 0 && offsets.numel() >= e0 + E + 1, "grouped_gemm: offsets must cover e0..e0+E");
-  TORCH_CHECK(!pre || E <= 8, "grouped_gemm: preshuffled weights take the streaming path (<= 8 local experts)");
+  TORCH_CHECK(!pre || (E <= 8 && K % 256 == 0),
+              "grouped_gemm: preshuffled weights take the streaming path (<= 8 local experts, K % 256)");
   const at::OptionalDeviceGuard g(xs.device());
   launch_grouped_gemm(ptr<bf16>(xs), ptr<bf16>(W), ptr<int>(offsets), y.data_ptr(), (int)R, (int)E, (int)e0, (int)N,
                       (int)K, (int)mode, cur_stream(xs), (int)(offsets.numel() - 1), pre);
+}
+
+// Dense medium-M projection on the weight-streaming kernel: mode 1 -> fp32 slabs y [S, M, N]; mode 3 -> SwiGLU of
+// the decode layout's tile-interleaved gate/up rows, y = act bf16 [M, N / 2].  W MFMA-preshuffled [N, K].
+void sgemm(const Tensor& x, const Tensor& Wshuf, Tensor& y, int64_t mode) {
+  check_gpu(x, "x");
+  check_gpu(Wshuf, "Wshuf");
+  check_gpu(y, "y");
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(Wshuf, at::kBFloat16, "Wshuf");
+  check_dtype(y, mode == 1 ? at::kFloat : at::kBFloat16, "y");
+  TORCH_CHECK(mode == 1 || mode == 3, "sgemm: mode 1 (fp32 slabs) or 3 (interleaved SwiGLU)");
+  TORCH_CHECK(x.dim() == 2 && Wshuf.dim() == 2 && x.is_contiguous() && Wshuf.is_contiguous() && y.is_contiguous(),
+              "sgemm: x [M, K], W [N, K] contiguous");
+  const int64_t M = x.size(0), K = x.size(1), N = Wshuf.size(0);
+  TORCH_CHECK(Wshuf.size(1) == K && M >= 1 && M <= 256 && N % 128 == 0 && K % 64 == 0, "sgemm: M <= 256, N % 128, K % 64");
+  int64_t S = 1;
+  if (mode == 1) {
+    TORCH_CHECK(y.dim() == 3 && y.size(1) == M && y.size(2) == N, "sgemm: y [S, M, N]");
+    S = y.size(0);
+    TORCH_CHECK(S >= 1 && (K / 64) % S == 0 && (K / 64 / S) % 4 == 0, "sgemm: S must divide K / 256");
+  } else {
+    TORCH_CHECK(y.dim() == 2 && y.size(0) == M && y.size(1) == N / 2 && K % 256 == 0, "sgemm: y [M, N / 2], K % 256");
+  }
+  TORCH_CHECK((long long)N * K * 2 < 0x7fffffffLL, "sgemm: W within one buffer descriptor");
+  const at::OptionalDeviceGuard g(x.device());
+  launch_stream_gemm(ptr<bf16>(x), ptr<bf16>(Wshuf), y.data_ptr(), (int)M, (int)N, (int)K, (int)S, (int)mode,
+                     cur_stream(x));
 }
 
 void grouped_skinny(const Tensor& xs, const Tensor& W, const Tensor& offsets, int64_t e0, Tensor& y) {
@@ -1014,6 +1043,7 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("grouped_skinny(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y) -> ()", &grouped_skinny);
   m.def("grouped_gemm(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y, int mode) -> ()", &grouped_gemm);
   m.def("grouped_stream_policy(int p) -> ()", [](int64_t p) { set_grouped_stream_policy((int)p); });
+  m.def("sgemm(Tensor x, Tensor Wshuf, Tensor(a!) y, int mode) -> ()", &sgemm);
   m.def("moe_route(Tensor logits, int T, int k, int E, Tensor(a!) ids, Tensor(b!) w) -> ()", &moe_route);
   m.def("moe_align(Tensor ids, int G, Tensor(a!) counts, Tensor(b!) offsets, Tensor(c!) cursor) -> ()", &moe_align);
   m.def(

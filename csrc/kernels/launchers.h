@@ -240,8 +240,12 @@ void launch_moe_scatter(const bf16* x, int T, int d, int k, int E, const int* id
 // pre: W MFMA-preshuffled per expert (the weight-streaming path only)
 void launch_grouped_gemm(const bf16* xs, const bf16* W, const int* offsets, void* y, int R, int E, int e0, int N,
                          int K, int out, hipStream_t s, int E_all = 0, bool pre = false);
-// grouped_gemm's weight-streaming path: 0 never, 1 medium routed batches (default), 2 always
+// grouped_gemm's weight-streaming path on row-major weights: 0 never, 1 where it measured faster (default),
+// 2 always; + 10 x (2 | 4): weight tiles per wave
 void set_grouped_stream_policy(int p);
+// dense medium-M projection on the weight-streaming kernel (moe.hip): preshuffled W [N][K], x [M][K], M <= 256;
+// out 1: fp32 slabs y [S][M][N]; out 3: SwiGLU of tile-interleaved gate/up rows -> act bf16 [M][N / 2] (S = 1)
+void launch_stream_gemm(const bf16* x, const bf16* Wshuf, void* y, int M, int N, int K, int S, int out, hipStream_t s);
 void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, float* y, int R, int E, int e0, int N,
                            int K, int S, hipStream_t s);
 void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_lo, int e_hi, const float* w, int T, int k,

@@ -436,15 +436,20 @@ SYM_DEV GsUnit gs_unit(int u, int ERB, const int (&a)[GS_EMAX], const int (&n)[G
 // + 2 MT KB of activations) in flight -- the LDS alone (weights and activations both staged) held 96-128 KB,
 // and the activation bytes queued in front of the weights capped the stream at ~3 TB/s from 128 rows.
 // Per chunk g: wait for X(g) (W(g) is older), barrier, DMA X(g+D-1) into the slot chunk g-1 freed, MFMAs of
-// chunk g, then load W(g+D) into the register slot chunk g freed.  The chunk count is padded to a multiple of D
-// and loads past the last unit use a zero-range descriptor, so every iteration issues the same instructions
-// and one constant vmcnt covers every wait.
+// chunk g, then load W(g+D) into the register slot chunk g freed.  A unit is a whole number of ring turns and
+// loads past the last unit use a zero-range descriptor, so every iteration issues the same instructions and one
+// constant vmcnt covers every wait.
+//
+// Dense use (ops.sgemm, medium-M prefill projections): offsets == nullptr is ONE segment of R rows; S > 1 splits K
+// over S units per n-block, each writing its fp32 slab y[ks] (OUT 1; the LinOut consumers sum the slabs);
+// OUT 3 is SwiGLU on the decode layout's tile-interleaved gate/up rows (models/layout.py: tile j = gate rows
+// 8j.. then up rows 8j..; a lane's up partner is lane ^ 32).
 template <int MT, int RW, int D, int OUT, bool PRE>
 __global__ __launch_bounds__(GS_THR, 1) void grouped_stream_kernel(const bf16* __restrict__ xs,
                                                                    const bf16* __restrict__ W,
                                                                    const int* __restrict__ offsets,
                                                                    void* __restrict__ y, int R, int Nw, int Ny, int K,
-                                                                   int E, int e0) {
+                                                                   int E, int e0, int S) {
   using C = GsCfg<MT, RW, D>;
   __shared__ __attribute__((aligned(1024))) char smem[D * C::XB];
   asm volatile("" ::: "a0");  // accumulators may live in AGPRs
@@ -459,20 +464,19 @@ __global__ __launch_bounds__(GS_THR, 1) void grouped_stream_kernel(const bf16* _
     n[i] = 0;
     nrb[i] = 0;
     if (i < E) {
-      a[i] = offsets[e0 + i];
-      n[i] = max(0, min(offsets[e0 + i + 1], R) - a[i]);
+      a[i] = offsets ? offsets[e0 + i] : 0;
+      n[i] = offsets ? max(0, min(offsets[e0 + i + 1], R) - a[i]) : R;
       nrb[i] = (n[i] + C::BM - 1) / C::BM;
       ERB += nrb[i];
     }
   }
   const int rows_nb = OUT == 2 ? 32 * RW : 64 * RW;  // expert-local weight rows per n-block (SwiGLU: gate rows)
   const int NB = (OUT == 2 ? Ny : Nw) / rows_nb;
-  const int U = NB * ERB;
+  const int U = NB * ERB * S;
   const int G = gridDim.x;
   if ((int)blockIdx.x >= U) return;  // uniform: the whole workgroup
-  const int nch = K / 64;
-  const int T = ((U - 1 - (int)blockIdx.x) / G + 1) * nch;  // chunks this workgroup streams
-  const int TP = (T + D - 1) / D * D;                       // padded to whole ring turns
+  const int nch = K / 64 / S;  // chunks per unit (its k slice)
+  const int T = ((U - 1 - (int)blockIdx.x) / G + 1) * nch;  // chunks this workgroup streams (nch % D == 0)
 
   // ---- per-lane offsets (unit-invariant: the unit lives in the descriptor bases)
   int vx[C::NX];
@@ -491,22 +495,24 @@ __global__ __launch_bounds__(GS_THR, 1) void grouped_stream_kernel(const bf16* _
   char* const dx = smem + (C::NX * wid) * 1024;
 
   // ---- issue cursors: activations (unit xu, chunk xc) and weights (unit wu, chunk wc)
-  int xu = blockIdx.x, xc = 0, wu = blockIdx.x, wc = 0;
+  int xu = blockIdx.x, xc = 0, wu = blockIdx.x, wc = 0, xk0 = 0, wk0 = 0;  // xk0 / wk0: the unit's first chunk
   const bf16* xb = xs;
   const bf16* wb = W;
   long long xbytes = 0, wbytes = 0;
   auto bind_x = [&](int u) {
     xbytes = 0;
     if (u < U) {
-      const GsUnit un = gs_unit(u, ERB, a, n, nrb, E, C::BM);
+      const GsUnit un = gs_unit(u / S, ERB, a, n, nrb, E, C::BM);
       xb = xs + (long long)un.row0 * K;
       xbytes = (long long)un.rows * K * 2;
+      xk0 = (u % S) * nch;
     }
   };
   auto bind_w = [&](int u) {
     wbytes = 0;
     if (u < U) {
-      const GsUnit un = gs_unit(u, ERB, a, n, nrb, E, C::BM);
+      const GsUnit un = gs_unit(u / S, ERB, a, n, nrb, E, C::BM);
+      wk0 = (u % S) * nch;
       const long long wrow = (long long)un.e * Nw + (long long)un.nb * rows_nb;
       wb = W + wrow * K;
       wbytes = ((long long)un.e * Nw + Nw - wrow) * K * 2;
@@ -517,7 +523,7 @@ __global__ __launch_bounds__(GS_THR, 1) void grouped_stream_kernel(const bf16* _
   auto issue_x = [&](int slot) {
     const __amdgpu_buffer_rsrc_t rx = gs_rsrc(xb, xbytes);
 #pragma unroll
-    for (int i = 0; i < C::NX; ++i) gs_dma(rx, vx[i], xc * 128, dx + slot * C::XB + i * 1024);
+    for (int i = 0; i < C::NX; ++i) gs_dma(rx, vx[i], (xk0 + xc) * 128, dx + slot * C::XB + i * 1024);
     if (++xc == nch) {
       xc = 0;
       xu += G;
@@ -527,7 +533,7 @@ __global__ __launch_bounds__(GS_THR, 1) void grouped_stream_kernel(const bf16* _
   bf16x8 wr[D][RW][2];
   auto issue_w = [&](bf16x8 (&dst)[RW][2]) {
     const __amdgpu_buffer_rsrc_t rw = gs_rsrc(wb, wbytes);
-    const int so = PRE ? wc * 2048 : wc * 128;
+    const int so = PRE ? (wk0 + wc) * 2048 : (wk0 + wc) * 128;
 #pragma unroll
     for (int rt = 0; rt < RW; ++rt)
 #pragma unroll
@@ -552,7 +558,7 @@ __global__ __launch_bounds__(GS_THR, 1) void grouped_stream_kernel(const bf16* _
     for (int mt = 0; mt < MT; ++mt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   int cu = blockIdx.x, cc = 0;
-  GsUnit cun = gs_unit(cu, ERB, a, n, nrb, E, C::BM);
+  GsUnit cun = gs_unit(cu / S, ERB, a, n, nrb, E, C::BM);
   int mact = (cun.rows + 15) / 16;
 
   // prologue in the steady state's order: W(0), then X(c), W(c + 1) for c = 0 .. D-2
@@ -563,7 +569,7 @@ __global__ __launch_bounds__(GS_THR, 1) void grouped_stream_kernel(const bf16* _
     issue_w(wr[c + 1]);
   }
 
-  for (int g0 = 0; g0 < TP; g0 += D) {
+  for (int g0 = 0; g0 < T; g0 += D) {
 #pragma unroll
     for (int j = 0; j < D; ++j) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::VM_KEEP) : "memory");
@@ -589,47 +595,69 @@ __global__ __launch_bounds__(GS_THR, 1) void grouped_stream_kernel(const bf16* _
         }
       }
       issue_w(wr[j]);  // W(g + D) into the register slot chunk g freed
-      if (++cc < nch || cu >= U) continue;
-      // ---- unit done: epilogue, lane holds features 4 (lane >> 4) .. + 3 of routed row 16 mt + (lane & 15)
-      cc = 0;
+    }
+    // a unit is a whole number of ring turns (host-checked nch % D == 0): its epilogue stays out of the unrolled
+    // body (inside it the SwiGLU variant's code size stopped the unroll and the register ring went to scratch)
+    cc += D;
+    if (cc < nch || cu >= U) continue;
+    // ---- unit done: epilogue, lane holds features 4 (lane >> 4) .. + 3 of routed row 16 mt + (lane & 15)
+    cc = 0;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int m = 16 * mt + (lane & 15);
-        if (mt < mact && m < cun.rows) {
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = 16 * mt + (lane & 15);
+      if constexpr (OUT == 3) {  // the up half of each tile sits 32 lanes over: exchange before any lane exits
+        f32x4 up[RW];
+#pragma unroll
+        for (int rt = 0; rt < RW; ++rt)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) up[rt][q] = __shfl_xor(acc[rt][mt][q], 32, 64);
+        if (mt < mact && m < cun.rows && lane < 32) {
           const long long yrow = (long long)(cun.row0 + m) * Ny;
-          if constexpr (OUT == 2) {
 #pragma unroll
-            for (int p = 0; p < RW / 2; ++p) {
-              const f32x4 gt = acc[2 * p][mt], up = acc[2 * p + 1][mt];
-              const int f = cun.nb * rows_nb + 16 * (wid * (RW / 2) + p) + 4 * (lane >> 4);
-              float o[4];
+          for (int rt = 0; rt < RW; ++rt) {
+            const f32x4 gt = acc[rt][mt];
+            const int f = 8 * (cun.nb * (rows_nb / 16) + wid * RW + rt) + 4 * (lane >> 4);
+            float o[4];
 #pragma unroll
-              for (int q = 0; q < 4; ++q) o[q] = gt[q] / (1.f + __expf(-gt[q])) * up[q];
-              bf16x4 pk = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+            for (int q = 0; q < 4; ++q) o[q] = gt[q] / (1.f + __expf(-gt[q])) * up[rt][q];
+            bf16x4 pk = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+            *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(y) + yrow + f) = pk;
+          }
+        }
+      } else if (mt < mact && m < cun.rows) {
+        const long long yrow = ((long long)(cu % S) * R + cun.row0 + m) * Ny;
+        if constexpr (OUT == 2) {
+#pragma unroll
+          for (int p = 0; p < RW / 2; ++p) {
+            const f32x4 gt = acc[2 * p][mt], up = acc[2 * p + 1][mt];
+            const int f = cun.nb * rows_nb + 16 * (wid * (RW / 2) + p) + 4 * (lane >> 4);
+            float o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = gt[q] / (1.f + __expf(-gt[q])) * up[q];
+            bf16x4 pk = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+            *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(y) + yrow + f) = pk;
+          }
+        } else {
+#pragma unroll
+          for (int rt = 0; rt < RW; ++rt) {
+            const f32x4 v = acc[rt][mt];
+            const int f = cun.nb * rows_nb + 16 * (wid * RW + rt) + 4 * (lane >> 4);
+            if constexpr (OUT == 1) {
+              *reinterpret_cast<float4*>(reinterpret_cast<float*>(y) + yrow + f) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+              bf16x4 pk = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
               *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(y) + yrow + f) = pk;
-            }
-          } else {
-#pragma unroll
-            for (int rt = 0; rt < RW; ++rt) {
-              const f32x4 v = acc[rt][mt];
-              const int f = cun.nb * rows_nb + 16 * (wid * RW + rt) + 4 * (lane >> 4);
-              if constexpr (OUT == 1) {
-                *reinterpret_cast<float4*>(reinterpret_cast<float*>(y) + yrow + f) = make_float4(v[0], v[1], v[2], v[3]);
-              } else {
-                bf16x4 pk = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-                *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(y) + yrow + f) = pk;
-              }
             }
           }
         }
+      }
 #pragma unroll
-        for (int rt = 0; rt < RW; ++rt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      cu += G;
-      if (cu < U) {
-        cun = gs_unit(cu, ERB, a, n, nrb, E, C::BM);
-        mact = (cun.rows + 15) / 16;
-      }
+      for (int rt = 0; rt < RW; ++rt) acc[rt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    cu += G;
+    if (cu < U) {
+      cun = gs_unit(cu / S, ERB, a, n, nrb, E, C::BM);
+      mact = (cun.rows + 15) / 16;
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup's LDS is released
@@ -637,9 +665,17 @@ __global__ __launch_bounds__(GS_THR, 1) void grouped_stream_kernel(const bf16* _
 
 template <int MT, int RW, int D, int OUT>
 void gs_launch(const bf16* xs, const bf16* W, const int* offsets, void* y, int R, int E, int e0, int Nw, int Ny, int K,
-               int G, bool pre, hipStream_t s) {
-  if (pre) grouped_stream_kernel<MT, RW, D, OUT, true><<<G, GS_THR, 0, s>>>(xs, W, offsets, y, R, Nw, Ny, K, E, e0);
-  else grouped_stream_kernel<MT, RW, D, OUT, false><<<G, GS_THR, 0, s>>>(xs, W, offsets, y, R, Nw, Ny, K, E, e0);
+               int G, bool pre, hipStream_t s, int S = 1) {
+  if (pre) grouped_stream_kernel<MT, RW, D, OUT, true><<<G, GS_THR, 0, s>>>(xs, W, offsets, y, R, Nw, Ny, K, E, e0, S);
+  else grouped_stream_kernel<MT, RW, D, OUT, false><<<G, GS_THR, 0, s>>>(xs, W, offsets, y, R, Nw, Ny, K, E, e0, S);
+}
+
+// dense medium-M projection on the streaming kernel (preshuffled W [N][K], x [M][K], M <= 256): out 1 -> fp32 slabs
+// y [S][M][N]; out 3 -> SwiGLU of the tile-interleaved gate/up rows, y = act bf16 [M][N / 2] (S = 1)
+template <int MT, int D>
+void sg_launch_mt(int out, const bf16* x, const bf16* W, void* y, int M, int N, int K, int S, int G, hipStream_t s) {
+  if (out == 3) grouped_stream_kernel<MT, 2, D, 3, true><<<G, GS_THR, 0, s>>>(x, W, nullptr, y, M, N, N / 2, K, 1, 0, 1);
+  else grouped_stream_kernel<MT, 2, D, 1, true><<<G, GS_THR, 0, s>>>(x, W, nullptr, y, M, N, N, K, 1, 0, S);
 }
 
 template <int MT, int RW, int D>
@@ -658,7 +694,7 @@ int g_gs_cus = 0;
 bool launch_grouped_stream(const bf16* xs, const bf16* W, const int* offsets, void* y, int R, int E, int E_all, int e0,
                            int N, int K, int out) {
   (void)y;
-  if (g_gs_policy == 0 || E > GS_EMAX || K % 64 || K > (1 << 16)) return false;
+  if (g_gs_policy == 0 || E > GS_EMAX || K % 256 || K > (1 << 16)) return false;  // K % 256: whole ring turns
   const int RW = 2;
   const int Nw = out == 2 ? 2 * N : N;
   if ((out == 2 ? N % (32 * RW) : N % (64 * RW)) != 0) return false;
@@ -1060,6 +1096,24 @@ void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, fl
 }
 
 // out: 0 bf16 [R][N], 1 fp32 [R][N], 2 SwiGLU act bf16 [R][N] with W holding 2N rows per expert
+void launch_stream_gemm(const bf16* x, const bf16* Wshuf, void* y, int M, int N, int K, int S, int out,
+                        hipStream_t s) {
+  if (M == 0) return;
+  if (!g_gs_cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&g_gs_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    g_gs_cus = std::max(8, g_gs_cus);
+  }
+  const int units = N / 128 * (M + 255) / 256 * S;
+  const int G = std::min(g_gs_cus, units);
+  const int nch = K / 64 / S;  // a multiple of 4 (checked by the op): whole ring turns per unit
+  if (M <= 128 && nch % 8 == 0) sg_launch_mt<8, 8>(out, x, Wshuf, y, M, N, K, S, G, s);
+  else if (M <= 128) sg_launch_mt<8, 4>(out, x, Wshuf, y, M, N, K, S, G, s);
+  else if (M <= 192) sg_launch_mt<12, 4>(out, x, Wshuf, y, M, N, K, S, G, s);
+  else sg_launch_mt<16, 4>(out, x, Wshuf, y, M, N, K, S, G, s);
+}
+
 void set_grouped_stream_policy(int p) {
   g_gs_policy = p % 10;
   g_gs_rw = p / 10;  // tens digit: weight tiles per wave (0 = auto)
@@ -1093,8 +1147,9 @@ void launch_grouped_gemm(const bf16* xs, const bf16* W, const int* offsets, void
     if (RW == 4 && MT == 8) {
       gs_launch_out<8, 4, 4>(out, xs, W, offsets, y, R, E, e0, Nw, N, K, G, pre, s);
     } else {
-      if (MT == 8) gs_launch_out<8, 2, 8>(out, xs, W, offsets, y, R, E, e0, Nw, N, K, G, pre, s);
-      else if (MT == 12) gs_launch_out<12, 2, 5>(out, xs, W, offsets, y, R, E, e0, Nw, N, K, G, pre, s);
+      if (MT == 8 && (K / 64) % 8 == 0) gs_launch_out<8, 2, 8>(out, xs, W, offsets, y, R, E, e0, Nw, N, K, G, pre, s);
+      else if (MT == 8) gs_launch_out<8, 2, 4>(out, xs, W, offsets, y, R, E, e0, Nw, N, K, G, pre, s);
+      else if (MT == 12) gs_launch_out<12, 2, 4>(out, xs, W, offsets, y, R, E, e0, Nw, N, K, G, pre, s);
       else gs_launch_out<16, 2, 4>(out, xs, W, offsets, y, R, E, e0, Nw, N, K, G, pre, s);
     }
     return;

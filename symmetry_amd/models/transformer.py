@@ -85,6 +85,11 @@ MG_FUSED_GU = MG_FUSED_MODE == "gu"
 # faster numbers measured earlier came from replayed graphs whose edge-counter memset had stopped working).
 # "auto": TP >= 2 with a GPU per rank (SYMMETRY_ENGINE_TP1=1: also TP = 1); "1": wherever the shape class is built;
 # "0" (default): the per-layer launches.
+# medium-M prefill projections (STREAM_MIN_M..256 rows) on the weight-streaming kernel (ops.sgemm: weights
+# straight into VGPRs from the preshuffled copies, activations through an LDS ring; gate_up with the SwiGLU epilogue)
+# instead of mgemm / hipBLASLt + swiglu
+STREAM_DENSE = os.environ.get("SYMMETRY_STREAM_DENSE", "0") != "0"
+STREAM_MIN_M = int(os.environ.get("SYMMETRY_STREAM_MIN_M", "65"))
 DECODE_ENGINE = os.environ.get("SYMMETRY_DECODE_ENGINE", "0")
 ENGINE_TP1 = os.environ.get("SYMMETRY_ENGINE_TP1", "0") != "0"
 # workgroups of the engine's grid (one per CU; a one-GPU multi-rank rehearsal gives each rank a share)
@@ -276,7 +281,11 @@ class TransformerLM:
         T, K = x.shape
         N = w.shape[0]
         pick = ops.choose_mgemm(T, N, K) if wshuf is not None else None
-        if pick is not None:
+        if STREAM_DENSE and wshuf is not None and STREAM_MIN_M <= T <= 256 and N % 128 == 0 and K % 256 == 0:
+            S = ops.sgemm_splits(T, N, K)
+            y = self._buf(name + ".slab", (S, T, N), torch.float32)
+            ops.sgemm(x, wshuf, y, 1)
+        elif pick is not None:
             rw, S = pick
             y = self._buf(name + ".slab", (S, T, N), torch.float32)
             ops.mgemm(x, wshuf, y, rw)
@@ -619,10 +628,17 @@ class TransformerLM:
                 mlp = self.moe.forward(i, x)
             else:
                 ops.add_rms_norm(o, resid, w.layer(i, "ln2"), eps, x)
-                gu = self._linear("gu", x, w.layer(i, "w_gu"), wshuf=self._shuf(i, "w_gu"))
-                F = gu.shape[-1] // 2
-                act = self._buf("act", (T, F), torch.bfloat16)
-                ops.swiglu(gu, act, interleaved=True)
+                gsh = self._shuf(i, "w_gu")
+                if (STREAM_DENSE and gsh is not None and STREAM_MIN_M <= T <= 256 and gsh.shape[0] % 128 == 0
+                        and gsh.shape[1] % 256 == 0):
+                    # gate_up + SwiGLU in one weight-streaming launch (no [T, 2F] intermediate)
+                    act = self._buf("act", (T, gsh.shape[0] // 2), torch.bfloat16)
+                    ops.sgemm(x, gsh, act, 3)
+                else:
+                    gu = self._linear("gu", x, w.layer(i, "w_gu"), wshuf=gsh)
+                    F = gu.shape[-1] // 2
+                    act = self._buf("act", (T, F), torch.bfloat16)
+                    ops.swiglu(gu, act, interleaved=True)
                 mlp = self._linear("down", act, w.layer(i, "w_down"), reduce=True, wshuf=self._shuf(i, "w_down"))
             nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
             ops.add_rms_norm(mlp, resid, nxt, eps, x)

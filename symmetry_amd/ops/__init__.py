@@ -326,6 +326,34 @@ def grouped_gemm(xs, W, offsets, e0, y, mode):
     return reference.grouped_gemm(xs, W, offsets, e0, y, mode)
 
 
+def sgemm(x, w_shuf, y, mode: int = 1):
+    """Dense medium-M projection (<= 256 rows) on the weight-streaming kernel (csrc/kernels/moe.hip): mode 1 ->
+    fp32 split-K slabs y [S, M, N] (the mgemm / skinny contract); mode 3 -> SwiGLU of the tile-interleaved gate/up
+    rows (models/layout.py), y = act bf16 [M, N / 2].  ``w_shuf``: the MFMA-preshuffled weight."""
+    if _gpu(x):
+        return _native.ops().sgemm(x, w_shuf, y, int(mode))
+    w = reference.unshuffled(w_shuf, True)
+    if mode == 3:
+        return reference.swiglu((x.float() @ w.float().t()).unsqueeze(0), y, True)
+    return reference.skinny_gemm(x, w, y)
+
+
+def sgemm_splits(M: int, N: int, K: int, cus: int = 256) -> int:
+    """k split of an sgemm fp32-slab launch: the smallest S (a divisor of K / 256: whole ring turns per unit)
+    whose N / 128 x S units fill >= 3/4 of the CUs in one round, else the largest single-round one."""
+    nb, nk = N // 128, K // 256
+    best = 1
+    for S in range(1, nk + 1):
+        if nk % S:
+            continue
+        if nb * S > cus:
+            break
+        best = S
+        if nb * S >= 3 * cus // 4:
+            break
+    return best
+
+
 def grouped_stream_policy(p: int) -> None:
     """grouped_gemm's weight-streaming kernel on row-major weights (csrc/kernels/moe.hip grouped_stream_kernel):
     0 never, 1 where it measured faster (default), 2 always (where the shapes tile); + 10 x (2 or 4): weight tiles
