@@ -48,6 +48,15 @@ def main():
         act = torch.randn(R, F, device=dev, generator=g).bfloat16()
         y13 = torch.empty(R, F, device=dev, dtype=torch.bfloat16)
         y2 = torch.empty(R, d, device=dev, dtype=torch.float32)
+        S13, S2 = ops.choose_splits(2 * F, d), ops.choose_splits(d, F)
+        y13s = torch.empty(S13, R, 2 * F, device=dev)
+        y2s = torch.empty(S2, R, d, device=dev)
+
+        def skinny13():
+            ops.grouped_skinny(xs, w13, offsets, 0, y13s)
+            ops.swiglu(y13s, y13)
+
+        skinny = {"w13_swiglu": skinny13, "w2_f32": lambda: ops.grouped_skinny(act, w2, offsets, 0, y2s)}
         for name, fn, wbytes in (("w13_swiglu", lambda pre=False: ops.grouped_gemm(xs, w13p if pre else w13, offsets, 0, y13,
                                                                                  2 + 4 * pre), w13.numel() * 2),
                                  ("w2_f32", lambda pre=False: ops.grouped_gemm(act, w2p if pre else w2, offsets, 0, y2,
@@ -55,11 +64,11 @@ def main():
             if name not in args.shapes.split(","):
                 continue
             for pol, kname in ((0, "tile128"), (2, "stream"), (2, "stream_pre"), (22, "stream_pre_rw2"),
-                               (42, "stream_pre_rw4")):
+                               (42, "stream_pre_rw4"), (1, "skinny")):
                 if kname not in args.kernels.split(","):
                     continue
                 ops.grouped_stream_policy(pol)
-                run = (lambda f=fn: f(True)) if kname.startswith("stream_pre") else fn
+                run = (lambda f=fn: f(True)) if kname.startswith("stream_pre") else (skinny[name] if kname == "skinny" else fn)
                 run()
                 torch.cuda.synchronize()
                 ts = []

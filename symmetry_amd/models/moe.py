@@ -35,6 +35,8 @@ SKINNY_ROWS = 64
 # 165; from ~128 rows the tile kernel is as fast on w13, and on w2 once uneven routing spills segments past the
 # 256-row unit: Mixtral 4 x 128-token prefill w2 324 vs 318 us, profiles/r5/prof_mixtral_prefill_4x128_stream.csv)
 PRE_ROWS = int(os.environ.get("SYMMETRY_MOE_PRE_ROWS", "100"))
+# decode steps stream the preshuffled copies from this many routed rows per local expert (every expert routed)
+STREAM_DECODE_ROWS = int(os.environ.get("SYMMETRY_MOE_STREAM_DECODE_ROWS", "4"))
 # "auto": expert all-to-all from this many tokens (prefill); decode steps (<= 64 rows under MoE) all-reduce
 A2A_ROWS = int(os.environ.get("SYMMETRY_MOE_A2A_ROWS", "128"))
 GROUPED = os.environ.get("SYMMETRY_MOE_GROUPED", "1") != "0"  # A/B: 0 = per-expert library GEMMs (host sync)
@@ -81,18 +83,20 @@ class MoEBlock:
         """MFMA-preshuffled copies of the expert weights for the weight-streaming grouped GEMM of prefill-sized
         routed batches (csrc/kernels/moe.hip grouped_stream_kernel: fragment loads of 1 KB contiguous; Mixtral at
         64-128 rows per expert: w2 303 -> 153 / 331 -> 212 us, w13 430 -> 352 us, profiles/r5/grouped_stream.jsonl).
-        The row-major tensors stay for decode (grouped skinny) and large batches (tile kernel), so this is one
-        extra copy: w2 first (the larger win), then w13, from 40 % of the free HBM (Mixtral on one GPU: w2 only)."""
+        Decode steps stream them too (1-8 rows per expert: w13 320 -> 299 us, w2 162 -> 144).  The row-major
+        tensors stay for the tile kernel (long segments), so this is one extra copy: w2 first (the larger win),
+        then w13, from half the free HBM (Mixtral on one GPU: both, 90 GB, leaving ~95 GB for the KV cache)."""
         mode = os.environ.get("SYMMETRY_MOE_PRESHUFFLE", "auto")
         dev = model.device
         if mode == "0" or dev.type != "cuda" or not GROUPED:
             return {}
         cfg = model.cfg
-        budget = float("inf") if mode == "1" else 0.4 * torch.cuda.mem_get_info(dev)[0]
+        budget = float("inf") if mode == "1" else 0.5 * torch.cuda.mem_get_info(dev)[0]
         out = {}
         for name in ("w2", "w13"):
             ws = [model.w.layer(i, name) for i in range(cfg.num_layers)]
-            if any(w.shape[1] % 16 or w.shape[2] % 32 for w in ws):
+            E, N, K = ws[0].shape  # the streaming kernel's tiling: <= 8 local experts, K % 256, 128-row n-blocks
+            if E > 8 or K % 256 or ((N // 2) % 64 if name == "w13" else N % 128):
                 continue
             need = sum(w.numel() * 2 for w in ws)
             if need > budget:
@@ -190,6 +194,29 @@ class MoEBlock:
         w2 = self.m.w.layer(i, "w2")
         F = self.F
         act = self._buf("act", (R, F), torch.bfloat16)
+        if STREAM_DECODE_ROWS * n_local <= R <= SKINNY_ROWS and ((i, "w13") in self.pre or (i, "w2") in self.pre):
+            # decode sizes on the preshuffled copies: the weight-streaming kernel (1 KB fragment loads, one unit per
+            # populated expert and n-block) beats the grouped skinny GEMM at 1-8 rows per expert when every expert
+            # is routed: w13 + SwiGLU 320 -> 299 us, w2 162 -> 144 (profiles/r5/grouped_stream.jsonl); with a few
+            # tokens (config 5: 4 clients, ~3 of 8 experts idle) its units leave a partial last round and the
+            # skinny GEMM's per-(tile, expert) grid balances better (85.6 vs 87.9 tok/s per client end to end)
+            p13, p2 = self.pre.get((i, "w13")), self.pre.get((i, "w2"))
+            if p13 is not None:
+                ops.grouped_gemm(xs, p13, offsets, e_lo, act, ops.GROUPED_SWIGLU + ops.GROUPED_PRESHUFFLED)
+            else:
+                s1 = ops.choose_splits(2 * F, d)
+                y1 = self._buf("y1", (s1, R, 2 * F), torch.float32)
+                ops.grouped_skinny(xs, w13, offsets, e_lo, y1)
+                ops.swiglu(y1, act)
+            if p2 is not None:
+                y2 = self._buf("y2f" if out_f32 else "y2b", (R, d), torch.float32 if out_f32 else torch.bfloat16)
+                ops.grouped_gemm(act, p2, offsets, e_lo, y2, (ops.GROUPED_F32 if out_f32 else ops.GROUPED_BF16)
+                                 + ops.GROUPED_PRESHUFFLED)
+                return y2
+            s2 = ops.choose_splits(d, F)
+            y2 = self._buf("y2", (s2, R, d), torch.float32)
+            ops.grouped_skinny(act, w2, offsets, e_lo, y2)
+            return y2
         if R <= SKINNY_ROWS:
             s1 = ops.choose_splits(2 * F, d)
             y1 = self._buf("y1", (s1, R, 2 * F), torch.float32)
