@@ -64,7 +64,7 @@ def main():
             if name not in args.shapes.split(","):
                 continue
             for pol, kname in ((0, "tile128"), (2, "stream"), (2, "stream_pre"), (22, "stream_pre_rw2"),
-                               (42, "stream_pre_rw4"), (1, "skinny")):
+                               (42, "stream_pre_rw4"), (1, "skinny"), (802, "stream_pre_mt8")):
                 if kname not in args.kernels.split(","):
                     continue
                 ops.grouped_stream_policy(pol)

@@ -688,6 +688,7 @@ void gs_launch_out(int out, const bf16* xs, const bf16* W, const int* offsets, v
 
 int g_gs_policy = 1;  // grouped_stream with row-major weights: 0 never, 1 where it measured faster, 2 always
 int g_gs_rw = 0;      // weight tiles per wave: 0 = by the unit count, 2, 4
+int g_gs_mt = 0;      // unit rows / 16: 0 = from the mean segment
 int g_gs_cus = 0;
 
 // E_all: experts of the global numbering (the routed rows R spread over them)
@@ -1116,7 +1117,8 @@ void launch_stream_gemm(const bf16* x, const bf16* Wshuf, void* y, int M, int N,
 
 void set_grouped_stream_policy(int p) {
   g_gs_policy = p % 10;
-  g_gs_rw = p / 10;  // tens digit: weight tiles per wave (0 = auto)
+  g_gs_rw = p / 10 % 10;  // tens digit: weight tiles per wave (0 = auto)
+  g_gs_mt = p / 100;      // hundreds: unit rows / 16 (8 / 12 / 16; 0 = from the mean segment)
 }
 
 void launch_grouped_gemm(const bf16* xs, const bf16* W, const int* offsets, void* y, int R, int E, int e0, int N,
@@ -1134,7 +1136,11 @@ void launch_grouped_gemm(const bf16* xs, const bf16* W, const int* offsets, void
     // unit rows: twice the mean segment (routing is uneven: a segment past the unit streams its weights again,
     // and extra units leave a partial last round), the compute skipping the unit's empty token tiles
     const int want = 2 * avg;
-    const int MT = want <= 128 ? 8 : want <= 192 ? 12 : 16;
+    // (SwiGLU gate/up: 128-row units always -- their 4-tile-per-wave variant outruns the larger units even when
+    // longer segments take two units: Mixtral w13 at 128 rows per expert 606 -> 468 us, tile kernel 598-614;
+    // profiles/r5/grouped_stream.jsonl)
+    const int MT = g_gs_mt == 8 || g_gs_mt == 12 || g_gs_mt == 16 ? g_gs_mt
+                   : (out == 2 || want <= 128) ? 8 : want <= 192 ? 12 : 16;
     // RW = 4 halves the activation LDS reads per weight byte, but its units (256 weight rows) must still
     // give every CU work: taken when there are >= 3 units per CU, at 128-row units (it spills at 192)
     const int rows4 = out == 2 ? 128 : 256;

@@ -35,6 +35,9 @@ SKINNY_ROWS = 64
 # 165; from ~128 rows the tile kernel is as fast on w13, and on w2 once uneven routing spills segments past the
 # 256-row unit: Mixtral 4 x 128-token prefill w2 324 vs 318 us, profiles/r5/prof_mixtral_prefill_4x128_stream.csv)
 PRE_ROWS = int(os.environ.get("SYMMETRY_MOE_PRE_ROWS", "100"))
+# gate/up (+ SwiGLU) streams further: 128-row units with 4 weight tiles per wave, longer segments in two units
+# (w13 at 128 rows per expert 468 vs 598-614 us on the tile kernel, at 160 rows 619-650 vs 673-707)
+PRE_ROWS_W13 = int(os.environ.get("SYMMETRY_MOE_PRE_ROWS_W13", "176"))
 # decode steps stream the preshuffled copies from this many routed rows per local expert (every expert routed)
 STREAM_DECODE_ROWS = int(os.environ.get("SYMMETRY_MOE_STREAM_DECODE_ROWS", "4"))
 # "auto": expert all-to-all from this many tokens (prefill); decode steps (<= 64 rows under MoE) all-reduce
@@ -229,9 +232,8 @@ class MoEBlock:
         if self._grouped_ok(d):
             # prefill-sized: grouped MFMA GEMMs, SwiGLU fused into the gate/up epilogue; up to PRE_ROWS routed rows
             # per expert the weight-streaming kernel on the preshuffled copies, beyond it the tile kernel
-            stream = R <= PRE_ROWS * self.E
-            p13 = self.pre.get((i, "w13")) if stream else None
-            p2 = self.pre.get((i, "w2")) if stream else None
+            p13 = self.pre.get((i, "w13")) if R <= PRE_ROWS_W13 * self.E else None
+            p2 = self.pre.get((i, "w2")) if R <= PRE_ROWS * self.E else None
             ops.grouped_gemm(xs, w13 if p13 is None else p13, offsets, e_lo, act,
                              ops.GROUPED_SWIGLU + (0 if p13 is None else ops.GROUPED_PRESHUFFLED))
             y2 = self._buf("y2f" if out_f32 else "y2b", (R, d), torch.float32 if out_f32 else torch.bfloat16)
