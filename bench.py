@@ -74,7 +74,40 @@ def _args():
     ap.add_argument("--max-batched-tokens", type=int, default=None, help="A/B: token budget of a pure-prefill step")
     ap.add_argument("--mixed-prefill-tokens", type=int, default=None, help="A/B: prompt budget of mixed steps")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra decode steps after timing (for rocprof)")
+    ap.add_argument("--verify-clients", type=int, default=2,
+                    help="after timing: check every token these clients received against the fp32 oracle (0: off)")
+    ap.add_argument("--verify-tol", type=float, default=VERIFY_TOL)
     return ap.parse_args()
+
+
+# A streamed token passes if its oracle logit is within this of the oracle's best at that position: the bf16
+# engine and the fp32 oracle differ by rounding, and a near-tie may go either way (tests/test_tp_gpu.py
+# _check_oracle).  A wrong kernel on the real shapes misses by whole logits, not by this.
+VERIFY_TOL = 0.08
+
+
+def verify_streams(eng, checks, group, tol):
+    """Every rank: the fp32 oracle (models/reference_model.py, teacher-forced over the streamed tokens) on the
+    engine's own weights; under TP each rank runs its shard and the oracle sums / gathers over ``group``.
+    ``checks`` (rank 0: [(prompt_ids, output_ids)], others: None) is broadcast first.  Returns the summary."""
+    import torch.distributed as dist
+
+    from symmetry_amd.models import reference_model as rm
+
+    if group is not None:
+        box = [checks]
+        dist.broadcast_object_list(box, src=0, group=eng.runner.cpu_group)
+        checks = box[0]
+    res = {"clients": len(checks), "tokens": 0, "mismatches": 0, "max_gap": 0.0, "tol": tol, "per_client": []}
+    for prompt, out in checks:
+        lg = rm.forward_logits(eng.weights, list(prompt) + list(out)[:-1], group=group)
+        r = rm.check_tokens(lg, len(prompt), list(out), tol)
+        del lg
+        res["per_client"].append(r)
+        res["tokens"] += r["tokens"]
+        res["mismatches"] += r["mismatches"]
+        res["max_gap"] = max(res["max_gap"], r["max_gap"])
+    return res
 
 
 SHARED_GPU_ENV = "SYMMETRY_BENCH_SHARED_GPU"
@@ -201,6 +234,8 @@ def main() -> int:
     if tp_worker:
         # mirror rank 0 (warmup, graph capture, timed steps, client-end run) until it stops the plane
         runner.worker_loop()
+        if args.verify_clients > 0:
+            verify_streams(eng, None, dist.group.WORLD, args.verify_tol)
         elapsed = runner.sync_times[1] - runner.sync_times[0] if len(runner.sync_times) >= 2 else 0.0
         _reduce_and_exit(group, elapsed, [], world)
         return 0
@@ -269,10 +304,19 @@ def main() -> int:
                                                     max_tokens=args.client_tokens))
         except Exception as exc:  # the engine-step measurement stands on its own
             client_end = {"error": f"{type(exc).__name__}: {exc}"}
+    # what the clients received must be the model's output: every streamed token of the first clients against
+    # the fp32 oracle of the same weights (a fast but wrong kernel fails the bench instead of posting a number)
+    checks = [(list(s.prompt_ids), list(s.output_ids)) for s in seqs[:max(0, args.verify_clients)]]
+    verified = None
     if parallel == "tp" and world > 1:
         eng.shutdown()
-    elif world > 1:
-        dist.barrier(group=group)
+        if checks:
+            verified = verify_streams(eng, checks, dist.group.WORLD, args.verify_tol)
+    else:
+        if checks:
+            verified = verify_streams(eng, checks, None, args.verify_tol)
+        if world > 1:
+            dist.barrier(group=group)
     elapsed, ttfts, rank_elapsed = _reduce(group, elapsed, ttfts, world, gather_ttft=parallel == "dp")
 
     p50_ttft = ttfts[len(ttfts) // 2] * 1e3
@@ -325,6 +369,8 @@ def main() -> int:
             line["tp"] = {"xgmi_calls": dict(getattr(tp, "calls", {})),
                           "prefill_allreduce_bytes_per_rank": dict(eng.model.tp_reduced_bytes),
                           "metadata_plane": type(runner.meta).__name__}
+        if verified is not None:
+            line["verified"] = verified
         if client_end is not None:
             line["client_end"] = client_end
             line["p50_ttft_ms"] = client_end.get("p50_ttft_ms")
@@ -334,6 +380,10 @@ def main() -> int:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if verified is not None and verified["mismatches"]:
+        print(f"bench: {verified['mismatches']} of {verified['tokens']} streamed tokens disagree with the fp32 "
+              "oracle", file=sys.stderr, flush=True)
+        return 3
     return 0
 
 

@@ -68,9 +68,6 @@ class LocalXgmi:
             self.calls["gemm_ar"] = self.calls.get("gemm_ar", 0) + 1
         return ok
 
-    def engine_xar_handle(self):
-        return -1  # world 1: the engine's O / down residual stays local (the fused launches' world-1 XAR does no push)
-
     def all_gather(self, t):
         import torch
 
@@ -89,13 +86,8 @@ def main():
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--max-model-len", type=int, default=2048)
-    ap.add_argument("--engine", type=int, default=0, help="1: decode steps as ONE persistent launch (decode_layers.hip)")
     args = ap.parse_args()
     import torch
-
-    from symmetry_amd.models import transformer as tr
-
-    tr.DECODE_ENGINE = "1" if args.engine else "0"
 
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
     from symmetry_amd.engine.sequence import SamplingParams
@@ -130,7 +122,6 @@ def main():
     print(json.dumps({"model": args.model, "tp": args.tp, "rank_shard": 0, "clients": C,
                       "ms_per_step": round(ms, 4), "per_client_tokens_per_s_upper_bound": round(1e3 / ms, 1),
                       "collective_kernels": comm.calls, "xgmi_error": err, "hipgraphs": eng.runner.use_graphs,
-                      "engine": bool(args.engine), "engine_steps": eng.model.engine_steps,
                       "note": "one shard on one GPU, collectives on a world-1 xGMI communicator (no peer latency)"}),
           flush=True)
 

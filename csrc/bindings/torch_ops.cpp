@@ -267,6 +267,64 @@ void mgemm(const Tensor& x, const Tensor& w, Tensor& y, int64_t rw) {
   launch_mgemm(ptr<bf16>(x), ptr<bf16>(w), ptr<float>(y), (int)M, (int)N, (int)K, (int)S, (int)rw, cur_stream(x));
 }
 
+// ---- prefill projection GEMM (pgemm.hip) ------------------------------------------------------------
+// Checks shared by every pgemm entry: tile config, split, 32-bit buffer offsets, optional split-K scratch.
+struct PgShape {
+  int64_t M, N, K, S, bm, bn;
+};
+
+PgShape pg_check(const Tensor& x, const Tensor& w, int64_t cfg, int64_t S, const c10::optional<Tensor>& slab,
+                 const c10::optional<Tensor>& counters) {
+  check_gpu(x, "x");
+  check_gpu(w, "w");
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(w, at::kBFloat16, "w");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "pgemm: x [M,K], w [N,K]");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  int bm = 0, bn = 0;
+  TORCH_CHECK(pgemm_cfg_shape((int)cfg, &bm, &bn), "pgemm: unknown tile config ", cfg);
+  TORCH_CHECK(M >= 1 && N % bn == 0, "pgemm: N must be a multiple of the tile width ", bn);
+  TORCH_CHECK(S >= 1 && K % (64 * S) == 0, "pgemm: K must be a multiple of 64 * S");
+  const int64_t mpad = (M + bm - 1) / bm * bm;
+  TORCH_CHECK(mpad * K * 2 < (1LL << 31) && N * K * 2 < (1LL << 31), "pgemm: operands exceed 2 GB");
+  const int64_t tiles = mpad / bm * (N / bn);
+  TORCH_CHECK(tiles < (1LL << 31) / 8, "pgemm: too many tiles");
+  if (S > 1) {
+    TORCH_CHECK(slab.has_value() && counters.has_value(), "pgemm: split-K needs slab + counters");
+    check_gpu(*slab, "slab");
+    check_dtype(*slab, at::kFloat, "slab");
+    check_gpu(*counters, "counters");
+    check_dtype(*counters, at::kInt, "counters");
+    TORCH_CHECK(slab->numel() >= S * M * N, "pgemm: slab must hold [S, M, N] fp32");
+    TORCH_CHECK(counters->numel() >= tiles, "pgemm: counters must hold one int per output tile");
+  }
+  return {M, N, K, S, bm, bn};
+}
+
+float* opt_f32(const c10::optional<Tensor>& t) { return t.has_value() ? ptr<float>(*t) : nullptr; }
+int* opt_i32(const c10::optional<Tensor>& t) { return t.has_value() ? ptr<int>(*t) : nullptr; }
+
+// y [M, N] bf16 or fp32 = x @ w^T (w MFMA-preshuffled)
+void pgemm(const Tensor& x, const Tensor& w, Tensor& y, int64_t cfg, int64_t S, const c10::optional<Tensor>& slab,
+           const c10::optional<Tensor>& counters) {
+  const auto sh = pg_check(x, w, cfg, S, slab, counters);
+  check_gpu(y, "y");
+  TORCH_CHECK(y.numel() == sh.M * sh.N, "pgemm: y must be [M, N]");
+  DecodeEpi e;
+  e.wshuf = 1;
+  int epi = DECODE_EPI_F32;
+  if (y.scalar_type() == at::kBFloat16) {
+    epi = DECODE_EPI_BF16;
+    e.out_bf = ptr<bf16>(y);
+  } else {
+    check_dtype(y, at::kFloat, "y");
+    e.y = ptr<float>(y);
+  }
+  const at::OptionalDeviceGuard g(x.device());
+  launch_pgemm(epi, (int)cfg, ptr<bf16>(x), ptr<bf16>(w), (int)sh.M, (int)sh.N, (int)sh.K, (int)S, e, opt_f32(slab),
+               opt_i32(counters), cur_stream(x));
+}
+
 void lm_head_sample(const Tensor& x, const Tensor& w, const Tensor& temps, const Tensor& seeds, const Tensor& step,
                     Tensor& tile_keys, Tensor& out_keys, Tensor& out_ids, int64_t n_offset,
                     const c10::optional<Tensor>& logits) {
@@ -443,31 +501,6 @@ void grouped_gemm(const Tensor& xs, const Tensor& W, const Tensor& offsets, int6
 
 // Dense medium-M projection on the weight-streaming kernel: mode 1 -> fp32 slabs y [S, M, N]; mode 3 -> SwiGLU of
 // the decode layout's tile-interleaved gate/up rows, y = act bf16 [M, N / 2].  W MFMA-preshuffled [N, K].
-void sgemm(const Tensor& x, const Tensor& Wshuf, Tensor& y, int64_t mode) {
-  check_gpu(x, "x");
-  check_gpu(Wshuf, "Wshuf");
-  check_gpu(y, "y");
-  check_dtype(x, at::kBFloat16, "x");
-  check_dtype(Wshuf, at::kBFloat16, "Wshuf");
-  check_dtype(y, mode == 1 ? at::kFloat : at::kBFloat16, "y");
-  TORCH_CHECK(mode == 1 || mode == 3, "sgemm: mode 1 (fp32 slabs) or 3 (interleaved SwiGLU)");
-  TORCH_CHECK(x.dim() == 2 && Wshuf.dim() == 2 && x.is_contiguous() && Wshuf.is_contiguous() && y.is_contiguous(),
-              "sgemm: x [M, K], W [N, K] contiguous");
-  const int64_t M = x.size(0), K = x.size(1), N = Wshuf.size(0);
-  TORCH_CHECK(Wshuf.size(1) == K && M >= 1 && M <= 256 && N % 128 == 0 && K % 64 == 0, "sgemm: M <= 256, N % 128, K % 64");
-  int64_t S = 1;
-  if (mode == 1) {
-    TORCH_CHECK(y.dim() == 3 && y.size(1) == M && y.size(2) == N, "sgemm: y [S, M, N]");
-    S = y.size(0);
-    TORCH_CHECK(S >= 1 && (K / 64) % S == 0 && (K / 64 / S) % 4 == 0, "sgemm: S must divide K / 256");
-  } else {
-    TORCH_CHECK(y.dim() == 2 && y.size(0) == M && y.size(1) == N / 2 && K % 256 == 0, "sgemm: y [M, N / 2], K % 256");
-  }
-  TORCH_CHECK((long long)N * K * 2 < 0x7fffffffLL, "sgemm: W within one buffer descriptor");
-  const at::OptionalDeviceGuard g(x.device());
-  launch_stream_gemm(ptr<bf16>(x), ptr<bf16>(Wshuf), y.data_ptr(), (int)M, (int)N, (int)K, (int)S, (int)mode,
-                     cur_stream(x));
-}
 
 void grouped_skinny(const Tensor& xs, const Tensor& W, const Tensor& offsets, int64_t e0, Tensor& y) {
   check_gpu(xs, "xs");
@@ -993,6 +1026,12 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) y, int variant=0) -> ()", &skinny_gemm);
   m.def("mgemm(Tensor x, Tensor w, Tensor(a!) y, int rw) -> ()", &mgemm);
   m.def("mgemm_nt(int on) -> ()", [](int64_t on) { set_mgemm_nt((int)on); });
+  m.def("pgemm(Tensor x, Tensor w, Tensor(a!) y, int cfg, int S, Tensor? slab, Tensor? counters) -> ()", &pgemm);
+  m.def("pgemm_shape(int cfg) -> int[]", [](int64_t cfg) {
+    int bm = 0, bn = 0;
+    if (!pgemm_cfg_shape((int)cfg, &bm, &bn)) return std::vector<int64_t>{};
+    return std::vector<int64_t>{bm, bn};
+  });
   m.def("decode_halves(int on) -> ()", [](int64_t on) { set_decode_halves((int)on); });
   m.def("attn_stream_min(int tokens) -> ()", [](int64_t t) { set_attn_stream_min((int)t); });
   m.def("attn_wave(int min_units, int min_span) -> ()",
@@ -1043,7 +1082,6 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("grouped_skinny(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y) -> ()", &grouped_skinny);
   m.def("grouped_gemm(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y, int mode) -> ()", &grouped_gemm);
   m.def("grouped_stream_policy(int p) -> ()", [](int64_t p) { set_grouped_stream_policy((int)p); });
-  m.def("sgemm(Tensor x, Tensor Wshuf, Tensor(a!) y, int mode) -> ()", &sgemm);
   m.def("moe_route(Tensor logits, int T, int k, int E, Tensor(a!) ids, Tensor(b!) w) -> ()", &moe_route);
   m.def("moe_align(Tensor ids, int G, Tensor(a!) counts, Tensor(b!) offsets, Tensor(c!) cursor) -> ()", &moe_align);
   m.def(

@@ -255,114 +255,6 @@ bool xgmi_gemm_ar_resid_multi(std::vector<Tensor> xs, const Tensor& W, bool wshu
                                       (int)W.size(0), (int)xs[0].size(1), xres ? 1 : 0, stream_of(xs[0]));
 }
 
-// ---- the decode-step engine (csrc/kernels/decode_layers.hip) -----------------------------------------------
-// table: int64 [L, 8] device pointers per layer {wqkv, wo, wgu, wdown (MFMA-preshuffled), ln2, lnn, k_cache,
-// v_cache}; xar: the fused all-reduce communicator's handle, or -1 (world 1: the residual stays local).
-void dl_check_t(const Tensor& t, at::ScalarType dt, const char* name) {
-  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == dt, "decode_layers: ", name,
-              " must be a contiguous GPU tensor of the expected dtype");
-}
-
-DLArgs dl_args(const Tensor& table, int64_t Hq, int64_t Hkv, int64_t Fl, int64_t KSq, const Tensor& positions,
-               const Tensor& slots, const Tensor& block_tables, const Tensor& ctx_lens, int64_t BS, const Tensor& cos_sin,
-               double scale, double eps, Tensor& resid, Tensor& xw, Tensor& ss, const Tensor& ss0, Tensor& qkv_ws,
-               Tensor& attn, Tensor& act, Tensor& edge, Tensor& fault, int64_t G, int64_t xar) {
-  dl_check_t(table, at::kLong, "table");
-  for (const Tensor* t : {&positions, &slots, &block_tables, &ctx_lens}) dl_check_t(*t, at::kInt, "step metadata");
-  for (const Tensor* t : {&cos_sin, (const Tensor*)&resid, (const Tensor*)&ss, &ss0, (const Tensor*)&qkv_ws})
-    dl_check_t(*t, at::kFloat, "fp32 operand");
-  for (const Tensor* t : {(const Tensor*)&xw, (const Tensor*)&attn, (const Tensor*)&act})
-    dl_check_t(*t, at::kBFloat16, "bf16 operand");
-  dl_check_t(edge, at::kInt, "edge");
-  // the fault word: device memory, or a pinned host word the host reads after every step without a sync
-  TORCH_CHECK(fault.scalar_type() == at::kInt && fault.is_contiguous() && (fault.is_cuda() || fault.is_pinned()),
-              "decode_layers: fault must be an int32 GPU tensor or pinned host word");
-  TORCH_CHECK(table.dim() == 2 && table.size(1) == 8, "decode_layers: table [L, 8]");
-  TORCH_CHECK(resid.dim() == 2 && xw.sizes() == resid.sizes(), "decode_layers: resid / xw [M, d]");
-  const int64_t L = table.size(0), M = resid.size(0), d = resid.size(1);
-  const int64_t Nq = (Hq + 2 * Hkv) * 128;
-  TORCH_CHECK(ss.dim() == 2 && ss.size(0) >= M && ss.size(1) == d / 16, "decode_layers: ss [M, d / 16]");
-  TORCH_CHECK(ss0.dim() == 2 && ss0.size(0) >= M, "decode_layers: ss0 [M, P]");
-  TORCH_CHECK(qkv_ws.numel() >= KSq * M * Nq && attn.numel() >= M * Hq * 128 && act.numel() >= M * Fl,
-              "decode_layers: workspace too small");
-  TORCH_CHECK(positions.numel() >= M && slots.numel() >= M && ctx_lens.numel() >= M && block_tables.dim() == 2 &&
-                  block_tables.size(0) >= M, "decode_layers: step metadata rows");
-  TORCH_CHECK(d % KSq == 0 && (d / KSq) % 256 == 0 && (Hq * 128) % 256 == 0 && d % 256 == 0 && Fl % 256 == 0,
-              "decode_layers: K of every unit must be a multiple of 256");
-  DLArgs a;
-  a.layers = reinterpret_cast<const DLLayer*>(table.data_ptr());
-  a.L = (int)L;
-  a.M = (int)M;
-  a.d = (int)d;
-  a.Hq = (int)Hq;
-  a.Hkv = (int)Hkv;
-  a.Fl = (int)Fl;
-  a.KSq = (int)KSq;
-  a.cq = (int)(d / KSq / 256);
-  a.co = (int)(Hq * 128 / 256);
-  a.KSg = 1;  // gate_up units at most 4096 deep (16 pieces per wave): K = 8192 in two tile-major splits
-  while (d / a.KSg / 256 > 16 && d % (a.KSg * 2 * 256) == 0) a.KSg *= 2;
-  a.cg = (int)(d / a.KSg / 256);
-  a.KSd = 1;
-  while (Fl / a.KSd / 256 > 16 && Fl % (a.KSd * 2 * 256) == 0) a.KSd *= 2;
-  a.cd = (int)(Fl / a.KSd / 256);
-  a.positions = positions.data_ptr<int>();
-  a.slots = slots.data_ptr<int>();
-  a.block_tables = block_tables.data_ptr<int>();
-  a.ctx_lens = ctx_lens.data_ptr<int>();
-  a.BS = (int)BS;
-  a.max_blocks = (int)block_tables.size(1);
-  a.cos_sin = cos_sin.data_ptr<float>();
-  a.scale_log2 = (float)(scale * 1.4426950408889634);
-  a.eps = (float)eps;
-  a.resid = resid.data_ptr<float>();
-  a.xw = reinterpret_cast<bf16*>(xw.data_ptr());
-  a.ss = ss.data_ptr<float>();
-  a.ss0 = ss0.data_ptr<float>();
-  a.ss0_tiles = (int)ss0.size(1);
-  a.qkv_ws = qkv_ws.data_ptr<float>();
-  a.attn = reinterpret_cast<bf16*>(attn.data_ptr());
-  a.act = reinterpret_cast<bf16*>(act.data_ptr());
-  a.edge = reinterpret_cast<unsigned*>(edge.data_ptr());
-  a.fault = fault.data_ptr<int>();
-  a.G = (int)G;
-  TORCH_CHECK(edge.numel() >= dl_edge_words((int)L, (int)M, (int)Hq, (int)Hkv) && fault.numel() >= 1,
-              "decode_layers: edge [decode_layers_edge_words(...)], fault [1]");
-  if (xar >= 0) {
-    Xgmi* x = get(xar);
-    check_ready(x, resid);
-    TORCH_CHECK(M * d * 8 <= x->args.slot_bytes, "decode_layers: all-reduce granules exceed the slot");
-    TORCH_CHECK(d / 16 <= XAR_CTR, "decode_layers: too many output tiles");
-    a.xp = x->args;
-    a.xar_ctr = x->xar_ctr;
-  }
-  return a;
-}
-
-bool decode_layers(const Tensor& table, int64_t Hq, int64_t Hkv, int64_t Fl, int64_t KSq, const Tensor& positions,
-                   const Tensor& slots, const Tensor& block_tables, const Tensor& ctx_lens, int64_t BS,
-                   const Tensor& cos_sin, double scale, double eps, Tensor& resid, Tensor& xw, Tensor& ss,
-                   const Tensor& ss0, Tensor& qkv_ws, Tensor& attn, Tensor& act, Tensor& edge, Tensor& fault, int64_t G,
-                   int64_t xar, const c10::optional<Tensor>& stamps) {
-  DLArgs a = dl_args(table, Hq, Hkv, Fl, KSq, positions, slots, block_tables, ctx_lens, BS, cos_sin, scale, eps,
-                     resid, xw, ss, ss0, qkv_ws, attn, act, edge, fault, G, xar);
-  if (stamps.has_value() && stamps->defined()) {
-    dl_check_t(*stamps, at::kLong, "stamps");
-    TORCH_CHECK(stamps->numel() >= G * a.L * 5 * 8, "decode_layers: stamps [G * L * 5 * 8]");
-    a.stamps = reinterpret_cast<unsigned long long*>(stamps->data_ptr());
-  }
-  return launch_decode_layers(a, stream_of(resid));
-}
-
-int64_t decode_layers_edge_words(int64_t L, int64_t M, int64_t Hq, int64_t Hkv, int64_t G) {
-  (void)G;
-  return dl_edge_words((int)L, (int)M, (int)Hq, (int)Hkv);
-}
-
-int64_t decode_layers_pieces(int64_t cq, int64_t co, int64_t cg, int64_t cd, int64_t ks, int64_t gh) {
-  return decode_layers_pieces_ok((int)cq, (int)co, (int)cg, (int)cd, (int)ks, (int)gh);
-}
-
 // test-only: every rank of this process in one launch (grid slice per rank; see xgmi_ar.hip)
 void xgmi_all_reduce_multi(std::vector<Tensor> ins, std::vector<Tensor> outs, std::vector<int64_t> comms,
                            int64_t delay_rank, int64_t delay_us) {
@@ -585,14 +477,6 @@ TORCH_LIBRARY_FRAGMENT(symmetry_amd, m) {
       "xgmi_gemm_ar_resid_multi(Tensor[] xs, Tensor W, bool wshuf, Tensor(a!)[] resids, Tensor w_next, "
       "Tensor(b!)[] xws, Tensor(c!)[] sss, int[] comms, bool xres, int delay_rank=-1, int delay_us=0) -> bool",
       &xgmi_gemm_ar_resid_multi);
-  m.def(
-      "decode_layers(Tensor table, int Hq, int Hkv, int Fl, int KSq, Tensor positions, Tensor slots, "
-      "Tensor block_tables, Tensor ctx_lens, int BS, Tensor cos_sin, float scale, float eps, Tensor(a!) resid, "
-      "Tensor(b!) xw, Tensor(c!) ss, Tensor ss0, Tensor(d!) qkv_ws, Tensor(e!) attn, Tensor(f!) act, "
-      "Tensor(g!) edge, Tensor(h!) fault, int G, int xar, Tensor(i!)? stamps=None) -> bool",
-      &decode_layers);
-  m.def("decode_layers_pieces(int cq, int co, int cg, int cd, int ks, int gh) -> int", &decode_layers_pieces);
-  m.def("decode_layers_edge_words(int L, int M, int Hq, int Hkv, int G) -> int", &decode_layers_edge_words);
   m.def("xgmi_keys_max_multi(Tensor[] keys, Tensor(a!)[] ids, int[] comms, int delay_rank=-1, int delay_us=0) -> ()",
         &xgmi_keys_max_multi);
   m.def(

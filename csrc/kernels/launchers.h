@@ -19,6 +19,7 @@ enum {
   // epoch-tagged granules, the tile's workgroup sums every rank's copy in rank order and runs the RESID
   // epilogue (residual add + next-norm prep, ss per 16-column tile) -- decode_epi.h, xar_push / xar_collect
   DECODE_EPI_XAR = 6,
+  DECODE_EPI_BF16 = 7,  // plain bf16 [M][N] output (pgemm.hip only)
   XAR_MAX_TILES = 32,  // output tiles per workgroup of an x-resident XAR launch (epoch slots in LDS)
 };
 
@@ -50,6 +51,7 @@ struct DecodeEpi {
   int ss_tiles = 0;
   float inv_d = 0.f, eps = 0.f;
   float* y = nullptr;  // F32 output / ARGMAX optional logits
+  bf16* out_bf = nullptr;  // BF16 output (pgemm.hip)
   // QKV: RoPE + paged cache write + q out
   const int* positions = nullptr;
   const int* slots = nullptr;
@@ -95,68 +97,6 @@ void launch_decode_gemm(int epi, const bf16* x, const bf16* W, int M, int N, int
 // (DECODE_EPI_XAR).  false (nothing launched): no variant whose whole grid is co-resident on this GPU (the
 // workgroups wait on their peers' tiles) -- the caller runs the two-launch form.
 bool launch_decode_gemm_xar(const bf16* x, const bf16* W, int M, int N, int K, const DecodeEpi& e, hipStream_t s);
-// decode_layers.hip -- the persistent decode-step engine for tensor-parallel shards: ONE launch runs every layer's
-// QKV -> attention -> O (+ all-reduce) -> gate_up -> down (+ all-reduce) with in-launch edges and each phase's
-// weights streamed into registers before the edge it waits on (see the file header)
-struct DLLayer {  // one layer's operands (a device array of L of them)
-  const bf16* wqkv;   // MFMA-preshuffled [Nq][d] (q / k head rows permuted, models/layout.py)
-  const bf16* wo;     // preshuffled [d][Hq * 128]
-  const bf16* wgu;    // preshuffled [2 Fl][d] (gate / up interleaved per 16-row tile)
-  const bf16* wdown;  // preshuffled [d][Fl]
-  const bf16* ln2;    // O epilogue's next-norm weight [d]
-  const bf16* lnn;    // down epilogue's next-norm weight [d] (the next layer's ln1, or the final norm)
-  bf16* k_cache;      // this layer's [NB][Hkv][BS][128]
-  bf16* v_cache;      // [NB][Hkv][128][BS]
-};
-struct DLArgs {
-  const DLLayer* layers = nullptr;
-  int L = 0;
-  int M = 0, d = 0, Hq = 0, Hkv = 0, Fl = 0;  // rows (<= 16), hidden, local q / kv heads, local intermediate
-  int KSq = 1;                                 // k-splits of the QKV projection (fp32 slabs, summed by attention)
-  int KSg = 1;                                 // k-splits of gate_up (consecutive units of one workgroup)
-  int KSd = 1;                                 // k-splits of down (likewise)
-  int cq = 0, co = 0, cg = 0, cd = 0;          // 32-deep k pieces per streamer wave per unit, per projection
-  const int* positions = nullptr;
-  const int* slots = nullptr;
-  const int* block_tables = nullptr;
-  const int* ctx_lens = nullptr;
-  int BS = 0, max_blocks = 0;
-  const float* cos_sin = nullptr;
-  float scale_log2 = 0.f, eps = 0.f;
-  float* resid = nullptr;    // [M][d] fp32 residual stream
-  bf16* xw = nullptr;        // [M][d] bf16 normed-input numerators (deferred RMSNorm)
-  float* ss = nullptr;       // [M][d / 16] sum-of-squares partials
-  const float* ss0 = nullptr;  // layer 0's partials (embed_prep: [M][ss0_tiles])
-  int ss0_tiles = 0;
-  float* qkv_ws = nullptr;   // [KSq][M][Nq] fp32
-  bf16* attn = nullptr;      // [M][Hq * 128]
-  bf16* act = nullptr;       // [M][Fl]
-  unsigned* edge = nullptr;  // edge counters + attention counters / partials (dl_edge_words), zero at allocation
-  int* fault = nullptr;      // device word: an edge wait gave up (sticky for the launch)
-  int G = 0;                 // workgroups of this rank (one per CU)
-  XgmiArgs xp;               // world > 1: the fused all-reduce communicator (decode_epi.h granules)
-  unsigned* xar_ctr = nullptr;
-  unsigned long long* stamps = nullptr;  // diagnostics: [G][L][5][8] wall clock: edge passed, signalled, sub-phases
-};
-// The edge tensor holds, in order: the edge counters ([L * 5][8], 128 B apart), one attention arrival counter per
-// (sequence, kv head) 128 B apart, then the attention partials (fp32 o [M * Hkv][DL_APARTS][Hq / Hkv][128], m / l
-// [M * Hkv][Hq / Hkv][DL_APARTS][2]).  Zero when allocated and never cleared again (decode_layers.hip: epochs).
-constexpr int DL_APARTS = 8;  // context partitions per (sequence, kv head): one wave each
-// (the attention counters are laid out for 16 rows whatever M: graphs of different batch buckets share the buffer,
-// and a smaller bucket's partials must not land on a larger one's counters)
-__host__ __device__ inline long long dl_edge_sync_words(int L, int M, int Hkv) {
-  (void)M;
-  return (long long)L * 5 * 8 * 32 + 16LL * Hkv * 32;
-}
-__host__ __device__ inline long long dl_edge_words(int L, int M, int Hq, int Hkv) {
-  return dl_edge_sync_words(L, M, Hkv) + (long long)M * Hq * DL_APARTS * 130;
-}
-// false: shapes outside the engine (the caller runs the per-layer launches); the launch itself is checked
-bool launch_decode_layers(const DLArgs& a, hipStream_t s);
-// 1 if this shape class (k pieces per wave of the QKV / O / gate_up / down units, QKV k-slabs, query heads per kv
-// head) is built
-int decode_layers_pieces_ok(int cq, int co, int cg, int cd, int ks, int gh);
-
 // test-only: every rank of this process in ONE launch (grid z = rank; co-residency checked)
 constexpr int XAR_MULTI_MAX = 8;
 struct XarMulti {
@@ -184,6 +124,15 @@ void launch_mgemm(const bf16* x, const bf16* Wshuf, float* y, int M, int N, int 
 void launch_mgemm_epi(int epi, const bf16* x, const bf16* Wshuf, float* y, int M, int N, int K, int S, int rw,
                       const DecodeEpi& e, int* counters, hipStream_t s);
 void set_mgemm_nt(int on);  // non-temporal weight DMA (A/B knob)
+
+// pgemm.hip -- prefill projection GEMM (hundreds+ rows) on the MFMA-preshuffled weights: tile shape `cfg`
+// (pgemm_cfg_shape: BM tokens x BN features per 512-thread block), S k-splits over grid.y (S > 1: slab
+// [S][M][N] fp32 scratch + counters [tiles] ints zero before the first launch, re-armed by the kernel), fused
+// epilogue `epi` (DECODE_EPI_F32 / BF16 / QKV / SWIGLU / RESID -- RESID writes ss_out [M][N / BN]).
+// N % BN == 0, K % (64 S) == 0; rows past M are padded in-kernel.
+int pgemm_cfg_shape(int cfg, int* bm, int* bn);
+void launch_pgemm(int epi, int cfg, const bf16* x, const bf16* Wshuf, int M, int N, int K, int S, const DecodeEpi& e,
+                  float* slab, int* counters, hipStream_t s);
 
 // norm.hip
 void launch_rms_norm(LinOut x, const bf16* w, bf16* out, int T, int d, float eps, hipStream_t s);
@@ -243,9 +192,6 @@ void launch_grouped_gemm(const bf16* xs, const bf16* W, const int* offsets, void
 // grouped_gemm's weight-streaming path on row-major weights: 0 never, 1 where it measured faster (default),
 // 2 always; + 10 x (2 | 4): weight tiles per wave
 void set_grouped_stream_policy(int p);
-// dense medium-M projection on the weight-streaming kernel (moe.hip): preshuffled W [N][K], x [M][K], M <= 256;
-// out 1: fp32 slabs y [S][M][N]; out 3: SwiGLU of tile-interleaved gate/up rows -> act bf16 [M][N / 2] (S = 1)
-void launch_stream_gemm(const bf16* x, const bf16* Wshuf, void* y, int M, int N, int K, int S, int out, hipStream_t s);
 void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, float* y, int R, int E, int e0, int N,
                            int K, int S, hipStream_t s);
 void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_lo, int e_hi, const float* w, int T, int k,

@@ -440,10 +440,8 @@ SYM_DEV GsUnit gs_unit(int u, int ERB, const int (&a)[GS_EMAX], const int (&n)[G
 // loads past the last unit use a zero-range descriptor, so every iteration issues the same instructions and one
 // constant vmcnt covers every wait.
 //
-// Dense use (ops.sgemm, medium-M prefill projections): offsets == nullptr is ONE segment of R rows; S > 1 splits K
-// over S units per n-block, each writing its fp32 slab y[ks] (OUT 1; the LinOut consumers sum the slabs);
-// OUT 3 is SwiGLU on the decode layout's tile-interleaved gate/up rows (models/layout.py: tile j = gate rows
-// 8j.. then up rows 8j..; a lane's up partner is lane ^ 32).
+// offsets == nullptr is ONE segment of R rows; S > 1 splits K over S units per n-block, each writing its fp32
+// slab y[ks] (OUT 1).
 template <int MT, int RW, int D, int OUT, bool PRE>
 __global__ __launch_bounds__(GS_THR, 1) void grouped_stream_kernel(const bf16* __restrict__ xs,
                                                                    const bf16* __restrict__ W,
@@ -605,26 +603,7 @@ __global__ __launch_bounds__(GS_THR, 1) void grouped_stream_kernel(const bf16* _
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int m = 16 * mt + (lane & 15);
-      if constexpr (OUT == 3) {  // the up half of each tile sits 32 lanes over: exchange before any lane exits
-        f32x4 up[RW];
-#pragma unroll
-        for (int rt = 0; rt < RW; ++rt)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) up[rt][q] = __shfl_xor(acc[rt][mt][q], 32, 64);
-        if (mt < mact && m < cun.rows && lane < 32) {
-          const long long yrow = (long long)(cun.row0 + m) * Ny;
-#pragma unroll
-          for (int rt = 0; rt < RW; ++rt) {
-            const f32x4 gt = acc[rt][mt];
-            const int f = 8 * (cun.nb * (rows_nb / 16) + wid * RW + rt) + 4 * (lane >> 4);
-            float o[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = gt[q] / (1.f + __expf(-gt[q])) * up[rt][q];
-            bf16x4 pk = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
-            *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(y) + yrow + f) = pk;
-          }
-        }
-      } else if (mt < mact && m < cun.rows) {
+      if (mt < mact && m < cun.rows) {
         const long long yrow = ((long long)(cu % S) * R + cun.row0 + m) * Ny;
         if constexpr (OUT == 2) {
 #pragma unroll
@@ -668,14 +647,6 @@ void gs_launch(const bf16* xs, const bf16* W, const int* offsets, void* y, int R
                int G, bool pre, hipStream_t s, int S = 1) {
   if (pre) grouped_stream_kernel<MT, RW, D, OUT, true><<<G, GS_THR, 0, s>>>(xs, W, offsets, y, R, Nw, Ny, K, E, e0, S);
   else grouped_stream_kernel<MT, RW, D, OUT, false><<<G, GS_THR, 0, s>>>(xs, W, offsets, y, R, Nw, Ny, K, E, e0, S);
-}
-
-// dense medium-M projection on the streaming kernel (preshuffled W [N][K], x [M][K], M <= 256): out 1 -> fp32 slabs
-// y [S][M][N]; out 3 -> SwiGLU of the tile-interleaved gate/up rows, y = act bf16 [M][N / 2] (S = 1)
-template <int MT, int D>
-void sg_launch_mt(int out, const bf16* x, const bf16* W, void* y, int M, int N, int K, int S, int G, hipStream_t s) {
-  if (out == 3) grouped_stream_kernel<MT, 2, D, 3, true><<<G, GS_THR, 0, s>>>(x, W, nullptr, y, M, N, N / 2, K, 1, 0, 1);
-  else grouped_stream_kernel<MT, 2, D, 1, true><<<G, GS_THR, 0, s>>>(x, W, nullptr, y, M, N, N, K, 1, 0, S);
 }
 
 template <int MT, int RW, int D>
@@ -1094,25 +1065,6 @@ void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, fl
   if (R == 0) return;
   dim3 grid(N / 16, E, S);
   grouped_skinny_kernel<<<grid, 256, 0, s>>>(xs, W, offsets, y, R, N, K, K / S, e0);
-}
-
-// out: 0 bf16 [R][N], 1 fp32 [R][N], 2 SwiGLU act bf16 [R][N] with W holding 2N rows per expert
-void launch_stream_gemm(const bf16* x, const bf16* Wshuf, void* y, int M, int N, int K, int S, int out,
-                        hipStream_t s) {
-  if (M == 0) return;
-  if (!g_gs_cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&g_gs_cus, hipDeviceAttributeMultiprocessorCount, dev);
-    g_gs_cus = std::max(8, g_gs_cus);
-  }
-  const int units = N / 128 * (M + 255) / 256 * S;
-  const int G = std::min(g_gs_cus, units);
-  const int nch = K / 64 / S;  // a multiple of 4 (checked by the op): whole ring turns per unit
-  if (M <= 128 && nch % 8 == 0) sg_launch_mt<8, 8>(out, x, Wshuf, y, M, N, K, S, G, s);
-  else if (M <= 128) sg_launch_mt<8, 4>(out, x, Wshuf, y, M, N, K, S, G, s);
-  else if (M <= 192) sg_launch_mt<12, 4>(out, x, Wshuf, y, M, N, K, S, G, s);
-  else sg_launch_mt<16, 4>(out, x, Wshuf, y, M, N, K, S, G, s);
 }
 
 void set_grouped_stream_policy(int p) {

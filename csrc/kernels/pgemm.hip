@@ -1,0 +1,420 @@
+// Prefill projection GEMM (hundreds to a few thousand rows): the compute-bound regime of a dense layer.
+//   y[m][n] = rs[m] * sum_k x[m][k] * W[n][k],   x [M][K] bf16 row-major, W [N][K] bf16 MFMA-preshuffled
+//   (models/layout.py::preshuffle -- the SAME copy the decode GEMMs stream, so no row-major weight copy is
+//   needed for the library), rs the deferred-RMSNorm row scale (optional).
+//
+// Why not hipBLASLt: config 3's first prefill step (6 x 128 = 768 tokens) spent 76 % of its time in four
+// library GEMMs at 0.78-1.16 PF (profiles/r4/prof_prefill768.csv), gate_up at 768 x 28672 runs 336 of the
+// library's 256x256 tiles = 1.31 waves on 256 CUs, and every consumer (RMSNorm, RoPE + cache write, SwiGLU,
+// residual add) re-read the library's output in its own launch.  Here:
+//
+//   * block tile BM x BN = (4 m-waves x WM 16-token tiles) x (2 n-waves x WN 16-feature tiles), 8 waves,
+//     the whole K (or a K slice) per block, tile sizes chosen per shape on the host so the grid is one
+//     (or a whole number of) waves of 256 CUs -- e.g. gate_up at 768 rows: 384 x 224 tiles, 2 x 128 = 256;
+//   * orientation Y^T = W . x^T on v_mfma_f32_16x16x32_bf16: a preshuffled weight block (16 rows x 32 k)
+//     is 1 KB in A-fragment order, so its LDS-DMA and its ds_read_b128 are lane-linear (conflict-free);
+//     x rows are the B operand, staged as 64-B rows per slot with the 16-B chunk XOR-swizzled by (row >> 1) & 3
+//     on the DMA source and on the read (conflict-free ds_read_b128, cdna_hip_programming.md T2 / rule 21);
+//   * both operands by LDS-DMA (buffer_load ... lds) into a ring of 32-deep k slots (4-6 slots, up to 155 KB of
+//     the 160 KB LDS): D = slots - 1 steps are in flight, one counted vmcnt per step (every wave issues the
+//     same number of DMAs per slot -- a surplus instruction fills a dummy region), one barrier per step, the
+//     refill of the slot freed by that barrier issued before the step's MFMAs (cdna_hip_programming.md
+//     "Pipelining across barriers": raw s_barrier, never vmcnt(0) in the loop); x rows past M read as zeros;
+//   * XCD-aware tile order (cdna_hip_programming.md T1, the bijective form): consecutive tiles -- the
+//     m-tiles of one weight column block -- run on one XCD, so each weight block is fetched from HBM once
+//     per XCD and the x slices stay L2-resident;
+//   * epilogues from the accumulators (decode_epi.h's 16x16 tile layout: lane (r16, h) holds features
+//     n0 + 4h .. + 3 of token row m): fp32 / bf16 out, QKV (RoPE + paged K/V write), SWIGLU (interleaved
+//     gate/up tiles), RESID (residual add + next-norm prep with ONE sum-of-squares partial per row and
+//     block column, so the consumer's row-scale prologue reads N / BN partials instead of N / 16);
+//   * optional split-K over grid.y: fp32 slabs (write-through stores) + a per-tile arrival counter; the
+//     last of the S blocks of a tile sums the slabs in a fixed order and runs the epilogue (the in-launch
+//     reduction of mgemm.hip).
+#include "common.h"
+#include "decode_epi.h"
+#include "launchers.h"
+
+namespace {
+
+constexpr int PG_THR = 512;
+#ifndef PG_MAX_SLOTS
+#define PG_MAX_SLOTS 4
+#endif
+
+typedef __attribute__((address_space(3))) void lds_t;
+
+SYM_DEV __amdgpu_buffer_rsrc_t pg_rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL), 0x00020000);
+}
+
+SYM_DEV void pg_dma(__amdgpu_buffer_rsrc_t r, int voff, int soff, char* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_t*)lds, 16, voff, soff, 0, 0);
+}
+
+template <int WM, int WN>
+struct PgCfg {
+  static constexpr int BM = 64 * WM;        // tokens per block
+  static constexpr int BN = 32 * WN;        // output features per block
+  static constexpr int XS = BM * 64;        // x bytes of one 32-deep slot ([BM rows][64 B], swizzled)
+  static constexpr int SLOT = XS + BN * 64;  // + weight blocks (BN / 16 tiles x one 1 KB k-block)
+  static constexpr int NX = BM / 16;        // x DMA instructions per slot (16 rows x 64 B each)
+  static constexpr int NW = BN / 16;        // weight DMA instructions per slot
+  static constexpr int NXU = (NX + 7) / 8;  // ... per wave (every wave issues the same count: the surplus of the
+  static constexpr int NWU = (NW + 7) / 8;  //     last round is a dummy fill, so one vmcnt immediate fits all)
+  static constexpr int PW = NXU + NWU;      // DMA instructions per wave per slot
+  static constexpr int EXTRA = BM * 4 + 1024 + 16;  // row scales, dummy-fill target, split-K "last" flag
+  static constexpr int SLOTS_FIT = (160 * 1024 - EXTRA) / SLOT;
+  static constexpr int SLOTS = SLOTS_FIT > PG_MAX_SLOTS ? PG_MAX_SLOTS : SLOTS_FIT;
+  static constexpr int KEEP = (SLOTS - 2) * PW;  // this wave's younger DMAs left in flight at a step's wait
+  static constexpr int RS_OFF = SLOTS * SLOT;
+  static constexpr int DUMMY_OFF = RS_OFF + BM * 4;
+  static constexpr int LAST_OFF = DUMMY_OFF + 1024;
+  static constexpr int LDS = LAST_OFF + 16;
+  static_assert(SLOTS >= 3 && KEEP <= 63 && LDS <= 160 * 1024, "pgemm tile config");
+};
+
+SYM_DEV void store4bf16(bf16* p, const f32x4& v) {
+  bf16x4 o;
+  o[0] = (bf16)v[0];
+  o[1] = (bf16)v[1];
+  o[2] = (bf16)v[2];
+  o[3] = (bf16)v[3];
+  *reinterpret_cast<bf16x4*>(p) = o;
+}
+
+// Block tile of M-rows [m0, m0 + BM) x features [n0, n0 + BN); K slice [k0, k0 + kslice).
+template <int WM, int WN, int EPI>
+__global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict__ x, const bf16* __restrict__ W,
+                                                           int M, int N, int K, int kslice, int mtiles, DecodeEpi e,
+                                                           float* __restrict__ slab, int* __restrict__ counters) {
+  using C = PgCfg<WM, WN>;
+  __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
+  // (no AGPR clobber: with none used the whole 256-register budget of 2 waves / SIMD goes to VGPRs)
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably wave-uniform (scalar branches)
+  const int wm = wid & 3, wn = wid >> 2;
+
+  // ---- XCD-aware tile order: blocks b, b + 8, ... share an XCD; each XCD gets a contiguous run of tiles
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int mt = t % mtiles, nt = t / mtiles;
+  const int m0 = mt * C::BM, n0 = nt * C::BN;
+  const int split = blockIdx.y;
+  const int k0 = split * kslice;
+
+  // ---- DMA sources (one 32-deep k slot per issue).  x: instruction g covers block rows 16g .. 16g + 15;
+  // lane -> (row lane >> 2, LDS chunk slot lane & 3), loading source chunk slot ^ ((row >> 1) & 3) (the read
+  // side's XOR: conflict-free ds_read_b128 over 64-B rows).  Rows >= M read as zeros.  Weights: instruction j
+  // is tile n0 / 16 + j's 1 KB block of the slot, lane-linear.  Every wave issues NXU + NWU instructions per
+  // slot (one vmcnt immediate fits all): a surplus instruction of a last round re-reads a valid 1 KB into the
+  // dummy region.  (One pooled x + weight list with a per-instruction kind branch measured 10-20 % slower.)
+  const __amdgpu_buffer_rsrc_t rx = pg_rsrc(x, (long long)M * K * 2);
+  const __amdgpu_buffer_rsrc_t rw = pg_rsrc(W, (long long)N * K * 2);
+  int vx[C::NXU], vw[C::NWU], dx[C::NXU], dw[C::NWU];
+#pragma unroll
+  for (int u = 0; u < C::NXU; ++u) {
+    const int g = u * 8 + wid;
+    const int row = 16 * g + (lane >> 2);
+    const bool real = g < C::NX;
+    vx[u] = real ? (m0 + row) * K * 2 + 2 * k0 + 16 * ((lane & 3) ^ ((row >> 1) & 3)) : 0;
+    dx[u] = real ? g * 1024 : -1;
+  }
+#pragma unroll
+  for (int u = 0; u < C::NWU; ++u) {
+    const int j = u * 8 + wid;
+    const bool real = j < C::NW;
+    vw[u] = ((n0 / 16 + (real ? j : 0)) * (K / 32) + k0 / 32) * 1024 + lane * 16;
+    dw[u] = real ? C::XS + j * 1024 : -1;
+  }
+
+  auto issue = [&](int c, int slot) {
+    char* const sb = smem + slot * C::SLOT;
+#pragma unroll
+    for (int u = 0; u < C::NXU; ++u) {
+      if ((C::NX % 8) == 0 || u + 1 < C::NXU || dx[u] >= 0) pg_dma(rx, vx[u], c * 64, sb + dx[u]);
+      else pg_dma(rw, vw[0], 0, smem + C::DUMMY_OFF);
+    }
+#pragma unroll
+    for (int u = 0; u < C::NWU; ++u) {
+      if ((C::NW % 8) == 0 || u + 1 < C::NWU || dw[u] >= 0) pg_dma(rw, vw[u], c * 1024, sb + dw[u]);
+      else pg_dma(rw, vw[u], 0, smem + C::DUMMY_OFF);
+    }
+  };
+
+  // ---- fragment addresses: x lane reads token row (lane & 15) of its 16-row tile, k 8 (lane >> 4) .. + 8 of the
+  // slot (swizzled chunk); weight reads lane-linear
+  const int fr = lane & 15;
+  const int xo = (wm * WM * 16 + fr) * 64 + 16 * ((lane >> 4) ^ ((fr >> 1) & 3));
+  const int wo = C::XS + wn * WN * 1024 + lane * 16;
+
+  f32x4 acc[WN][WM];
+#pragma unroll
+  for (int j = 0; j < WN; ++j)
+#pragma unroll
+    for (int i = 0; i < WM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 wf[WN], xf[WM];
+  auto read_frags = [&](int slot) {
+    const char* const sb = smem + slot * C::SLOT;
+#pragma unroll
+    for (int j = 0; j < WN; ++j) wf[j] = *(const bf16x8*)(sb + wo + j * 1024);
+#pragma unroll
+    for (int i = 0; i < WM; ++i) xf[i] = *(const bf16x8*)(sb + xo + i * 1024);
+  };
+  auto mfmas = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int i = 0; i < WM; ++i) acc[j][i] = mfma16(wf[j], xf[i], acc[j][i]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // ---- deferred-RMSNorm row scales of the block's rows: tpr threads per row sum the producer's partials
+  // (loads issued ahead of the first stage's DMAs, summed behind them)
+  float* const rs = reinterpret_cast<float*>(smem + C::RS_OFF);
+  constexpr int TPR = (PG_THR / C::BM) >= 8 ? 8 : (PG_THR / C::BM) >= 4 ? 4 : (PG_THR / C::BM) >= 2 ? 2 : 1;
+  const int rrow = threadIdx.x / TPR, rsub = threadIdx.x % TPR;
+  float rpart = 0.f;
+  const bool has_rs = e.ss_in != nullptr;
+  if (has_rs && rrow < C::BM && m0 + rrow < M) {
+    const float* sp = e.ss_in + (long long)(m0 + rrow) * e.ss_tiles;
+    for (int i = rsub; i < e.ss_tiles; i += TPR) rpart += sp[i];
+  }
+
+  const int nch = kslice / 32;
+#pragma unroll
+  for (int c = 0; c < C::SLOTS - 1; ++c)
+    if (c < nch) issue(c, c);
+
+  if (has_rs) {
+#pragma unroll
+    for (int o = 1; o < TPR; o *= 2) rpart += __shfl_xor(rpart, o, 64);
+    if (rrow < C::BM && rsub == 0) rs[rrow] = rsqrtf(rpart * e.inv_d + e.eps);
+  }
+
+  // Ping-pong over two wave groups (one wave of each per SIMD): group A (waves 0-3) reads step c's fragments in
+  // phase 2c and runs its MFMAs in phase 2c + 1; group B (waves 4-7) reads in 2c + 1 and computes in 2c + 2 -- in
+  // every phase one wave of each SIMD feeds the matrix pipe while its partner reads LDS and issues DMAs
+  // (MI355X_MICROARCH.md "Two waves per SIMD").  Step c lives in slot c % SLOTS; a wave's read phase of step c
+  // also issues its share of step c + SLOTS - 1 into the slot of step c - 1 (read by both groups before).  Before
+  // the barrier that opens phase 2c every wave has waited for its own DMAs of step c (vmcnt, the SLOTS - 2
+  // younger steps stay in flight), so the barrier publishes the whole slot.
+  const int grp = wid >> 2;
+  auto wait_step = [&](int c) {
+    if (c + C::SLOTS - 2 < nch) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::KEEP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  auto bar = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto read_phase = [&](int c, int slot) {
+    if (c + C::SLOTS - 1 < nch) issue(c + C::SLOTS - 1, slot == 0 ? C::SLOTS - 1 : slot - 1);
+    read_frags(slot);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  int slot = 0;
+  if (grp == 0) {
+    for (int c = 0; c < nch; ++c) {
+      wait_step(c);
+      bar();
+      read_phase(c, slot);
+      bar();
+      mfmas();
+      slot = slot == C::SLOTS - 1 ? 0 : slot + 1;
+    }
+    bar();  // B's last compute phase
+  } else {
+    wait_step(0);
+    bar();  // phase 0: A reads step 0
+    for (int c = 0; c < nch; ++c) {
+      bar();
+      read_phase(c, slot);
+      wait_step(c + 1);
+      bar();
+      mfmas();
+      slot = slot == C::SLOTS - 1 ? 0 : slot + 1;
+    }
+  }
+
+  // ---- epilogue
+  const int h = lane >> 4;
+  const int S = gridDim.y;
+  if (S > 1) {
+    // split-K: write-through slab stores, then the last arriving split of this tile reduces
+    float* ys = slab + (long long)split * M * N;
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int n = n0 + (wn * WN + j) * 16 + 4 * h;
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        const int m = m0 + (wm * WM + i) * 16 + fr;
+        if (m >= M) continue;
+        const float4 f4 = make_float4(acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]);
+        unsigned long long* qd = reinterpret_cast<unsigned long long*>(ys + (long long)m * N + n);
+        const unsigned long long* w64 = reinterpret_cast<const unsigned long long*>(&f4);
+        __hip_atomic_store(qd, w64[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(qd + 1, w64[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* last = reinterpret_cast<int*>(smem + C::LAST_OFF);
+    if (threadIdx.x == 0) {
+      const int got = __hip_atomic_fetch_add(counters + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int is_last = got == S - 1;
+      if (is_last) __hip_atomic_store(counters + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *last = is_last;
+    }
+    __syncthreads();
+    if (!*last) return;
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int n = n0 + (wn * WN + j) * 16 + 4 * h;
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        const int m = m0 + (wm * WM + i) * 16 + fr;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (m < M)
+          for (int sp = 0; sp < S; ++sp) {  // fixed split order: bitwise reproducible
+            const unsigned long long* qs =
+                reinterpret_cast<const unsigned long long*>(slab + ((long long)sp * M + m) * N + n);
+            unsigned long long rr[2];
+            rr[0] = __hip_atomic_load(qs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            rr[1] = __hip_atomic_load(qs + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const float* p = reinterpret_cast<const float*>(rr);
+            v += f32x4{p[0], p[1], p[2], p[3]};
+          }
+        acc[j][i] = v;
+      }
+    }
+  }
+
+  if constexpr (EPI == DECODE_EPI_RESID) {
+    // residual add + next-norm prep; ONE sum-of-squares partial per (row, block column): the wave sums its WN
+    // tiles, the two n-waves meet in LDS (the stage buffers are free once every wave is past the last compute)
+    float sq[WM];
+#pragma unroll
+    for (int i = 0; i < WM; ++i) sq[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int n = n0 + (wn * WN + j) * 16 + 4 * h;
+      Pack8 wp;
+      const uint2 raw = *reinterpret_cast<const uint2*>(e.w_next + n);
+      wp.u = make_uint4(raw.x, raw.y, 0, 0);
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        const int mloc = (wm * WM + i) * 16 + fr;
+        const int m = m0 + mloc;
+        if (m >= M) continue;
+        f32x4 v = acc[j][i];
+        float* rp = e.resid + (long long)m * N + n;
+        const float4 r = *reinterpret_cast<const float4*>(rp);
+        const float rr[4] = {r.x + v[0], r.y + v[1], r.z + v[2], r.w + v[3]};
+        *reinterpret_cast<float4*>(rp) = make_float4(rr[0], rr[1], rr[2], rr[3]);
+        store4bf(e.xw_out + (long long)m * N + n, rr[0] * (float)wp.h[0], rr[1] * (float)wp.h[1],
+                 rr[2] * (float)wp.h[2], rr[3] * (float)wp.h[3]);
+        sq[i] += rr[0] * rr[0] + rr[1] * rr[1] + rr[2] * rr[2] + rr[3] * rr[3];
+      }
+    }
+    __syncthreads();  // every wave is past its last LDS read
+    float* part = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+      float s2 = sq[i];
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (h == 0) part[wn * C::BM + (wm * WM + i) * 16 + fr] = s2;
+    }
+    __syncthreads();
+    const int P = N / C::BN;
+    for (int rloc = threadIdx.x; rloc < C::BM; rloc += PG_THR) {
+      const int m = m0 + rloc;
+      if (m < M) e.ss_out[(long long)m * P + nt] = part[rloc] + part[C::BM + rloc];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int tile = n0 / 16 + wn * WN + j;
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        const int mloc = (wm * WM + i) * 16 + fr;
+        const int m = m0 + mloc;
+        const bool mok = m < M;
+        f32x4 v = acc[j][i];
+        if (has_rs) {
+          const float sc = rs[mloc];
+          v *= sc;
+        }
+        if constexpr (EPI == DECODE_EPI_BF16) {
+          if (mok) store4bf16(e.out_bf + (long long)m * N + tile * 16 + 4 * h, v);
+        } else {
+          epilogue<EPI>(e, v, tile, m, mok, h, N);
+        }
+      }
+    }
+  }
+}
+
+template <int WM, int WN, int EPI>
+void launch_cfg(const bf16* x, const bf16* W, int M, int N, int K, int S, const DecodeEpi& e, float* slab,
+                int* counters, hipStream_t s) {
+  using C = PgCfg<WM, WN>;
+  const int mtiles = (M + C::BM - 1) / C::BM;
+  const int ntiles = N / C::BN;
+  pgemm_kernel<WM, WN, EPI><<<dim3(mtiles * ntiles, S), dim3(PG_THR), 0, s>>>(x, W, M, N, K, K / S, mtiles, e, slab,
+                                                                              counters);
+}
+
+// the instantiated tile shapes (index = PG_CFG id, kept in sync with pgemm_cfg_shape below)
+#define PG_CFGS(X) \
+  X(0, 6, 7)       \
+  X(1, 4, 8)       \
+  X(2, 3, 6)       \
+  X(3, 3, 4)       \
+  X(4, 4, 4)       \
+  X(5, 2, 4)       \
+  X(6, 5, 7)       \
+  X(7, 4, 7)       \
+  X(8, 3, 7)       \
+  X(9, 3, 8)       \
+  X(10, 2, 8)
+
+template <int EPI>
+void launch_epi(int cfg, const bf16* x, const bf16* W, int M, int N, int K, int S, const DecodeEpi& e, float* slab,
+                int* counters, hipStream_t s) {
+  switch (cfg) {
+#define PG_CASE(id, wm, wn) \
+  case id: launch_cfg<wm, wn, EPI>(x, W, M, N, K, S, e, slab, counters, s); break;
+    PG_CFGS(PG_CASE)
+#undef PG_CASE
+    default: break;
+  }
+}
+
+}  // namespace
+
+int pgemm_cfg_shape(int cfg, int* bm, int* bn) {
+  switch (cfg) {
+#define PG_SHAPE(id, wm, wn) \
+  case id: *bm = 64 * wm; *bn = 32 * wn; return 1;
+    PG_CFGS(PG_SHAPE)
+#undef PG_SHAPE
+    default: return 0;
+  }
+}
+
+void launch_pgemm(int epi, int cfg, const bf16* x, const bf16* Wshuf, int M, int N, int K, int S, const DecodeEpi& e,
+                  float* slab, int* counters, hipStream_t s) {
+  switch (epi) {
+    case DECODE_EPI_QKV: launch_epi<DECODE_EPI_QKV>(cfg, x, Wshuf, M, N, K, S, e, slab, counters, s); break;
+    case DECODE_EPI_RESID: launch_epi<DECODE_EPI_RESID>(cfg, x, Wshuf, M, N, K, S, e, slab, counters, s); break;
+    case DECODE_EPI_SWIGLU: launch_epi<DECODE_EPI_SWIGLU>(cfg, x, Wshuf, M, N, K, S, e, slab, counters, s); break;
+    case DECODE_EPI_BF16: launch_epi<DECODE_EPI_BF16>(cfg, x, Wshuf, M, N, K, S, e, slab, counters, s); break;
+    default: launch_epi<DECODE_EPI_F32>(cfg, x, Wshuf, M, N, K, S, e, slab, counters, s); break;
+  }
+}

@@ -361,10 +361,6 @@ class ModelRunner:
         if "event" in handle:
             handle["event"].synchronize()
             ids = handle["pin"].tolist()
-            fault = getattr(self.model, "engine_fault", None)  # the decode engine's pinned fault word
-            if fault is not None and fault():
-                raise RuntimeError("decode engine: an in-launch edge timed out (a workgroup never arrived); this "
-                                   "step's outputs are invalid")
             check = getattr(self.model.tp, "error", None)  # xGMI collectives: host-mapped word, no sync
             if check is not None and check():
                 from ..parallel.health import TPFaultError

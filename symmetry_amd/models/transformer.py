@@ -73,27 +73,8 @@ ROPE_DECODE_ROWS = os.environ.get("SYMMETRY_ROPE_DECODE_ROWS", "1") != "0"
 #   the in-launch reduction's tail (one of S workgroups per column group sums the slabs) costs o / down /
 #   qkv more than the separate consumer kernel they save.
 MG_FUSED_MODE = os.environ.get("SYMMETRY_MG_FUSED", "gu")
-# prefill steps of <= 256 tokens on the fused general path too (A/B knob)
-MG_FUSED_PREFILL = os.environ.get("SYMMETRY_MG_FUSED_PREFILL", "0") != "0"
 MG_FUSED = MG_FUSED_MODE in ("1", "all")
 MG_FUSED_GU = MG_FUSED_MODE == "gu"
-# Dense decode steps of <= 16 rows run every layer as ONE persistent launch (csrc/kernels/decode_layers.hip: QKV ->
-# attention -> O (+ all-reduce) -> gate_up -> down with in-launch edges, each phase's weights streamed into registers
-# before the edge it waits on).  Off by default: with correct in-launch edges under hipGraphs it does not beat the
-# per-layer launches (one shard on one GPU, bench/tp_shard.py, 10 clients, profiles/r5/engine_tp_shard_epoch.jsonl:
-# 8B TP = 8 1.206 vs 1.201 ms, TP = 4 1.55 vs 1.45, TP = 1 3.44 vs 3.11, 70B TP = 8 4 clients 5.59 vs 4.93; the
-# faster numbers measured earlier came from replayed graphs whose edge-counter memset had stopped working).
-# "auto": TP >= 2 with a GPU per rank (SYMMETRY_ENGINE_TP1=1: also TP = 1); "1": wherever the shape class is built;
-# "0" (default): the per-layer launches.
-# medium-M prefill projections (STREAM_MIN_M..256 rows) on the weight-streaming kernel (ops.sgemm: weights
-# straight into VGPRs from the preshuffled copies, activations through an LDS ring; gate_up with the SwiGLU epilogue)
-# instead of mgemm / hipBLASLt + swiglu
-STREAM_DENSE = os.environ.get("SYMMETRY_STREAM_DENSE", "0") != "0"
-STREAM_MIN_M = int(os.environ.get("SYMMETRY_STREAM_MIN_M", "65"))
-DECODE_ENGINE = os.environ.get("SYMMETRY_DECODE_ENGINE", "0")
-ENGINE_TP1 = os.environ.get("SYMMETRY_ENGINE_TP1", "0") != "0"
-# workgroups of the engine's grid (one per CU; a one-GPU multi-rank rehearsal gives each rank a share)
-ENGINE_GRID = int(os.environ.get("SYMMETRY_ENGINE_GRID", "0"))
 # MFMA-preshuffled copy of the lm_head for the fused decode path's dg_argmax (1 KB per wave load like the layer
 # weights; +1 GB for Llama-3-8B): SYMMETRY_LMHEAD_SHUF=0 keeps the row-major stream
 LMHEAD_SHUF = os.environ.get("SYMMETRY_LMHEAD_SHUF", "1") != "0"
@@ -210,9 +191,6 @@ class TransformerLM:
             ops.decode_ks_ws(self.device)  # allocated before any graph capture (stable address)
         self.dgw = self._decode_copies(decode_weights)
         self.tp_reduced_bytes: dict[str, int] = {}  # bytes per rank of the last general-path all-reduce
-        self.engine_steps = 0  # forward passes (incl. graph captures) that ran the decode-step engine
-        self._engine_cache: dict = {}  # its plan and layer tables (per KV cache)
-        self.engine_stamps = None  # diagnostics: int64 [G * L * 5 * 8] per-phase wall clock (bench/kernels/bench_engine.py)
 
     def _decode_copies(self, mode: str) -> dict:
         """MFMA-preshuffled copies of the decode-GEMM weights (1 KB contiguous per wave load:
@@ -281,11 +259,7 @@ class TransformerLM:
         T, K = x.shape
         N = w.shape[0]
         pick = ops.choose_mgemm(T, N, K) if wshuf is not None else None
-        if STREAM_DENSE and wshuf is not None and STREAM_MIN_M <= T <= 256 and N % 128 == 0 and K % 256 == 0:
-            S = ops.sgemm_splits(T, N, K)
-            y = self._buf(name + ".slab", (S, T, N), torch.float32)
-            ops.sgemm(x, wshuf, y, 1)
-        elif pick is not None:
+        if pick is not None:
             rw, S = pick
             y = self._buf(name + ".slab", (S, T, N), torch.float32)
             ops.mgemm(x, wshuf, y, rw)
@@ -337,8 +311,6 @@ class TransformerLM:
         if self.fused and b.num_tokens <= SKINNY_MAX_M and not self._general_rows(b.num_tokens):
             return self._forward_fused(b, kv)
         mgs = self._mg_plan(b)
-        if mgs is None and MG_FUSED_PREFILL and b.kind != "decode":
-            mgs = self._mg_plan(b, any_kind=True)
         if mgs is not None:
             return self._forward_general_fused(b, kv, mgs)
         return self._forward_general(b, kv)
@@ -410,96 +382,6 @@ class TransformerLM:
         ops.dg_resid(x, W, resid, w_next, xw, ss_t, wshuf=sh)
         return ss_t
 
-    def _engine_plan(self, b: ForwardBatch, kv: KVCache):
-        """(KSq, pieces, grid, xar handle) of the decode-step engine for this step, or None (per-layer launches)."""
-        if (DECODE_ENGINE == "0" or self.device.type == "cpu" or self.cfg.is_moe or not self.dgw
-                or b.kind != "decode" or b.num_tokens > 16 or b.num_tokens != b.num_seqs):
-            return None
-        xar = -1
-        if self._tp_active():
-            get = getattr(self.tp, "engine_xar_handle", None)
-            xar = get() if get is not None else None
-            if xar is None:
-                return None  # the engine all-reduces in-launch: needs the peer-memory communicator
-            if DECODE_ENGINE == "auto" and not ENGINE_GRID and torch.cuda.device_count() < self.tp_size:
-                # ranks sharing a GPU (one-GPU rehearsals): two whole-GPU persistent grids whose edges wait on each
-                # other's all-reduce granules cannot both be resident -- only with an explicit per-rank grid
-                return None
-        elif DECODE_ENGINE == "auto" and not ENGINE_TP1:
-            return None
-
-        bs = kv.block_size
-        if bs < 32 or bs & (bs - 1) or (self.hq % self.hkv) or (self.hq // self.hkv) not in (4, 8):
-            return None
-        plan = self._engine_cache.get("plan")
-        if plan is None:
-            d = self.cfg.hidden_size
-            Fl = self.w.layer(0, "w_gu").shape[0] // 2
-            G = ENGINE_GRID or torch.cuda.get_device_properties(self.device).multi_processor_count
-            ntq = (self.hq + 2 * self.hkv) * self.D // 16
-            # QKV k-slabs: the fewest weight bytes on the busiest workgroup (units dealt round-robin), then the
-            # fewest slabs (TP = 8: 48 tiles -> 4 slabs, every unit 1024 deep; TP = 1: 384 tiles -> 2 slabs, 3
-            # units per workgroup instead of 2 whole-K ones on half of them)
-            cands = [k for k in (1, 2, 4) if d % (k * 256) == 0 and d // k // 256 <= 16]
-            ksq = min(cands, key=lambda k: (-(-ntq * k // G)) / k)
-            ksg = 1  # gate_up / down k-splits (csrc/bindings/xgmi_comm.cpp dl_args: units at most 4096 deep)
-            while d // ksg // 256 > 16 and d % (ksg * 2 * 256) == 0:
-                ksg *= 2
-            ksd = 1
-            while Fl // ksd // 256 > 16 and Fl % (ksd * 2 * 256) == 0:
-                ksd *= 2
-            pieces = (d // ksq // 256, self.hq * self.D // 256, d // ksg // 256, Fl // ksd // 256)
-            ok = (d % (ksq * 256) == 0 and (self.hq * self.D) % 256 == 0 and Fl % 256 == 0
-                  and ops.decode_layers_built(*pieces, ksq, self.hq // self.hkv))
-            plan = (ksq, Fl, G) if ok else ()
-            self._engine_cache["plan"] = plan
-        if not plan:
-            return None
-        return plan + (xar,)
-
-    def _engine_table(self, kv: KVCache) -> torch.Tensor:
-        """int64 [L, 8] device table of every layer's engine operands (csrc/kernels/launchers.h DLLayer)."""
-        key = ("table", kv.k.data_ptr(), kv.v.data_ptr())
-        t = self._engine_cache.get(key)
-        if t is None:
-            w, L = self.w, self.cfg.num_layers
-            rows = []
-            for i in range(L):
-                lnn = w.layer(i + 1, "ln1") if i + 1 < L else w["norm"]
-                rows.append([self.dgw[(i, "wqkv")].data_ptr(), self.dgw[(i, "wo")].data_ptr(),
-                             self.dgw[(i, "w_gu")].data_ptr(), self.dgw[(i, "w_down")].data_ptr(),
-                             w.layer(i, "ln2").data_ptr(), lnn.data_ptr(), kv.k[i].data_ptr(), kv.v[i].data_ptr()])
-            t = torch.tensor(rows, dtype=torch.int64, device=self.device)
-            self._engine_cache[key] = t
-        return t
-
-    def _run_engine(self, b: ForwardBatch, kv: KVCache, plan, resid, xw, ss_t, ss_1, attn) -> bool:
-        ksq, Fl, G, xar = plan
-        T, L = b.num_tokens, self.cfg.num_layers
-        nq = (self.hq + 2 * self.hkv) * self.D
-        qkv_ws = self._buf("dl.qkv", (ksq * T * nq,), torch.float32)
-        act = self._buf("act", (T, Fl), torch.bfloat16)
-        edge = self.ws.get("dl.edge", (ops.decode_layers_edge_words(L, T, self.hq, self.hkv, G),), torch.int32,
-                           self.device, zeros=True)
-        fault = self._engine_cache.get("fault")
-        if fault is None:  # pinned host word: the runner reads it after every step without a sync
-            fault = self._engine_cache["fault"] = torch.zeros(1, dtype=torch.int32).pin_memory()
-        return ops.decode_layers(self._engine_table(kv), self.hq, self.hkv, Fl, ksq, b.positions, b.slot_mapping,
-                                 b.block_tables, b.ctx_lens, kv.block_size, self.cos_sin, self.scale, self.cfg.rms_eps,
-                                 resid, xw, ss_t, ss_1, qkv_ws, attn.view(T, -1), act, edge, fault, G, xar,
-                                 self.engine_stamps)
-
-    def engine_fault(self) -> int:
-        """Nonzero (1 + the phase event) once an engine edge gave up waiting: that step's outputs are invalid.
-        Read after the step's completion event; re-armed by the reader."""
-        f = self._engine_cache.get("fault")
-        if f is None:
-            return 0
-        v = int(f[0])
-        if v:
-            f.zero_()
-        return v
-
     def _forward_fused(self, b: ForwardBatch, kv: KVCache) -> torch.Tensor:
         cfg, w = self.cfg, self.w
         T, d, eps = b.num_tokens, cfg.hidden_size, cfg.rms_eps
@@ -511,14 +393,7 @@ class TransformerLM:
         attn = self._buf("attn", (T, self.hq, self.D), torch.bfloat16)
         ops.embed_prep(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), xw, ss_1, b.src, self.last_ids)
         ss = ss_1
-        plan = self._engine_plan(b, kv)
-        if plan is not None and self._run_engine(b, kv, plan, resid, xw, ss_t, ss_1, attn):
-            self.engine_steps += 1
-            layers = range(0)  # every layer ran in the engine's launch
-            ss = ss_t
-        else:
-            layers = range(cfg.num_layers)
-        for i in layers:
+        for i in range(cfg.num_layers):
             wq, shq = self._dgw(i, "wqkv")
             attn2d = attn.view(T, self.hq * self.D)
             nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
@@ -628,17 +503,10 @@ class TransformerLM:
                 mlp = self.moe.forward(i, x)
             else:
                 ops.add_rms_norm(o, resid, w.layer(i, "ln2"), eps, x)
-                gsh = self._shuf(i, "w_gu")
-                if (STREAM_DENSE and gsh is not None and STREAM_MIN_M <= T <= 256 and gsh.shape[0] % 128 == 0
-                        and gsh.shape[1] % 256 == 0):
-                    # gate_up + SwiGLU in one weight-streaming launch (no [T, 2F] intermediate)
-                    act = self._buf("act", (T, gsh.shape[0] // 2), torch.bfloat16)
-                    ops.sgemm(x, gsh, act, 3)
-                else:
-                    gu = self._linear("gu", x, w.layer(i, "w_gu"), wshuf=gsh)
-                    F = gu.shape[-1] // 2
-                    act = self._buf("act", (T, F), torch.bfloat16)
-                    ops.swiglu(gu, act, interleaved=True)
+                gu = self._linear("gu", x, w.layer(i, "w_gu"), wshuf=self._shuf(i, "w_gu"))
+                F = gu.shape[-1] // 2
+                act = self._buf("act", (T, F), torch.bfloat16)
+                ops.swiglu(gu, act, interleaved=True)
                 mlp = self._linear("down", act, w.layer(i, "w_down"), reduce=True, wshuf=self._shuf(i, "w_down"))
             nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
             ops.add_rms_norm(mlp, resid, nxt, eps, x)

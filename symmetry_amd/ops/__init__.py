@@ -129,9 +129,6 @@ def mgemm(x, w_shuf, y, rw: int):
     return reference.skinny_gemm(x, reference.unshuffled(w_shuf, True), y)
 
 
-_MG_GU_WIDE = os.environ.get("SYMMETRY_MG_GU_WIDE", "0") != "0"  # A/B: the wide gate_up (+ SwiGLU) on mgemm
-
-
 def choose_mgemm(M: int, N: int, K: int, cus: int = 256, fused: bool = False):
     """(rw, S) of mgemm for an [M, K] x [N, K]^T projection, or None where another kernel is the better
     choice.  Measured on MI355X (profiles/mgemm_r2.jsonl, mgemm_small_r2.jsonl; each arm followed by its
@@ -145,8 +142,7 @@ def choose_mgemm(M: int, N: int, K: int, cus: int = 256, fused: bool = False):
     workgroup spread over the grid."""
     if not _MGEMM_ON or M > MGEMM_MAX_M or K % 64:
         return None
-    wide = fused and _MG_GU_WIDE and N > 8192  # fused epilogue: no fp32 slabs to write / re-read at S = 1
-    if M > 64 and not wide and (N > 8192 or (M > 192 and K < 8192 and N < 6144)):
+    if M > 64 and (N > 8192 or (M > 192 and K < 8192 and N < 6144)):
         return None
     mt = 2 if M <= 32 else 4 if M <= 64 else 8 if M <= 128 else 16
     a_us_mb, b_us_mb = {2: (11.5, 2.2), 4: (11.5, 2.2), 8: (20.0, 1.0), 16: (30.0, 1.0)}[mt]
@@ -160,7 +156,7 @@ def choose_mgemm(M: int, N: int, K: int, cus: int = 256, fused: bool = False):
             wgs = N // (64 * rw) * S
             if wgs < cus // 2 or wgs > cus:
                 continue
-            slabs = 0 if (wide and S == 1) else b_us_mb * S * M * N * 4 / 1e6
+            slabs = b_us_mb * S * M * N * 4 / 1e6
             t = (a_us_mb * (64 * rw + M) * (K // S) * 2 / 1e6 + slabs
                  + 1000.0 / wgs)  # per-workgroup fixed cost (prologue, epilogue), spread over the grid
             if best is None or t < best[0]:
@@ -243,33 +239,6 @@ def dg_argmax(x, W, ss_in, eps, temps, seeds, step, tile_keys, out_keys, out_ids
                                out_keys, out_ids, n_offset, logits)
 
 
-def decode_layers_built(cq: int, co: int, cg: int, cd: int, ks: int, gh: int) -> bool:
-    """Is the decode-step engine instantiated for this shape class (k pieces per wave of QKV / O / gate_up / down
-    units, QKV k-slabs, query heads per kv head; csrc/kernels/decode_layers.hip DL_SHAPES)?"""
-    return native_available() and bool(_native.ops().decode_layers_pieces(int(cq), int(co), int(cg), int(cd), int(ks),
-                                                                           int(gh)))
-
-
-def decode_layers_edge_words(L: int, M: int, Hq: int, Hkv: int, G: int) -> int:
-    """int32 words of the engine's edge tensor: edge words, attention counters, attention partials
-    (csrc/kernels/launchers.h dl_edge_words)."""
-    return int(_native.ops().decode_layers_edge_words(int(L), int(M), int(Hq), int(Hkv), int(G)))
-
-
-def decode_layers(table, Hq, Hkv, Fl, KSq, positions, slots, block_tables, ctx_lens, BS, cos_sin, scale, eps, resid,
-                  xw, ss, ss0, qkv_ws, attn, act, edge, fault, G, xar=-1, stamps=None) -> bool:
-    """Every layer of a dense decode step in ONE persistent launch (csrc/kernels/decode_layers.hip): QKV ->
-    attention -> O (+ all-reduce on the ``xar`` communicator, -1 = world 1) -> gate_up -> down, edges in-launch,
-    next-phase weights streamed before each edge.  resid / xw / ss: the residual stream and the deferred-norm
-    inputs (layer 0's partials in ``ss0``), updated in place to the last layer's outputs.  ``stamps`` (int64
-    [G * L * 5 * 8], diagnostics): every workgroup's wall clock when each phase's edge passed / it signalled the
-    phase.  False: the shape class is not built or the grid would not be resident (nothing launched; run the
-    per-layer launches)."""
-    return bool(_native.ops().decode_layers(table, int(Hq), int(Hkv), int(Fl), int(KSq), positions, slots,
-                                            block_tables, ctx_lens, int(BS), cos_sin, float(scale), float(eps), resid,
-                                            xw, ss, ss0, qkv_ws, attn, act, edge, fault, int(G), int(xar), stamps))
-
-
 def embed_prep(ids, table, resid, w, xw, ss, src=None, prev=None):
     """Embedding gather + deferred-norm prep; with ``src``/``prev`` a row whose src >= 0 takes its token
     from ``prev[src]`` (the previous step's device-resident samples: pipelined decode)."""
@@ -324,34 +293,6 @@ def grouped_gemm(xs, W, offsets, e0, y, mode):
     if _gpu(xs):
         return _native.ops().grouped_gemm(xs, W, offsets, int(e0), y, int(mode))
     return reference.grouped_gemm(xs, W, offsets, e0, y, mode)
-
-
-def sgemm(x, w_shuf, y, mode: int = 1):
-    """Dense medium-M projection (<= 256 rows) on the weight-streaming kernel (csrc/kernels/moe.hip): mode 1 ->
-    fp32 split-K slabs y [S, M, N] (the mgemm / skinny contract); mode 3 -> SwiGLU of the tile-interleaved gate/up
-    rows (models/layout.py), y = act bf16 [M, N / 2].  ``w_shuf``: the MFMA-preshuffled weight."""
-    if _gpu(x):
-        return _native.ops().sgemm(x, w_shuf, y, int(mode))
-    w = reference.unshuffled(w_shuf, True)
-    if mode == 3:
-        return reference.swiglu((x.float() @ w.float().t()).unsqueeze(0), y, True)
-    return reference.skinny_gemm(x, w, y)
-
-
-def sgemm_splits(M: int, N: int, K: int, cus: int = 256) -> int:
-    """k split of an sgemm fp32-slab launch: the smallest S (a divisor of K / 256: whole ring turns per unit)
-    whose N / 128 x S units fill >= 3/4 of the CUs in one round, else the largest single-round one."""
-    nb, nk = N // 128, K // 256
-    best = 1
-    for S in range(1, nk + 1):
-        if nk % S:
-            continue
-        if nb * S > cus:
-            break
-        best = S
-        if nb * S >= 3 * cus // 4:
-            break
-    return best
 
 
 def grouped_stream_policy(p: int) -> None:

@@ -302,13 +302,6 @@ class XgmiComm(Comm):
             self.calls["gemm_ar"] = self.calls.get("gemm_ar", 0) + 1
         return ok
 
-    def engine_xar_handle(self):
-        """The fused all-reduce communicator the decode-step engine pushes its O / down tiles through (or None:
-        the engine then stays off under TP)."""
-        if not XAR or self.xar is None:
-            return None
-        return self.xar.handle
-
     def argmax_keys(self, keys, ids):
         if keys.is_cuda and keys.is_contiguous() and keys.numel() <= 4096:
             self.ops.xgmi_keys_max(keys, ids, self.handle)

@@ -48,6 +48,10 @@ def _check(r, n, mode):
     assert r["p50_ttft_ms"] == ce["p50_ttft_ms"] and r["client_end_per_client_tokens_per_s"] > 0
     assert r["unit"] == "tokens/s per client" and r["value"] == ce["per_client_tokens_per_s_median"]
     assert r["value_source"].startswith("client_end")
+    # every token the first two clients were streamed agrees with the fp32 oracle of the same weights (under TP the
+    # oracle runs sharded over the ranks and sums / gathers like the engine)
+    v = r["verified"]
+    assert v["clients"] == 2 and v["tokens"] >= 2 * 3 and v["mismatches"] == 0, v
 
 
 def test_bench_single_process():

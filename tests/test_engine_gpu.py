@@ -545,42 +545,6 @@ def test_grouped_stream_mixtral_shapes(gpu, mode, pre):
         torch.testing.assert_close(yc[a:b], p, atol=tol, rtol=tol)
 
 
-@pytest.mark.parametrize("M", [70, 128, 200, 256])
-@pytest.mark.parametrize("shape", [(6144, 4096), (4096, 14336), (1024, 512)])
-def test_sgemm_slabs_vs_fp32(gpu, M, shape):
-    """Dense medium-M projection on the weight-streaming kernel: fp32 split-K slabs (k split from sgemm_splits
-    and S = 1) against the fp32 product, MFMA-preshuffled weights."""
-    from symmetry_amd.models.layout import preshuffle
-
-    N, K = shape
-    g = torch.Generator(device=gpu).manual_seed(M + N)
-    x = torch.randn(M, K, device=gpu, generator=g).bfloat16()
-    W = (torch.randn(N, K, device=gpu, generator=g) * 0.02).bfloat16()
-    ref = x.float() @ W.float().t()
-    for S in sorted({1, ops.sgemm_splits(M, N, K)}):
-        y = torch.full((S, M, N), 7.0, device=gpu)
-        ops.sgemm(x, preshuffle(W), y, 1)
-        torch.testing.assert_close(y.sum(0), ref, atol=2e-3, rtol=2e-3)
-
-
-@pytest.mark.parametrize("M", [64, 128, 176, 256])
-def test_sgemm_interleaved_swiglu_vs_fp32(gpu, M):
-    """The streaming kernel's SwiGLU epilogue on the decode layout's tile-interleaved gate/up rows (lane ^ 32
-    exchange) against fp32 silu(gate) * up."""
-    from symmetry_amd.models.layout import preshuffle
-    from symmetry_amd.ops import reference
-
-    F, K = 1024, 4096
-    g = torch.Generator(device=gpu).manual_seed(M)
-    x = torch.randn(M, K, device=gpu, generator=g).bfloat16()
-    W = (torch.randn(2 * F, K, device=gpu, generator=g) * 0.02).bfloat16()
-    act = torch.zeros(M, F, device=gpu, dtype=torch.bfloat16)
-    ops.sgemm(x, preshuffle(W), act, 3)
-    want = torch.empty(M, F, device=gpu)
-    reference.swiglu((x.float() @ W.float().t()).unsqueeze(0), want, True)
-    torch.testing.assert_close(act.float(), want, atol=2e-2, rtol=2e-2)
-
-
 def test_mixtral_prefill_grouped_path_matches_oracle(gpu):
     """tiny-mixtral prefill of more than 64 routed rows: the grouped MFMA GEMM path (no host sync) end to
     end against the fp32 oracle, with the decode steps in hipGraphs."""

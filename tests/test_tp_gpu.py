@@ -27,7 +27,7 @@ def _port():
     return p
 
 
-def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False, engine=False):
+def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False):
     import traceback
 
     prompts = prompts or PROMPTS
@@ -37,10 +37,7 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False, en
                       # (<= 64 workgroups per rank) are co-resident on the one GPU
                       SYMMETRY_XGMI_FUSED="force",
                       # graphs: decode steps captured and replayed with every collective on the xGMI kernels
-                      SYMMETRY_XGMI_GRAPHS="1" if graphs else "0",
-                      # engine: every decode step as ONE persistent launch per rank, 128 workgroups each (both ranks'
-                      # grids co-resident on the one GPU)
-                      SYMMETRY_DECODE_ENGINE="auto" if engine else "0", SYMMETRY_ENGINE_GRID="128")
+                      SYMMETRY_XGMI_GRAPHS="1" if graphs else "0")
     try:
         from symmetry_amd.engine.llm_engine import EngineConfig
         from symmetry_amd.engine.sequence import SamplingParams
@@ -66,9 +63,7 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False, en
             eng.shutdown()  # the worker leaves its loop whatever happened here
         if graphs:
             assert eng.runner.use_graphs and eng.runner.graph_replays > 0, "decode steps did not replay graphs"
-        if engine:
-            assert eng.runner.model.engine_steps > 0, "the decode-step engine never ran"
-        if xgmi == "1" and not engine:
+        if xgmi == "1":
             calls = eng.runner.model.tp.calls
             # decode steps ran the peer-memory all-reduce: fused into the row-parallel GEMMs (one XAR launch each:
             # GEMM + all-reduce + residual) for the dense model, the fused add_prep kernel around the MoE block
@@ -92,13 +87,13 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False, en
             dist.destroy_process_group()
 
 
-def _run(model, world=2, xgmi="0", prompts=None, extra=False, graphs=False, engine=False):
+def _run(model, world=2, xgmi="0", prompts=None, extra=False, graphs=False):
     import torch.multiprocessing as mp
 
     port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    procs = [ctx.Process(target=_entry, args=(model, r, world, port, q, xgmi, prompts, graphs, engine))
+    procs = [ctx.Process(target=_entry, args=(model, r, world, port, q, xgmi, prompts, graphs))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -189,9 +184,3 @@ def test_tp2_fused_xar_under_hipgraphs_on_one_gpu(gpu):
     _check_oracle("small-llama", PROMPTS, outs)
 
 
-def test_tp2_decode_engine_on_one_gpu(gpu):
-    """The decode-step engine under TP = 2 between two processes on one GPU: one persistent launch per rank per
-    decode step (128 workgroups each), the O / down all-reduces pushed through the fused communicator's peer slots
-    inside it, decode steps captured into hipGraphs; every token within bf16 noise of the fp32 oracle."""
-    outs = _run("small-llama", xgmi="1", graphs=True, engine=True)
-    _check_oracle("small-llama", PROMPTS, outs)
