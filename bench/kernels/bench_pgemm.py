@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--splits", type=int, nargs="+", default=[1, 2, 4])
     ap.add_argument("--max-waves", type=float, default=2.2, help="skip grids above this many waves of 256 CUs")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--profile", type=int, nargs=2, default=None, metavar=("CFG", "S"),
+                    help="rocprof mode: run only this config and the library GEMM, 10 plain launches each per shape")
     args = ap.parse_args()
     ops = _native.ops()
     dev = torch.device("cuda")
@@ -53,6 +55,25 @@ def main():
     cfgs = [(c, tuple(ops.pgemm_shape(c))) for c in args.cfgs]
     cfgs = [(c, s) for c, s in cfgs if s]
     out = open(args.out, "a") if args.out else None
+    if args.profile:
+        c, S = args.profile
+        bm, bn = cfgs[[cc for cc, _ in cfgs].index(c)][1]
+        for name in args.shapes:
+            N, K = SHAPES[name]
+            w = preshuffle((torch.rand(N, K, device=dev) * 2 - 1).mul_(0.05).bfloat16())
+            for T in args.tokens:
+                x = (torch.rand(T, K, device=dev) * 2 - 1).bfloat16()
+                y = torch.empty(T, N, device=dev, dtype=torch.bfloat16)
+                tiles = -(-T // bm) * (N // bn)
+                slab = torch.empty(S, T, N, device=dev) if S > 1 else None
+                cnt = torch.zeros(tiles, dtype=torch.int32, device=dev) if S > 1 else None
+                for _ in range(10):
+                    ops.pgemm(x, w, y, c, S, slab, cnt)
+                for _ in range(10):
+                    torch.matmul(x, w.t(), out=y)
+                torch.cuda.synchronize()
+                print(json.dumps({"profiled": name, "T": T, "cfg": c, "S": S}), flush=True)
+        return
     for name in args.shapes:
         N, K = SHAPES[name]
         w = (torch.rand(N, K, device=dev) * 2 - 1).mul_(0.05).bfloat16()

@@ -289,8 +289,8 @@ PgShape pg_check(const Tensor& x, const Tensor& w, int64_t cfg, int64_t S, const
   TORCH_CHECK(mpad * K * 2 < (1LL << 31) && N * K * 2 < (1LL << 31), "pgemm: operands exceed 2 GB");
   const int64_t tiles = mpad / bm * (N / bn);
   TORCH_CHECK(tiles < (1LL << 31) / 8, "pgemm: too many tiles");
-  if (S > 1) {
-    TORCH_CHECK(slab.has_value() && counters.has_value(), "pgemm: split-K needs slab + counters");
+  if (S > 1 && counters.has_value()) {  // in-launch reduction (without counters: y itself is the slab array)
+    TORCH_CHECK(slab.has_value(), "pgemm: the in-launch split-K reduction needs a slab");
     check_gpu(*slab, "slab");
     check_dtype(*slab, at::kFloat, "slab");
     check_gpu(*counters, "counters");
@@ -304,11 +304,22 @@ PgShape pg_check(const Tensor& x, const Tensor& w, int64_t cfg, int64_t S, const
 float* opt_f32(const c10::optional<Tensor>& t) { return t.has_value() ? ptr<float>(*t) : nullptr; }
 int* opt_i32(const c10::optional<Tensor>& t) { return t.has_value() ? ptr<int>(*t) : nullptr; }
 
-// y [M, N] bf16 or fp32 = x @ w^T (w MFMA-preshuffled)
+// y [M, N] bf16 or fp32 = x @ w^T (w MFMA-preshuffled).  S > 1 with counters: the k splits are summed in-launch
+// (slab scratch); S > 1 without counters: y is fp32 [S, M, N], one partial slab per split (LinOut consumers sum).
 void pgemm(const Tensor& x, const Tensor& w, Tensor& y, int64_t cfg, int64_t S, const c10::optional<Tensor>& slab,
            const c10::optional<Tensor>& counters) {
   const auto sh = pg_check(x, w, cfg, S, slab, counters);
   check_gpu(y, "y");
+  if (S > 1 && !counters.has_value()) {
+    check_dtype(y, at::kFloat, "y");
+    TORCH_CHECK(y.dim() == 3 && y.size(0) == S && y.size(1) == sh.M && y.size(2) == sh.N, "pgemm: y must be [S, M, N]");
+    DecodeEpi e;
+    e.wshuf = 1;
+    const at::OptionalDeviceGuard g(x.device());
+    launch_pgemm(DECODE_EPI_F32, (int)cfg, ptr<bf16>(x), ptr<bf16>(w), (int)sh.M, (int)sh.N, (int)sh.K, (int)S, e,
+                 ptr<float>(y), nullptr, cur_stream(x));
+    return;
+  }
   TORCH_CHECK(y.numel() == sh.M * sh.N, "pgemm: y must be [M, N]");
   DecodeEpi e;
   e.wshuf = 1;
@@ -323,6 +334,96 @@ void pgemm(const Tensor& x, const Tensor& w, Tensor& y, int64_t cfg, int64_t S, 
   const at::OptionalDeviceGuard g(x.device());
   launch_pgemm(epi, (int)cfg, ptr<bf16>(x), ptr<bf16>(w), (int)sh.M, (int)sh.N, (int)sh.K, (int)S, e, opt_f32(slab),
                opt_i32(counters), cur_stream(x));
+}
+
+// pgemm with a fused epilogue (S = 1): QKV (RoPE + paged K/V write + q out), SWIGLU (tile-interleaved gate/up rows
+// -> act [M, N / 2]), RESID (resid += y; xw = bf16(resid * w_next); ss_out [M, N / BN] one partial per row and
+// block column).  ss_in: the producer's sum-of-squares partials of x's rows (deferred RMSNorm) or none.
+void pg_norm_in(DecodeEpi& e, const c10::optional<Tensor>& ss_in, int64_t M, int64_t K, double eps) {
+  if (!ss_in.has_value()) return;
+  check_gpu(*ss_in, "ss_in");
+  check_dtype(*ss_in, at::kFloat, "ss_in");
+  TORCH_CHECK(ss_in->dim() == 2 && ss_in->size(0) >= M && ss_in->size(1) >= 1, "ss_in must be [>=M, P]");
+  e.ss_in = ptr<float>(*ss_in);
+  e.ss_tiles = (int)ss_in->size(1);
+  e.inv_d = 1.f / (float)K;
+  e.eps = (float)eps;
+}
+
+void pg_qkv(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, const Tensor& positions,
+            const Tensor& slots, const Tensor& cos_sin, Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t Hq,
+            int64_t Hkv, int64_t cfg) {
+  const auto sh = pg_check(x, W, cfg, 1, c10::nullopt, c10::nullopt);
+  for (auto* t : {&positions, &slots}) {
+    check_gpu(*t, "index tensor");
+    check_dtype(*t, at::kInt, "index tensor");
+  }
+  check_gpu(cos_sin, "cos_sin");
+  check_dtype(cos_sin, at::kFloat, "cos_sin");
+  check_cache(k_cache, v_cache);
+  check_gpu(q_out, "q_out");
+  check_dtype(q_out, at::kBFloat16, "q_out");
+  TORCH_CHECK(sh.N == (Hq + 2 * Hkv) * 128, "pg_qkv: N must be (Hq + 2 Hkv) * 128");
+  TORCH_CHECK(k_cache.size(1) == Hkv, "pg_qkv: cache head count");
+  TORCH_CHECK(positions.numel() >= sh.M && slots.numel() >= sh.M, "pg_qkv: positions/slots too short");
+  TORCH_CHECK(q_out.numel() >= sh.M * Hq * 128, "pg_qkv: q_out too small");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == 128, "pg_qkv: cos_sin [max_pos, 128]");
+  DecodeEpi e;
+  e.wshuf = 1;
+  pg_norm_in(e, ss_in, sh.M, sh.K, eps);
+  e.positions = ptr<int>(positions);
+  e.slots = ptr<int>(slots);
+  e.cos_sin = ptr<float>(cos_sin);
+  e.q_out = ptr<bf16>(q_out);
+  e.k_cache = ptr<bf16>(k_cache);
+  e.v_cache = ptr<bf16>(v_cache);
+  e.Hq = (int)Hq;
+  e.Hkv = (int)Hkv;
+  e.BS = (int)k_cache.size(2);
+  const at::OptionalDeviceGuard g(x.device());
+  launch_pgemm(DECODE_EPI_QKV, (int)cfg, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, 1, e, nullptr,
+               nullptr, cur_stream(x));
+}
+
+void pg_swiglu(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss_in, double eps, Tensor& act,
+               int64_t cfg) {
+  const auto sh = pg_check(x, W, cfg, 1, c10::nullopt, c10::nullopt);
+  check_gpu(act, "act");
+  check_dtype(act, at::kBFloat16, "act");
+  TORCH_CHECK(act.numel() == sh.M * sh.N / 2, "pg_swiglu: act must be [M, N / 2]");
+  DecodeEpi e;
+  e.wshuf = 1;
+  pg_norm_in(e, ss_in, sh.M, sh.K, eps);
+  e.act = ptr<bf16>(act);
+  const at::OptionalDeviceGuard g(x.device());
+  launch_pgemm(DECODE_EPI_SWIGLU, (int)cfg, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, 1, e, nullptr,
+               nullptr, cur_stream(x));
+}
+
+void pg_resid(const Tensor& x, const Tensor& W, Tensor& resid, const Tensor& w_next, Tensor& xw_out, Tensor& ss_out,
+              int64_t cfg) {
+  const auto sh = pg_check(x, W, cfg, 1, c10::nullopt, c10::nullopt);
+  check_gpu(resid, "resid");
+  check_dtype(resid, at::kFloat, "resid");
+  check_gpu(w_next, "w_next");
+  check_dtype(w_next, at::kBFloat16, "w_next");
+  check_gpu(xw_out, "xw_out");
+  check_dtype(xw_out, at::kBFloat16, "xw_out");
+  check_gpu(ss_out, "ss_out");
+  check_dtype(ss_out, at::kFloat, "ss_out");
+  TORCH_CHECK(resid.numel() == sh.M * sh.N && xw_out.numel() == sh.M * sh.N && w_next.numel() == sh.N,
+              "pg_resid: shape mismatch");
+  TORCH_CHECK(ss_out.dim() == 2 && ss_out.size(0) >= sh.M && ss_out.size(1) == sh.N / sh.bn,
+              "pg_resid: ss_out must be [M, N / BN]");
+  DecodeEpi e;
+  e.wshuf = 1;
+  e.resid = ptr<float>(resid);
+  e.w_next = ptr<bf16>(w_next);
+  e.xw_out = ptr<bf16>(xw_out);
+  e.ss_out = ptr<float>(ss_out);
+  const at::OptionalDeviceGuard g(x.device());
+  launch_pgemm(DECODE_EPI_RESID, (int)cfg, ptr<bf16>(x), ptr<bf16>(W), (int)sh.M, (int)sh.N, (int)sh.K, 1, e, nullptr,
+               nullptr, cur_stream(x));
 }
 
 void lm_head_sample(const Tensor& x, const Tensor& w, const Tensor& temps, const Tensor& seeds, const Tensor& step,
@@ -1027,6 +1128,13 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("mgemm(Tensor x, Tensor w, Tensor(a!) y, int rw) -> ()", &mgemm);
   m.def("mgemm_nt(int on) -> ()", [](int64_t on) { set_mgemm_nt((int)on); });
   m.def("pgemm(Tensor x, Tensor w, Tensor(a!) y, int cfg, int S, Tensor? slab, Tensor? counters) -> ()", &pgemm);
+  m.def(
+      "pg_qkv(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor positions, Tensor slots, Tensor cos_sin, "
+      "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int cfg) -> ()",
+      &pg_qkv);
+  m.def("pg_swiglu(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor(a!) act, int cfg) -> ()", &pg_swiglu);
+  m.def("pg_resid(Tensor x, Tensor W, Tensor(a!) resid, Tensor w_next, Tensor(b!) xw_out, Tensor(c!) ss_out, int cfg) -> ()",
+        &pg_resid);
   m.def("pgemm_shape(int cfg) -> int[]", [](int64_t cfg) {
     int bm = 0, bn = 0;
     if (!pgemm_cfg_shape((int)cfg, &bm, &bn)) return std::vector<int64_t>{};

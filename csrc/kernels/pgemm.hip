@@ -37,6 +37,12 @@
 namespace {
 
 constexpr int PG_THR = 512;
+#ifndef PG_ABLATE
+#define PG_ABLATE 0
+#endif
+#ifndef PG_SPLIT_ISSUE  // 1: a wave's weight DMAs go out between its MFMAs (compute phase), 0: right after them
+#define PG_SPLIT_ISSUE 1
+#endif
 #ifndef PG_MAX_SLOTS
 #define PG_MAX_SLOTS 4
 #endif
@@ -66,7 +72,8 @@ struct PgCfg {
   static constexpr int EXTRA = BM * 4 + 1024 + 16;  // row scales, dummy-fill target, split-K "last" flag
   static constexpr int SLOTS_FIT = (160 * 1024 - EXTRA) / SLOT;
   static constexpr int SLOTS = SLOTS_FIT > PG_MAX_SLOTS ? PG_MAX_SLOTS : SLOTS_FIT;
-  static constexpr int KEEP = (SLOTS - 2) * PW;  // this wave's younger DMAs left in flight at a step's wait
+  static constexpr int KEEP = (SLOTS - 2) * PW;  // this wave's younger DMAs left in flight at a step's wait (A)
+  static constexpr int KEEP_B = (SLOTS - 3) * PW + NXU;  // ... at group B's wait (see the main loop)
   static constexpr int RS_OFF = SLOTS * SLOT;
   static constexpr int DUMMY_OFF = RS_OFF + BM * 4;
   static constexpr int LAST_OFF = DUMMY_OFF + 1024;
@@ -130,18 +137,25 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
     dw[u] = real ? C::XS + j * 1024 : -1;
   }
 
-  auto issue = [&](int c, int slot) {
+  auto issue_x = [&](int c, int slot) {
     char* const sb = smem + slot * C::SLOT;
 #pragma unroll
     for (int u = 0; u < C::NXU; ++u) {
       if ((C::NX % 8) == 0 || u + 1 < C::NXU || dx[u] >= 0) pg_dma(rx, vx[u], c * 64, sb + dx[u]);
       else pg_dma(rw, vw[0], 0, smem + C::DUMMY_OFF);
     }
+  };
+  auto issue_w = [&](int c, int slot) {
+    char* const sb = smem + slot * C::SLOT;
 #pragma unroll
     for (int u = 0; u < C::NWU; ++u) {
       if ((C::NW % 8) == 0 || u + 1 < C::NWU || dw[u] >= 0) pg_dma(rw, vw[u], c * 1024, sb + dw[u]);
       else pg_dma(rw, vw[u], 0, smem + C::DUMMY_OFF);
     }
+  };
+  auto issue = [&](int c, int slot) {
+    issue_x(c, slot);
+    issue_w(c, slot);
   };
 
   // ---- fragment addresses: x lane reads token row (lane & 15) of its 16-row tile, k 8 (lane >> 4) .. + 8 of the
@@ -164,37 +178,40 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
 #pragma unroll
     for (int i = 0; i < WM; ++i) xf[i] = *(const bf16x8*)(sb + xo + i * 1024);
   };
-  auto mfmas = [&]() {
+  // the compute phase: the MFMAs of the fragments in registers, with this wave's weight DMAs of step ci (into
+  // slot si) issued after the first two rows (DMA issue spread over both phases of every wave)
+  auto mfmas = [&](int ci, int si) {
+#if PG_ABLATE == 1  // probe builds only (bench/kernels/pgemm_probe.py): no MFMAs, fragments kept live
+#pragma unroll
+    for (int j = 0; j < WN; ++j) asm volatile("" ::"v"(wf[j]));
+#pragma unroll
+    for (int i = 0; i < WM; ++i) asm volatile("" ::"v"(xf[i]));
+    if (ci >= 0) issue_w(ci, si);
+#else
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int j = 0; j < WN; ++j)
+    for (int j = 0; j < WN; ++j) {
 #pragma unroll
       for (int i = 0; i < WM; ++i) acc[j][i] = mfma16(wf[j], xf[i], acc[j][i]);
+      if (PG_SPLIT_ISSUE && (j == 1 || (WN == 1 && j == 0))) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (ci >= 0) issue_w(ci, si);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
+    if (!PG_SPLIT_ISSUE && ci >= 0) issue_w(ci, si);
+#endif
   };
 
-  // ---- deferred-RMSNorm row scales of the block's rows: tpr threads per row sum the producer's partials
-  // (loads issued ahead of the first stage's DMAs, summed behind them)
   float* const rs = reinterpret_cast<float*>(smem + C::RS_OFF);
-  constexpr int TPR = (PG_THR / C::BM) >= 8 ? 8 : (PG_THR / C::BM) >= 4 ? 4 : (PG_THR / C::BM) >= 2 ? 2 : 1;
-  const int rrow = threadIdx.x / TPR, rsub = threadIdx.x % TPR;
-  float rpart = 0.f;
   const bool has_rs = e.ss_in != nullptr;
-  if (has_rs && rrow < C::BM && m0 + rrow < M) {
-    const float* sp = e.ss_in + (long long)(m0 + rrow) * e.ss_tiles;
-    for (int i = rsub; i < e.ss_tiles; i += TPR) rpart += sp[i];
-  }
 
   const int nch = kslice / 32;
 #pragma unroll
   for (int c = 0; c < C::SLOTS - 1; ++c)
     if (c < nch) issue(c, c);
 
-  if (has_rs) {
-#pragma unroll
-    for (int o = 1; o < TPR; o *= 2) rpart += __shfl_xor(rpart, o, 64);
-    if (rrow < C::BM && rsub == 0) rs[rrow] = rsqrtf(rpart * e.inv_d + e.eps);
-  }
 
   // Ping-pong over two wave groups (one wave of each per SIMD): group A (waves 0-3) reads step c's fragments in
   // phase 2c and runs its MFMAs in phase 2c + 1; group B (waves 4-7) reads in 2c + 1 and computes in 2c + 2 -- in
@@ -203,48 +220,101 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
   // also issues its share of step c + SLOTS - 1 into the slot of step c - 1 (read by both groups before).  Before
   // the barrier that opens phase 2c every wave has waited for its own DMAs of step c (vmcnt, the SLOTS - 2
   // younger steps stay in flight), so the barrier publishes the whole slot.
+  // A wave issues step c + SLOTS - 1 in two parts: its x DMAs in its read phase of step c, its weight DMAs in its
+  // compute phase of step c.  Waits: A (top of step c) has issued every DMA of steps <= c + SLOTS - 2, so it keeps
+  // (SLOTS - 2) PW younger ones; B waits for step c + 1 inside its read phase of step c, after the x part of step
+  // c + SLOTS - 1: (SLOTS - 3) PW + NXU younger ones.  At the tail both wait for everything.
   const int grp = wid >> 2;
-  auto wait_step = [&](int c) {
-    if (c + C::SLOTS - 2 < nch) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::KEEP) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
   auto bar = [&]() {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
   auto read_phase = [&](int c, int slot) {
-    if (c + C::SLOTS - 1 < nch) issue(c + C::SLOTS - 1, slot == 0 ? C::SLOTS - 1 : slot - 1);
+#if PG_ABLATE != 2  // probe builds: 2 = no DMAs after the prologue (MFMAs on stale slots)
+    if (c + C::SLOTS - 1 < nch) issue_x(c + C::SLOTS - 1, slot == 0 ? C::SLOTS - 1 : slot - 1);
+#endif
     read_frags(slot);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto wnext = [&](int c, int slot) {  // (step, slot) of the weight DMAs of this compute phase, or (-1, 0)
+#if PG_ABLATE == 2
+    return -1;
+#endif
+    return c + C::SLOTS - 1 < nch ? c + C::SLOTS - 1 : -1;
   };
   int slot = 0;
   if (grp == 0) {
     for (int c = 0; c < nch; ++c) {
-      wait_step(c);
+      if (c + C::SLOTS - 2 < nch) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::KEEP) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       bar();
       read_phase(c, slot);
       bar();
-      mfmas();
+      mfmas(wnext(c, slot), slot == 0 ? C::SLOTS - 1 : slot - 1);
       slot = slot == C::SLOTS - 1 ? 0 : slot + 1;
     }
     bar();  // B's last compute phase
   } else {
-    wait_step(0);
+    if (C::SLOTS - 2 < nch) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::KEEP) : "memory");  // prologue: step 0
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();  // phase 0: A reads step 0
     for (int c = 0; c < nch; ++c) {
       bar();
       read_phase(c, slot);
-      wait_step(c + 1);
+      if (c + C::SLOTS - 1 < nch) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::KEEP_B) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       bar();
-      mfmas();
+      mfmas(wnext(c, slot), slot == 0 ? C::SLOTS - 1 : slot - 1);
       slot = slot == C::SLOTS - 1 ? 0 : slot + 1;
     }
+  }
+
+  // ---- deferred-RMSNorm row scales of the block's rows (after the main loop: the fragment registers are free
+  // then; computed in the prologue they pushed the big tiles' register count into scratch): TPR threads per row
+  // sum the producer's partials with independent 16-B loads
+  if (has_rs) {
+    constexpr int TPR = (PG_THR / C::BM) >= 8 ? 8 : (PG_THR / C::BM) >= 4 ? 4 : (PG_THR / C::BM) >= 2 ? 2 : 1;
+    float rpart = 0.f;
+    for (int rrow = threadIdx.x / TPR; rrow < C::BM; rrow += PG_THR / TPR) {
+      const int rsub = threadIdx.x % TPR;
+      rpart = 0.f;
+      if (m0 + rrow < M) {
+        const float* sp = e.ss_in + (long long)(m0 + rrow) * e.ss_tiles;
+        if ((e.ss_tiles & 3) == 0) {
+          const float4* s4 = reinterpret_cast<const float4*>(sp);
+          float4 a[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = rsub + u * TPR;
+            a[u] = i < e.ss_tiles / 4 ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) rpart += (a[u].x + a[u].y) + (a[u].z + a[u].w);
+          for (int i = rsub + 4 * TPR; i < e.ss_tiles / 4; i += TPR) {
+            const float4 b4 = s4[i];
+            rpart += (b4.x + b4.y) + (b4.z + b4.w);
+          }
+        } else {
+          for (int i = rsub; i < e.ss_tiles; i += TPR) rpart += sp[i];
+        }
+      }
+#pragma unroll
+      for (int o = 1; o < TPR; o *= 2) rpart += __shfl_xor(rpart, o, 64);
+      if (rsub == 0) rs[rrow] = rsqrtf(rpart * e.inv_d + e.eps);
+    }
+    __syncthreads();
   }
 
   // ---- epilogue
   const int h = lane >> 4;
   const int S = gridDim.y;
-  if (S > 1) {
+  // split-K without counters (F32 only): every split stores its own fp32 slab [S][M][N] through the plain F32
+  // epilogue below; the consumer kernel sums the slabs (LinOut).  (A separate early-return store loop here pushed
+  // the big tiles' register allocation into scratch.)
+  if constexpr (EPI == DECODE_EPI_F32) {
+    if (S > 1 && counters == nullptr) e.y = slab + (long long)split * M * N;
+  }
+  if (S > 1 && counters != nullptr) {
     // split-K: write-through slab stores, then the last arriving split of this tile reduces
     float* ys = slab + (long long)split * M * N;
 #pragma unroll
@@ -295,46 +365,205 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
   }
 
   if constexpr (EPI == DECODE_EPI_RESID) {
-    // residual add + next-norm prep; ONE sum-of-squares partial per (row, block column): the wave sums its WN
-    // tiles, the two n-waves meet in LDS (the stage buffers are free once every wave is past the last compute)
-    float sq[WM];
-#pragma unroll
-    for (int i = 0; i < WM; ++i) sq[i] = 0.f;
-#pragma unroll
-    for (int j = 0; j < WN; ++j) {
-      const int n = n0 + (wn * WN + j) * 16 + 4 * h;
-      Pack8 wp;
-      const uint2 raw = *reinterpret_cast<const uint2*>(e.w_next + n);
+    // residual add + next-norm prep through an fp32 LDS image of the accumulators (NP passes of whole m-waves when
+    // the image is bigger than the ring): then TW threads per row walk the row's BN columns in 16-B steps --
+    // coalesced resid read-modify-write, 8-B xw stores back to back, and ONE sum-of-squares partial per (row, block
+    // column) reduced across the row's lanes (ss_out [M][N / BN])
+    constexpr int RBF = C::BN * 4 + 16;
+    constexpr int NP = C::BM * RBF <= C::RS_OFF ? 1 : (C::BM / 2) * RBF <= C::RS_OFF ? 2 : 4;
+    constexpr int PR = C::BM / NP;
+    static_assert(PR * RBF <= C::RS_OFF, "pgemm: resid image exceeds the ring");
+    constexpr int TW = C::BN / 4 <= 32 ? 32 : 64;  // threads per row (lanes past BN / 4 idle)
+    constexpr int RPI = PG_THR / TW;               // rows per iteration
+    char* const img = smem;
+    const int P = N / C::BN;
+    const int tc = threadIdx.x % TW, tr = threadIdx.x / TW;
+    Pack8 wp;
+    if (4 * tc < C::BN) {
+      const uint2 raw = *reinterpret_cast<const uint2*>(e.w_next + n0 + 4 * tc);
       wp.u = make_uint4(raw.x, raw.y, 0, 0);
+    }
 #pragma unroll
-      for (int i = 0; i < WM; ++i) {
-        const int mloc = (wm * WM + i) * 16 + fr;
-        const int m = m0 + mloc;
-        if (m >= M) continue;
-        f32x4 v = acc[j][i];
-        float* rp = e.resid + (long long)m * N + n;
-        const float4 r = *reinterpret_cast<const float4*>(rp);
-        const float rr[4] = {r.x + v[0], r.y + v[1], r.z + v[2], r.w + v[3]};
-        *reinterpret_cast<float4*>(rp) = make_float4(rr[0], rr[1], rr[2], rr[3]);
-        store4bf(e.xw_out + (long long)m * N + n, rr[0] * (float)wp.h[0], rr[1] * (float)wp.h[1],
-                 rr[2] * (float)wp.h[2], rr[3] * (float)wp.h[3]);
-        sq[i] += rr[0] * rr[0] + rr[1] * rr[1] + rr[2] * rr[2] + rr[3] * rr[3];
+    for (int pass = 0; pass < NP; ++pass) {
+      __syncthreads();  // every wave is past its last fragment read / the previous pass's rows
+      if (NP == 1 || (wm / (4 / NP)) == pass) {
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+#pragma unroll
+          for (int i = 0; i < WM; ++i) {
+            const int r = (wm * WM + i) * 16 + fr - pass * PR;
+            *reinterpret_cast<f32x4*>(img + r * RBF + (16 * (wn * WN + j) + 4 * h) * 4) = acc[j][i];
+          }
+      }
+      __syncthreads();
+      for (int r = tr; r < PR; r += RPI) {
+        const int m = m0 + pass * PR + r;
+        float sq = 0.f;
+        if (m < M && 4 * tc < C::BN) {
+          const f32x4 y = *reinterpret_cast<const f32x4*>(img + r * RBF + tc * 16);
+          float* rp = e.resid + (long long)m * N + n0 + 4 * tc;
+          const float4 q = *reinterpret_cast<const float4*>(rp);
+          const float rr[4] = {q.x + y[0], q.y + y[1], q.z + y[2], q.w + y[3]};
+          *reinterpret_cast<float4*>(rp) = make_float4(rr[0], rr[1], rr[2], rr[3]);
+          store4bf(e.xw_out + (long long)m * N + n0 + 4 * tc, rr[0] * (float)wp.h[0], rr[1] * (float)wp.h[1],
+                   rr[2] * (float)wp.h[2], rr[3] * (float)wp.h[3]);
+          sq = rr[0] * rr[0] + rr[1] * rr[1] + rr[2] * rr[2] + rr[3] * rr[3];
+        }
+#pragma unroll
+        for (int o = 1; o < TW; o *= 2) sq += __shfl_xor(sq, o, 64);
+        if (m < M && tc == 0) e.ss_out[(long long)m * P + nt] = sq;
       }
     }
-    __syncthreads();  // every wave is past its last LDS read
-    float* part = reinterpret_cast<float*>(smem);
+  } else if constexpr (EPI == DECODE_EPI_QKV && C::BN % 128 == 0) {
+    // QKV: the row scale and RoPE in registers (a rotate-half pair sits in lanes l and l ^ 32 of one accumulator,
+    // models/layout.py), the roped heads as a bf16 LDS image [rows][BN] in natural dim order, then whole 256-B head
+    // rows out: q rows and paged K rows with 16-B stores; V (dim-major cache blocks) as 16-B runs of 8 tokens where
+    // the 8 rows' slots are consecutive and aligned in one cache block (a prefill sequence's tokens), else per token
+    constexpr int D = 128;
+    constexpr int RB = C::BN * 2 + 16;
+    constexpr int NP = C::BM * RB <= C::RS_OFF ? 1 : 2;
+    constexpr int PR = C::BM / NP;
+    static_assert(PR * RB <= C::RS_OFF, "pgemm: qkv image exceeds the ring");
+    constexpr int HB = C::BN / D;  // heads per block
+    char* const img = smem;
+    const int head0 = n0 / D;
 #pragma unroll
-    for (int i = 0; i < WM; ++i) {
-      float s2 = sq[i];
-      s2 += __shfl_xor(s2, 16, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (h == 0) part[wn * C::BM + (wm * WM + i) * 16 + fr] = s2;
+    for (int pass = 0; pass < NP; ++pass) {
+      __syncthreads();
+      if (NP == 1 || (wm >> 1) == pass) {
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          const int tl = wn * WN + j;
+          const int hl = tl / 8, jj = tl % 8;  // head within the block, 16-row tile within the head
+#pragma unroll
+          for (int i = 0; i < WM; ++i) {
+            const int mloc = (wm * WM + i) * 16 + fr;
+            const int m = m0 + mloc;
+            f32x4 v = acc[j][i];
+            if (has_rs) v *= rs[mloc];
+            float pr[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pr[q] = __shfl_xor(v[q], 32, 64);
+            f32x4 o = v;
+            int d;
+            if (head0 + hl < e.Hq + e.Hkv) {  // q / k head: RoPE
+              const bool lo = h < 2;
+              const int dh = 8 * jj + 4 * (h & 1);
+              const float* cs = e.cos_sin + (long long)(m < M ? e.positions[m] : 0) * D;
+              const float4 c4 = *reinterpret_cast<const float4*>(cs + dh);
+              const float4 s4 = *reinterpret_cast<const float4*>(cs + 64 + dh);
+              const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss4[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+              for (int q = 0; q < 4; ++q) o[q] = lo ? (v[q] * cc[q] - pr[q] * ss4[q]) : (v[q] * cc[q] + pr[q] * ss4[q]);
+              d = (lo ? 0 : 64) + dh;
+            } else {
+              d = 16 * jj + 4 * h;
+            }
+            store4bf16(reinterpret_cast<bf16*>(img + (mloc - pass * PR) * RB + (hl * D + d) * 2), o);
+          }
+        }
+      }
+      __syncthreads();
+      // q / k rows: (row, head, 16-B chunk) per thread
+      for (int q = threadIdx.x; q < PR * HB * 16; q += PG_THR) {
+        const int r = q / (HB * 16), hl = (q / 16) % HB, ch = q % 16;
+        const int m = m0 + pass * PR + r, head = head0 + hl;
+        if (m >= M || head >= e.Hq + e.Hkv) continue;
+        bf16* dst;
+        if (head < e.Hq) {
+          dst = e.q_out + ((long long)m * e.Hq + head) * D;
+        } else {
+          const int slot = e.slots[m];
+          if (slot < 0) continue;
+          dst = e.k_cache + (((long long)(slot / e.BS) * e.Hkv + (head - e.Hq)) * e.BS + slot % e.BS) * D;
+        }
+        *reinterpret_cast<uint4*>(dst + ch * 8) = *reinterpret_cast<const uint4*>(img + r * RB + hl * D * 2 + ch * 16);
+      }
+      // V heads: (8-row group, head, dim) per thread
+      if (head0 + HB > e.Hq + e.Hkv) {
+        for (int q = threadIdx.x; q < (PR / 8) * HB * D; q += PG_THR) {
+          const int g8 = q / (HB * D), hl = (q / D) % HB, dd = q % D;
+          const int head = head0 + hl;
+          if (head < e.Hq + e.Hkv) continue;
+          const int vh = head - e.Hq - e.Hkv;
+          const int r0 = 8 * g8, mb = m0 + pass * PR + r0;
+          bf16 vals[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            vals[k] = *reinterpret_cast<const bf16*>(img + (r0 + k) * RB + (hl * D + dd) * 2);
+          const int s0 = mb < M ? e.slots[mb] : -1;
+          bool run = s0 >= 0 && (s0 % 8) == 0 && (s0 % e.BS) + 8 <= e.BS && mb + 8 <= M;
+          if (run) {
+#pragma unroll
+            for (int k = 1; k < 8; ++k) run = run && e.slots[mb + k] == s0 + k;
+          }
+          if (run) {
+            Pack8 pk;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pk.h[k] = vals[k];
+            *reinterpret_cast<uint4*>(e.v_cache + (((long long)(s0 / e.BS) * e.Hkv + vh) * D + dd) * e.BS + s0 % e.BS) =
+                pk.u;
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const int m = mb + k;
+              const int sl = m < M ? e.slots[m] : -1;
+              if (sl >= 0) e.v_cache[(((long long)(sl / e.BS) * e.Hkv + vh) * D + dd) * e.BS + sl % e.BS] = vals[k];
+            }
+          }
+        }
+      }
     }
-    __syncthreads();
-    const int P = N / C::BN;
-    for (int rloc = threadIdx.x; rloc < C::BM; rloc += PG_THR) {
-      const int m = m0 + rloc;
-      if (m < M) e.ss_out[(long long)m * P + nt] = part[rloc] + part[C::BM + rloc];
+  } else if constexpr (EPI == DECODE_EPI_BF16 || EPI == DECODE_EPI_SWIGLU) {
+    // bf16 outputs through an LDS image of the block's output tile [BM][OW] (OW = BN, or BN / 2 after SwiGLU),
+    // then coalesced 16-B row stores: an accumulator tile alone would store 8 B per lane into 16 rows
+    constexpr int OW = EPI == DECODE_EPI_SWIGLU ? C::BN / 2 : C::BN;
+    constexpr int RB = OW * 2 + 16;  // row bytes in LDS (+16: rows of a lane group land on distinct banks)
+    constexpr int NP = C::BM * RB <= C::RS_OFF ? 1 : 2;  // passes (half the m-waves each when the image is big)
+    constexpr int PR = C::BM / NP;                       // rows per pass
+    static_assert(PR * RB <= C::RS_OFF, "pgemm: output image exceeds the ring");
+    char* const img = smem;
+    bf16* const out = EPI == DECODE_EPI_SWIGLU ? e.act : e.out_bf;
+    const int ldo = EPI == DECODE_EPI_SWIGLU ? N / 2 : N;
+    const int c0 = EPI == DECODE_EPI_SWIGLU ? n0 / 2 : n0;
+    constexpr int CPR = OW * 2 / 16;  // 16-B chunks per row
+#pragma unroll
+    for (int pass = 0; pass < NP; ++pass) {
+      __syncthreads();  // every wave is past its last fragment read / the previous pass's copy-out
+      if (NP == 1 || (wm >> 1) == pass) {
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          const int tl = wn * WN + j;  // tile within the block
+#pragma unroll
+          for (int i = 0; i < WM; ++i) {
+            const int mloc = (wm * WM + i) * 16 + fr;
+            const int r = mloc - pass * PR;
+            f32x4 v = acc[j][i];
+            if (has_rs) v *= rs[mloc];
+            if constexpr (EPI == DECODE_EPI_SWIGLU) {
+              f32x4 u;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) u[q] = __shfl_xor(v[q], 32, 64);
+              if (h < 2) {
+                f32x4 a;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a[q] = silu(v[q]) * u[q];
+                store4bf16(reinterpret_cast<bf16*>(img + r * RB + (8 * tl + 4 * h) * 2), a);
+              }
+            } else {
+              store4bf16(reinterpret_cast<bf16*>(img + r * RB + (16 * tl + 4 * h) * 2), v);
+            }
+          }
+        }
+      }
+      __syncthreads();
+      for (int q = threadIdx.x; q < PR * CPR; q += PG_THR) {
+        const int r = q / CPR, ch = q % CPR;
+        const int m = m0 + pass * PR + r;
+        if (m < M)
+          *reinterpret_cast<uint4*>(out + (long long)m * ldo + c0 + ch * 8) =
+              *reinterpret_cast<const uint4*>(img + r * RB + ch * 16);
+      }
     }
   } else {
 #pragma unroll
@@ -350,11 +579,7 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
           const float sc = rs[mloc];
           v *= sc;
         }
-        if constexpr (EPI == DECODE_EPI_BF16) {
-          if (mok) store4bf16(e.out_bf + (long long)m * N + tile * 16 + 4 * h, v);
-        } else {
-          epilogue<EPI>(e, v, tile, m, mok, h, N);
-        }
+        epilogue<EPI>(e, v, tile, m, mok, h, N);
       }
     }
   }
@@ -418,3 +643,20 @@ void launch_pgemm(int epi, int cfg, const bf16* x, const bf16* Wshuf, int M, int
     default: launch_epi<DECODE_EPI_F32>(cfg, x, Wshuf, M, N, K, S, e, slab, counters, s); break;
   }
 }
+
+#ifdef PG_PROBE
+// standalone probe entry (bench/kernels/pgemm_probe.py builds this file with -DPG_PROBE and PG_ABLATE / PG_MAX_SLOTS
+// variants into its own .so): bf16 y [M][N] = x @ W^T
+// S > 1: y is the fp32 slab array [S][M][N] (no in-launch reduction)
+extern "C" int pg_probe(int cfg, const void* x, const void* w, void* y, int M, int N, int K, int S, void* stream) {
+  int bm = 0, bn = 0;
+  if (!pgemm_cfg_shape(cfg, &bm, &bn) || N % bn || K % (64 * S)) return -1;
+  DecodeEpi e;
+  e.wshuf = 1;
+  e.out_bf = reinterpret_cast<bf16*>(y);
+  launch_pgemm(S > 1 ? DECODE_EPI_F32 : DECODE_EPI_BF16, cfg, reinterpret_cast<const bf16*>(x),
+               reinterpret_cast<const bf16*>(w), M, N, K, S, e, reinterpret_cast<float*>(y), nullptr,
+               reinterpret_cast<hipStream_t>(stream));
+  return 0;
+}
+#endif

@@ -315,6 +315,20 @@ class TransformerLM:
             return self._forward_general_fused(b, kv, mgs)
         return self._forward_general(b, kv)
 
+    def _pg_gate_up(self, T: int):
+        """Tile config of the prefill GEMM (csrc/kernels/pgemm.hip) for this step's gate_up + SwiGLU, or None (library
+        GEMM + swiglu kernel).  Dense model on one GPU with the preshuffled copies, PGEMM_GU_MIN_M..PGEMM_GU_MAX_M
+        rows: where one wave of 320 / 384 x 224 tiles covers the projection it beats hipBLASLt + the swiglu launch
+        (768 rows: 149 vs 155.5 + 13.8 us per layer, profiles/r6/prof_prefill768_pg_gu.csv); elsewhere the library
+        wins (profiles/r6/pgemm_gu_sweep.jsonl, prefill_pgemm_ab3.jsonl).  The other three projections measured faster on the library path even
+        against fused pgemm epilogues (profiles/r6/prefill_pgemm_ab.jsonl: qkv 76 vs 59, o 56 vs 45, down 99 vs 81 us
+        with their consumers), so they stay there."""
+        if (self.cfg.is_moe or self._tp_active() or not self.dgw or self.device.type == "cpu"
+                or not ops.PGEMM_GU_MIN_M <= T <= ops.PGEMM_GU_MAX_M):
+            return None
+        pick = ops.choose_pgemm(T, self.dgw[(0, "w_gu")].shape[0], self.cfg.hidden_size)
+        return None if pick is None else pick[0]
+
     def _mg_plan(self, b: ForwardBatch, names=("qkv", "o", "gu", "down"), need_all: bool = True,
                  any_kind: bool = False):
         """mgemm (rw, split) + scratch per projection for the fused general path, or None."""
@@ -478,6 +492,7 @@ class TransformerLM:
         src = b.src if b.src is not None and b.kind == "decode" else None
         ops.embed_rms_norm(b.input_ids, w["embed"], resid, w.layer(0, "ln1"), eps, x, src,
                            self.last_ids if src is not None else None)
+        pg_gu = self._pg_gate_up(T) if b.kind != "decode" else None
         gu_plan = None
         if MG_FUSED_GU and self.dgw and self.device.type != "cpu" and not cfg.is_moe and T <= 256:
             gu_plan = (self._mg_plan(b, names=("gu",), need_all=False, any_kind=True) or {}).get("gu")
@@ -503,10 +518,16 @@ class TransformerLM:
                 mlp = self.moe.forward(i, x)
             else:
                 ops.add_rms_norm(o, resid, w.layer(i, "ln2"), eps, x)
-                gu = self._linear("gu", x, w.layer(i, "w_gu"), wshuf=self._shuf(i, "w_gu"))
-                F = gu.shape[-1] // 2
-                act = self._buf("act", (T, F), torch.bfloat16)
-                ops.swiglu(gu, act, interleaved=True)
+                if pg_gu is not None:
+                    # gate_up + SwiGLU in one prefill-GEMM launch on the preshuffled copy (no [T, 2F] intermediate)
+                    w_gu = self.dgw[(i, "w_gu")]
+                    act = self._buf("act", (T, w_gu.shape[0] // 2), torch.bfloat16)
+                    ops.pg_swiglu(x, w_gu, None, eps, act, pg_gu)
+                else:
+                    gu = self._linear("gu", x, w.layer(i, "w_gu"), wshuf=self._shuf(i, "w_gu"))
+                    F = gu.shape[-1] // 2
+                    act = self._buf("act", (T, F), torch.bfloat16)
+                    ops.swiglu(gu, act, interleaved=True)
                 mlp = self._linear("down", act, w.layer(i, "w_down"), reduce=True, wshuf=self._shuf(i, "w_down"))
             nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
             ops.add_rms_norm(mlp, resid, nxt, eps, x)

@@ -164,6 +164,103 @@ def choose_mgemm(M: int, N: int, K: int, cus: int = 256, fused: bool = False):
     return None if best is None else (best[1], best[2])
 
 
+# ---- prefill projection GEMM (csrc/kernels/pgemm.hip): hundreds+ rows on the MFMA-preshuffled weights -------
+def pgemm_shape(cfg: int):
+    """(BM, BN) of tile config ``cfg`` (tokens x features per 512-thread block), or None."""
+    if not native_available():
+        return PG_CFG_SHAPES.get(cfg)
+    s = _native.ops().pgemm_shape(int(cfg))
+    return tuple(s) if s else None
+
+
+# kept in sync with csrc/kernels/pgemm.hip PG_CFGS (used off-GPU, e.g. by the planner's CPU tests)
+PG_CFG_SHAPES = {0: (384, 224), 1: (256, 256), 2: (192, 192), 3: (192, 128), 4: (256, 128), 5: (128, 128),
+                 6: (320, 224), 7: (256, 224), 8: (192, 224), 9: (192, 256), 10: (128, 256)}
+
+
+def pgemm(x, w_shuf, y, cfg: int, S: int = 1, slab=None, counters=None):
+    """y [M, N] (bf16 or fp32) = x @ W^T with W MFMA-preshuffled; tile config ``cfg``, ``S`` k-splits (S > 1: fp32
+    ``slab`` [S, M, N] scratch + int32 ``counters`` [tiles], zero before the first launch)."""
+    if _gpu(x):
+        return _native.ops().pgemm(x, w_shuf, y, int(cfg), int(S), slab, counters)
+    w = reference.unshuffled(w_shuf, True)
+    if y.dim() == 3:  # split-K slabs
+        return reference.skinny_gemm(x, w, y)
+    y.copy_(x.float() @ w.float().t())
+    return y
+
+
+_PGEMM_ON = os.environ.get("SYMMETRY_PGEMM", "1") != "0"  # A/B switch: 0 keeps long prefills on the library path
+PGEMM_MIN_M = int(os.environ.get("SYMMETRY_PGEMM_MIN_M", "257"))  # below: mgemm (medium-M, weight-streaming)
+# gate_up + SwiGLU on pgemm for prefill steps of PGEMM_GU_MIN_M..PGEMM_GU_MAX_M rows (one wave of 320 / 384 x 224
+# tiles); 384 / 512 rows measured 4 / 1 % slower than the library + swiglu, 600 / 768 rows 4.5 / 3 % faster
+# (profiles/r6/prefill_pgemm_ab3.jsonl), 1024+ the library's tiles win (profiles/r6/pgemm_gu_sweep.jsonl)
+PGEMM_GU_MIN_M = int(os.environ.get("SYMMETRY_PGEMM_GU_MIN_M", "576"))
+PGEMM_GU_MAX_M = int(os.environ.get("SYMMETRY_PGEMM_GU_MAX_M", "896"))
+
+
+def choose_pgemm(M: int, N: int, K: int, slabs: bool = False, cus: int = 256, align: int = 16):
+    """(cfg, S) of the prefill GEMM for an [M, K] x [N, K]^T projection, or None.  ``slabs``: the consumer can sum
+    fp32 split-K slabs (S > 1 allowed; fused epilogues need S = 1).  ``align``: the tile width must be a multiple
+    of it (the QKV epilogue writes whole 128-dim heads).
+
+    Cost model fitted to the 768-row sweeps on MI355X (bench/kernels/bench_pgemm.py, pgemm_probe.py;
+    profiles/r6/pgemm_*.jsonl): a k-step (32 deep) of a BM x BN tile is bound by the per-CU LDS-DMA intake --
+    ~50 GB/s per CU while at most 3/4 of the CUs stream, ~35 GB/s with all of them (L2 / fabric contention)
+    -- or by its MFMAs at ~6.5 TFLOP/s per CU; plus ~3 us of prologue + epilogue per wave of blocks and the
+    slabs written for the consumer."""
+    if not _PGEMM_ON or M < PGEMM_MIN_M or K % 64:
+        return None
+    best = None
+    for cfg, (bm, bn) in PG_CFG_SHAPES.items():
+        if N % bn or bn % align:
+            continue
+        for S in ((1, 2, 4) if slabs else (1,)):
+            if K % (64 * S):
+                continue
+            tiles = -(-M // bm) * (N // bn) * S
+            waves = -(-tiles // cus)
+            busy = min(tiles, cus)
+            rate = 50e9 if busy <= 3 * cus // 4 else 35e9
+            step = max((bm + bn) * 64 / rate, 2 * bm * bn * 32 / 6.5e12)
+            t = waves * (K // S // 32) * step + waves * 3e-6 + (S * M * N * 4 / 10e12 if S > 1 else 0.0)
+            if best is None or t < best[0]:
+                best = (t, cfg, S)
+    return None if best is None else (best[1], best[2])
+
+
+def _pg_resid_ref(x, W, resid, w_next, xw_out, ss_out):
+    M = x.shape[0]
+    r = resid[:M]
+    r.add_(x.float() @ W.float().t())
+    xw_out[:M].copy_((r * w_next.float()).to(xw_out.dtype))
+    ss_out[:M].copy_(r.pow(2).view(M, ss_out.shape[1], -1).sum(-1))
+
+
+def pg_qkv(x, W, ss_in, eps, positions, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, cfg):
+    """Prefill QKV projection (W preshuffled, decode row layout) + deferred-norm row scale + RoPE + paged K/V write."""
+    if _gpu(x):
+        return _native.ops().pg_qkv(x, W, ss_in, float(eps), positions, slots, cos_sin, q_out, k_cache, v_cache,
+                                    int(Hq), int(Hkv), int(cfg))
+    return reference.dg_qkv(x, reference.unshuffled(W, True), ss_in, eps, positions, slots, cos_sin, q_out, k_cache,
+                            v_cache, Hq, Hkv)
+
+
+def pg_swiglu(x, W, ss_in, eps, act, cfg):
+    """Prefill gate_up projection (tile-interleaved gate/up rows, preshuffled) + row scale + SwiGLU -> act."""
+    if _gpu(x):
+        return _native.ops().pg_swiglu(x, W, ss_in, float(eps), act, int(cfg))
+    return reference.dg_swiglu(x, reference.unshuffled(W, True), ss_in, eps, act)
+
+
+def pg_resid(x, W, resid, w_next, xw_out, ss_out, cfg):
+    """Prefill row-parallel projection + residual add + next-norm prep; ss_out [M, N / BN]: one sum-of-squares
+    partial per row and block column of tile config ``cfg``."""
+    if _gpu(x):
+        return _native.ops().pg_resid(x, W, resid, w_next, xw_out, ss_out, int(cfg))
+    return _pg_resid_ref(x, reference.unshuffled(W, True), resid, w_next, xw_out, ss_out)
+
+
 def lm_head_sample(x, w, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset=0, logits=None):
     if _gpu(x):
         return _native.ops().lm_head_sample(x, w, temps, seeds, step, tile_keys, out_keys, out_ids, int(n_offset),

@@ -162,3 +162,42 @@ def test_wide_decode_batches_sample_from_logits(monkeypatch):
     ops.lm_head_sample(x, w, temps, seeds, step, torch.empty(3 * 6, dtype=torch.int64), k1, i1, 32, lg)
     ops.logits_argmax(lg, temps, seeds, step, k2, i2, 32)
     assert torch.equal(k1, k2) and torch.equal(i1, i2)
+
+
+def test_pgemm_planner_respects_kernel_contract():
+    for M in (257, 384, 640, 768, 1290, 4096):
+        for N, K in ((6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (7168, 1024), (1536, 1024)):
+            for slabs in (False, True):
+                pick = ops.choose_pgemm(M, N, K, slabs=slabs)
+                assert pick is not None
+                cfg, S = pick
+                bm, bn = ops.PG_CFG_SHAPES[cfg]
+                assert N % bn == 0 and K % (64 * S) == 0 and (slabs or S == 1)
+    assert ops.choose_pgemm(256, 4096, 4096) is None  # medium-M rows stay on mgemm
+
+
+def test_long_prefill_gate_up_on_pgemm(monkeypatch):
+    """A 300-token prefill with gate_up + SwiGLU on the prefill GEMM (CPU reference op on the preshuffled copy of the
+    decode row layout) generates the fp32 oracle's greedy tokens."""
+    from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from symmetry_amd.engine.sequence import SamplingParams
+    from symmetry_amd.models import reference_model as rm
+
+    eng = LLMEngine(EngineConfig(model="small-llama", device="cpu", max_num_seqs=2, max_model_len=512,
+                                 num_kv_blocks=64, block_size=16, use_graphs=False, seed=0))
+    m = eng.model
+    m.dgw = {(i, n): preshuffle(m.w.layer(i, n)) for i in range(m.cfg.num_layers)
+             for n in ("wqkv", "wo", "w_gu", "w_down")}
+    calls = []
+    real = ops.pg_swiglu
+    monkeypatch.setattr(m, "fused", False)
+    monkeypatch.setattr(m, "_pg_gate_up", lambda T: ops.choose_pgemm(T, m.dgw[(0, "w_gu")].shape[0],
+                                                                     m.cfg.hidden_size)[0] if T >= 257 else None)
+    monkeypatch.setattr(ops, "pg_swiglu", lambda *a: calls.append(a[0].shape[0]) or real(*a))
+    prompt = [3 + (7 * i) % 30000 for i in range(300)]
+    out = eng.generate(prompt, SamplingParams(max_tokens=4, temperature=0.0))
+    assert calls and set(calls) == {300}
+    lg = rm.forward_logits(eng.weights.to("cpu"), prompt + out[:-1])
+    for j, t in enumerate(out):
+        row = lg[len(prompt) - 1 + j]
+        assert float(row.max() - row[t]) <= 0.05, (j, t, int(row.argmax()))

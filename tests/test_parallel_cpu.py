@@ -496,3 +496,40 @@ def test_tp2_bf16_prefill_reduce_matches_oracle():
         for j, t in enumerate(out):
             row = lg[len(p) - 1 + j]
             assert float(row.max() - row[t]) <= 0.06, (j, t, float(row.max() - row[t]))
+
+
+# ---- the bench's streamed-token check: the fp32 oracle sharded over TP ranks ---------------------------------
+def _oracle_shard_worker(rank, world):
+    from symmetry_amd.models import reference_model as rm
+    from symmetry_amd.models.config import resolve
+    from symmetry_amd.models.layout import apply_decode_layout
+    from symmetry_amd.models.weights import ShardSpec, random_weights
+
+    cfg = resolve("tiny-llama")
+    w = random_weights(cfg, ShardSpec(rank, world), seed=5, mode="full")
+    apply_decode_layout(w)  # the engine's layout: the oracle must undo it per shard
+    return rm.forward_logits(w, list(range(3, 40)), group=dist.group.WORLD)
+
+
+def test_sharded_oracle_matches_full_oracle():
+    """bench.py's check under TP runs the fp32 oracle on each rank's shard and sums / gathers over the group: it
+    must give the unsharded model's logits on every rank."""
+    from symmetry_amd.models import reference_model as rm
+    from symmetry_amd.models.config import resolve
+    from symmetry_amd.models.weights import random_weights
+
+    full = rm.forward_logits(random_weights(resolve("tiny-llama"), seed=5, mode="full"), list(range(3, 40)))
+    for _, lg in _run(_oracle_shard_worker, world=2):
+        torch.testing.assert_close(lg, full, atol=1e-4, rtol=1e-4)
+
+
+def test_check_tokens_flags_a_wrong_token():
+    from symmetry_amd.models import reference_model as rm
+
+    lg = torch.zeros(6, 10)
+    lg[2:, 7] = 3.0
+    lg[3, 4] = 2.95  # a near-tie: either token passes
+    ok = rm.check_tokens(lg, 3, [7, 4, 7])
+    assert ok["mismatches"] == 0 and ok["max_gap"] == 0.05
+    bad = rm.check_tokens(lg, 3, [7, 7, 1])
+    assert bad["mismatches"] == 1 and bad["first_mismatch"] == 2
