@@ -137,13 +137,23 @@ class LLMEngine:
             weights = load_hf_weights(cfg.weights, mcfg, shard, device=self.device)
         self.weights: ModelWeights = weights
         self.load_time = time.perf_counter() - t0
+        # what the KV cache needs for the admission limit at full context: the optional weight copies (preshuffled decode
+        # / expert streams) are sized from the HBM left after it, never from the KV cache's share
+        per_block = mcfg.kv_bytes_per_token() // cfg.tp_size * cfg.block_size
+        kv_need = (cfg.num_kv_blocks or -(-cfg.max_num_seqs * max_model_len // cfg.block_size)) * per_block
         self.model = TransformerLM(weights, self.device, tp_comm=tp_comm, ep_comm=ep_comm,
-                                   max_decode_ctx=max_model_len, decode_weights=cfg.decode_weights)
+                                   max_decode_ctx=max_model_len, decode_weights=cfg.decode_weights,
+                                   kv_reserve_bytes=kv_need)
         self.tokenizer = load_tokenizer(mcfg, cfg.tokenizer or (cfg.weights if cfg.weights != "random" else None))
         nb = cfg.num_kv_blocks or self._auto_blocks(max_model_len)
         self.kv = KVCache(mcfg.num_layers, nb, mcfg.num_kv_heads // cfg.tp_size, mcfg.head_dim, cfg.block_size,
                           self.device)
         self.blocks = BlockManager(nb, cfg.block_size, prefix_caching=cfg.enable_prefix_caching)
+        if self.device.type != "cpu":
+            extra = self.model.extra_weight_bytes()
+            print(f"symmetry: {mcfg.name} weights {weights.nbytes() / 1e9:.1f} GB + layout copies {extra / 1e9:.1f} GB; "
+                  f"KV cache {nb} blocks x {cfg.block_size} = {nb * cfg.block_size} tokens ({self.kv.nbytes() / 1e9:.1f} GB; "
+                  f"{cfg.max_num_seqs} seqs x {max_model_len} need {kv_need / 1e9:.1f} GB)", file=sys.stderr, flush=True)
         self.scheduler = Scheduler(
             SchedulerConfig(max_num_seqs=min(cfg.max_num_seqs, self._max_decode_rows(mcfg)),
                             max_num_batched_tokens=cfg.max_num_batched_tokens, max_model_len=max_model_len,

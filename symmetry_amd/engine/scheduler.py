@@ -109,11 +109,13 @@ class BlockManager:
         # same-scope prefix was still being prefilled finds it once that prefill registered its blocks
         if seq.prefix_checked and seq.prefix_epoch == self.cache_gen:
             return 0
+        first = not seq.prefix_checked
         seq.prefix_checked, seq.prefix_epoch = True, self.cache_gen
         tokens = seq.token_ids
         target = seq.prefill_target
         nfull = max(0, target - 1) // self.block_size  # >= 1 token left to prefill
-        self.query_tokens += target
+        if first:  # a re-look after new blocks were cached is the same query: its tokens count once
+            self.query_tokens += target
         for _, h in self._chain(tokens, nfull, seq.cache_scope):
             b = self.cached.get(h)
             if b is None:

@@ -88,13 +88,16 @@ class MoEBlock:
         64-128 rows per expert: w2 303 -> 153 / 331 -> 212 us, w13 430 -> 352 us, profiles/r5/grouped_stream.jsonl).
         Decode steps stream them too (1-8 rows per expert: w13 320 -> 299 us, w2 162 -> 144).  The row-major
         tensors stay for the tile kernel (long segments), so this is one extra copy: w2 first (the larger win),
-        then w13, from half the free HBM (Mixtral on one GPU: both, 90 GB, leaving ~95 GB for the KV cache)."""
+        then w13, from the HBM left after the KV cache's need (admission limit x context) and a workspace reserve
+        (transformer.copy_budget; Mixtral on one GPU at 64 seqs x 8K: both copies, 90 GB)."""
         mode = os.environ.get("SYMMETRY_MOE_PRESHUFFLE", "auto")
         dev = model.device
         if mode == "0" or dev.type != "cuda" or not GROUPED:
             return {}
         cfg = model.cfg
-        budget = float("inf") if mode == "1" else 0.5 * torch.cuda.mem_get_info(dev)[0]
+        from .transformer import copy_budget
+
+        budget = float("inf") if mode == "1" else copy_budget(dev, getattr(model, "kv_reserve", 0))
         out = {}
         for name in ("w2", "w13"):
             ws = [model.w.layer(i, name) for i in range(cfg.num_layers)]

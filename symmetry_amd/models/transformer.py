@@ -80,6 +80,12 @@ MG_FUSED_GU = MG_FUSED_MODE == "gu"
 LMHEAD_SHUF = os.environ.get("SYMMETRY_LMHEAD_SHUF", "1") != "0"
 
 
+def copy_budget(device, kv_reserve: int, workspace: int = 6 << 30) -> float:
+    """HBM an optional weight-layout copy may take: free memory minus the KV cache's need and a workspace reserve
+    (the copies used to take half of the free HBM before the KV cache was sized)."""
+    return max(0.0, float(torch.cuda.mem_get_info(device)[0]) - kv_reserve - workspace)
+
+
 @dataclass
 class ForwardBatch:
     """Device-side metadata of one engine step.
@@ -158,7 +164,7 @@ class Workspace:
 
 class TransformerLM:
     def __init__(self, weights: ModelWeights, device, tp_comm=None, ep_comm=None, max_decode_ctx: int | None = None,
-                 decode_weights: str = "auto"):
+                 decode_weights: str = "auto", kv_reserve_bytes: int = 0):
         self.cfg: ModelConfig = weights.cfg
         self.w = weights
         self.device = torch.device(device)
@@ -176,6 +182,8 @@ class TransformerLM:
         self.cos_sin = reference.rope_table(max_pos, cfg.head_dim, cfg.rope_theta, cfg.rope_scaling,
                                             device=self.device)
         self.ws = Workspace()
+        # HBM the KV cache needs (admission limit x context): the optional layout copies never eat into it
+        self.kv_reserve = int(kv_reserve_bytes)
         self.moe = None
         if cfg.is_moe:
             from .moe import MoEBlock
@@ -206,8 +214,9 @@ class TransformerLM:
             head = None
         if mode == "auto":
             # the layer copies first (-9 % per layer); the head copy (~1 GB for Llama-3-8B, -12 % of one lm_head
-            # launch) only from what the same budget has left, so it never costs a model its layer copies
-            budget = 0.4 * torch.cuda.mem_get_info(self.device)[0]
+            # launch) only from what the same budget has left, so it never costs a model its layer copies.  The
+            # budget: what is left after the KV cache's need and a 6 GB workspace reserve
+            budget = copy_budget(self.device, self.kv_reserve)
             if extra > budget:
                 return {}
             if head is not None and extra + head.numel() * 2 > budget:
@@ -221,6 +230,13 @@ class TransformerLM:
         if head is not None:
             out[(-1, "lm_head")] = preshuffle(head)
         return out
+
+    def extra_weight_bytes(self) -> int:
+        """Bytes of the optional layout copies (preshuffled decode weights, preshuffled expert streams)."""
+        n = sum(t.numel() * t.element_size() for t in self.dgw.values())
+        if self.moe is not None:
+            n += sum(t.numel() * t.element_size() for t in self.moe.pre.values())
+        return n
 
     def _lm_head(self, rows: int):
         """(weight, wshuf) of the decode lm_head for a ``rows``-row sampling launch: the MFMA-preshuffled copy up

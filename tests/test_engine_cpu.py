@@ -472,3 +472,22 @@ def test_scheduler_burst_split_counts_uncached_tokens():
     b = sch.schedule()
     assert b.kind == "prefill" and len(b.seqs) == n // 2 + 1
     assert all(c == 200 for c in b.num_new_tokens)  # the cached 512 tokens are skipped
+
+
+def test_prefix_requery_counts_the_query_once():
+    """A queued prompt that missed is looked up again once new blocks are cached: the re-look may hit,
+    but its tokens enter the hit-rate denominator once, not on every schedule()."""
+    bm = BlockManager(64, 4, prefix_caching=True)
+    waiting = Sequence("w", list(range(12)) + [99], SamplingParams(max_tokens=1))
+    assert bm.match_prefix(waiting) == 0 and bm.query_tokens == 13  # miss: nothing cached yet
+    assert bm.match_prefix(waiting) == 0 and bm.query_tokens == 13  # no new blocks: no re-look
+    other = Sequence("o", [500, 501, 502, 503], SamplingParams(max_tokens=1))
+    bm.grow(other, 4)
+    other.num_computed = 4
+    bm.register(other)  # unrelated blocks cached: the waiting prompt looks again, still a miss
+    assert bm.match_prefix(waiting) == 0 and bm.query_tokens == 13
+    src = Sequence("s", list(range(12)), SamplingParams(max_tokens=1))
+    bm.grow(src, 12)
+    src.num_computed = 12
+    bm.register(src)  # its prefix is cached now: the re-look hits, the query still counted once
+    assert bm.match_prefix(waiting) == 12 and bm.query_tokens == 13 and bm.hit_tokens == 12

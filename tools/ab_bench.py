@@ -1,10 +1,16 @@
-"""Alternating A/B runs of bench.py (run on the GPU box; each arm is its own child process).
+"""Alternating A/B runs of a benchmark script (run on the GPU box; each arm is its own child process).
 
-usage: python tools/ab_bench.py OUT.jsonl --reps 3 --arm NAME 'ENV=V ...' 'bench args' [--arm ...]
+usage: python tools/ab_bench.py OUT.jsonl [--script bench/prefill.py] --reps 3 --arm NAME 'ENV=V ...' 'args' [--arm ...]
+
+The script (default bench.py; e.g. bench/prefill.py, bench/host/prefill_step.py, bench/e2e.py) must print its
+result as a JSON line; the last one is kept.  Examples of the single-purpose wrappers this replaces:
+  Mixtral w2 streaming:  --script bench/prefill.py --arm tile '' '--model mixtral:8x7b --clients 4'
+                         --arm stream 'SYMMETRY_MOE_PRE_ROWS=176' '--model mixtral:8x7b --clients 4'
+  prefill GEMM path:     --script bench/prefill.py --arm lib 'SYMMETRY_PGEMM=0' '--clients 6' --arm pg '' '--clients 6'
 
 Arms run interleaved (A B A B ...) so drift hits both; every run appends one JSON line
 {"arm", "rep", "env", "args", "result"} and the script ends with a summary line per arm
-(mean / min / max of ms_per_step and p50 TTFT).  A run that fails or times out stops the script
+(mean / min / max of every numeric timing key the script reports: ms_per_step, p50_ttft_ms, ttft_ms).  A run that fails or times out stops the script
 (no retries: a failing GPU step is read, not repeated).
 """
 from __future__ import annotations
@@ -17,10 +23,13 @@ import subprocess
 import sys
 
 
+KEYS = ("ms_per_step", "p50_ttft_ms", "ttft_ms", "value")
+
+
 def main() -> int:
     argv = sys.argv[1:]
     out = argv.pop(0)
-    reps, timeout = 3, 240
+    reps, timeout, script = 3, 240, "bench.py"
     arms = []
     while argv:
         a = argv.pop(0)
@@ -28,6 +37,8 @@ def main() -> int:
             reps = int(argv.pop(0))
         elif a == "--timeout":
             timeout = int(argv.pop(0))
+        elif a == "--script":
+            script = argv.pop(0)
         elif a == "--arm":
             arms.append((argv.pop(0), argv.pop(0), argv.pop(0)))
         else:
@@ -40,7 +51,7 @@ def main() -> int:
                 for kv in shlex.split(env_s):
                     k, v = kv.split("=", 1)
                     env[k] = v
-                cmd = ["timeout", "-k", "10", str(timeout), sys.executable, "bench.py"] + shlex.split(args_s)
+                cmd = ["timeout", "-k", "10", str(timeout), sys.executable, script] + shlex.split(args_s)
                 p = subprocess.run(cmd, env=env, capture_output=True, text=True)
                 line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
                 if p.returncode != 0 or not line:
@@ -52,14 +63,14 @@ def main() -> int:
                 res[name].append(r)
                 f.write(json.dumps({"arm": name, "rep": rep, "env": env_s, "args": args_s, "result": r}) + "\n")
                 f.flush()
-                print(name, rep, r["ms_per_step"], r["p50_ttft_ms"], flush=True)
+                print(name, rep, {k: r[k] for k in KEYS if k in r}, flush=True)
         for name, env_s, args_s in arms:
-            ms = [r["ms_per_step"] for r in res[name]]
-            tt = [r["p50_ttft_ms"] for r in res[name]]
-            summ = {"arm": name, "env": env_s, "args": args_s, "summary": {
-                "ms_per_step_mean": round(statistics.mean(ms), 4), "ms_per_step_min": min(ms),
-                "ms_per_step_max": max(ms), "p50_ttft_mean": round(statistics.mean(tt), 2),
-                "p50_ttft_min": min(tt), "p50_ttft_max": max(tt), "n": len(ms)}}
+            summ = {"arm": name, "env": env_s, "args": args_s, "summary": {"n": len(res[name])}}
+            for k in KEYS:
+                vals = [r[k] for r in res[name] if isinstance(r.get(k), (int, float))]
+                if vals:
+                    summ["summary"].update({k + "_mean": round(statistics.mean(vals), 4), k + "_min": min(vals),
+                                            k + "_max": max(vals)})
             f.write(json.dumps(summ) + "\n")
             print(json.dumps(summ), flush=True)
     return 0
