@@ -38,6 +38,8 @@ async def _serve(args):
 
     t0 = time.perf_counter()
     cfg = {"modelName": args.model, "maxConnections": args.clients}
+    if args.decode_weights:
+        cfg["decodeWeights"] = args.decode_weights
     eng = LLMEngine(EngineConfig.from_provider(cfg, max_model_len=args.max_model_len, device="auto",
                                                max_num_batched_tokens=max(8192, args.clients * 512)))
     warm = eng.warmup() if eng.device.type != "cpu" else 0.0
@@ -46,6 +48,8 @@ async def _serve(args):
     out.update(await client_end_run(eng, args.model, args.clients, prompt_tokens=args.prompt_tokens,
                                     max_tokens=args.max_tokens, data_collection=args.data_collection))
     out.update({"load_and_warmup_s": round(load_s, 1), "warmup_s": round(warm, 1),
+                "weight_layout": "single preshuffled copy" if eng.model.single_copy else
+                ("row-major + preshuffled copy" if eng.model.dgw else "row-major"),
                 "dtype": "bf16", "data": "synthetic prompts, random-init weights"})
     eng.shutdown()
     print(json.dumps(out), flush=True)
@@ -59,6 +63,8 @@ def main():
     ap.add_argument("--prompt-tokens", type=int, default=128)
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--data-collection", action="store_true")
+    ap.add_argument("--decode-weights", default=None, choices=("auto", "preshuffled", "replace", "shared"),
+                    help="weight layout (engine default: auto)")
     args = ap.parse_args()
     asyncio.run(_serve(args))
 

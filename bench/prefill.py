@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--ab-moe-grouped", action="store_true",
                     help="MoE: alternate grouped MFMA GEMMs / per-expert library GEMMs (host sync) per rep")
+    ap.add_argument("--ab-moe-pg", action="store_true",
+                    help="MoE: alternate the prefill GEMM kernel's grouped mode (ops.pg_grouped) / the grouped_gemm "
+                         "kernels per rep")
     ap.add_argument("--ab-pgemm", action="store_true",
                     help="dense: alternate the prefill GEMM path (pgemm, fused epilogues) / the library path per rep")
     args = ap.parse_args()
@@ -39,10 +42,13 @@ def main():
     if args.ab_pgemm:
         def set_arm(a):
             ops._PGEMM_ON = a
+    elif args.ab_moe_pg:
+        def set_arm(a):
+            moe_mod.PG_GROUPED = a
     else:
         def set_arm(a):
             moe_mod.GROUPED = a
-    arms = [True, False] if (args.ab_moe_grouped or args.ab_pgemm) else [moe_mod.GROUPED]
+    arms = [True, False] if (args.ab_moe_grouped or args.ab_pgemm or args.ab_moe_pg) else [moe_mod.GROUPED]
     times = {a: [] for a in arms}
     for r in range(args.reps):  # arms interleaved per rep: drift hits both
         for k, arm in enumerate(arms):
@@ -59,6 +65,8 @@ def main():
                "prefill_tokens_per_s": round(toks / t), "tflops": round(flops / t / 1e12, 1)}
         if args.ab_pgemm:
             out["pgemm"] = arm
+        elif args.ab_moe_pg:
+            out["moe_pg_grouped"] = arm
         elif cfg.is_moe:
             out["moe_grouped_gemm"] = arm
         print(json.dumps(out), flush=True)

@@ -400,6 +400,57 @@ void pg_swiglu(const Tensor& x, const Tensor& W, const c10::optional<Tensor>& ss
                nullptr, cur_stream(x));
 }
 
+// grouped experts (MoE prefill): W [E, N, K] preshuffled per expert, xs [R, K] rows permuted into expert segments
+// (offsets [>= e_lo + E + 1] int32 on the device, global expert numbering), expert e < E of W = global e_lo + e.
+// epi SWIGLU_SPLIT: y = act [R, N / 2] bf16 (W rows [gate; up]); BF16: y [R, N] bf16; F32: y [R, N] fp32, or
+// [S, R, N] fp32 partial slabs for S > 1.  Rows outside the E segments are not written.
+void pg_grouped(const Tensor& xs, const Tensor& W, const Tensor& offsets, int64_t e_lo, Tensor& y, int64_t epi,
+                int64_t cfg, int64_t S) {
+  check_gpu(xs, "xs");
+  check_gpu(W, "W");
+  check_gpu(offsets, "offsets");
+  check_gpu(y, "y");
+  check_dtype(xs, at::kBFloat16, "xs");
+  check_dtype(W, at::kBFloat16, "W");
+  check_dtype(offsets, at::kInt, "offsets");
+  TORCH_CHECK(xs.dim() == 2 && W.dim() == 3 && W.size(2) == xs.size(1), "pg_grouped: xs [R, K], W [E, N, K]");
+  const int64_t R = xs.size(0), K = xs.size(1), E = W.size(0), N = W.size(1);
+  TORCH_CHECK(offsets.numel() >= e_lo + E + 1, "pg_grouped: offsets too short");
+  int bm = 0, bn = 0;
+  TORCH_CHECK(pgemm_cfg_shape((int)cfg, &bm, &bn), "pg_grouped: unknown tile config ", cfg);
+  TORCH_CHECK(R >= 1 && N % bn == 0, "pg_grouped: N must be a multiple of the tile width ", bn);
+  TORCH_CHECK(S >= 1 && K % (64 * S) == 0, "pg_grouped: K must be a multiple of 64 * S");
+  TORCH_CHECK(S == 1 || epi == DECODE_EPI_F32, "pg_grouped: split-K slabs are fp32 only");
+  TORCH_CHECK((int64_t)bm * K * 2 < (1LL << 31) && N * K * 2 < (1LL << 31) && R * N < (1LL << 31),
+              "pg_grouped: operands exceed 2 GB");
+  TORCH_CHECK(((R + bm - 1) / bm + E) * (N / bn) < (1LL << 31) / 8, "pg_grouped: too many tiles");
+  DecodeEpi e;
+  e.wshuf = 1;
+  if (epi == DECODE_EPI_SWIGLU_SPLIT) {
+    check_dtype(y, at::kBFloat16, "act");
+    TORCH_CHECK(y.dim() == 2 && y.size(0) == R && y.size(1) == N / 2, "pg_grouped: act must be [R, N / 2]");
+    e.act = ptr<bf16>(y);
+  } else if (epi == DECODE_EPI_BF16) {
+    check_dtype(y, at::kBFloat16, "y");
+    TORCH_CHECK(y.dim() == 2 && y.size(0) == R && y.size(1) == N, "pg_grouped: y must be [R, N]");
+    e.out_bf = ptr<bf16>(y);
+  } else {
+    TORCH_CHECK(epi == DECODE_EPI_F32, "pg_grouped: epi must be SWIGLU_SPLIT, BF16 or F32");
+    check_dtype(y, at::kFloat, "y");
+    TORCH_CHECK(y.numel() == S * R * N && y.size(-1) == N, "pg_grouped: y must be [S, R, N] fp32");
+    e.y = ptr<float>(y);
+  }
+  TORCH_CHECK(xs.is_contiguous() && W.is_contiguous() && y.is_contiguous(), "pg_grouped: contiguous tensors");
+  PgGroup g;
+  g.offsets = ptr<int>(offsets);
+  g.e_lo = (int)e_lo;
+  g.E = (int)E;
+  g.wstride = N * K;
+  const at::OptionalDeviceGuard dg(xs.device());
+  launch_pgemm_grouped((int)epi, (int)cfg, ptr<bf16>(xs), ptr<bf16>(W), (int)R, (int)N, (int)K, (int)S, g, e,
+                       ptr<float>(y), cur_stream(xs));
+}
+
 void pg_resid(const Tensor& x, const Tensor& W, Tensor& resid, const Tensor& w_next, Tensor& xw_out, Tensor& ss_out,
               int64_t cfg) {
   const auto sh = pg_check(x, W, cfg, 1, c10::nullopt, c10::nullopt);
@@ -1135,6 +1186,8 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("pg_swiglu(Tensor x, Tensor W, Tensor? ss_in, float eps, Tensor(a!) act, int cfg) -> ()", &pg_swiglu);
   m.def("pg_resid(Tensor x, Tensor W, Tensor(a!) resid, Tensor w_next, Tensor(b!) xw_out, Tensor(c!) ss_out, int cfg) -> ()",
         &pg_resid);
+  m.def("pg_grouped(Tensor xs, Tensor W, Tensor offsets, int e_lo, Tensor(a!) y, int epi, int cfg, int S) -> ()",
+        &pg_grouped);
   m.def("pgemm_shape(int cfg) -> int[]", [](int64_t cfg) {
     int bm = 0, bn = 0;
     if (!pgemm_cfg_shape((int)cfg, &bm, &bn)) return std::vector<int64_t>{};

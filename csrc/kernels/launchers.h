@@ -20,6 +20,7 @@ enum {
   // epilogue (residual add + next-norm prep, ss per 16-column tile) -- decode_epi.h, xar_push / xar_collect
   DECODE_EPI_XAR = 6,
   DECODE_EPI_BF16 = 7,  // plain bf16 [M][N] output (pgemm.hip only)
+  DECODE_EPI_SWIGLU_SPLIT = 8,  // SwiGLU of [gate rows; up rows] halves (pgemm.hip grouped experts: act [M][N / 2])
   XAR_MAX_TILES = 32,  // output tiles per workgroup of an x-resident XAR launch (epoch slots in LDS)
 };
 
@@ -133,6 +134,17 @@ void set_mgemm_nt(int on);  // non-temporal weight DMA (A/B knob)
 int pgemm_cfg_shape(int cfg, int* bm, int* bn);
 void launch_pgemm(int epi, int cfg, const bf16* x, const bf16* Wshuf, int M, int N, int K, int S, const DecodeEpi& e,
                   float* slab, int* counters, hipStream_t s);
+// grouped (MoE expert) mode: expert e < E owns rows [offsets[e_lo + e], offsets[e_lo + e + 1]) of x [R][K] and of
+// the output, weights Wshuf + e * wstride ([N][K] preshuffled per expert).  The grid covers ceil(R / BM) + E m-tiles
+// per n-tile (segment bounds stay on the device: graph-capturable); blocks past the real tiles exit.  epi:
+// DECODE_EPI_SWIGLU_SPLIT (act [R][N / 2]), BF16 (out_bf [R][N]) or F32 (y [R][N]; S > 1: slab [S][R][N]).
+struct PgGroup {
+  const int* offsets = nullptr;
+  int e_lo = 0, E = 0;
+  long long wstride = 0;
+};
+void launch_pgemm_grouped(int epi, int cfg, const bf16* x, const bf16* Wshuf, int R, int N, int K, int S,
+                          const PgGroup& g, const DecodeEpi& e, float* slab, hipStream_t s);
 
 // norm.hip
 void launch_rms_norm(LinOut x, const bf16* w, bf16* out, int T, int d, float eps, hipStream_t s);

@@ -91,10 +91,12 @@ SYM_DEV void store4bf16(bf16* p, const f32x4& v) {
 }
 
 // Block tile of M-rows [m0, m0 + BM) x features [n0, n0 + BN); K slice [k0, k0 + kslice).
-template <int WM, int WN, int EPI>
+// GRP: grouped experts (launch_pgemm_grouped): m-tile slot -> (expert, tile of its segment) from the device offsets.
+template <int WM, int WN, int EPI, bool GRP>
 __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict__ x, const bf16* __restrict__ W,
                                                            int M, int N, int K, int kslice, int mtiles, DecodeEpi e,
-                                                           float* __restrict__ slab, int* __restrict__ counters) {
+                                                           float* __restrict__ slab, int* __restrict__ counters,
+                                                           PgGroup g) {
   using C = PgCfg<WM, WN>;
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
   // (no AGPR clobber: with none used the whole 256-register budget of 2 waves / SIMD goes to VGPRs)
@@ -107,8 +109,30 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
   const int nwg = gridDim.x, b = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b & 7;
   const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-  const int mt = t % mtiles, nt = t / mtiles;
-  const int m0 = mt * C::BM, n0 = nt * C::BN;
+  int mt = t % mtiles;
+  const int nt = t / mtiles;
+  const int n0 = nt * C::BN;
+  // block rows [m0, Mend) (Mend: the end of the block's segment -- M, or its expert's last row); rows past Mend
+  // are zero-filled by the x buffer range and never stored
+  int m0, Mend;
+  const bf16* wb = W;
+  if constexpr (GRP) {
+    int ex = 0, s0 = 0, s1 = 0;
+    for (; ex < g.E; ++ex) {  // <= 64 scalar loads (segment bounds in device memory: graph-capturable)
+      s0 = g.offsets[g.e_lo + ex];
+      s1 = g.offsets[g.e_lo + ex + 1];
+      const int nmt = (s1 - s0 + C::BM - 1) / C::BM;
+      if (mt < nmt) break;
+      mt -= nmt;
+    }
+    if (ex == g.E) return;  // a surplus slot of the grid (the whole block, before any barrier)
+    m0 = s0 + mt * C::BM;
+    Mend = s1;
+    wb = W + ex * g.wstride;
+  } else {
+    m0 = mt * C::BM;
+    Mend = M;
+  }
   const int split = blockIdx.y;
   const int k0 = split * kslice;
 
@@ -118,22 +142,25 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
   // is tile n0 / 16 + j's 1 KB block of the slot, lane-linear.  Every wave issues NXU + NWU instructions per
   // slot (one vmcnt immediate fits all): a surplus instruction of a last round re-reads a valid 1 KB into the
   // dummy region.  (One pooled x + weight list with a per-instruction kind branch measured 10-20 % slower.)
-  const __amdgpu_buffer_rsrc_t rx = pg_rsrc(x, (long long)M * K * 2);
-  const __amdgpu_buffer_rsrc_t rw = pg_rsrc(W, (long long)N * K * 2);
+  const __amdgpu_buffer_rsrc_t rx = pg_rsrc(x + (long long)m0 * K, (long long)(Mend - m0) * K * 2);
+  const __amdgpu_buffer_rsrc_t rw = pg_rsrc(wb, (long long)N * K * 2);
   int vx[C::NXU], vw[C::NWU], dx[C::NXU], dw[C::NWU];
 #pragma unroll
   for (int u = 0; u < C::NXU; ++u) {
     const int g = u * 8 + wid;
     const int row = 16 * g + (lane >> 2);
     const bool real = g < C::NX;
-    vx[u] = real ? (m0 + row) * K * 2 + 2 * k0 + 16 * ((lane & 3) ^ ((row >> 1) & 3)) : 0;
+    vx[u] = real ? row * K * 2 + 2 * k0 + 16 * ((lane & 3) ^ ((row >> 1) & 3)) : 0;
     dx[u] = real ? g * 1024 : -1;
   }
 #pragma unroll
   for (int u = 0; u < C::NWU; ++u) {
     const int j = u * 8 + wid;
     const bool real = j < C::NW;
-    vw[u] = ((n0 / 16 + (real ? j : 0)) * (K / 32) + k0 / 32) * 1024 + lane * 16;
+    // SWIGLU_SPLIT: local tiles alternate gate (even) and up (odd) rows of the same 16 features (W = [gate; up])
+    const int jt = real ? j : 0;
+    const int tile = EPI == DECODE_EPI_SWIGLU_SPLIT ? (jt & 1 ? N / 32 : 0) + nt * (C::NW / 2) + jt / 2 : n0 / 16 + jt;
+    vw[u] = (tile * (K / 32) + k0 / 32) * 1024 + lane * 16;
     dw[u] = real ? C::XS + j * 1024 : -1;
   }
 
@@ -278,7 +305,7 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
     for (int rrow = threadIdx.x / TPR; rrow < C::BM; rrow += PG_THR / TPR) {
       const int rsub = threadIdx.x % TPR;
       rpart = 0.f;
-      if (m0 + rrow < M) {
+      if (m0 + rrow < Mend) {
         const float* sp = e.ss_in + (long long)(m0 + rrow) * e.ss_tiles;
         if ((e.ss_tiles & 3) == 0) {
           const float4* s4 = reinterpret_cast<const float4*>(sp);
@@ -323,7 +350,7 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
 #pragma unroll
       for (int i = 0; i < WM; ++i) {
         const int m = m0 + (wm * WM + i) * 16 + fr;
-        if (m >= M) continue;
+        if (m >= Mend) continue;
         const float4 f4 = make_float4(acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]);
         unsigned long long* qd = reinterpret_cast<unsigned long long*>(ys + (long long)m * N + n);
         const unsigned long long* w64 = reinterpret_cast<const unsigned long long*>(&f4);
@@ -349,7 +376,7 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
       for (int i = 0; i < WM; ++i) {
         const int m = m0 + (wm * WM + i) * 16 + fr;
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (m < M)
+        if (m < Mend)
           for (int sp = 0; sp < S; ++sp) {  // fixed split order: bitwise reproducible
             const unsigned long long* qs =
                 reinterpret_cast<const unsigned long long*>(slab + ((long long)sp * M + m) * N + n);
@@ -399,7 +426,7 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
       for (int r = tr; r < PR; r += RPI) {
         const int m = m0 + pass * PR + r;
         float sq = 0.f;
-        if (m < M && 4 * tc < C::BN) {
+        if (m < Mend && 4 * tc < C::BN) {
           const f32x4 y = *reinterpret_cast<const f32x4*>(img + r * RBF + tc * 16);
           float* rp = e.resid + (long long)m * N + n0 + 4 * tc;
           const float4 q = *reinterpret_cast<const float4*>(rp);
@@ -411,7 +438,7 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
         }
 #pragma unroll
         for (int o = 1; o < TW; o *= 2) sq += __shfl_xor(sq, o, 64);
-        if (m < M && tc == 0) e.ss_out[(long long)m * P + nt] = sq;
+        if (m < Mend && tc == 0) e.ss_out[(long long)m * P + nt] = sq;
       }
     }
   } else if constexpr (EPI == DECODE_EPI_QKV && C::BN % 128 == 0) {
@@ -449,7 +476,7 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
             if (head0 + hl < e.Hq + e.Hkv) {  // q / k head: RoPE
               const bool lo = h < 2;
               const int dh = 8 * jj + 4 * (h & 1);
-              const float* cs = e.cos_sin + (long long)(m < M ? e.positions[m] : 0) * D;
+              const float* cs = e.cos_sin + (long long)(m < Mend ? e.positions[m] : 0) * D;
               const float4 c4 = *reinterpret_cast<const float4*>(cs + dh);
               const float4 s4 = *reinterpret_cast<const float4*>(cs + 64 + dh);
               const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss4[4] = {s4.x, s4.y, s4.z, s4.w};
@@ -468,7 +495,7 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
       for (int q = threadIdx.x; q < PR * HB * 16; q += PG_THR) {
         const int r = q / (HB * 16), hl = (q / 16) % HB, ch = q % 16;
         const int m = m0 + pass * PR + r, head = head0 + hl;
-        if (m >= M || head >= e.Hq + e.Hkv) continue;
+        if (m >= Mend || head >= e.Hq + e.Hkv) continue;
         bf16* dst;
         if (head < e.Hq) {
           dst = e.q_out + ((long long)m * e.Hq + head) * D;
@@ -491,8 +518,8 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
 #pragma unroll
           for (int k = 0; k < 8; ++k)
             vals[k] = *reinterpret_cast<const bf16*>(img + (r0 + k) * RB + (hl * D + dd) * 2);
-          const int s0 = mb < M ? e.slots[mb] : -1;
-          bool run = s0 >= 0 && (s0 % 8) == 0 && (s0 % e.BS) + 8 <= e.BS && mb + 8 <= M;
+          const int s0 = mb < Mend ? e.slots[mb] : -1;
+          bool run = s0 >= 0 && (s0 % 8) == 0 && (s0 % e.BS) + 8 <= e.BS && mb + 8 <= Mend;
           if (run) {
 #pragma unroll
             for (int k = 1; k < 8; ++k) run = run && e.slots[mb + k] == s0 + k;
@@ -507,25 +534,27 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
               const int m = mb + k;
-              const int sl = m < M ? e.slots[m] : -1;
+              const int sl = m < Mend ? e.slots[m] : -1;
               if (sl >= 0) e.v_cache[(((long long)(sl / e.BS) * e.Hkv + vh) * D + dd) * e.BS + sl % e.BS] = vals[k];
             }
           }
         }
       }
     }
-  } else if constexpr (EPI == DECODE_EPI_BF16 || EPI == DECODE_EPI_SWIGLU) {
+  } else if constexpr (EPI == DECODE_EPI_BF16 || EPI == DECODE_EPI_SWIGLU || EPI == DECODE_EPI_SWIGLU_SPLIT) {
     // bf16 outputs through an LDS image of the block's output tile [BM][OW] (OW = BN, or BN / 2 after SwiGLU),
     // then coalesced 16-B row stores: an accumulator tile alone would store 8 B per lane into 16 rows
-    constexpr int OW = EPI == DECODE_EPI_SWIGLU ? C::BN / 2 : C::BN;
+    constexpr bool SW = EPI == DECODE_EPI_SWIGLU || EPI == DECODE_EPI_SWIGLU_SPLIT;
+    static_assert(EPI != DECODE_EPI_SWIGLU_SPLIT || WN % 2 == 0, "pgemm: split SwiGLU pairs a wave's tiles");
+    constexpr int OW = SW ? C::BN / 2 : C::BN;
     constexpr int RB = OW * 2 + 16;  // row bytes in LDS (+16: rows of a lane group land on distinct banks)
     constexpr int NP = C::BM * RB <= C::RS_OFF ? 1 : 2;  // passes (half the m-waves each when the image is big)
     constexpr int PR = C::BM / NP;                       // rows per pass
     static_assert(PR * RB <= C::RS_OFF, "pgemm: output image exceeds the ring");
     char* const img = smem;
-    bf16* const out = EPI == DECODE_EPI_SWIGLU ? e.act : e.out_bf;
-    const int ldo = EPI == DECODE_EPI_SWIGLU ? N / 2 : N;
-    const int c0 = EPI == DECODE_EPI_SWIGLU ? n0 / 2 : n0;
+    bf16* const out = SW ? e.act : e.out_bf;
+    const int ldo = SW ? N / 2 : N;
+    const int c0 = SW ? n0 / 2 : n0;
     constexpr int CPR = OW * 2 / 16;  // 16-B chunks per row
 #pragma unroll
     for (int pass = 0; pass < NP; ++pass) {
@@ -540,7 +569,16 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
             const int r = mloc - pass * PR;
             f32x4 v = acc[j][i];
             if (has_rs) v *= rs[mloc];
-            if constexpr (EPI == DECODE_EPI_SWIGLU) {
+            if constexpr (EPI == DECODE_EPI_SWIGLU_SPLIT) {
+              if (j % 2 == 0) {  // (gate, up) = tiles (j, j + 1) of this wave, features 16 (tl / 2) + 4h ..
+                f32x4 u = acc[j + 1][i];
+                if (has_rs) u *= rs[mloc];
+                f32x4 a;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a[q] = silu(v[q]) * u[q];
+                store4bf16(reinterpret_cast<bf16*>(img + r * RB + (16 * (tl / 2) + 4 * h) * 2), a);
+              }
+            } else if constexpr (EPI == DECODE_EPI_SWIGLU) {
               f32x4 u;
 #pragma unroll
               for (int q = 0; q < 4; ++q) u[q] = __shfl_xor(v[q], 32, 64);
@@ -560,7 +598,7 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
       for (int q = threadIdx.x; q < PR * CPR; q += PG_THR) {
         const int r = q / CPR, ch = q % CPR;
         const int m = m0 + pass * PR + r;
-        if (m < M)
+        if (m < Mend)
           *reinterpret_cast<uint4*>(out + (long long)m * ldo + c0 + ch * 8) =
               *reinterpret_cast<const uint4*>(img + r * RB + ch * 16);
       }
@@ -573,7 +611,7 @@ __global__ __launch_bounds__(PG_THR, 1) void pgemm_kernel(const bf16* __restrict
       for (int i = 0; i < WM; ++i) {
         const int mloc = (wm * WM + i) * 16 + fr;
         const int m = m0 + mloc;
-        const bool mok = m < M;
+        const bool mok = m < Mend;
         f32x4 v = acc[j][i];
         if (has_rs) {
           const float sc = rs[mloc];
@@ -591,8 +629,18 @@ void launch_cfg(const bf16* x, const bf16* W, int M, int N, int K, int S, const 
   using C = PgCfg<WM, WN>;
   const int mtiles = (M + C::BM - 1) / C::BM;
   const int ntiles = N / C::BN;
-  pgemm_kernel<WM, WN, EPI><<<dim3(mtiles * ntiles, S), dim3(PG_THR), 0, s>>>(x, W, M, N, K, K / S, mtiles, e, slab,
-                                                                              counters);
+  pgemm_kernel<WM, WN, EPI, false><<<dim3(mtiles * ntiles, S), dim3(PG_THR), 0, s>>>(x, W, M, N, K, K / S, mtiles, e,
+                                                                                     slab, counters, PgGroup{});
+}
+
+template <int WM, int WN, int EPI>
+void launch_cfg_grouped(const bf16* x, const bf16* W, int R, int N, int K, int S, const PgGroup& g,
+                        const DecodeEpi& e, float* slab, hipStream_t s) {
+  using C = PgCfg<WM, WN>;
+  const int mslots = (R + C::BM - 1) / C::BM + g.E;  // >= sum over experts of ceil(rows / BM)
+  const int ntiles = N / C::BN;
+  pgemm_kernel<WM, WN, EPI, true><<<dim3(mslots * ntiles, S), dim3(PG_THR), 0, s>>>(x, W, R, N, K, K / S, mslots, e,
+                                                                                    slab, nullptr, g);
 }
 
 // the instantiated tile shapes (index = PG_CFG id, kept in sync with pgemm_cfg_shape below)
@@ -621,6 +669,26 @@ void launch_epi(int cfg, const bf16* x, const bf16* W, int M, int N, int K, int 
   }
 }
 
+// grouped experts: the shapes the MoE layers use (WN even for the split SwiGLU)
+#define PG_GRP_CFGS(X) \
+  X(1, 4, 8)           \
+  X(4, 4, 4)           \
+  X(5, 2, 4)           \
+  X(9, 3, 8)           \
+  X(10, 2, 8)
+
+template <int EPI>
+bool launch_grp_epi(int cfg, const bf16* x, const bf16* W, int R, int N, int K, int S, const PgGroup& g,
+                    const DecodeEpi& e, float* slab, hipStream_t s) {
+  switch (cfg) {
+#define PG_GCASE(id, wm, wn) \
+  case id: launch_cfg_grouped<wm, wn, EPI>(x, W, R, N, K, S, g, e, slab, s); return true;
+    PG_GRP_CFGS(PG_GCASE)
+#undef PG_GCASE
+    default: return false;
+  }
+}
+
 }  // namespace
 
 int pgemm_cfg_shape(int cfg, int* bm, int* bn) {
@@ -641,6 +709,15 @@ void launch_pgemm(int epi, int cfg, const bf16* x, const bf16* Wshuf, int M, int
     case DECODE_EPI_SWIGLU: launch_epi<DECODE_EPI_SWIGLU>(cfg, x, Wshuf, M, N, K, S, e, slab, counters, s); break;
     case DECODE_EPI_BF16: launch_epi<DECODE_EPI_BF16>(cfg, x, Wshuf, M, N, K, S, e, slab, counters, s); break;
     default: launch_epi<DECODE_EPI_F32>(cfg, x, Wshuf, M, N, K, S, e, slab, counters, s); break;
+  }
+}
+
+void launch_pgemm_grouped(int epi, int cfg, const bf16* x, const bf16* Wshuf, int R, int N, int K, int S,
+                          const PgGroup& g, const DecodeEpi& e, float* slab, hipStream_t s) {
+  switch (epi) {
+    case DECODE_EPI_SWIGLU_SPLIT: launch_grp_epi<DECODE_EPI_SWIGLU_SPLIT>(cfg, x, Wshuf, R, N, K, 1, g, e, slab, s); break;
+    case DECODE_EPI_BF16: launch_grp_epi<DECODE_EPI_BF16>(cfg, x, Wshuf, R, N, K, 1, g, e, slab, s); break;
+    default: launch_grp_epi<DECODE_EPI_F32>(cfg, x, Wshuf, R, N, K, S, g, e, slab, s); break;
   }
 }
 

@@ -56,7 +56,7 @@ class EngineConfig:
     weight_init: str = "auto"            # "full" | "shard" | "auto"
     pipeline: bool = True                # enqueue decode step N+1 before step N's tokens reach the host
     mixed_prefill_tokens: int = 512      # prompt-chunk budget of steps that also carry decodes
-    decode_weights: str = "auto"         # "preshuffled" | "shared" | "auto": extra MFMA-ordered decode copies
+    decode_weights: str = "auto"         # "preshuffled" | "replace" | "shared" | "auto": MFMA-ordered decode weights
     enable_prefix_caching: bool = True   # adopt cached KV blocks of a known prompt prefix (multi-turn chats)
     # a burst of >= 4 prompts totalling >= this many tokens, arriving while nothing decodes, prefills its
     # first n // 2 + 1 prompts in one step and the rest in the next (0 = one step for the whole burst)

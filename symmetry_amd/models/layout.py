@@ -57,12 +57,18 @@ def apply_decode_layout(w: ModelWeights) -> None:
 
 
 def natural_tensors(w: ModelWeights) -> dict:
-    """Tensors in natural (HF) row order, whatever layout ``w`` is stored in (reference model, export)."""
-    if getattr(w, "layout", "natural") != "decode":
+    """Tensors in natural (HF) row order, whatever layout ``w`` is stored in (reference model, export): preshuffled
+    tensors (decode_weights="replace") are unshuffled first, then the decode row permutations undone."""
+    shuffled = getattr(w, "shuffled", frozenset())
+    if getattr(w, "layout", "natural") != "decode" and not shuffled:
         return w.tensors
     cfg, tp = w.cfg, w.shard.tp_size
     hq, hkv = cfg.num_heads // tp, cfg.num_kv_heads // tp
     out = dict(w.tensors)
+    for k in shuffled:
+        out[k] = unshuffle(out[k])
+    if getattr(w, "layout", "natural") != "decode":
+        return out
     for i in range(cfg.num_layers):
         k = f"layers.{i}.wqkv"
         t = out[k]
@@ -76,13 +82,18 @@ def natural_tensors(w: ModelWeights) -> dict:
 
 # ---- MFMA-preshuffled weight stream (csrc/kernels/decode_gemm.hip, DecodeEpi::wshuf) -----------------
 def preshuffle(w: torch.Tensor) -> torch.Tensor:
-    """[N, K] row-major -> the same elements ordered [N/16][K/32][lane 64][8]: block (t, kb) holds rows
-    16t.. and k 32kb.. with lane l = 16 * (k8 group) + row, i.e. exactly the MFMA 16x16x32 A-fragment
-    order, so one wave load instruction reads 1 KB contiguous.  Returned with the original [N, K] shape."""
-    N, K = w.shape
-    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N, K)
+    """[..., N, K] row-major -> the same elements ordered [N/16][K/32][lane 64][8] per leading index (an expert
+    stack [E, N, K] is preshuffled per expert): block (t, kb) holds rows 16t.. and k 32kb.. with lane l =
+    16 * (k8 group) + row, i.e. exactly the MFMA 16x16x32 A-fragment order, so one wave load instruction reads 1 KB
+    contiguous.  Returned with the original shape."""
+    *lead, N, K = w.shape
+    L = len(lead)
+    perm = list(range(L)) + [L, L + 2, L + 3, L + 1, L + 4]
+    return w.reshape(*lead, N // 16, 16, K // 32, 4, 8).permute(*perm).contiguous().view(w.shape)
 
 
 def unshuffle(w: torch.Tensor) -> torch.Tensor:
-    N, K = w.shape
-    return w.reshape(N // 16, K // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).contiguous().view(N, K)
+    *lead, N, K = w.shape
+    L = len(lead)
+    perm = list(range(L)) + [L, L + 3, L + 1, L + 2, L + 4]
+    return w.reshape(*lead, N // 16, K // 32, 4, 16, 8).permute(*perm).contiguous().view(w.shape)

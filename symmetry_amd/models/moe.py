@@ -3,8 +3,10 @@
 Routing, permutation into expert segments, the per-expert GEMMs and the weighted combine run as HIP
 kernels (``csrc/kernels/moe.hip``) whose segment bounds live in device memory: no host sync anywhere in
 the block, so every step (decode and prefill, with or without expert parallelism) is hipGraph-capturable.
-Small routed batches (<= 64 rows: decode steps) use the grouped skinny MFMA GEMM; larger ones the grouped
-128 x 128 MFMA GEMM (``ops.grouped_gemm``) with SwiGLU fused into the gate/up epilogue.
+Small routed batches (<= 64 rows: decode steps) use the grouped skinny MFMA GEMM or the weight-streaming kernel;
+prefill-sized ones the prefill GEMM kernel in grouped mode (``ops.pg_grouped``, csrc/kernels/pgemm.hip) or, below
+its row thresholds, the weight-streaming / 128 x 128 tile grouped GEMMs (``ops.grouped_gemm``), SwiGLU fused into
+the gate/up epilogue everywhere.
 
 Expert parallelism, ``ep_size = N`` ranks each owning ``E / N`` experts (attention is tensor-parallel, so
 every rank holds the same T tokens when the block starts):
@@ -38,6 +40,14 @@ PRE_ROWS = int(os.environ.get("SYMMETRY_MOE_PRE_ROWS", "100"))
 # gate/up (+ SwiGLU) streams further: 128-row units with 4 weight tiles per wave, longer segments in two units
 # (w13 at 128 rows per expert 468 vs 598-614 us on the tile kernel, at 160 rows 619-650 vs 673-707)
 PRE_ROWS_W13 = int(os.environ.get("SYMMETRY_MOE_PRE_ROWS_W13", "176"))
+# mean routed rows per local expert from which prefill runs an expert GEMM on the prefill GEMM kernel's grouped mode
+# (ops.pg_grouped) instead of the two kernels above (A/B switch: SYMMETRY_MOE_PG=0).  Mixtral shapes, segments
+# 0.4x .. 2.0x the mean (bench/kernels/bench_pg_grouped.py, profiles/r6/pg_grouped_sweep*.jsonl): w2 at 80 rows
+# 206 vs 247 us (streaming), at 128 236 vs 350, at 256 336 vs 594 (tile); at 48 / 64 rows streaming keeps a 5-9 %
+# lead.  w13 + SwiGLU even at 80-96 rows, 421 vs 475 at 112, 451 vs 474 at 128, 649 vs 889 at 256.
+PG_GROUPED = os.environ.get("SYMMETRY_MOE_PG", "1") != "0"
+PG_ROWS_W13 = int(os.environ.get("SYMMETRY_MOE_PG_ROWS_W13", "100"))
+PG_ROWS_W2 = int(os.environ.get("SYMMETRY_MOE_PG_ROWS_W2", "72"))
 # decode steps stream the preshuffled copies from this many routed rows per local expert (every expert routed)
 STREAM_DECODE_ROWS = int(os.environ.get("SYMMETRY_MOE_STREAM_DECODE_ROWS", "4"))
 # "auto": expert all-to-all from this many tokens (prefill); decode steps (<= 64 rows under MoE) all-reduce
@@ -70,6 +80,7 @@ class MoEBlock:
         self.a2a_bytes = {"dispatch": 0, "return": 0, "routed_rows": 0, "padded_dispatch": 0, "gather": 0}
         # router rows padded to a multiple of 16 for the skinny GEMM (padded logits are never read)
         self.router = {}
+        self.single_copy = False  # adopt_single_copy: the expert tensors themselves are preshuffled
         self.pre = self._preshuffled_copies(model)
         pol = os.environ.get("SYMMETRY_MOE_STREAM_POLICY")  # A/B: grouped_gemm's row-major streaming policy
         if pol is not None and model.device.type == "cuda":
@@ -112,6 +123,39 @@ class MoEBlock:
                 E, N, K = w.shape
                 out[(i, name)] = w.reshape(E, N // 16, 16, K // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous().view(E, N, K)
         return out
+
+    def single_copy_ok(self) -> bool:
+        """The expert shapes tile for the kernels that read the preshuffled layout (streaming: <= 8 local experts,
+        K % 256, 128-row n-blocks; the grouped prefill GEMM: 64-deep k steps)."""
+        cfg = self.m.cfg
+        d, F = cfg.hidden_size, self.F
+        return GROUPED and self.E_local <= 8 and d % 256 == 0 and F % 256 == 0 and F % 64 == 0 and d % 128 == 0
+
+    def all_copies(self) -> bool:
+        """Every layer has both preshuffled expert copies (the budget allowed them)."""
+        L = self.m.cfg.num_layers
+        return all((i, n) in self.pre for i in range(L) for n in ("w13", "w2"))
+
+    def adopt_single_copy(self) -> list:
+        """decode_weights="replace": the expert weights exist ONLY preshuffled (per expert, models/layout.py) -- an
+        existing copy becomes the weight and the row-major tensor is released, else the tensor is preshuffled in
+        place.  Every expert GEMM then reads that layout: decode steps the weight-streaming kernel, prefill the
+        streaming or the grouped prefill GEMM kernel.  Returns the tensor names now stored preshuffled."""
+        from .layout import preshuffle
+
+        w = self.m.w
+        keys = []
+        for i in range(self.m.cfg.num_layers):
+            for name in ("w13", "w2"):
+                key = f"layers.{i}.{name}"
+                t = self.pre.get((i, name))
+                if t is None:
+                    t = preshuffle(w.tensors[key])
+                w.tensors[key] = t
+                self.pre[(i, name)] = t
+                keys.append(key)
+        self.single_copy = True
+        return keys
 
     def _buf(self, name, shape, dtype):
         return self.m._buf("moe." + name, shape, dtype)
@@ -200,7 +244,8 @@ class MoEBlock:
         w2 = self.m.w.layer(i, "w2")
         F = self.F
         act = self._buf("act", (R, F), torch.bfloat16)
-        if STREAM_DECODE_ROWS * n_local <= R <= SKINNY_ROWS and ((i, "w13") in self.pre or (i, "w2") in self.pre):
+        if R <= SKINNY_ROWS and (self.single_copy or (STREAM_DECODE_ROWS * n_local <= R and (
+                (i, "w13") in self.pre or (i, "w2") in self.pre))):
             # decode sizes on the preshuffled copies: the weight-streaming kernel (1 KB fragment loads, one unit per
             # populated expert and n-block) beats the grouped skinny GEMM at 1-8 rows per expert when every expert
             # is routed: w13 + SwiGLU 320 -> 299 us, w2 162 -> 144 (profiles/r5/grouped_stream.jsonl); with a few
@@ -233,12 +278,32 @@ class MoEBlock:
             ops.grouped_skinny(act, w2, offsets, e_lo, y2)
             return y2
         if self._grouped_ok(d):
-            # prefill-sized: grouped MFMA GEMMs, SwiGLU fused into the gate/up epilogue; up to PRE_ROWS routed rows
-            # per expert the weight-streaming kernel on the preshuffled copies, beyond it the tile kernel
-            p13 = self.pre.get((i, "w13")) if R <= PRE_ROWS_W13 * self.E else None
-            p2 = self.pre.get((i, "w2")) if R <= PRE_ROWS * self.E else None
-            ops.grouped_gemm(xs, w13 if p13 is None else p13, offsets, e_lo, act,
-                             ops.GROUPED_SWIGLU + (0 if p13 is None else ops.GROUPED_PRESHUFFLED))
+            # prefill-sized.  From PG_ROWS_* mean routed rows per local expert: the prefill GEMM kernel in grouped mode
+            # on the preshuffled copies (csrc/kernels/pgemm.hip: block -> (expert, m-tile) from the device offsets)
+            # -- SwiGLU of the [gate; up] halves in the gate/up epilogue, w2 into fp32 k-split slabs the combine
+            # sums.  Below: the weight-streaming kernel on the preshuffled copies up to PRE_ROWS* rows, the 128 x 128
+            # tile kernel beyond
+            rpe = R / max(1, n_local)
+            pg13 = self.pre.get((i, "w13")) if PG_GROUPED and rpe >= PG_ROWS_W13 else None
+            pg2 = self.pre.get((i, "w2")) if PG_GROUPED and rpe >= PG_ROWS_W2 else None
+            c13 = ops.choose_pg_grouped(R, 2 * F, d, n_local, even_wn=True) if pg13 is not None else None
+            c2 = ops.choose_pg_grouped(R, d, F, n_local, slabs=out_f32) if pg2 is not None else None
+            if c13 is not None:
+                ops.pg_grouped(xs, pg13, offsets, e_lo, act, ops.PG_EPI_SWIGLU_SPLIT, c13[0])
+            else:
+                p13 = self.pre.get((i, "w13")) if self.single_copy or R <= PRE_ROWS_W13 * self.E else None
+                ops.grouped_gemm(xs, w13 if p13 is None else p13, offsets, e_lo, act,
+                                 ops.GROUPED_SWIGLU + (0 if p13 is None else ops.GROUPED_PRESHUFFLED))
+            if c2 is not None:
+                cfg2, s2 = c2
+                if out_f32:
+                    y2 = self._buf(f"y2pg{s2}", (s2, R, d), torch.float32)
+                    ops.pg_grouped(act, pg2, offsets, e_lo, y2, ops.PG_EPI_F32, cfg2, s2)
+                else:
+                    y2 = self._buf("y2b", (R, d), torch.bfloat16)
+                    ops.pg_grouped(act, pg2, offsets, e_lo, y2, ops.PG_EPI_BF16, cfg2)
+                return y2
+            p2 = self.pre.get((i, "w2")) if self.single_copy or R <= PRE_ROWS * self.E else None
             y2 = self._buf("y2f" if out_f32 else "y2b", (R, d), torch.float32 if out_f32 else torch.bfloat16)
             ops.grouped_gemm(act, w2 if p2 is None else p2, offsets, e_lo, y2,
                              (ops.GROUPED_F32 if out_f32 else ops.GROUPED_BF16)

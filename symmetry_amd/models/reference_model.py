@@ -76,7 +76,7 @@ def forward_logits(w: ModelWeights, ids: list[int], router_gaps: list | None = N
     way."""
     from .layout import natural_tensors
 
-    if getattr(w, "layout", "natural") != "natural":
+    if getattr(w, "layout", "natural") != "natural" or getattr(w, "shuffled", None):
         w = ModelWeights(w.cfg, w.shard, natural_tensors(w), "natural")
     cfg = w.cfg
     tp = w.shard.tp_size if group is not None else 1

@@ -197,15 +197,25 @@ class TransformerLM:
         self.last_ids = torch.zeros(MAX_STEP_SEQS, dtype=torch.int32, device=self.device)
         if self.device.type != "cpu":
             ops.decode_ks_ws(self.device)  # allocated before any graph capture (stable address)
+        self.single_copy = False  # decode_weights="replace": the layer weights exist only MFMA-preshuffled
         self.dgw = self._decode_copies(decode_weights)
         self.tp_reduced_bytes: dict[str, int] = {}  # bytes per rank of the last general-path all-reduce
 
     def _decode_copies(self, mode: str) -> dict:
-        """MFMA-preshuffled copies of the decode-GEMM weights (1 KB contiguous per wave load:
-        profiles/decode_gemm_preshuffle_r1.jsonl, -9 % per layer).  The row-major tensors stay for the
-        hipBLASLt prefill GEMMs, so this costs one extra copy of the layer weights: on by default when it
-        fits comfortably in HBM (8B: +14.5 GB of 288 GB), off for e.g. 70B on one GPU."""
-        if not self.fused or self.device.type == "cpu" or mode == "shared":
+        """MFMA-preshuffled decode-GEMM weights (1 KB contiguous per wave load: profiles/decode_gemm_preshuffle_r1.jsonl,
+        -9 % per layer).  ``mode``:
+
+        * "preshuffled": an extra copy next to the row-major tensors, which stay for the hipBLASLt prefill GEMMs
+          (8B: +14.5 GB of 288 GB);
+        * "replace": ONE copy -- the layer weights are preshuffled in place (models with the fused decode GEMMs)
+          and every consumer reads that layout: decode GEMMs, mgemm / the prefill GEMM (pgemm) for prefill,
+          dg_f32 for the few-row projections; MoE experts likewise (MoEBlock.adopt_single_copy: the streaming and
+          grouped prefill GEMM kernels); the fp32 oracle and exports unshuffle (layout.natural_tensors);
+        * "shared": row-major only (the decode GEMMs' row-major variants);
+        * "auto": "preshuffled" when the copies fit next to the KV cache's need (transformer.copy_budget), "replace"
+          otherwise (70B on one GPU: 141 GB of layer weights; Mixtral when its expert copies did not all fit),
+          row-major only where neither applies."""
+        if not self.fused or mode == "shared" or (self.device.type == "cpu" and mode != "replace"):
             return {}
         names = ["wqkv", "wo"] + ([] if self.cfg.is_moe else ["w_gu", "w_down"])
         extra = sum(self.w.layer(i, n).numel() * 2 for i in range(self.cfg.num_layers) for n in names)
@@ -217,13 +227,28 @@ class TransformerLM:
             # launch) only from what the same budget has left, so it never costs a model its layer copies.  The
             # budget: what is left after the KV cache's need and a 6 GB workspace reserve
             budget = copy_budget(self.device, self.kv_reserve)
-            if extra > budget:
-                return {}
-            if head is not None and extra + head.numel() * 2 > budget:
+            if extra > budget or (self.moe is not None and not self.moe.all_copies()):
+                mode = "replace"
+            if head is not None and (mode == "replace" or extra + head.numel() * 2 > budget):
                 head = None
         from .layout import preshuffle
 
         out = {}
+        if mode == "replace":
+            if self.moe is not None and not self.moe.single_copy_ok():
+                raise ValueError("decode_weights=replace: the expert shapes do not tile for the preshuffled kernels")
+            for i in range(self.cfg.num_layers):
+                for n in names:
+                    key = f"layers.{i}.{n}"
+                    t = preshuffle(self.w.tensors[key])
+                    self.w.tensors[key] = t  # the row-major tensor is released here
+                    out[(i, n)] = t
+            shuffled = {f"layers.{i}.{n}" for i in range(self.cfg.num_layers) for n in names}
+            if self.moe is not None:
+                shuffled |= set(self.moe.adopt_single_copy())
+            self.w.shuffled = frozenset(shuffled)
+            self.single_copy = True
+            return out
         for i in range(self.cfg.num_layers):
             for n in names:
                 out[(i, n)] = preshuffle(self.w.layer(i, n))
@@ -231,10 +256,15 @@ class TransformerLM:
             out[(-1, "lm_head")] = preshuffle(head)
         return out
 
+    def _row_major(self, i: int, name: str):
+        """The row-major layer weight, or None when only the preshuffled layout exists (decode_weights="replace")."""
+        return None if self.single_copy else self.w.layer(i, name)
+
     def extra_weight_bytes(self) -> int:
-        """Bytes of the optional layout copies (preshuffled decode weights, preshuffled expert streams)."""
-        n = sum(t.numel() * t.element_size() for t in self.dgw.values())
-        if self.moe is not None:
+        """Bytes of the optional layout copies (preshuffled decode weights, preshuffled expert streams); 0 for the
+        layer weights of a single-copy model (decode_weights="replace": the preshuffled tensors ARE the weights)."""
+        n = sum(t.numel() * t.element_size() for k, t in self.dgw.items() if not (self.single_copy and k[0] >= 0))
+        if self.moe is not None and not self.single_copy:
             n += sum(t.numel() * t.element_size() for t in self.moe.pre.values())
         return n
 
@@ -273,12 +303,24 @@ class TransformerLM:
         """x [T, K] bf16 -> LinOut: fp32 slabs [S, T, N] (skinny / medium-M) or bf16 [T, N] (library GEMM).
         ``wshuf``: the MFMA-preshuffled copy of ``w`` if one exists (enables the medium-M kernel)."""
         T, K = x.shape
-        N = w.shape[0]
+        N = (w if w is not None else wshuf).shape[0]
         pick = ops.choose_mgemm(T, N, K) if wshuf is not None else None
         if pick is not None:
             rw, S = pick
             y = self._buf(name + ".slab", (S, T, N), torch.float32)
             ops.mgemm(x, wshuf, y, rw)
+        elif w is None and T <= SKINNY_MAX_M:
+            # only the preshuffled layout exists: the decode GEMM's fp32 form (one slab)
+            y = self._buf(name + ".slab", (1, T, N), torch.float32)
+            ops.dg_f32(x, wshuf, None, 0.0, y.view(T, N), wshuf=True)
+        elif w is None:
+            # ... and the prefill GEMM past the medium range: k-split fp32 slabs where they pay, else bf16 out
+            cfg, S = ops.choose_pgemm(max(T, ops.PGEMM_MIN_M), N, K, slabs=True, force=True)
+            if S > 1:
+                y = self._buf(name + ".slab", (S, T, N), torch.float32)
+            else:
+                y = self._buf(name + ".bf16", (T, N), torch.bfloat16)
+            ops.pgemm(x, wshuf, y, cfg, S)
         elif T <= SKINNY_MAX_M:
             S = ops.choose_splits(N, K)
             y = self._buf(name + ".slab", (S, T, N), torch.float32)
@@ -431,7 +473,7 @@ class TransformerLM:
                        self.hkv, wshuf=shq)
             self._attention(b, kv, i, q, attn)
             ss = self._resid_proj("o", attn2d, self._dgw(i, "wo"), resid, w.layer(i, "ln2"), xw, ss_t, ss_1,
-                                  w.layer(i, "wo"))
+                                  self._row_major(i, "wo"))
             if cfg.is_moe:
                 if self.moe.decode_fused_ok(T, d):
                     ss = self.moe.forward_decode(i, resid, w.layer(i, "ln2"), eps, nxt, xw, ss_1)
@@ -446,7 +488,7 @@ class TransformerLM:
                 act = self._buf("act", (T, w_gu.shape[0] // 2), torch.bfloat16)
                 ops.dg_swiglu(xw, w_gu, ss, eps, act, wshuf=shg)
                 ss = self._resid_proj("down", act, self._dgw(i, "w_down"), resid, nxt, xw, ss_t, ss_1,
-                                      w.layer(i, "w_down"))
+                                      self._row_major(i, "w_down"))
         n = b.num_seqs
         if b.kind == "decode":
             xl, sl = xw, ss
@@ -516,11 +558,11 @@ class TransformerLM:
             xw = self._buf("xw", (T, d), torch.bfloat16)
             ss_p = self._buf("ss_pgu", (T, 4 if d % 32 == 0 else 1), torch.float32)
         for i in range(cfg.num_layers):
-            qkv = self._linear("qkv", x, w.layer(i, "wqkv"), wshuf=self._shuf(i, "wqkv"))
+            qkv = self._linear("qkv", x, self._row_major(i, "wqkv"), wshuf=self._shuf(i, "wqkv"))
             ops.rope_cache(qkv, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq, self.hkv,
                            perm=True, decode=ROPE_DECODE_ROWS and b.kind == "decode")
             self._attention(b, kv, i, q, attn)
-            o = self._linear("o", attn.view(T, self.hq * self.D), w.layer(i, "wo"), reduce=True,
+            o = self._linear("o", attn.view(T, self.hq * self.D), self._row_major(i, "wo"), reduce=True,
                              wshuf=self._shuf(i, "wo"))
             if gu_plan is not None:
                 # deferred norm into gate_up + SwiGLU epilogue (one mgemm launch instead of GEMM + swiglu)
@@ -528,7 +570,7 @@ class TransformerLM:
                 w_gu = self.dgw[(i, "w_gu")]
                 act = self._buf("act", (T, w_gu.shape[0] // 2), torch.bfloat16)
                 ops.dg_swiglu(xw, w_gu, ss_p, eps, act, wshuf=True, mg=gu_plan)
-                mlp = self._linear("down", act, w.layer(i, "w_down"), reduce=True, wshuf=self._shuf(i, "w_down"))
+                mlp = self._linear("down", act, self._row_major(i, "w_down"), reduce=True, wshuf=self._shuf(i, "w_down"))
             elif cfg.is_moe:
                 ops.add_rms_norm(o, resid, w.layer(i, "ln2"), eps, x)
                 mlp = self.moe.forward(i, x)
@@ -540,11 +582,11 @@ class TransformerLM:
                     act = self._buf("act", (T, w_gu.shape[0] // 2), torch.bfloat16)
                     ops.pg_swiglu(x, w_gu, None, eps, act, pg_gu)
                 else:
-                    gu = self._linear("gu", x, w.layer(i, "w_gu"), wshuf=self._shuf(i, "w_gu"))
+                    gu = self._linear("gu", x, self._row_major(i, "w_gu"), wshuf=self._shuf(i, "w_gu"))
                     F = gu.shape[-1] // 2
                     act = self._buf("act", (T, F), torch.bfloat16)
                     ops.swiglu(gu, act, interleaved=True)
-                mlp = self._linear("down", act, w.layer(i, "w_down"), reduce=True, wshuf=self._shuf(i, "w_down"))
+                mlp = self._linear("down", act, self._row_major(i, "w_down"), reduce=True, wshuf=self._shuf(i, "w_down"))
             nxt = w.layer(i + 1, "ln1") if i + 1 < cfg.num_layers else w["norm"]
             ops.add_rms_norm(mlp, resid, nxt, eps, x)
         return self.sample(b, x)

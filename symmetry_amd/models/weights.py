@@ -71,10 +71,13 @@ class ModelWeights:
     shard: ShardSpec
     tensors: dict = field(default_factory=dict)
     layout: str = "natural"  # "decode" after models.layout.apply_decode_layout
+    # names of tensors stored MFMA-preshuffled in place (decode_weights="replace": one copy per weight)
+    shuffled: frozenset = frozenset()
 
     def to(self, device) -> "ModelWeights":
-        """Copy on ``device`` (keeps the layout tag)."""
-        return ModelWeights(self.cfg, self.shard, {k: v.to(device) for k, v in self.tensors.items()}, self.layout)
+        """Copy on ``device`` (keeps the layout tags)."""
+        return ModelWeights(self.cfg, self.shard, {k: v.to(device) for k, v in self.tensors.items()}, self.layout,
+                            self.shuffled)
 
     def __getitem__(self, k):
         return self.tensors[k]

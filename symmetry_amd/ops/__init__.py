@@ -199,17 +199,18 @@ PGEMM_GU_MIN_M = int(os.environ.get("SYMMETRY_PGEMM_GU_MIN_M", "576"))
 PGEMM_GU_MAX_M = int(os.environ.get("SYMMETRY_PGEMM_GU_MAX_M", "896"))
 
 
-def choose_pgemm(M: int, N: int, K: int, slabs: bool = False, cus: int = 256, align: int = 16):
+def choose_pgemm(M: int, N: int, K: int, slabs: bool = False, cus: int = 256, align: int = 16, force: bool = False):
     """(cfg, S) of the prefill GEMM for an [M, K] x [N, K]^T projection, or None.  ``slabs``: the consumer can sum
     fp32 split-K slabs (S > 1 allowed; fused epilogues need S = 1).  ``align``: the tile width must be a multiple
-    of it (the QKV epilogue writes whole 128-dim heads).
+    of it (the QKV epilogue writes whole 128-dim heads).  ``force``: plan even where the library would be chosen
+    (single-copy weights: the preshuffled layout is all there is).
 
     Cost model fitted to the 768-row sweeps on MI355X (bench/kernels/bench_pgemm.py, pgemm_probe.py;
     profiles/r6/pgemm_*.jsonl): a k-step (32 deep) of a BM x BN tile is bound by the per-CU LDS-DMA intake --
     ~50 GB/s per CU while at most 3/4 of the CUs stream, ~35 GB/s with all of them (L2 / fabric contention)
     -- or by its MFMAs at ~6.5 TFLOP/s per CU; plus ~3 us of prologue + epilogue per wave of blocks and the
     slabs written for the consumer."""
-    if not _PGEMM_ON or M < PGEMM_MIN_M or K % 64:
+    if K % 64 or (not force and (not _PGEMM_ON or M < PGEMM_MIN_M)):
         return None
     best = None
     for cfg, (bm, bn) in PG_CFG_SHAPES.items():
@@ -259,6 +260,65 @@ def pg_resid(x, W, resid, w_next, xw_out, ss_out, cfg):
     if _gpu(x):
         return _native.ops().pg_resid(x, W, resid, w_next, xw_out, ss_out, int(cfg))
     return _pg_resid_ref(x, reference.unshuffled(W, True), resid, w_next, xw_out, ss_out)
+
+
+# grouped-expert mode (MoE prefill): tile configs instantiated for it (csrc/kernels/pgemm.hip PG_GRP_CFGS) and the
+# epilogues (launchers.h DECODE_EPI_*)
+PG_GRP_CFGS = (1, 4, 5, 9, 10)
+PG_EPI_F32, PG_EPI_BF16, PG_EPI_SWIGLU_SPLIT = 0, 7, 8
+
+
+def pg_grouped(xs, W, offsets, e_lo: int, y, epi: int, cfg: int, S: int = 1):
+    """Grouped expert GEMM on the prefill GEMM kernel: expert e of W [E, N, K] (MFMA-preshuffled per expert) applied
+    to rows [offsets[e_lo + e], offsets[e_lo + e + 1]) of xs [R, K].  epi PG_EPI_SWIGLU_SPLIT: act [R, N / 2] =
+    silu(gate) * up of the [gate; up] halves; PG_EPI_BF16: y [R, N]; PG_EPI_F32: y [R, N] fp32 or [S, R, N] k-split
+    partial slabs (LinOut).  Rows outside the segments are left untouched."""
+    if _gpu(xs):
+        return _native.ops().pg_grouped(xs, W, offsets, int(e_lo), y, int(epi), int(cfg), int(S))
+    from ..models.layout import unshuffle
+
+    offs = [int(v) for v in offsets[e_lo: e_lo + W.shape[0] + 1].tolist()]
+    for e in range(W.shape[0]):
+        a, b = offs[e], offs[e + 1]
+        if b <= a:
+            continue
+        p = xs[a:b].float() @ unshuffle(W[e]).float().t()
+        if epi == PG_EPI_SWIGLU_SPLIT:
+            F = p.shape[1] // 2
+            p = torch.nn.functional.silu(p[:, :F]) * p[:, F:]
+        if y.dim() == 3:
+            y[:, a:b] = 0
+            y[0, a:b] = p
+        else:
+            y[a:b] = p.to(y.dtype)
+    return y
+
+
+def choose_pg_grouped(R: int, N: int, K: int, E: int, slabs: bool = False, cus: int = 256, even_wn: bool = False):
+    """(cfg, S) of the grouped prefill GEMM for R routed rows over E local experts ([N, K] weights each), or None.
+    The m-tile count is not known on the host (segment bounds live on the device): the estimate ceil(R / BM) + E / 2
+    covers one partial tile per expert on average; otherwise choose_pgemm's cost model.  ``even_wn``: the split
+    SwiGLU epilogue pairs a wave's tiles."""
+    if K % 64:
+        return None
+    best = None
+    for cfg in PG_GRP_CFGS:
+        bm, bn = PG_CFG_SHAPES[cfg]
+        if N % bn or (even_wn and (bn // 32) % 2):
+            continue
+        for S in ((1, 2, 4) if slabs else (1,)):
+            if K % (64 * S):
+                continue
+            mt = -(-R // bm) + E // 2
+            tiles = mt * (N // bn) * S
+            waves = -(-tiles // cus)
+            busy = min(tiles, cus)
+            rate = 50e9 if busy <= 3 * cus // 4 else 35e9
+            step = max((bm + bn) * 64 / rate, 2 * bm * bn * 32 / 6.5e12)
+            t = waves * (K // S // 32) * step + waves * 3e-6 + (S * R * N * 4 / 10e12 if S > 1 else 0.0)
+            if best is None or t < best[0]:
+                best = (t, cfg, S)
+    return None if best is None else (best[1], best[2])
 
 
 def lm_head_sample(x, w, temps, seeds, step, tile_keys, out_keys, out_ids, n_offset=0, logits=None):

@@ -491,3 +491,52 @@ def test_prefix_requery_counts_the_query_once():
     src.num_computed = 12
     bm.register(src)  # its prefix is cached now: the re-look hits, the query still counted once
     assert bm.match_prefix(waiting) == 12 and bm.query_tokens == 13 and bm.hit_tokens == 12
+
+
+def test_single_copy_preshuffled_weights_match_oracle():
+    """decode_weights="replace": the layer weights exist once, MFMA-preshuffled in place (70B on one GPU), and every
+    path reads that layout -- fused decode, the general path's few-row (dg_f32) and long (prefill GEMM) projections --
+    with the fp32 oracle unshuffling them: greedy tokens of a short and a 300-token prompt match the oracle."""
+    from symmetry_amd.models import reference_model as rm
+
+    eng = LLMEngine(EngineConfig(model="small-llama", device="cpu", max_num_seqs=2, max_model_len=512,
+                                 num_kv_blocks=64, block_size=16, use_graphs=False, seed=0,
+                                 decode_weights="replace"))
+    m = eng.model
+    assert m.single_copy and m.dgw[(0, "wqkv")] is eng.weights.tensors["layers.0.wqkv"]
+    assert "layers.3.w_down" in eng.weights.shuffled
+    assert m.extra_weight_bytes() == 0  # the preshuffled tensors are the weights, not a copy
+    w = eng.weights.to("cpu")
+    for n in (20, 300):
+        prompt = [3 + (11 * i) % 30000 for i in range(n)]
+        out = eng.generate(prompt, SamplingParams(max_tokens=4, temperature=0.0))
+        r = rm.check_tokens(rm.forward_logits(w, prompt + out[:-1]), len(prompt), out, tol=0.05)
+        assert r["mismatches"] == 0, (n, r)
+
+
+def test_single_copy_moe_experts_match_oracle(monkeypatch):
+    """decode_weights="replace" on a MoE model: attention weights AND the expert stacks exist once, preshuffled per
+    expert; decode steps run the streaming grouped GEMM, a 300-token prefill the grouped prefill GEMM (pg_grouped)
+    -- greedy tokens match the fp32 oracle on the unshuffled weights."""
+    from symmetry_amd import ops
+    from symmetry_amd.models import reference_model as rm
+
+    eng = LLMEngine(EngineConfig(model="tiny-mixtral", device="cpu", max_num_seqs=2, max_model_len=512,
+                                 num_kv_blocks=64, block_size=16, use_graphs=False, seed=0,
+                                 decode_weights="replace"))
+    m = eng.model
+    assert m.single_copy and m.moe.single_copy and m.extra_weight_bytes() == 0
+    assert m.moe.pre[(1, "w13")] is eng.weights.tensors["layers.1.w13"]
+    assert {"layers.0.w2", "layers.1.wqkv"} <= eng.weights.shuffled
+    calls = []
+    for name in ("pg_grouped", "grouped_gemm", "grouped_skinny"):
+        f = getattr(ops, name)
+        monkeypatch.setattr(ops, name, lambda *a, _f=f, _n=name, **k: calls.append((_n, a[0].shape[0])) or _f(*a, **k))
+    w = eng.weights.to("cpu")
+    for n in (20, 300):
+        prompt = [3 + (11 * i) % 500 for i in range(n)]
+        out = eng.generate(prompt, SamplingParams(max_tokens=4, temperature=0.0))
+        r = rm.check_tokens(rm.forward_logits(w, prompt + out[:-1]), len(prompt), out, tol=0.05)
+        assert r["mismatches"] == 0, (n, r)
+    names = {c[0] for c in calls}
+    assert "grouped_skinny" not in names and {"pg_grouped", "grouped_gemm"} <= names, calls

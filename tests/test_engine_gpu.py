@@ -545,28 +545,38 @@ def test_grouped_stream_mixtral_shapes(gpu, mode, pre):
         torch.testing.assert_close(yc[a:b], p, atol=tol, rtol=tol)
 
 
-def test_mixtral_prefill_grouped_path_matches_oracle(gpu):
-    """tiny-mixtral prefill of more than 64 routed rows: the grouped MFMA GEMM path (no host sync) end to
-    end against the fp32 oracle, with the decode steps in hipGraphs."""
+@pytest.mark.parametrize("pg", [True, False])
+def test_mixtral_prefill_grouped_path_matches_oracle(gpu, pg):
+    """tiny-mixtral prefill of more than 64 routed rows: the grouped expert GEMMs (no host sync) end to end against
+    the fp32 oracle, with the decode steps in hipGraphs -- on the prefill GEMM kernel's grouped mode (pg) and on the
+    tile / weight-streaming grouped kernels."""
+    import symmetry_amd.models.moe as moe_mod
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
     from symmetry_amd.engine.sequence import SamplingParams
 
     eng = LLMEngine(EngineConfig(model="tiny-mixtral", device="cuda:0", max_num_seqs=4, max_model_len=1024,
                                  num_kv_blocks=64, use_graphs=True))
+    assert eng.model.moe.pre, "expected the preshuffled expert copies"
     prompts = [list(range(40 + 7 * i, 40 + 7 * i + 90 + 20 * i)) for i in range(3)]  # 90..130 tokens each
-    calls = []
-    orig = ops.grouped_gemm
-    import symmetry_amd.models.moe as moe_mod
-
-    moe_mod.ops.grouped_gemm = lambda *a, **k: calls.append(a[0].shape[0]) or orig(*a, **k)
+    calls = {"grouped_gemm": [], "pg_grouped": []}
+    origs = {n: getattr(ops, n) for n in calls}
+    saved = moe_mod.PG_GROUPED
+    moe_mod.PG_GROUPED = pg
+    for n, f in origs.items():
+        setattr(moe_mod.ops, n, lambda *a, _n=n, _f=f, **k: calls[_n].append(a[0].shape[0]) or _f(*a, **k))
     try:
         seqs = [eng.add_request(f"m{i}", p, SamplingParams(max_tokens=6, ignore_eos=True))
                 for i, p in enumerate(prompts)]
         while eng.has_unfinished():
             eng.step()
     finally:
-        moe_mod.ops.grouped_gemm = orig
-    assert calls and max(calls) > 64
+        for n, f in origs.items():
+            setattr(moe_mod.ops, n, f)
+        moe_mod.PG_GROUPED = saved
+    used = calls["pg_grouped" if pg else "grouped_gemm"]
+    assert used and max(used) > 64, calls
+    if pg:
+        assert not calls["grouped_gemm"] or max(calls["grouped_gemm"]) <= 64
     for p, s in zip(prompts, seqs):
         assert len(s.output_ids) == 6
         _agree(eng.weights, p, s.output_ids, tol=0.08)

@@ -201,3 +201,31 @@ def test_long_prefill_gate_up_on_pgemm(monkeypatch):
     for j, t in enumerate(out):
         row = lg[len(prompt) - 1 + j]
         assert float(row.max() - row[t]) <= 0.05, (j, t, int(row.argmax()))
+
+
+def test_grouped_pgemm_planner_and_reference():
+    """The grouped prefill GEMM's planner only returns instantiated configs that tile the shape (even tile pairs for
+    the split SwiGLU), and its CPU reference agrees with the grouped GEMM reference on [gate; up] experts."""
+    for R in (300, 1024, 4096):
+        c13 = ops.choose_pg_grouped(R, 2 * 14336, 4096, 8, even_wn=True)
+        c2 = ops.choose_pg_grouped(R, 4096, 14336, 8, slabs=True)
+        for (cfg, S), (N, K) in ((c13, (2 * 14336, 4096)), (c2, (4096, 14336))):
+            bm, bn = ops.PG_CFG_SHAPES[cfg]
+            assert cfg in ops.PG_GRP_CFGS and N % bn == 0 and K % (64 * S) == 0
+        assert (ops.PG_CFG_SHAPES[c13[0]][1] // 32) % 2 == 0 and c13[1] == 1
+    g = torch.Generator().manual_seed(0)
+    E, N, K = 3, 64, 64
+    W = torch.randn(E, N, K, generator=g).bfloat16()
+    xs = torch.randn(10, K, generator=g).bfloat16()
+    offsets = torch.tensor([0, 2, 2, 7, 10], dtype=torch.int32)  # expert 0 foreign (e_lo = 1)
+    Wp = torch.stack([preshuffle(W[e]) for e in range(E)])
+    want = torch.zeros(10, N // 2)
+    reference.grouped_gemm(xs, W, offsets, 1, want, ops.GROUPED_SWIGLU)
+    got = torch.zeros(10, N // 2)
+    ops.pg_grouped(xs, Wp, offsets, 1, got, ops.PG_EPI_SWIGLU_SPLIT, 5)
+    assert torch.allclose(got, want, atol=1e-5)
+    slabs = torch.full((2, 10, N), 5.0)
+    ops.pg_grouped(xs, Wp, offsets, 1, slabs, ops.PG_EPI_F32, 5, 2)
+    ref = torch.zeros(10, N)
+    reference.grouped_gemm(xs, W, offsets, 1, ref, ops.GROUPED_F32)
+    assert torch.allclose(slabs.sum(0)[2:], ref[2:], atol=1e-4) and (slabs[:, :2] == 5.0).all()

@@ -135,3 +135,52 @@ def test_engine_long_prefill_on_pgemm_matches_oracle(gpu, monkeypatch):
         lg = rm.forward_logits(w, p + s.output_ids[:-1])
         r = rm.check_tokens(lg, len(p), s.output_ids)
         assert r["mismatches"] == 0, r
+
+
+@pytest.mark.parametrize("cfg", list(ops.PG_GRP_CFGS))
+@pytest.mark.parametrize("case", ["skewed", "sparse_ep"])
+def test_pg_grouped_vs_fp32(gpu, cfg, case):
+    """Grouped experts (MoE prefill): uneven segments (one longer than two tiles, one empty, one of a single row),
+    experts [e_lo, e_lo + E) of a global numbering (expert parallelism: rows of other ranks' experts untouched);
+    split SwiGLU of [gate; up] halves, bf16, fp32 and fp32 k-split slabs against the fp32 product."""
+    bm, bn = ops.pgemm_shape(cfg)
+    E, K = 4, 512
+    if case == "skewed":
+        counts, e_lo, pre = [2 * bm + 37, 1, 0, bm - 5], 0, 0
+    else:  # two foreign experts' rows in front of and behind the local ones
+        counts, e_lo, pre = [70, 3, bm + 9, 0, 130, 19], 1, 70
+        E = 4
+    offs = [0]
+    for c in counts:
+        offs.append(offs[-1] + c)
+    R = offs[-1]
+    offsets = torch.tensor(offs, dtype=torch.int32, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(cfg * 7 + len(case))
+    xs = (torch.rand(R, K, device=gpu, generator=g) * 2 - 1).bfloat16()
+    N = 2 * bn
+    W = ((torch.rand(E, N, K, device=gpu, generator=g) * 2 - 1) * 0.05).bfloat16()
+    Wp = torch.stack([preshuffle(W[e]) for e in range(E)])
+    ref = torch.full((R, N), float("nan"), device=gpu)
+    for e in range(E):
+        a, b = offs[e_lo + e], offs[e_lo + e + 1]
+        ref[a:b] = xs[a:b].float() @ W[e].float().t()
+    own = ~torch.isnan(ref[:, 0])
+    assert own.sum() == offs[e_lo + E] - offs[e_lo] and (pre == 0 or not own[:pre].any())
+    sentinel = -7.0
+    y = torch.full((R, N), sentinel, device=gpu)
+    ops.pg_grouped(xs, Wp, offsets, e_lo, y, ops.PG_EPI_F32, cfg)
+    _close(y[own], ref[own], atol=1e-3 * math.sqrt(K) * 0.05 + 1e-4, rtol=1e-3)
+    assert (y[~own] == sentinel).all(), "rows of foreign experts written"
+    yb = torch.full((R, N), sentinel, device=gpu, dtype=torch.bfloat16)
+    ops.pg_grouped(xs, Wp, offsets, e_lo, yb, ops.PG_EPI_BF16, cfg)
+    _close(yb[own], ref[own], atol=2e-2, rtol=8e-3)
+    ys = torch.full((2, R, N), sentinel, device=gpu)
+    ops.pg_grouped(xs, Wp, offsets, e_lo, ys, ops.PG_EPI_F32, cfg, 2)
+    _close(ys.sum(0)[own], ref[own], atol=1e-3 * math.sqrt(K) * 0.05 + 1e-4, rtol=1e-3)
+    if (bn // 32) % 2 == 0:
+        F = N // 2
+        act = torch.full((R, F), sentinel, device=gpu, dtype=torch.bfloat16)
+        ops.pg_grouped(xs, Wp, offsets, e_lo, act, ops.PG_EPI_SWIGLU_SPLIT, cfg)
+        want = torch.nn.functional.silu(ref[:, :F]) * ref[:, F:]
+        _close(act[own], want[own], atol=1.5e-2, rtol=2e-2)
+        assert (act[~own] == sentinel).all()
