@@ -4,6 +4,8 @@ MFMAs on stale slots), per tile config -- which side bounds a k-step (cdna_hip_p
 
   python bench/kernels/pgemm_probe.py --build     (CPU: compiles bench/kernels/pg_probe_*.so)
   python bench/kernels/pgemm_probe.py --tokens 768 --shape 28672 4096 --cfgs 0 1
+  python bench/kernels/pgemm_probe.py --grouped 64 128 --shape 28672 4096 --cfgs 1 10 --variants full noskip
+  (--grouped: rows per expert of 8 experts, segments 0.4x .. 2.0x the mean, weights [8, N, K])
 """
 import argparse
 import ctypes
@@ -15,7 +17,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 VARIANTS = {"full": [], "no_mfma": ["-DPG_ABLATE=1"], "no_dma": ["-DPG_ABLATE=2"], "nosplit": ["-DPG_SPLIT_ISSUE=0"],
-            "slots3": ["-DPG_MAX_SLOTS=3"]}
+            "slots3": ["-DPG_MAX_SLOTS=3"], "slots5": ["-DPG_MAX_SLOTS=5"], "slots6": ["-DPG_MAX_SLOTS=6"]}
 
 
 def build(names):
@@ -38,6 +40,7 @@ def main():
     ap.add_argument("--S", type=int, default=1, help="k splits (> 1: fp32 slabs, no in-launch reduction)")
     ap.add_argument("--rounds", type=int, default=3, help="interleaved rounds over the variants (min reported)")
     ap.add_argument("--variants", nargs="+", default=list(VARIANTS))
+    ap.add_argument("--grouped", type=int, nargs="+", default=None, metavar="ROWS")
     args = ap.parse_args()
     if args.build:
         return build(args.variants)
@@ -49,6 +52,8 @@ def main():
     libs = {v: ctypes.CDLL(os.path.join(HERE, f"pg_probe_{v}.so")) for v in args.variants}
     N, K = args.shape
     dev = torch.device("cuda")
+    if args.grouped:
+        return grouped(args, libs, N, K, dev, timeit)
     w = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).bfloat16()
     for T in args.tokens:
         x = (torch.rand(T, K, device=dev) * 2 - 1).bfloat16()
@@ -61,6 +66,34 @@ def main():
                         s = torch.cuda.current_stream().cuda_stream
                         rc = lib.pg_probe(c, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(w.data_ptr()),
                                           ctypes.c_void_p(y.data_ptr()), T, N, K, args.S, ctypes.c_void_p(s))
+                        assert rc == 0
+                    t = round(timeit(run), 1)
+                    row[v + "_us"] = min(row.get(v + "_us", 1e9), t)
+            print(json.dumps(row), flush=True)
+
+
+def grouped(args, libs, N, K, dev, timeit):
+    import torch
+
+    E = 8
+    w = ((torch.rand(E, N, K, device=dev) * 2 - 1) * 0.05).bfloat16()
+    for rows in args.grouped:
+        counts = [max(1, int(rows * f)) for f in (0.4, 2.0, 0.8, 1.2, 0.6, 1.4, 1.0, 0.6)]
+        R = sum(counts)
+        off = torch.zeros(E + 1, dtype=torch.int32)
+        off[1:] = torch.cumsum(torch.tensor(counts), 0)
+        off = off.to(dev)
+        x = (torch.rand(R, K, device=dev) * 2 - 1).bfloat16()
+        y = torch.empty(R, N, device=dev, dtype=torch.bfloat16)
+        for c in args.cfgs:
+            row = {"grouped_rows": rows, "R": R, "N": N, "K": K, "cfg": c}
+            for _ in range(args.rounds):
+                for v, lib in libs.items():
+                    def run():
+                        s = torch.cuda.current_stream().cuda_stream
+                        rc = lib.pg_probe_grouped(c, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(w.data_ptr()),
+                                                  ctypes.c_void_p(off.data_ptr()), E, ctypes.c_void_p(y.data_ptr()),
+                                                  R, N, K, ctypes.c_void_p(s))
                         assert rc == 0
                     t = round(timeit(run), 1)
                     row[v + "_us"] = min(row.get(v + "_us", 1e9), t)

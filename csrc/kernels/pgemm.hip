@@ -736,4 +736,21 @@ extern "C" int pg_probe(int cfg, const void* x, const void* w, void* y, int M, i
                reinterpret_cast<hipStream_t>(stream));
   return 0;
 }
+
+// grouped probe: experts [0, E) of W [E][N][K] over the rows of offsets[0..E] (device int32), bf16 y [R][N]
+extern "C" int pg_probe_grouped(int cfg, const void* x, const void* w, const void* offsets, int E, void* y, int R, int N,
+                                int K, void* stream) {
+  int bm = 0, bn = 0;
+  if (!pgemm_cfg_shape(cfg, &bm, &bn) || N % bn || K % 64) return -1;
+  DecodeEpi e;
+  e.wshuf = 1;
+  e.out_bf = reinterpret_cast<bf16*>(y);
+  PgGroup g;
+  g.offsets = reinterpret_cast<const int*>(offsets);
+  g.E = E;
+  g.wstride = (long long)N * K;
+  launch_pgemm_grouped(DECODE_EPI_BF16, cfg, reinterpret_cast<const bf16*>(x), reinterpret_cast<const bf16*>(w), R, N,
+                       K, 1, g, e, nullptr, reinterpret_cast<hipStream_t>(stream));
+  return 0;
+}
 #endif

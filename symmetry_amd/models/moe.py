@@ -53,7 +53,8 @@ STREAM_DECODE_ROWS = int(os.environ.get("SYMMETRY_MOE_STREAM_DECODE_ROWS", "4"))
 # "auto": expert all-to-all from this many tokens (prefill); decode steps (<= 64 rows under MoE) all-reduce
 A2A_ROWS = int(os.environ.get("SYMMETRY_MOE_A2A_ROWS", "128"))
 GROUPED = os.environ.get("SYMMETRY_MOE_GROUPED", "1") != "0"  # A/B: 0 = per-expert library GEMMs (host sync)
-# count the all-to-all bytes this rank pushes (reads the device counts: a host sync per layer -- tests / benches)
+# count the bytes this rank's MoE collectives push (device-side counts are summed lazily: ``a2a_stats()`` syncs
+# once per call -- tests / benches read it once per step)
 A2A_STATS = os.environ.get("SYMMETRY_MOE_A2A_STATS", "0") == "1"
 # decode steps: routing in one launch and the combine fused with the residual prep (A/B: 0 = five routing launches
 # + combine + add_prep; profiles/r4/moe_decode_fused.jsonl)
@@ -77,7 +78,9 @@ class MoEBlock:
         self.mode = mode or os.environ.get("SYMMETRY_MOE_MODE", "auto")
         self.F = cfg.intermediate_size
         self.calls = {"allreduce": 0, "a2a": 0}
-        self.a2a_bytes = {"dispatch": 0, "return": 0, "routed_rows": 0, "padded_dispatch": 0, "gather": 0}
+        self.a2a_bytes = {"dispatch": 0, "return": 0, "routed_rows": 0, "padded_dispatch": 0, "gather": 0,
+                          "allreduce": 0}
+        self._pending = []  # (key, device int64 scalar) byte / row counts not yet read back
         # router rows padded to a multiple of 16 for the skinny GEMM (padded logits are never read)
         self.router = {}
         self.single_copy = False  # adopt_single_copy: the expert tensors themselves are preshuffled
@@ -156,6 +159,51 @@ class MoEBlock:
                 keys.append(key)
         self.single_copy = True
         return keys
+
+    def _stat(self, key: str, v) -> None:
+        """Add ``v`` (an int, or a device scalar: no sync here) to a2a_bytes[key] when A2A_STATS is on."""
+        if A2A_STATS:
+            if isinstance(v, torch.Tensor):
+                self._pending.append((key, v.to(torch.int64)))
+            else:
+                self.a2a_bytes[key] += int(v)
+
+    def a2a_stats(self) -> dict:
+        """The byte / row counters with every pending device count read back in ONE transfer."""
+        if self._pending:
+            keys = [k for k, _ in self._pending]
+            vals = torch.stack([v.reshape(()) for _, v in self._pending]).tolist()
+            for k, v in zip(keys, vals):
+                self.a2a_bytes[k] += int(v)
+            self._pending = []
+        return dict(self.a2a_bytes)
+
+    @staticmethod
+    def _block_rows(counts, cap: int, dev) -> torch.Tensor:
+        """Row indices of the first counts[q] rows of every cap-row block q."""
+        idx = [torch.arange(q * cap, q * cap + int(c)) for q, c in enumerate(counts) if c]
+        return (torch.cat(idx) if idx else torch.zeros(0, dtype=torch.int64)).to(dev)
+
+    def _exchange_counted(self, send: torch.Tensor, counts, recv_counts, cap: int, fill=None) -> torch.Tensor:
+        """All-to-all of block-laid-out rows on RCCL / gloo with the real counts as splits (all_to_all_single):
+        block q of ``send`` ([N * cap, ...]) holds counts[q] real rows for rank q; the result has block s = the
+        recv_counts[s] rows rank s sent here, the rest ``fill`` (or unset).  Only real rows cross the links."""
+        N, dev = self.ep, send.device
+        payload = send.index_select(0, self._block_rows(counts, cap, dev))
+        got = self.comm.all_to_all_rows(payload, list(counts), list(recv_counts))
+        shape = (N * cap,) + tuple(send.shape[1:])
+        recv = torch.empty(shape, dtype=send.dtype, device=dev) if fill is None else \
+            torch.full(shape, fill, dtype=send.dtype, device=dev)
+        recv.index_copy_(0, self._block_rows(recv_counts, cap, dev), got)
+        return recv
+
+    def _counts_exchange(self, cursor: torch.Tensor):
+        """(send counts, receive counts) as host lists: the per-peer counts all-to-all (one int each) + ONE
+        readback -- the split sizes all_to_all_single needs."""
+        N = self.ep
+        rc = self.comm.all_to_all_rows(cursor.view(N, 1).contiguous(), [1] * N, [1] * N).view(N)
+        both = torch.cat([cursor.view(N).to(rc.device), rc]).tolist()
+        return [int(v) for v in both[:N]], [int(v) for v in both[N:]]
 
     def _buf(self, name, shape, dtype):
         return self.m._buf("moe." + name, shape, dtype)
@@ -332,7 +380,16 @@ class MoEBlock:
         ops.moe_combine(y2, dst, ids, self.e_lo, self.e_hi, w, self.k, out)
         if reduce:
             self.comm.all_reduce(out)
+            self._stat("allreduce", self.allreduce_bytes(T, d))
         return out
+
+    def allreduce_bytes(self, T: int, d: int) -> int:
+        """Bytes one rank pushes for the fp32 [T, d] all-reduce combine: the one-shot xGMI kernel writes its
+        partial into every peer ((N - 1) T d 4, decode sizes), a ring all-reduce 2 (N - 1) / N T d 4."""
+        N = self.ep
+        if T * d * 4 <= getattr(self.comm, "oneshot_bytes", 0):
+            return (N - 1) * T * d * 4
+        return 2 * (N - 1) * T * d * 4 // N
 
     # ------------------------------------------------------------------------------------------
     def forward_a2a(self, i: int, x: torch.Tensor) -> torch.Tensor:
@@ -356,30 +413,30 @@ class MoEBlock:
         cursor = self._buf("own.cursor", (N,), torch.int32)
         xg = getattr(self.comm, "a2a_fits", None)
         xg = xg is not None and xg(cap, d * 4)
-        if not xg:
-            side.fill_(-1)  # whole blocks move: slots past each owner's count must read "empty"
         ops.moe_owner_pack(y, dst, ids, w, self.e_lo, self.e_hi, k, S, cursor, send, side)
         if xg:
             recv = self._buf("own.recv", (N * cap, d), torch.float32)
             rside = self._buf("own.rside", (N * cap,), torch.int32)
             rcnt = self._buf("own.rcnt", (N,), torch.int32)
             self.comm.a2a_rows(send, cursor, side, recv, rside, rcnt)
-            if A2A_STATS:
-                sent = int(cursor.sum()) - int(cursor[r])  # rows that left this GPU
-                self.a2a_bytes["return"] += sent * d * 4
-                self.a2a_bytes["routed_rows"] += int(cursor.sum())
+            self._stat("return", (cursor.sum() - cursor[r]) * (d * 4))  # rows that left this GPU (device count)
+            self._stat("routed_rows", cursor.sum())
         else:
-            splits = [cap] * N
-            recv = self.comm.all_to_all_rows(send, splits, splits)
-            rside = self.comm.all_to_all_rows(side.view(-1, 1), splits, splits).view(-1)
-            rcnt = self._buf("own.rcnt_full", (N,), torch.int32)
-            rcnt.fill_(cap)
+            # RCCL / gloo: the per-owner counts first, then all_to_all_single with them as splits (the side ints
+            # ride as one extra fp32 column): only the real rows move
+            sc, rc = self._counts_exchange(cursor)
+            packed = torch.cat([send, side.view(-1, 1).view(torch.float32)], 1)
+            got = self._exchange_counted(packed, sc, rc, cap)
+            recv = got[:, :d].contiguous()
+            rside = got[:, d:].contiguous().view(torch.int32).view(-1)
+            rcnt = torch.tensor(rc, dtype=torch.int32, device=x.device)
+            self._stat("return", (sum(sc) - sc[r]) * (d * 4 + 4))
+            self._stat("routed_rows", sum(sc))
         pos = self._buf("own.pos", (N * S,), torch.int32)
         mine = self._buf("own.slice", (S, d), torch.bfloat16)
         ops.moe_owner_combine(recv, rside, rcnt, hi - lo, pos, mine)
         g = self.comm.all_gather(mine)  # [N * S, d] bf16
-        if A2A_STATS:
-            self.a2a_bytes["gather"] += (N - 1) * S * d * 2
+        self._stat("gather", (N - 1) * S * d * 2)
         return g[:T]
 
     def forward_tokens(self, i: int, x: torch.Tensor, S: int) -> torch.Tensor:
@@ -398,12 +455,10 @@ class MoEBlock:
         send_e = self._buf("a2a.send_e", (N * cap, 1), torch.int32)
         cursor = self._buf("a2a.cursor", (N,), torch.int32)  # after moe_scatter: routed rows per owner
         cursor.zero_()
-        # xGMI path: only the routed rows cross the links (counts stay on the device); else RCCL moves whole
-        # capacity blocks with -1 marking the empty slots
+        # only the routed rows cross the links: on xGMI with the counts on the device, on RCCL / gloo with the
+        # counts exchanged first and used as all_to_all_single splits (slots past a count read "empty", -1)
         xg = getattr(self.comm, "a2a_fits", None)
         xg = xg is not None and xg(cap, d * 4)
-        if not xg:
-            send_e.fill_(-1)
         if Tr > 0:
             logits = self.m._linear("router", x, self.router[i])
             ops.moe_route(logits, Tr, k, E, ids, w)
@@ -413,15 +468,23 @@ class MoEBlock:
             ops.moe_scatter(x, owner, k, N, blocks, cursor, send, dst)
             send_e.view(-1).index_copy_(0, dst[:R].long(), ids[:R])
         # ---- dispatch: block q of every rank's send buffer goes to rank q
-        splits = [cap] * N
         if xg:
             recv = self._buf("a2a.recv", (N * cap, d), torch.bfloat16)
             recv_e = self._buf("a2a.recv_e", (N * cap,), torch.int32)
             rcnt = self._buf("a2a.rcnt", (N,), torch.int32)
             self.comm.a2a_rows(send, cursor, send_e.view(-1), recv, recv_e, rcnt)
         else:
-            recv = self.comm.all_to_all_rows(send, splits, splits)            # [N * cap, d]  (src-major)
-            recv_e = self.comm.all_to_all_rows(send_e, splits, splits).view(-1)  # expert id per slot, -1 = empty
+            sc, rc = self._counts_exchange(cursor)
+            # the expert id rides as two bf16 columns of the row; empty slots decode as -1
+            packed = torch.cat([send, send_e.view(torch.bfloat16)], 1)
+            fill_row = torch.cat([torch.zeros(d, dtype=torch.bfloat16),
+                                  torch.tensor([-1], dtype=torch.int32).view(torch.bfloat16)])
+            got = self._exchange_counted(packed, sc, rc, cap)
+            empty = torch.ones(N * cap, dtype=torch.bool, device=dev)
+            empty[self._block_rows(rc, cap, dev)] = False
+            got[empty] = fill_row.to(dev)
+            recv = got[:, :d].contiguous()                                      # [N * cap, d]  (src-major)
+            recv_e = got[:, d:].contiguous().view(torch.int32).view(-1)         # expert id per slot, -1 = empty
         # ---- group the received rows by local expert, run the grouped GEMMs
         counts = self._buf("a2a.counts", (E,), torch.int32)
         offsets = self._buf("a2a.offsets", (E + 1,), torch.int32)
@@ -443,14 +506,16 @@ class MoEBlock:
         if xg:  # the return is the transpose: block s of `back` holds rcnt[s] real rows for rank s
             ret = self._buf("a2a.ret", (N * cap, d), torch.float32)
             self.comm.a2a_rows(back, rcnt, None, ret)
-            if A2A_STATS:
-                sent, got = int(cursor.sum()), int(rcnt.sum())
-                self.a2a_bytes["dispatch"] += sent * d * 2
-                self.a2a_bytes["return"] += got * d * 4
-                self.a2a_bytes["routed_rows"] += R
-                self.a2a_bytes["padded_dispatch"] += N * cap * d * 2
+            r = self.ep_rank  # rows a rank keeps never cross a link
+            self._stat("dispatch", (cursor.sum() - cursor[r]) * (d * 2))
+            self._stat("return", (rcnt.sum() - rcnt[r]) * (d * 4))
         else:
-            ret = self.comm.all_to_all_rows(back, splits, splits)             # [N * cap, d]: my slots' results
+            ret = self._exchange_counted(back, rc, sc, cap)                    # [N * cap, d]: my slots' results
+            r = self.ep_rank
+            self._stat("dispatch", (sum(sc) - sc[r]) * (d * 2 + 4))
+            self._stat("return", (sum(rc) - rc[r]) * (d * 4))
+        self._stat("routed_rows", R)
+        self._stat("padded_dispatch", N * cap * d * 2)
         out = self._buf("a2a.out", (max(Tr, 1), d), torch.float32)[:Tr]
         if Tr > 0:
             ops.moe_combine(ret, dst, ids, 0, E, w, k, out)

@@ -325,6 +325,35 @@ def _ep_worker(rank, world, model="tiny-mixtral"):
         outs[name] = got.dtype == torch.bfloat16 and bool(
             ((got.float() - ref_r).abs() <= 1e-5 + ref_r.abs() * 2.0 ** -8).all())
         outs[name + "_err"] = float((got.float() - ref_r).abs().max())
+    # bytes per rank of the owner exchange on gloo (counts exchanged, then all_to_all_single with them as splits):
+    # exactly one fp32 row (+ its int side word) per token that has a local expert and another owner, the bf16
+    # all-gather of the owners' slices -- against the fp32 all-reduce combine and the old whole-block exchange
+    import symmetry_amd.models.moe as moe_mod
+
+    moe = ep_model.moe
+    T, d, k = x_long.shape[0], cfg.hidden_size, cfg.top_k
+    S = -(-T // world)
+    ids = moe._route(1, x_long)[0][: T * k].view(T, k)
+    local = ((ids >= moe.e_lo) & (ids < moe.e_hi)).any(1)
+    leaving = sum(1 for t in range(T) if local[t] and t // S != rank)
+    moe_mod.A2A_STATS = True
+    try:
+        moe._pending, moe.a2a_bytes = [], {key: 0 for key in moe.a2a_bytes}
+        moe.forward(1, x_long)
+        b = moe.a2a_stats()
+        outs["a2a_bytes_exact"] = (b["return"] == leaving * (d * 4 + 4) and b["gather"] == (world - 1) * S * d * 2
+                                   and b["dispatch"] == 0)
+        outs["a2a_bytes_vs_padded"] = b["return"] <= (world - 1) * S * (d * 4 + 4)
+        moe.mode = "allreduce"
+        moe._pending, moe.a2a_bytes = [], {key: 0 for key in moe.a2a_bytes}
+        moe.forward(1, x_long)
+        ar = moe.a2a_stats()["allreduce"]
+        outs["allreduce_bytes_exact"] = ar == 2 * (world - 1) * T * d * 4 // world
+        outs["a2a_fewer_bytes"] = b["return"] + b["gather"] < ar
+        outs["bytes"] = {"a2a": b["return"] + b["gather"], "allreduce": ar, "leaving_rows": leaving}
+        moe.mode = "a2a"
+    finally:
+        moe_mod.A2A_STATS = False
     # expert all-to-all with DIFFERENT tokens per rank (data-parallel attention in front of EP)
     ref_t = ref_model.moe.forward(1, x_all[rank]).clone()
     got_t = ep_model.moe.forward_tokens(1, x_all[rank], 6)
@@ -342,7 +371,7 @@ def _ep8_worker(rank, world):
 def test_expert_parallel_modes_match_local_moe(world):
     res = _run(_ep_worker, world=world)
     for _, r in res:
-        assert all(v for k, v in r.items() if not k.endswith("_err")), str(r)
+        assert all(v for k, v in r.items() if not k.endswith("_err") and k != "bytes"), str(r)
 
 
 def test_expert_parallel_a2a_world8():
@@ -350,7 +379,7 @@ def test_expert_parallel_a2a_world8():
     return exchange of different tokens per rank."""
     res = _run(_ep8_worker, world=8)
     for _, r in res:
-        assert all(v for k, v in r.items() if not k.endswith("_err")), str(r)
+        assert all(v for k, v in r.items() if not k.endswith("_err") and k != "bytes"), str(r)
 
 
 def _capture_worker(rank, world):

@@ -75,7 +75,7 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False):
         extra = {}
         moe = eng.runner.model.moe
         if moe is not None:
-            extra = {"moe_calls": dict(moe.calls), "a2a_bytes": dict(moe.a2a_bytes),
+            extra = {"moe_calls": dict(moe.calls), "a2a_bytes": moe.a2a_stats(),
                      "xgmi_a2a": eng.runner.model.tp.calls.get("a2a", 0) if xgmi == "1" else 0}
         q.put((rank, ([s.output_ids for s in seqs], extra)))
     except Exception:
