@@ -11,10 +11,10 @@ the gate/up epilogue everywhere.
 Expert parallelism, ``ep_size = N`` ranks each owning ``E / N`` experts (attention is tensor-parallel, so
 every rank holds the same T tokens when the block starts):
 
-* all-reduce combine (``mode="allreduce"``, and ``"auto"`` below ``A2A_ROWS`` rows -- decode steps): each
+* all-reduce combine (``mode="allreduce"``, and ``"auto"`` below ``A2A_ROWS`` rows -- the default): each
   rank applies its own experts to all routed rows and one all-reduce sums the partial outputs (on the
   one-shot xGMI kernel at decode sizes);
-* owner exchange (``mode="a2a"``, and ``"auto"`` from ``A2A_ROWS`` rows -- prefill; :meth:`forward_a2a`):
+* owner exchange (``mode="a2a"``, and ``"auto"`` from ``A2A_ROWS`` rows -- opt-in; :meth:`forward_a2a`):
   no dispatch leg (every rank already holds the tokens) -- every rank routes all T tokens and runs its own
   experts on its own routed rows; per token with a local expert ONE fp32 row (the weighted partial over those
   experts) goes to the token's slice owner (``XgmiComm.a2a_rows``: only counted rows cross the links, counts
@@ -50,8 +50,13 @@ PG_ROWS_W13 = int(os.environ.get("SYMMETRY_MOE_PG_ROWS_W13", "100"))
 PG_ROWS_W2 = int(os.environ.get("SYMMETRY_MOE_PG_ROWS_W2", "72"))
 # decode steps stream the preshuffled copies from this many routed rows per local expert (every expert routed)
 STREAM_DECODE_ROWS = int(os.environ.get("SYMMETRY_MOE_STREAM_DECODE_ROWS", "4"))
-# "auto": expert all-to-all from this many tokens (prefill); decode steps (<= 64 rows under MoE) all-reduce
-A2A_ROWS = int(os.environ.get("SYMMETRY_MOE_A2A_ROWS", "128"))
+# "auto": the owner exchange (forward_a2a) from this many tokens, the fp32 all-reduce combine below.  Off by default:
+# the one-GPU rehearsal (bench/ep_rehearsal.py, profiles/r6/ep_crossover.jsonl) found no crossover up to 1024 tokens
+# at 2 and 4 ranks -- the exchange moves 35-51 % fewer bytes per rank (world 4, 1024 tokens: 12.2 vs 25.2 MB per
+# layer) but costs three collectives and a counts readback per layer against one all-reduce (TTFT 1016 vs 299 ms at
+# world 2 on the shared GPU's host-staged transport); a node with one GPU per rank and the peer-memory exchange
+# kernel is the measurement that could set it lower (SYMMETRY_MOE_A2A_ROWS / SYMMETRY_MOE_MODE=a2a)
+A2A_ROWS = int(os.environ.get("SYMMETRY_MOE_A2A_ROWS", str(1 << 30)))
 GROUPED = os.environ.get("SYMMETRY_MOE_GROUPED", "1") != "0"  # A/B: 0 = per-expert library GEMMs (host sync)
 # count the bytes this rank's MoE collectives push (device-side counts are summed lazily: ``a2a_stats()`` syncs
 # once per call -- tests / benches read it once per step)

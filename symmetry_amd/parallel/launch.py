@@ -186,9 +186,14 @@ def init_tp_engine(ecfg):
         if not mcfg.is_moe:
             ks.add(mcfg.intermediate_size // world)
         _attach_xar_checked(comm, cpu_group, mcfg.hidden_size, ks=tuple(sorted(k for k in ks if k % 256 == 0)) or (256,))
-    if ep_comm is not None and isinstance(comm, XgmiComm) and os.environ.get("SYMMETRY_MOE_XGMI_A2A", "1") != "0":
+    a2a = os.environ.get("SYMMETRY_MOE_XGMI_A2A", "1")
+    if ep_comm is not None and isinstance(comm, XgmiComm) and a2a != "0" and (
+            torch.cuda.device_count() >= world or a2a == "force"):
         # the unpadded expert all-to-all (prefill: expert results pushed to the token-slice owners) on its own
-        # peer buffers, sized by the largest prefill step
+        # peer buffers, sized by the largest prefill step.  Not when ranks share a GPU (the one-GPU rehearsal,
+        # bench/ep_rehearsal.py): a rank's spinning exchange grid holds CUs its peers need to arrive -- at 4 ranks
+        # a 256-token Mixtral step hit the wait limit (profiles/r6/ep_crossover.jsonl); the counted RCCL / gloo
+        # exchange runs instead (SYMMETRY_MOE_XGMI_A2A=force: tests whose grids are small enough)
         _attach_a2a_checked(comm, cpu_group, ecfg.max_num_batched_tokens, mcfg, world)
     engine = LLMEngine(ecfg, tp_comm=comm, ep_comm=ep_comm, cpu_group=cpu_group)
     if rank == 0 and world > 1:

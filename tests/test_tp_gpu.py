@@ -27,7 +27,7 @@ def _port():
     return p
 
 
-def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False):
+def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False, moe_mode="auto"):
     import traceback
 
     prompts = prompts or PROMPTS
@@ -35,7 +35,7 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False):
                       LOCAL_RANK="0", SYMMETRY_TP_COMM="gloo", SYMMETRY_XGMI=xgmi, SYMMETRY_MOE_A2A_STATS="1",
                       # the fused GEMM + all-reduce launches between the two processes: the small test models' grids
                       # (<= 64 workgroups per rank) are co-resident on the one GPU
-                      SYMMETRY_XGMI_FUSED="force",
+                      SYMMETRY_XGMI_FUSED="force", SYMMETRY_MOE_XGMI_A2A="force", SYMMETRY_MOE_MODE=moe_mode,
                       # graphs: decode steps captured and replayed with every collective on the xGMI kernels
                       SYMMETRY_XGMI_GRAPHS="1" if graphs else "0")
     try:
@@ -87,13 +87,13 @@ def _entry(model, rank, world, port, q, xgmi="0", prompts=None, graphs=False):
             dist.destroy_process_group()
 
 
-def _run(model, world=2, xgmi="0", prompts=None, extra=False, graphs=False):
+def _run(model, world=2, xgmi="0", prompts=None, extra=False, graphs=False, moe_mode="auto"):
     import torch.multiprocessing as mp
 
     port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    procs = [ctx.Process(target=_entry, args=(model, r, world, port, q, xgmi, prompts, graphs))
+    procs = [ctx.Process(target=_entry, args=(model, r, world, port, q, xgmi, prompts, graphs, moe_mode))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -133,12 +133,12 @@ LONG_PROMPTS = [list(range(300, 420)), list(range(400, 490)), list(range(7, 40))
 
 
 def test_tp2_mixtral_unpadded_a2a_on_one_gpu(gpu):
-    """tiny-mixtral attention TP=2 + EP=2 with a 243-token prefill step (>= A2A_ROWS): the replicated-token owner
+    """tiny-mixtral attention TP=2 + EP=2 with a 243-token prefill step (SYMMETRY_MOE_MODE=a2a): the replicated-token owner
     exchange (models/moe.py forward_a2a) on the xGMI a2a kernel between the two processes (IPC-mapped buffers on
     one GPU) -- no dispatch leg, at most one pre-combined fp32 row per token leaves a rank, the slices come back
     by a bf16 all-gather -- fewer bytes than the fp32 all-reduce combine, and every token agrees with the fp32
     oracle."""
-    outs, extra = _run("tiny-mixtral", xgmi="1", prompts=LONG_PROMPTS, extra=True)
+    outs, extra = _run("tiny-mixtral", xgmi="1", prompts=LONG_PROMPTS, extra=True, moe_mode="a2a")
     assert extra["moe_calls"]["a2a"] > 0 and extra["xgmi_a2a"] > 0, extra
     b = extra["a2a_bytes"]
     from symmetry_amd.models.config import resolve
