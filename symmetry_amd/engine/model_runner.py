@@ -44,9 +44,13 @@ HEADER_LEN = 7  # kind, T, rows, max_blocks, prefill tiles, real seqs, filtered-
 # Captured at start-up only (capture_all: every token bucket x one sequence x every context bucket): a bucket
 # captured lazily in serving cost its first request ~14 ms of TTFT (multi-turn turn 2: 6.7 -> 21 ms,
 # profiles/r4/multiturn_prefill_graph_ab.jsonl); a step whose bucket was not captured runs eagerly.
-PREFILL_GRAPH_BUCKETS = (16, 32, 64, 128, 192, 256)
-PREFILL_GRAPH_SEQS = (1, 2, 4)  # padding buckets of the sequence count
-PREFILL_CAPTURE_SEQS = (1,)     # the ones captured at start-up
+def _ints(name: str, default: str) -> tuple:
+    return tuple(int(v) for v in os.environ.get(name, default).split(",") if v.strip())
+
+
+PREFILL_GRAPH_BUCKETS = _ints("SYMMETRY_PREFILL_GRAPH_BUCKETS", "16,32,64,128,192,256")
+PREFILL_GRAPH_SEQS = _ints("SYMMETRY_PREFILL_GRAPH_SEQS", "1,2,4")  # padding buckets of the sequence count
+PREFILL_CAPTURE_SEQS = _ints("SYMMETRY_PREFILL_CAPTURE_SEQS", "1")  # the ones captured at start-up
 PREFILL_GRAPH_TOKENS = int(os.environ.get("SYMMETRY_PREFILL_GRAPH_TOKENS", "256"))
 _PAD_TILE_ROW = 1 << 24  # query row of a padding attention tile: past every qlen, so its workgroups exit
 _SEED_MIX = 0x9E3779B97F4A7C15
