@@ -654,7 +654,7 @@ void grouped_gemm(const Tensor& xs, const Tensor& W, const Tensor& offsets, int6
 // Dense medium-M projection on the weight-streaming kernel: mode 1 -> fp32 slabs y [S, M, N]; mode 3 -> SwiGLU of
 // the decode layout's tile-interleaved gate/up rows, y = act bf16 [M, N / 2].  W MFMA-preshuffled [N, K].
 
-void grouped_skinny(const Tensor& xs, const Tensor& W, const Tensor& offsets, int64_t e0, Tensor& y) {
+void grouped_skinny(const Tensor& xs, const Tensor& W, const Tensor& offsets, int64_t e0, Tensor& y, bool wshuf) {
   check_gpu(xs, "xs");
   check_gpu(W, "W");
   check_gpu(offsets, "offsets");
@@ -670,8 +670,9 @@ void grouped_skinny(const Tensor& xs, const Tensor& W, const Tensor& offsets, in
   TORCH_CHECK(N % 16 == 0 && K % (256 * S) == 0, "grouped_skinny: N % 16 and K % (256 S)");
   TORCH_CHECK(R <= 64, "grouped_skinny: at most 64 routed rows on this path (larger batches use library GEMMs)");
   const at::OptionalDeviceGuard g(xs.device());
+  TORCH_CHECK(!wshuf || K % 32 == 0, "grouped_skinny: preshuffled weights need K % 32");
   launch_grouped_skinny(ptr<bf16>(xs), ptr<bf16>(W), ptr<int>(offsets), ptr<float>(y), (int)R, (int)E, (int)e0,
-                        (int)N, (int)K, (int)S, cur_stream(xs));
+                        (int)N, (int)K, (int)S, cur_stream(xs), wshuf);
 }
 
 void moe_combine(const Tensor& y, const Tensor& dst, const Tensor& ids, int64_t e_lo, int64_t e_hi, const Tensor& w,
@@ -1240,7 +1241,8 @@ TORCH_LIBRARY(symmetry_amd, m) {
   m.def("decode_gemm_variant(int v) -> ()", [](int64_t v) { set_decode_gemm_variant((int)v); });
   m.def("decode_ksplit(int on) -> ()", [](int64_t on) { set_decode_ksplit((int)on); });
   m.def("decode_gemm_nt(int on) -> ()", [](int64_t on) { set_decode_gemm_nt((int)on); });
-  m.def("grouped_skinny(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y) -> ()", &grouped_skinny);
+  m.def("grouped_skinny(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y, bool wshuf=False) -> ()",
+        &grouped_skinny);
   m.def("grouped_gemm(Tensor xs, Tensor W, Tensor offsets, int e0, Tensor(a!) y, int mode) -> ()", &grouped_gemm);
   m.def("grouped_stream_policy(int p) -> ()", [](int64_t p) { set_grouped_stream_policy((int)p); });
   m.def("moe_route(Tensor logits, int T, int k, int E, Tensor(a!) ids, Tensor(b!) w) -> ()", &moe_route);

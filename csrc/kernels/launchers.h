@@ -205,7 +205,7 @@ void launch_grouped_gemm(const bf16* xs, const bf16* W, const int* offsets, void
 // 2 always; + 10 x (2 | 4): weight tiles per wave
 void set_grouped_stream_policy(int p);
 void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, float* y, int R, int E, int e0, int N,
-                           int K, int S, hipStream_t s);
+                           int K, int S, hipStream_t s, bool wshuf = false);
 void launch_moe_combine(LinOut y, int R, const int* dst, const int* ids, int e_lo, int e_hi, const float* w, int T, int k,
                         int d, float* out, int accumulate, hipStream_t s);
 // decode (T <= 8, E <= 64, k <= 8, d <= 4096, d % 8 == 0): rms_norm + router + route + align + scatter as one launch

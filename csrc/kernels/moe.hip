@@ -123,6 +123,10 @@ __global__ __launch_bounds__(256) void moe_scatter_kernel(const bf16* __restrict
 // Grouped skinny GEMM: grid (N/16, E, S).  W [E][N][K] holds experts e0 .. e0+E-1 of the global
 // numbering; rows of expert e: [off[e0+e], off[e0+e+1]) (absolute rows of xs / y).
 // Up to 64 rows per expert (4 MFMA column tiles); the prefill path uses library GEMMs instead.
+// wshuf: W MFMA-preshuffled per expert (models/layout.py): a lane's 16 B of k-block kb of its 16-row tile sit at
+// lane * 16 B of that 1 KB block -- the same (row r16, k group h) fragment as the row-major read, one contiguous
+// 1 KB per wave instruction (decode_weights="replace": the expert stacks exist only in this layout).
+template <bool WSHUF>
 __global__ __launch_bounds__(256) void grouped_skinny_kernel(const bf16* __restrict__ xs, const bf16* __restrict__ W,
                                                              const int* __restrict__ offsets, float* __restrict__ y,
                                                              int R, int N, int K, int kchunk, int e0) {
@@ -136,7 +140,8 @@ __global__ __launch_bounds__(256) void grouped_skinny_kernel(const bf16* __restr
   const int wk = kchunk / 4;
   const int kbeg = split * kchunk + wid * wk;
   const int nblk = wk / 64;
-  const bf16* wrow = W + ((long long)e * N + n0 + r16) * K + kbeg + 8 * h;
+  const bf16* wrow = WSHUF ? W + (((long long)e * (N / 16) + tile) * (K / 32) + kbeg / 32) * 512 + lane * 8
+                          : W + ((long long)e * N + n0 + r16) * K + kbeg + 8 * h;
   const int MT = min(4, (n_e + 15) / 16);
   const bf16* xrow[4];
 #pragma unroll
@@ -150,8 +155,13 @@ __global__ __launch_bounds__(256) void grouped_skinny_kernel(const bf16* __restr
   for (int b = 0; b < nblk; ++b) {
     const int ko = b * 64;
     Pack8 w0, w1;
-    w0.u = *reinterpret_cast<const uint4*>(wrow + ko);
-    w1.u = *reinterpret_cast<const uint4*>(wrow + ko + 32);
+    if constexpr (WSHUF) {  // k-blocks (kbeg + ko) / 32 and the next one: 1 KB apart
+      w0.u = *reinterpret_cast<const uint4*>(wrow + ko * 16);
+      w1.u = *reinterpret_cast<const uint4*>(wrow + ko * 16 + 512);
+    } else {
+      w0.u = *reinterpret_cast<const uint4*>(wrow + ko);
+      w1.u = *reinterpret_cast<const uint4*>(wrow + ko + 32);
+    }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       if (mt < MT) {
@@ -1061,10 +1071,11 @@ void launch_moe_scatter(const bf16* x, int T, int d, int k, int E, const int* id
 }
 
 void launch_grouped_skinny(const bf16* xs, const bf16* W, const int* offsets, float* y, int R, int E, int e0, int N,
-                           int K, int S, hipStream_t s) {
+                           int K, int S, hipStream_t s, bool wshuf) {
   if (R == 0) return;
   dim3 grid(N / 16, E, S);
-  grouped_skinny_kernel<<<grid, 256, 0, s>>>(xs, W, offsets, y, R, N, K, K / S, e0);
+  if (wshuf) grouped_skinny_kernel<true><<<grid, 256, 0, s>>>(xs, W, offsets, y, R, N, K, K / S, e0);
+  else grouped_skinny_kernel<false><<<grid, 256, 0, s>>>(xs, W, offsets, y, R, N, K, K / S, e0);
 }
 
 void set_grouped_stream_policy(int p) {

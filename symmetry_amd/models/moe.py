@@ -111,8 +111,8 @@ class MoEBlock:
         (transformer.copy_budget; Mixtral on one GPU at 64 seqs x 8K: both copies, 90 GB)."""
         mode = os.environ.get("SYMMETRY_MOE_PRESHUFFLE", "auto")
         dev = model.device
-        if mode == "0" or dev.type != "cuda" or not GROUPED:
-            return {}
+        if mode == "0" or dev.type != "cuda" or not GROUPED or getattr(model, "plan_single_copy", False):
+            return {}  # (single copy: adopt_single_copy preshuffles the stacks in place instead)
         cfg = model.cfg
         from .transformer import copy_budget
 
@@ -138,11 +138,6 @@ class MoEBlock:
         cfg = self.m.cfg
         d, F = cfg.hidden_size, self.F
         return GROUPED and self.E_local <= 8 and d % 256 == 0 and F % 256 == 0 and F % 64 == 0 and d % 128 == 0
-
-    def all_copies(self) -> bool:
-        """Every layer has both preshuffled expert copies (the budget allowed them)."""
-        L = self.m.cfg.num_layers
-        return all((i, n) in self.pre for i in range(L) for n in ("w13", "w2"))
 
     def adopt_single_copy(self) -> list:
         """decode_weights="replace": the expert weights exist ONLY preshuffled (per expert, models/layout.py) -- an
@@ -297,8 +292,7 @@ class MoEBlock:
         w2 = self.m.w.layer(i, "w2")
         F = self.F
         act = self._buf("act", (R, F), torch.bfloat16)
-        if R <= SKINNY_ROWS and (self.single_copy or (STREAM_DECODE_ROWS * n_local <= R and (
-                (i, "w13") in self.pre or (i, "w2") in self.pre))):
+        if STREAM_DECODE_ROWS * n_local <= R <= SKINNY_ROWS and ((i, "w13") in self.pre or (i, "w2") in self.pre):
             # decode sizes on the preshuffled copies: the weight-streaming kernel (1 KB fragment loads, one unit per
             # populated expert and n-block) beats the grouped skinny GEMM at 1-8 rows per expert when every expert
             # is routed: w13 + SwiGLU 320 -> 299 us, w2 162 -> 144 (profiles/r5/grouped_stream.jsonl); with a few
@@ -321,14 +315,14 @@ class MoEBlock:
             y2 = self._buf("y2", (s2, R, d), torch.float32)
             ops.grouped_skinny(act, w2, offsets, e_lo, y2)
             return y2
-        if R <= SKINNY_ROWS:
+        if R <= SKINNY_ROWS:  # (single copy: the skinny GEMM reads the preshuffled expert stacks)
             s1 = ops.choose_splits(2 * F, d)
             y1 = self._buf("y1", (s1, R, 2 * F), torch.float32)
-            ops.grouped_skinny(xs, w13, offsets, e_lo, y1)
+            ops.grouped_skinny(xs, w13, offsets, e_lo, y1, wshuf=self.single_copy)
             ops.swiglu(y1, act)
             s2 = ops.choose_splits(d, F)
             y2 = self._buf("y2", (s2, R, d), torch.float32)
-            ops.grouped_skinny(act, w2, offsets, e_lo, y2)
+            ops.grouped_skinny(act, w2, offsets, e_lo, y2, wshuf=self.single_copy)
             return y2
         if self._grouped_ok(d):
             # prefill-sized.  From PG_ROWS_* mean routed rows per local expert: the prefill GEMM kernel in grouped mode

@@ -185,6 +185,11 @@ class TransformerLM:
         # HBM the KV cache needs (admission limit x context): the optional layout copies never eat into it
         self.kv_reserve = int(kv_reserve_bytes)
         self.moe = None
+        # MoE models default to ONE preshuffled copy of every weight: the expert stacks are read only by kernels
+        # that take that layout (measured equal to the two-copy layout end to end, 90 GB less on one GPU:
+        # profiles/r6/e2e_mixtral_c5_single_copy.jsonl), so MoEBlock makes no separate copies
+        self.plan_single_copy = self._fused_supported() and (decode_weights == "replace" or (
+            decode_weights == "auto" and cfg.is_moe and self.device.type != "cpu"))
         if cfg.is_moe:
             from .moe import MoEBlock
 
@@ -212,9 +217,10 @@ class TransformerLM:
           dg_f32 for the few-row projections; MoE experts likewise (MoEBlock.adopt_single_copy: the streaming and
           grouped prefill GEMM kernels); the fp32 oracle and exports unshuffle (layout.natural_tensors);
         * "shared": row-major only (the decode GEMMs' row-major variants);
-        * "auto": "preshuffled" when the copies fit next to the KV cache's need (transformer.copy_budget), "replace"
-          otherwise (70B on one GPU: 141 GB of layer weights; Mixtral when its expert copies did not all fit),
-          row-major only where neither applies."""
+        * "auto": MoE models "replace" (profiles/r6/e2e_mixtral_c5_single_copy.jsonl: equal end to end, 90 GB
+          less); dense models "preshuffled" when the copy fits next to the KV cache's need (transformer.copy_budget;
+          their prefill is faster on the library GEMMs), "replace" otherwise (70B on one GPU: 141 GB of layer
+          weights), row-major only where neither applies."""
         if not self.fused or mode == "shared" or (self.device.type == "cpu" and mode != "replace"):
             return {}
         names = ["wqkv", "wo"] + ([] if self.cfg.is_moe else ["w_gu", "w_down"])
@@ -227,7 +233,11 @@ class TransformerLM:
             # launch) only from what the same budget has left, so it never costs a model its layer copies.  The
             # budget: what is left after the KV cache's need and a 6 GB workspace reserve
             budget = copy_budget(self.device, self.kv_reserve)
-            if extra > budget or (self.moe is not None and not self.moe.all_copies()):
+            if self.moe is not None:
+                mode = "replace" if self.moe.single_copy_ok() else "shared"
+                if mode == "shared":
+                    return {}
+            elif extra > budget:
                 mode = "replace"
             if head is not None and (mode == "replace" or extra + head.numel() * 2 > budget):
                 head = None

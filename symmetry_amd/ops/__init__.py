@@ -459,9 +459,14 @@ def grouped_stream_policy(p: int) -> None:
     _native.ops().grouped_stream_policy(int(p))
 
 
-def grouped_skinny(xs, W, offsets, e0, y):
+def grouped_skinny(xs, W, offsets, e0, y, wshuf: bool = False):
+    """``wshuf``: W MFMA-preshuffled per expert (models/layout.py::preshuffle)."""
     if _gpu(xs):
-        return _native.ops().grouped_skinny(xs, W, offsets, int(e0), y)
+        return _native.ops().grouped_skinny(xs, W, offsets, int(e0), y, bool(wshuf))
+    if wshuf:
+        from ..models.layout import unshuffle
+
+        W = unshuffle(W)
     return reference.grouped_skinny(xs, W, offsets, e0, y)
 
 

@@ -240,6 +240,12 @@ def test_moe_kernels_vs_reference(gpu):
         a, b = int(off[e]), int(off[e + 1])
         ref_y[a:b] = xs[a:b].float().cpu() @ W[e].float().cpu().t()
     assert torch.allclose(y.sum(0).cpu(), ref_y, atol=2e-2, rtol=1e-2)
+    # the same product on the per-expert MFMA-preshuffled stacks (single-copy expert weights)
+    from symmetry_amd.models.layout import preshuffle
+
+    ys = torch.full_like(y, float("nan"))
+    ops.grouped_skinny(xs, preshuffle(W), offsets, 0, ys, wshuf=True)
+    assert torch.equal(ys.sum(0), y.sum(0)), "preshuffled skinny GEMM differs from the row-major one"
     out = torch.empty(T, 2 * F, device=gpu)
     ops.moe_combine(y, dst, ids, 0, E, w, k, out)
     c_out = torch.empty(T, 2 * F)
