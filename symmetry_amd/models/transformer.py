@@ -388,13 +388,14 @@ class TransformerLM:
         GEMM + swiglu kernel).  Dense model on one GPU with the preshuffled copies, PGEMM_GU_MIN_M..PGEMM_GU_MAX_M
         rows: where one wave of 320 / 384 x 224 tiles covers the projection it beats hipBLASLt + the swiglu launch
         (768 rows: 149 vs 155.5 + 13.8 us per layer, profiles/r6/prof_prefill768_pg_gu.csv); elsewhere the library
-        wins (profiles/r6/pgemm_gu_sweep.jsonl, prefill_pgemm_ab3.jsonl).  The other three projections measured faster on the library path even
-        against fused pgemm epilogues (profiles/r6/prefill_pgemm_ab.jsonl: qkv 76 vs 59, o 56 vs 45, down 99 vs 81 us
-        with their consumers), so they stay there."""
+        wins (profiles/r6/pgemm_gu_sweep.jsonl, prefill_pgemm_ab3.jsonl).  The other three projections measured faster on
+        the library path even against fused pgemm epilogues (profiles/r6/prof_prefill768_pg_all4_fused.csv: qkv 76 vs
+        59, o 56 vs 45, down 99 vs 81 us with their consumers), so they stay there.  (Single-copy models at every
+        prefill size instead of pgemm + swiglu measured even: Llama-3-70B 4 x 128-token TTFT 76.98 vs 76.5 ms.)"""
         if (self.cfg.is_moe or self._tp_active() or not self.dgw or self.device.type == "cpu"
                 or not ops.PGEMM_GU_MIN_M <= T <= ops.PGEMM_GU_MAX_M):
             return None
-        pick = ops.choose_pgemm(T, self.dgw[(0, "w_gu")].shape[0], self.cfg.hidden_size)
+        pick = ops.choose_pgemm(T, self.dgw[(0, "w_gu")].shape[0], self.cfg.hidden_size, force=self.single_copy)
         return None if pick is None else pick[0]
 
     def _mg_plan(self, b: ForwardBatch, names=("qkv", "o", "gu", "down"), need_all: bool = True,

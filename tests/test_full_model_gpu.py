@@ -10,12 +10,16 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def engine8b():
+@pytest.fixture(scope="module", params=["auto", "replace"])
+def engine8b(request):
+    """auto: preshuffled decode copies + row-major weights (library / pgemm prefill); replace: the single
+    preshuffled copy, every prefill projection on pgemm / mgemm (the 70B-on-one-GPU layout at 8B shapes)."""
     from symmetry_amd.engine.llm_engine import EngineConfig, LLMEngine
 
     eng = LLMEngine(EngineConfig(model="llama3:8b", device="cuda:0", max_num_seqs=16, max_model_len=2048,
-                                 num_kv_blocks=16 * 2048 // 64 + 16, use_graphs=True))
+                                 num_kv_blocks=16 * 2048 // 64 + 16, use_graphs=True,
+                                 decode_weights=request.param))
+    assert eng.model.single_copy == (request.param == "replace")
     eng.warmup([16, 128, 512, 768])
     yield eng
     del eng
