@@ -559,9 +559,28 @@ void moe_route_permute(const Tensor& logits, const Tensor& x, int64_t k, int64_t
   const int64_t ld = logits.size(logits.dim() - 1);
   TORCH_CHECK(ld >= E, "moe: logits narrower than E");
   launch_moe_route(linout(logits, T, ld, "logits"), (int)ld, (int)T, (int)E, (int)k, ptr<int>(ids), ptr<float>(w), s);
-  launch_moe_align(ptr<int>(ids), (int)(T * k), (int)E, ptr<int>(counts), ptr<int>(offsets), ptr<int>(cursor), s);
-  launch_moe_scatter(ptr<bf16>(x), (int)T, (int)d, (int)k, (int)E, ptr<int>(ids), ptr<int>(offsets), ptr<int>(cursor),
+  // rows placed by the align kernel (LDS atomics): the scatter is a plain copy
+  launch_moe_align(ptr<int>(ids), (int)(T * k), (int)E, ptr<int>(counts), ptr<int>(offsets), ptr<int>(cursor), s,
+                   ptr<int>(dst));
+  launch_moe_scatter(ptr<bf16>(x), (int)T, (int)d, (int)k, (int)E, ptr<int>(ids), ptr<int>(offsets), nullptr,
                      ptr<bf16>(xs), (int)(T * k), ptr<int>(dst), nullptr, s);
+}
+
+// Router logits: fp32 [T, 16] = x [T, d] @ Wr[16, d]^T (router rows padded to 16).
+void moe_router(const Tensor& x, const Tensor& Wr, Tensor& logits) {
+  check_gpu(x, "x");
+  check_gpu(Wr, "Wr");
+  check_gpu(logits, "logits");
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(Wr, at::kBFloat16, "Wr");
+  check_dtype(logits, at::kFloat, "logits");
+  TORCH_CHECK(x.dim() == 2 && Wr.dim() == 2 && Wr.size(0) == 16 && Wr.size(1) == x.size(1),
+              "moe_router: x [T, d], Wr [16, d]");
+  TORCH_CHECK(x.size(1) % 128 == 0, "moe_router: d % 128");
+  TORCH_CHECK(logits.numel() == x.size(0) * 16 && logits.is_contiguous(), "moe_router: logits [T, 16]");
+  TORCH_CHECK(x.is_contiguous() && Wr.is_contiguous(), "moe_router: contiguous inputs");
+  const at::OptionalDeviceGuard g(x.device());
+  launch_moe_router(ptr<bf16>(x), ptr<bf16>(Wr), ptr<float>(logits), (int)x.size(0), (int)x.size(1), cur_stream(x));
 }
 
 // Routing only: logits LinOut [T][E] -> top-k ids [T*k] + softmax-renormalised weights [T*k].
@@ -1203,6 +1222,8 @@ TORCH_LIBRARY(symmetry_amd, m) {
       "Tensor(b!) out_keys, Tensor(c!) out_ids, int n_offset, Tensor(d!)? logits) -> ()",
       &lm_head_sample);
   m.def("swiglu(Tensor gu, Tensor(a!) out, bool interleaved=False) -> ()", &swiglu);
+  m.def(
+      "moe_router(Tensor x, Tensor Wr, Tensor(a!) logits) -> ()", &moe_router);
   m.def(
       "moe_route_permute(Tensor logits, Tensor x, int k, int E, Tensor(a!) ids, Tensor(b!) w, Tensor(c!) counts, "
       "Tensor(d!) offsets, Tensor(e!) cursor, Tensor(f!) xs, Tensor(g!) dst) -> ()",

@@ -194,7 +194,11 @@ void launch_swiglu(LinOut gu, bf16* out, int T, int F, hipStream_t s, int interl
 
 // moe.hip
 void launch_moe_route(LinOut logits, int ld, int T, int E, int k, int* ids, float* w, hipStream_t s);
-void launch_moe_align(const int* ids, int n, int E, int* counts, int* offsets, int* cursor, hipStream_t s);
+// fp32 logits [T][16] = x [T][d] . Wr[16][d]^T (router rows padded to 16), d % 128 == 0
+void launch_moe_router(const bf16* x, const bf16* Wr, float* logits, int T, int d, hipStream_t s);
+// dst (optional): each assignment's row in its segment (the scatter then runs with cursor == nullptr)
+void launch_moe_align(const int* ids, int n, int E, int* counts, int* offsets, int* cursor, hipStream_t s,
+                      int* dst = nullptr);
 void launch_moe_scatter(const bf16* x, int T, int d, int k, int E, const int* ids, const int* offsets, int* cursor,
                         bf16* xs, int R, int* dst, int* src_tok, hipStream_t s);
 // E_all: experts in the global numbering of `offsets` (sizes the streaming path's row blocks); 0 = E.

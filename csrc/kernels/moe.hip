@@ -20,6 +20,39 @@
 namespace {
 
 
+// Router logits of a prefill-sized step: fp32 [T][16] = x [T][d] . Wr[16][d]^T (Wr: the router rows padded to 16).
+// One workgroup per 16 tokens, its NW waves splitting d (16 waves when d % 512 == 0: every wave's loads are in
+// flight at once -- with 4 waves the 32-deep k loop was latency-bound, 14.2 us at 512 tokens); v_mfma_f32_16x16x32_bf16
+// with the router rows as the A operand (a lane (token r16, h) ends with experts 4h .. 4h + 3 of its token), the
+// partials summed through LDS.  Replaces a library GEMM of N = 16 (15.3 us per Mixtral layer at 512 tokens).
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void moe_router_kernel(const bf16* __restrict__ x, const bf16* __restrict__ Wr,
+                                                             float* __restrict__ logits, int T, int d) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, h = lane >> 4;
+  const int row = blockIdx.x * 16 + r16;
+  const int kw = d / NW;  // this wave's k range (a multiple of 32)
+  const bf16* xr = x + (long long)min(row, T - 1) * d + wid * kw + 8 * h;
+  const bf16* wr = Wr + (long long)r16 * d + wid * kw + 8 * h;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+  for (int k0 = 0; k0 < kw; k0 += 32) {
+    Pack8 a, b;
+    a.u = *reinterpret_cast<const uint4*>(wr + k0);
+    b.u = *reinterpret_cast<const uint4*>(xr + k0);
+    acc = mfma16(a.v, b.v, acc);
+  }
+  __shared__ f32x4 red[NW][64];
+  red[wid][lane] = acc;
+  __syncthreads();
+  if (wid == 0 && row < T) {
+    f32x4 v = red[0][lane];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) v += red[w][lane];
+    *reinterpret_cast<float4*>(logits + (long long)row * 16 + 4 * h) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 // One wave per token.  E <= 64 experts (lane e holds logit e), k <= 8.
 __global__ __launch_bounds__(256) void moe_route_kernel(LinOut logits, int ld, int T, int E, int k,
                                                         int* __restrict__ ids, float* __restrict__ w) {
@@ -74,10 +107,13 @@ __global__ __launch_bounds__(256) void moe_route_kernel(LinOut logits, int ld, i
 // Single workgroup: histogram of the routed expert ids (LDS atomics), exclusive prefix sum ->
 // offsets[E+1], counts[E], and the scatter cursor zeroed.  Doing the zeroing here (instead of a
 // hipMemsetAsync node) keeps the whole MoE step a plain kernel chain under hipGraph replay.
+// dst (optional): each assignment's row in its segment, placed here with LDS atomics, so the scatter needs no
+// global atomics (1024 workgroups bumping 8 global cursors serialised a 4 x 128-token Mixtral scatter: 15.6 us).
 __global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__ ids, int n, int E,
                                                          int* __restrict__ counts, int* __restrict__ offsets,
-                                                         int* __restrict__ cursor) {
+                                                         int* __restrict__ cursor, int* __restrict__ dst) {
   __shared__ int hist[64];
+  __shared__ int base[64];
   if (threadIdx.x < 64) hist[threadIdx.x] = 0;
   __syncthreads();
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -91,14 +127,22 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__
       offsets[e] = acc;
       counts[e] = hist[e];
       cursor[e] = 0;
+      base[e] = acc;
       acc += hist[e];
     }
     offsets[E] = acc;
   }
+  if (dst == nullptr) return;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int e = ids[i];
+    if (e >= 0 && e < E) dst[i] = atomicAdd(&base[e], 1);
+  }
 }
 
 // one 256-thread block per (token, slot); cursor[E] zeroed by the op.  Assignments with an expert id
-// outside [0, E) (empty slots of an expert-parallel receive buffer) are skipped.
+// outside [0, E) (empty slots of an expert-parallel receive buffer) are skipped.  cursor == nullptr: the rows
+// were placed by moe_align (dst precomputed).
 __global__ __launch_bounds__(256) void moe_scatter_kernel(const bf16* __restrict__ x, int d, int k, int R, int E,
                                                           const int* __restrict__ ids, const int* __restrict__ offsets,
                                                           int* __restrict__ cursor, bf16* __restrict__ xs,
@@ -109,8 +153,8 @@ __global__ __launch_bounds__(256) void moe_scatter_kernel(const bf16* __restrict
   if (e < 0 || e >= E) return;
   __shared__ int row;
   if (threadIdx.x == 0) {
-    row = offsets[e] + atomicAdd(&cursor[e], 1);
-    dst[a] = row;
+    row = cursor != nullptr ? offsets[e] + atomicAdd(&cursor[e], 1) : dst[a];
+    if (cursor != nullptr) dst[a] = row;
     if (src_tok) src_tok[row] = t;
   }
   __syncthreads();
@@ -1055,13 +1099,19 @@ void launch_moe_combine_prep(LinOut y, int R, const int* dst, const int* ids, in
   moe_combine_prep_kernel<<<dim3(T, parts), 64, 0, s>>>(y, R, dst, ids, E, w, k, d, resid, w_next, xw, ss);
 }
 
+void launch_moe_router(const bf16* x, const bf16* Wr, float* logits, int T, int d, hipStream_t s) {
+  if (T == 0) return;
+  if (d % 512 == 0) moe_router_kernel<16><<<(T + 15) / 16, 1024, 0, s>>>(x, Wr, logits, T, d);
+  else moe_router_kernel<4><<<(T + 15) / 16, 256, 0, s>>>(x, Wr, logits, T, d);
+}
+
 void launch_moe_route(LinOut logits, int ld, int T, int E, int k, int* ids, float* w, hipStream_t s) {
   if (T == 0) return;
   moe_route_kernel<<<(T + 3) / 4, 256, 0, s>>>(logits, ld, T, E, k, ids, w);
 }
 
-void launch_moe_align(const int* ids, int n, int E, int* counts, int* offsets, int* cursor, hipStream_t s) {
-  moe_align_kernel<<<1, 1024, 0, s>>>(ids, n, E, counts, offsets, cursor);
+void launch_moe_align(const int* ids, int n, int E, int* counts, int* offsets, int* cursor, hipStream_t s, int* dst) {
+  moe_align_kernel<<<1, 1024, 0, s>>>(ids, n, E, counts, offsets, cursor, dst);
 }
 
 void launch_moe_scatter(const bf16* x, int T, int d, int k, int E, const int* ids, const int* offsets, int* cursor,

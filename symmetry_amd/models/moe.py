@@ -248,7 +248,7 @@ class MoEBlock:
         else:  # the one-workgroup routing launch stops paying off past a few rows (bench_moe_decode.py)
             xn = self._buf("xn", (T, d), torch.bfloat16)
             ops.rms_norm(resid, lnw, eps, xn)
-            logits = self.m._linear("router", xn, self.router[i])
+            logits = self._router_logits(i, xn)
             ops.moe_route_permute(logits, xn, k, E, ids, w, counts, offsets, cursor, xs, dst)
         y2 = self._experts(i, xs, offsets, self.e_lo, self.E_local, out_f32=True)
         if self.ep > 1:
@@ -264,11 +264,20 @@ class MoEBlock:
         return ss
 
     # ------------------------------------------------------------------------------------------
+    def _router_logits(self, i, x):
+        """Router logits of x's rows: the 16-expert-row MFMA kernel (fp32, one launch) where the padded router is
+        16 rows, else the projection path."""
+        if self.router[i].shape[0] == 16 and x.shape[1] % 128 == 0 and x.is_contiguous():
+            logits = self._buf("router_logits", (x.shape[0], 16), torch.float32)
+            ops.moe_router(x, self.router[i], logits)
+            return logits
+        return self.m._linear("router", x, self.router[i])
+
     def _route(self, i, x):
         T, d = x.shape
         k, E = self.k, self.E
         R = T * k
-        logits = self.m._linear("router", x, self.router[i])
+        logits = self._router_logits(i, x)
         ids = self._buf("ids", (R,), torch.int32)
         w = self._buf("w", (R,), torch.float32)
         dst = self._buf("dst", (R,), torch.int32)
@@ -459,7 +468,7 @@ class MoEBlock:
         xg = getattr(self.comm, "a2a_fits", None)
         xg = xg is not None and xg(cap, d * 4)
         if Tr > 0:
-            logits = self.m._linear("router", x, self.router[i])
+            logits = self._router_logits(i, x)
             ops.moe_route(logits, Tr, k, E, ids, w)
             owner = self._buf("a2a.owner", (R,), torch.int32)
             torch.floor_divide(ids[:R], El, out=owner)

@@ -568,10 +568,21 @@ class TransformerLM:
         if gu_plan is not None:
             xw = self._buf("xw", (T, d), torch.bfloat16)
             ss_p = self._buf("ss_pgu", (T, 4 if d % 32 == 0 else 1), torch.float32)
+        # single-copy models past the medium-M range: QKV + RoPE + paged K/V write in one prefill-GEMM launch (the
+        # pgemm path would write fp32 k-split slabs that rope_cache then reads: Mixtral 4 x 128 tokens, rope 9.4 ->
+        # 19.8 us per layer, profiles/r6/prof_mixtral_prefill_4x128_r6b.csv)
+        pg_qkv = None
+        if self.single_copy and T >= ops.PGEMM_MIN_M and b.kind != "decode" and self.device.type != "cpu":
+            pick = ops.choose_pgemm(T, (self.hq + 2 * self.hkv) * self.D, d, align=128, force=True)
+            pg_qkv = None if pick is None else pick[0]
         for i in range(cfg.num_layers):
-            qkv = self._linear("qkv", x, self._row_major(i, "wqkv"), wshuf=self._shuf(i, "wqkv"))
-            ops.rope_cache(qkv, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq, self.hkv,
-                           perm=True, decode=ROPE_DECODE_ROWS and b.kind == "decode")
+            if pg_qkv is not None:
+                ops.pg_qkv(x, self.dgw[(i, "wqkv")], None, eps, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i],
+                           kv.v[i], self.hq, self.hkv, pg_qkv)
+            else:
+                qkv = self._linear("qkv", x, self._row_major(i, "wqkv"), wshuf=self._shuf(i, "wqkv"))
+                ops.rope_cache(qkv, b.positions, b.slot_mapping, self.cos_sin, q, kv.k[i], kv.v[i], self.hq,
+                               self.hkv, perm=True, decode=ROPE_DECODE_ROWS and b.kind == "decode")
             self._attention(b, kv, i, q, attn)
             o = self._linear("o", attn.view(T, self.hq * self.D), self._row_major(i, "wo"), reduce=True,
                              wshuf=self._shuf(i, "wo"))

@@ -459,6 +459,14 @@ def grouped_stream_policy(p: int) -> None:
     _native.ops().grouped_stream_policy(int(p))
 
 
+def moe_router(x, Wr, logits):
+    """Router logits fp32 [T, 16] = x [T, d] @ Wr[16, d]^T (router rows padded to 16; csrc/kernels/moe.hip)."""
+    if _gpu(x):
+        return _native.ops().moe_router(x, Wr, logits)
+    logits.copy_(x.float() @ Wr.float().t())
+    return logits
+
+
 def grouped_skinny(xs, W, offsets, e0, y, wshuf: bool = False):
     """``wshuf``: W MFMA-preshuffled per expert (models/layout.py::preshuffle)."""
     if _gpu(xs):

@@ -202,6 +202,18 @@ def test_graph_replay_equals_eager(gpu):
     assert outs[0] == outs[1]
 
 
+@pytest.mark.parametrize("T", [1, 16, 37, 512])
+def test_moe_router_logits_vs_fp32(gpu, T):
+    """The 16-row router kernel (prefill routing) against the fp32 product; rows past T untouched."""
+    d = 4096
+    g = torch.Generator(device=gpu).manual_seed(T)
+    x = torch.randn(T, d, device=gpu, generator=g).bfloat16()
+    Wr = (torch.randn(16, d, device=gpu, generator=g) * 0.02).bfloat16()
+    logits = torch.full((T, 16), float("nan"), device=gpu)
+    ops.moe_router(x, Wr, logits)
+    torch.testing.assert_close(logits, x.float() @ Wr.float().t(), atol=2e-3, rtol=2e-3)
+
+
 def test_moe_kernels_vs_reference(gpu):
     T, d, E, k, F = 11, 256, 8, 2, 512
     g = torch.Generator(device=gpu).manual_seed(0)
