@@ -105,3 +105,22 @@ def test_bench_too_few_gpus_is_an_error(monkeypatch, capsys):
     assert "8 GPUs, 1 visible" in line["error"] and line["value"] is None
     plan = bench.launch_plan(["--gpus", "8"], 8, 29555)
     assert "--nproc-per-node=8" in plan and "--master-addr" in plan and "127.0.0.1" in plan
+
+
+def test_ep_rehearsal_reports_bytes_per_mode():
+    """bench/ep_rehearsal.py (the EP operating-point sweep) on gloo with tiny-mixtral: one JSON line per prompt total
+    and mode; the owner exchange pushes fewer bytes per layer than the fp32 all-reduce combine at world 2."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    out = {}
+    for mode in ("a2a", "allreduce"):
+        p = subprocess.run([sys.executable, "bench/ep_rehearsal.py", "--world", "2", "--mode", mode, "--model",
+                            "tiny-mixtral", "--tokens", "256", "--reps", "1", "--device", "cpu", "--kv-blocks", "64"],
+                           cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-3000:]
+        rows = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+        assert len(rows) == 1 and rows[0]["mode"] == mode and rows[0]["tokens"] == 256, rows
+        out[mode] = rows[0]
+    assert out["a2a"]["moe_calls"]["a2a"] > 0 and out["allreduce"]["moe_calls"]["allreduce"] > 0
+    d = 256  # tiny-mixtral hidden size
+    assert out["allreduce"]["bytes_per_layer_rank0"] == 2 * (2 - 1) * 256 * d * 4 // 2
+    assert 0 < out["a2a"]["bytes_per_layer_rank0"] < out["allreduce"]["bytes_per_layer_rank0"]
