@@ -2,7 +2,7 @@
 between them), the span from its first to its last kernel, the summed kernel time, the idle time and the
 largest idle gaps (where the GPU waited for the host).
 
-usage: python tools/prefill_gaps.py DB [--min-gemms 64]"""
+usage: python tools/prefill_gaps.py DB [--min-gemms 64] [--detail]"""
 import sqlite3
 import sys
 
@@ -42,6 +42,14 @@ def main():
         print(f"step: {len(st)} GEMMs, {len(win)} kernels, span {span / 1e6:.3f} ms, busy {busy / 1e6:.3f} ms, "
               f"idle {(span - busy) / 1e6:.3f} ms; largest gaps (us): "
               + ", ".join(f"{g / 1e3:.1f} before {n}" for g, n in gaps[:5]))
+        if "--detail" in sys.argv:  # per-kernel totals of the step (us): which kernels the span is made of
+            tot = {}
+            for name, s, e in win:
+                k = name[:70]
+                n, t = tot.get(k, (0, 0.0))
+                tot[k] = (n + 1, t + (e - s) / 1e3)
+            for k, (n, t) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:8]:
+                print(f"    {t:9.1f} us  {n:4d} x {t / n:7.2f}  {k}")
 
 
 if __name__ == "__main__":
