@@ -316,6 +316,12 @@ def _ep_worker(rank, world, model="tiny-mixtral"):
     ref = ref_model.moe.forward(0, x_all[0]).clone()
     ep_model.moe.mode = "allreduce"
     outs["allreduce"] = torch.allclose(ep_model.moe.forward(0, x_all[0]), ref, atol=1e-4)
+    # the same with every rank's expert shard held once, MFMA-preshuffled (decode_weights="replace")
+    sc_model = TransformerLM(random_weights(cfg, ShardSpec(0, 1, rank, world), seed=3), "cpu", ep_comm=comm,
+                             decode_weights="replace")
+    sc_model.moe.mode = "allreduce"
+    outs["single_copy_allreduce"] = sc_model.moe.single_copy and torch.allclose(
+        sc_model.moe.forward(0, x_all[0]), ref, atol=1e-4)
     # owner exchange over token slices: identical tokens, every rank's local-expert partials go to the slice
     # owners, a bf16 all-gather rebuilds the output (within one bf16 rounding of the fp32 local block)
     ep_model.moe.mode = "a2a"
