@@ -227,7 +227,11 @@ class LLMEngine:
             return max(16, min(want, (1 << 30) // per_block))
         free, total = torch.cuda.mem_get_info(self.device)
         reserve = 6 << 30  # workspace, graphs, library GEMM scratch
-        budget = max(0, int((free - reserve) * self.cfg.kv_cache_fraction))
+        # ranks sharing one GPU (the one-GPU TP/EP rehearsal) each read the same free memory at about the same time:
+        # each takes its share of it, or the later allocation runs out of HBM
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", max(self.cfg.tp_size, self.cfg.ep_size)))
+        sharing = max(1, -(-local // max(1, torch.cuda.device_count())))
+        budget = max(0, int((free - reserve) * self.cfg.kv_cache_fraction) // sharing)
         return max(16, budget // per_block)
 
     # ---- fault containment ----------------------------------------------------------------------
