@@ -48,7 +48,9 @@ class BlockManager:
         self.ref = [0] * num_blocks
         self.block_hash: dict[int, bytes] = {}      # block -> content key (registered blocks)
         self.cached: dict[bytes, int] = {}          # content key -> block
-        self.cache_gen = 0                          # blocks ever registered (queued misses re-look when it grows)
+        self.cache_gen = 0                          # blocks ever registered
+        self.scope_gen: dict[bytes, int] = {}       # blocks ever registered per scope (queued misses re-look when
+                                                    # their own scope's count grows: no other scope can match them)
         self.evictable: collections.OrderedDict[int, None] = collections.OrderedDict()  # ref 0, LRU order
         self.hit_tokens = 0
         self.query_tokens = 0
@@ -107,10 +109,11 @@ class BlockManager:
         # a miss is not re-queried on every schedule() (which kept the hit-rate denominator growing while a
         # prompt waited) unless blocks were cached since the last look: a queued prompt that missed while a
         # same-scope prefix was still being prefilled finds it once that prefill registered its blocks
-        if seq.prefix_checked and seq.prefix_epoch == self.cache_gen:
+        gen = self.scope_gen.get(seq.cache_scope, 0)
+        if seq.prefix_checked and seq.prefix_epoch == gen:
             return 0
         first = not seq.prefix_checked
-        seq.prefix_checked, seq.prefix_epoch = True, self.cache_gen
+        seq.prefix_checked, seq.prefix_epoch = True, gen
         tokens = seq.token_ids
         target = seq.prefill_target
         nfull = max(0, target - 1) // self.block_size  # >= 1 token left to prefill
@@ -145,6 +148,7 @@ class BlockManager:
             self.block_hash[b] = h
             self.cached[h] = b
             self.cache_gen += 1
+            self.scope_gen[seq.cache_scope] = self.scope_gen.get(seq.cache_scope, 0) + 1
 
     def release(self, seq: Sequence) -> None:
         self.register(seq)

@@ -493,6 +493,27 @@ def test_prefix_requery_counts_the_query_once():
     assert bm.match_prefix(waiting) == 12 and bm.query_tokens == 13 and bm.hit_tokens == 12
 
 
+def test_prefix_requery_only_on_own_scope_blocks(monkeypatch):
+    """A queued miss is looked up again only when blocks of its own scope (client) were cached:
+    another client's blocks can never match it, so they do not trigger a re-look (hash chain) every step."""
+    bm = BlockManager(64, 4, prefix_caching=True)
+    waiting = Sequence("w", list(range(12)) + [99], SamplingParams(max_tokens=1), cache_scope=b"A")
+    assert bm.match_prefix(waiting) == 0
+    looks = []
+    chain = bm._chain
+    monkeypatch.setattr(bm, "_chain", lambda *a: (looks.append(a[2]), chain(*a))[1])
+    other = Sequence("o", list(range(12)), SamplingParams(max_tokens=1), cache_scope=b"B")
+    bm.grow(other, 12)
+    other.num_computed = 12
+    bm.register(other)  # same tokens, other client: not adoptable, no re-look
+    assert bm.match_prefix(waiting) == 0 and looks == [b"B"]
+    mine = Sequence("m", list(range(12)), SamplingParams(max_tokens=1), cache_scope=b"A")
+    bm.grow(mine, 12)
+    mine.num_computed = 12
+    bm.register(mine)
+    assert bm.match_prefix(waiting) == 12 and looks == [b"B", b"A", b"A"]
+
+
 def test_single_copy_preshuffled_weights_match_oracle():
     """decode_weights="replace": the layer weights exist once, MFMA-preshuffled in place (70B on one GPU), and every
     path reads that layout -- fused decode, the general path's few-row (dg_f32) and long (prefill GEMM) projections --
