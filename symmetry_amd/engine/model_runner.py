@@ -22,6 +22,7 @@ from __future__ import annotations
 import itertools
 import math
 import os
+import sys
 import time
 
 import numpy as np
@@ -44,6 +45,9 @@ HEADER_LEN = 7  # kind, T, rows, max_blocks, prefill tiles, real seqs, filtered-
 # Captured at start-up only (capture_all: every token bucket x one sequence x every context bucket): a bucket
 # captured lazily in serving cost its first request ~14 ms of TTFT (multi-turn turn 2: 6.7 -> 21 ms,
 # profiles/r4/multiturn_prefill_graph_ab.jsonl); a step whose bucket was not captured runs eagerly.
+_DEBUG_PREFILL = os.environ.get("SYMMETRY_DEBUG_PREFILL") == "1"
+
+
 def _ints(name: str, default: str) -> tuple:
     return tuple(int(v) for v in os.environ.get(name, default).split(",") if v.strip())
 
@@ -334,6 +338,11 @@ class ModelRunner:
         host_t = self._host(lay.size, f"{batch.kind}{self._parity}")  # double-buffered: the previous
         host = host_t.numpy()                                          # step's H2D may still be queued
         self._fill(lay, host, seqs, counts, prev_rows)
+        if _DEBUG_PREFILL and batch.kind != "decode":  # the shape a prefill step's kernels see (bench diagnosis)
+            bts = [b for s in seqs for b in s.block_table]
+            print(f"symmetry: prefill step T={sum(counts)} seqs={nseq} new={list(counts)} "
+                  f"computed={[s.num_computed for s in seqs]} blocks={[len(s.block_table) for s in seqs]} "
+                  f"block ids {min(bts)}..{max(bts)} kind={kind}", file=sys.stderr, flush=True)
         header = np.array([kind, lay.T, lay.nseq, lay.max_blocks, lay.ntiles, nseq, filt], dtype=np.int32)
         t1 = time.perf_counter()
         if self.meta is not None:

@@ -2,7 +2,10 @@
 between them), the span from its first to its last kernel, the summed kernel time, the idle time and the
 largest idle gaps (where the GPU waited for the host).
 
-usage: python tools/prefill_gaps.py DB [--min-gemms 64] [--detail]"""
+usage: python tools/prefill_gaps.py DB [--min-gemms 64] [--detail] [--series SUBSTR[,SUBSTR...]]
+
+--series: the per-launch durations (us, in launch order) of the kernels whose name contains SUBSTR -- whether a
+slow kernel is slow in every layer or only at the step's start (clock ramp after idle)."""
 import sqlite3
 import sys
 
@@ -50,6 +53,11 @@ def main():
                 tot[k] = (n + 1, t + (e - s) / 1e3)
             for k, (n, t) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:8]:
                 print(f"    {t:9.1f} us  {n:4d} x {t / n:7.2f}  {k}")
+        if "--series" in sys.argv:
+            for sub in sys.argv[sys.argv.index("--series") + 1].split(","):
+                ds = [(e - s) / 1e3 for name, s, e in win if sub in name]
+                if ds:
+                    print(f"    series {sub}: " + " ".join(f"{d:.1f}" for d in ds))
 
 
 if __name__ == "__main__":
