@@ -296,6 +296,10 @@ def test_xgmi_gemm_all_reduce_resid_one_launch(gpu, world, M, form):
 
     ops = _native.ops()
     N, K = {"gemm8": (1024, 512), "gemm4": (1024, 1792), "xres": (2048, 1024), "gemm8_shuf": (1024, 512)}[form]
+    if world == 8 and form.startswith("gemm8"):
+        # all 8 ranks' grids share this one GPU: 8 x 64 512-thread workgroups are not co-resident, 8 x 32 are (on 8
+        # GPUs each rank's grid has a GPU of its own: the TP = 8 o projection is N = 4096, K = 512 per rank)
+        N = 512
     shuf = form in ("xres", "gemm8_shuf")
     hs = _comms(ops, world, slot_bytes=16 * N * 8 + 256)
     g = torch.Generator(device="cpu").manual_seed(M * 31 + world)
@@ -338,7 +342,7 @@ def test_xgmi_gemm_ar_resid_skewed_alternating(gpu, world, xres):
     from symmetry_amd.ops import _native
 
     ops = _native.ops()
-    N = 1024
+    N = 512 if world == 8 and not xres else 1024  # 8 ranks' 512-thread grids on one GPU: 8 x 32 fit, 8 x 64 do not
     # (K, preshuffled) of the o- and down-shaped calls: the x-resident walk needs K % 1024 == 0 and preshuffled W
     shapes = [(1024, True), (2048, True)] if xres else [(512, False), (1792, False)]
     M = 4
