@@ -561,3 +561,24 @@ def test_single_copy_moe_experts_match_oracle(monkeypatch):
         assert r["mismatches"] == 0, (n, r)
     names = {c[0] for c in calls}
     assert {"pg_grouped", "grouped_skinny"} <= names, calls
+
+
+@pytest.mark.parametrize("local,devices,share", [(None, 8, 1), ("2", 1, 2), ("4", 1, 4), ("8", 8, 1), ("4", 2, 2)])
+def test_kv_auto_blocks_split_a_shared_gpu(monkeypatch, local, devices, share):
+    """Ranks that share one GPU (the one-GPU TP / EP rehearsal) read the same free HBM at about the same time: each
+    sizes its KV cache from its share of it, or the later rank's allocation runs out of memory."""
+    import types
+
+    free = 200 << 30
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda dev=None: (free, 288 << 30))
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: devices)
+    if local is None:
+        monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    else:
+        monkeypatch.setenv("LOCAL_WORLD_SIZE", local)
+    mcfg = resolve("llama3:8b")
+    cfg = EngineConfig(model="llama3:8b", tp_size=1)
+    fake = types.SimpleNamespace(model_cfg=mcfg, cfg=cfg, device=torch.device("cuda", 0))
+    per_block = mcfg.kv_bytes_per_token() * cfg.block_size
+    want = int((free - (6 << 30)) * cfg.kv_cache_fraction) // share // per_block
+    assert LLMEngine._auto_blocks(fake, 8192) == want
