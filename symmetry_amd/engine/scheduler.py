@@ -148,6 +148,8 @@ class BlockManager:
             self.block_hash[b] = h
             self.cached[h] = b
             self.cache_gen += 1
+            if seq.cache_scope not in self.scope_gen and len(self.scope_gen) >= 1 << 16:
+                self.scope_gen.clear()  # bounded (one entry per client ever seen); a reset costs a re-look each
             self.scope_gen[seq.cache_scope] = self.scope_gen.get(seq.cache_scope, 0) + 1
 
     def release(self, seq: Sequence) -> None:
