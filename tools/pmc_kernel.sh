@@ -10,7 +10,8 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES" \
            "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TA_BUSY_avr" \
-           "GRBM_GUI_ACTIVE SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_INSTS_SALU"; do
+           "GRBM_GUI_ACTIVE SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_INSTS_SALU" \
+           "FETCH_SIZE"; do
   i=$((i + 1))
   timeout -s KILL 120 rocprofv3 --pmc $set --output-format rocpd -d /tmp/pmc_$tag$i -o run -- "$@" \
     > "$root/gpurun_out/pmc_$tag$i.log" 2>&1 || exit $?
